@@ -1,0 +1,180 @@
+"""Benchmark of the offline hot path (BASELINE.json metric).
+
+Workload (default = BASELINE config C3): 1920x1080, 4 spp full path (voxel DDA +
+Disney BSDF + NEE/ReSTIR-DI, bounce limits 3/1 as RayGen.cu:146-147) + ReLAX
+denoiser (TA, history fix, clamping, a-trous 1+3), synthetic 256^3 Perlin voxel
+world (8x8x8 chunks, C1 terrain scaled x4: heights 128, freq 1/256, world-y
+heights), camera = C1 camera with position x4.  One step = one
+OfflineBackend::renderFrame = 4 trace passes + 1 denoise.
+
+value = whole-job Mpaths/s = n_gpus * W*H*spp * K / max-over-ranks wall time of K steps.
+roofline = the denoiser chain (HBM-bound): algorithmic bytes 568 B/px * W*H per
+frame / its HIP-event duration on the context's stream.
+cpu_baseline = the oracle (C++ restatement, OpenMP) tracing a bounded band of
+rows of the same frame on this host's cores (rank 0, N=1 only).
+
+Multi-GPU (N>1, launched by torch.distributed.run): each rank renders its own
+independent frame sequence of the workload (replicas, weak scaling, no
+collective on the data path).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "real-time-path-tracing-voxel-blocks_amd"))
+
+B_ALG_PER_PX = 568  # D1 24 + D2 4 + D3 148 + D4 8 + D5 92 + D6 60 + D7 180 + D8 52
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+C1_POS = (35.6184, 11.8733, 42.0387)
+C1_DIR = (-0.321564, -0.0129988, -0.946799)
+
+
+def scene_args(a):
+    scale = a.world // 64
+    pos = tuple(p * scale for p in C1_POS)
+    chunks = (a.world // 32, a.world // 32, a.world // 32)
+    return chunks, 32.0 * scale, 64.0 * scale, pos
+
+
+def cpu_baseline(a, target_s):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    chunks, hs, fd, pos = scene_args(a)
+    o = oracle.Oracle(a.width, a.height)
+    o.terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
+    o.set_camera(pos, C1_DIR, 90.0)
+    o.set_camera(pos, C1_DIR, 90.0, which=1)
+    o.set_sky()
+    # grow a band around the middle of the frame until it takes about target_s;
+    # past a full frame, trace further 1-spp passes (iterationIndex 1, 2, ...)
+    mid, rows, dt, passes = a.height // 2, 8, 0.0, 1
+    while True:
+        y0 = max(0, mid - rows // 2)
+        t0 = time.perf_counter()
+        for it in range(passes):
+            o.trace(it, y0, y0 + rows, primary_only=a.primary_only)
+        dt = time.perf_counter() - t0
+        if dt >= 0.5 * target_s:
+            break
+        grow = max(2.0, target_s / max(dt, 1e-3))
+        if rows < a.height:
+            rows = int(min(a.height, rows * grow))
+        else:
+            passes = int(passes * grow) + 1
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": passes * rows * a.width / dt / 1e6, "unit": "Mpaths/s", "cores": cores, "kind": "port",
+            "sample": "oracle trace of rows [%d,%d) x %d pass(es) at %dx%d, 1 spp each, %s, same scene (%.1f s)" % (
+                y0, y0 + rows, passes, a.width, a.height, "primary rays only" if a.primary_only else "full path", dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=4)
+    ap.add_argument("--world", type=int, default=256, help="world edge in voxels (multiple of 64)")
+    ap.add_argument("--primary-only", action="store_true", help="C2: primary rays + sky + G-buffer, no denoiser")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import torch
+    import vxpt
+
+    chunks, hs, fd, pos = scene_args(a)
+    r = vxpt.Renderer(a.width, a.height, device=local)
+    r.load_settings()
+    r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
+    r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
+    r.set_sky()
+    params = vxpt.DenoiseParams.defaults()
+
+    def step(frame):
+        if a.primary_only:
+            r.trace(frame, primary_only=True)
+            r.sync()
+        else:
+            r.render_frame(frame, a.spp, params)
+
+    frame = 0
+    for _ in range(a.warmup):
+        step(frame)
+        frame += 1
+
+    def barrier():
+        torch.cuda.synchronize(local)
+        if dist is not None:
+            dist.barrier()
+        r.sync()
+
+    trace_ms, denoise_ms = [], []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(frame)
+        frame += 1
+        t = r.timings()
+        trace_ms.append(t["trace_ms"])
+        denoise_ms.append(t["denoise_ms"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    spp = 1 if a.primary_only else a.spp
+    paths = a.width * a.height * spp
+    value = world * paths * a.steps / elapsed / 1e6
+    avg_trace = sum(trace_ms) / len(trace_ms)
+    avg_dn = sum(denoise_ms) / len(denoise_ms)
+    if a.primary_only:
+        # trace-only mode: compulsory G-buffer writes (illum 16 + depth 4 + normRough 16 + geoNormal 16 +
+        # matParam 16 + albedo 16 + material 4 + motion 16 = 104 B/px)
+        alg_bytes, dur_ms, kern = 104 * a.width * a.height, avg_trace, "k_trace (primary only)"
+    else:
+        alg_bytes, dur_ms, kern = B_ALG_PER_PX * a.width * a.height, avg_dn, "denoiser chain"
+    achieved = alg_bytes / (dur_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a, a.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": "Mpaths/s @1080p 4spp (+ms/frame, denoiser HBM GB/s vs roofline)",
+            "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "C2: %dx%d primary-only DDA + sky + G-buffer" % (a.width, a.height) if
+                       a.primary_only else "C3: %dx%d, %d spp full path + ReLAX denoiser" % (a.width, a.height, a.spp),
+                       "width": a.width, "height": a.height, "spp": spp, "world": "%d^3 voxels, Perlin seed 124" % a.world,
+                       "bounces": "3 total / 1 diffuse", "parallelism": "replicas%d" % world},
+            "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "alg_bytes_per_launch": alg_bytes, "avg_duration_ms": round(dur_ms, 4)},
+            "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * vxpt -- C ABI of the MI355X-native voxel path-tracing hot path.
+ *
+ * Drop-in boundary for the reference's offline render path
+ * (mainOffline.cpp -> OfflineBackend::renderFrame, OfflineBackend.cpp:46-89).
+ * The reference's entry points are C++ singletons with no ABI; each function
+ * below names the reference interface it replaces.
+ *
+ * Conventions: every call returns 0 on success or a negative vxpt_status;
+ * vxpt_last_error() returns a message for the last failure on that context.
+ * No exceptions cross this boundary.  One context per GPU; calls on one
+ * context are not thread safe.  All work is enqueued on the context's HIP
+ * stream; vxpt_sync() waits for it.  Host pointers are plain host memory.
+ */
+#ifndef VXPT_H
+#define VXPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vxpt_ctx vxpt_ctx;
+
+enum vxpt_status {
+    VXPT_OK = 0,
+    VXPT_ERR_ARG = -1,
+    VXPT_ERR_HIP = -2,
+    VXPT_ERR_IO = -3,
+    VXPT_ERR_STATE = -4,
+    VXPT_ERR_NODEV = -5
+};
+
+/* Logical per-pixel buffers (BufferManager.cpp:150-206).  float4 planes are
+ * W*H*16 B, float planes W*H*4 B, RESERVOIRS is 2*W*H*20 B (both parities). */
+enum vxpt_buffer {
+    VXPT_BUF_ILLUM = 0, VXPT_BUF_DEPTH = 1, VXPT_BUF_NORMAL_ROUGH = 2, VXPT_BUF_GEO_NORMAL_THIN = 3,
+    VXPT_BUF_ALBEDO = 4, VXPT_BUF_MATERIAL = 5, VXPT_BUF_MAT_PARAM = 6, VXPT_BUF_MOTION = 7,
+    VXPT_BUF_PREV_NORMAL_ROUGH = 8, VXPT_BUF_PREV_GEO_NORMAL_THIN = 9, VXPT_BUF_PREV_ALBEDO = 10,
+    VXPT_BUF_PREV_MAT_PARAM = 11, VXPT_BUF_PREV_DEPTH = 12, VXPT_BUF_PREV_MATERIAL = 13,
+    VXPT_BUF_RESERVOIRS = 14, VXPT_BUF_PING = 15, VXPT_BUF_PONG = 16, VXPT_BUF_PREV_ILLUM = 17,
+    VXPT_BUF_PREV_FAST = 18, VXPT_BUF_HIST_LEN = 19, VXPT_BUF_PREV_HIST_LEN = 20, VXPT_BUF_OUTPUT = 21,
+    VXPT_BUF_SKY = 32,       /* 1024*512 float4 sky map (Sky.cu:259-303)      */
+    VXPT_BUF_SUN = 33,       /* 32*32 float4 sun map (Sky.cu:305-327)          */
+    VXPT_BUF_VOXELS = 34     /* chunk-major u8 block ids                        */
+};
+
+typedef struct vxpt_config {
+    int32_t width, height;   /* frame size; must be multiples of 8 (Atrous.h has no bounds guard) */
+    int32_t device;          /* HIP device ordinal                                                */
+    int32_t row_begin, row_end; /* band of rows this context traces (multi-GPU); 0,0 = all      */
+    int32_t total_bounce_limit;   /* RayGen.cu:146 (3)  */
+    int32_t diffuse_bounce_limit; /* RayGen.cu:147 (1)  */
+    const char *data_dir;    /* directory holding tables/, settings/, scene/, assets/             */
+} vxpt_config;
+
+typedef struct vxpt_camera {
+    float pos[3];
+    float dir[3];            /* scene_export.yaml camera.direction (normalised internally) */
+    float fov_deg;           /* horizontal field of view                                   */
+} vxpt_camera;
+
+typedef struct vxpt_material {
+    float albedo[3];
+    float roughness;
+    float translucency;
+    int32_t metallic;
+    int32_t material_id;     /* MaterialParameter.materialId, written to the material G-buffer */
+    int32_t thinfilm;
+} vxpt_material;
+
+typedef struct vxpt_denoise_params { /* DenoisingParams, GlobalSettings.h:82-141 */
+    float max_accumulated_frame_num, max_fast_accumulated_frame_num, phi_luminance;
+    float lobe_angle_fraction, roughness_fraction, depth_threshold;
+    float disocclusion_threshold, disocclusion_threshold_alternate, denoising_range;
+    int32_t enable_temporal_accumulation, enable_history_fix, enable_history_clamping;
+    int32_t enable_spatial_filtering, enable_firefly_filter, atrous_iteration_num;
+} vxpt_denoise_params;
+
+typedef struct vxpt_timing {  /* HIP-event times of the last frame, ms (replaces PerformanceTracker) */
+    float trace_ms;
+    float denoise_ms;
+    float sky_ms;
+    float frame_ms;
+} vxpt_timing;
+
+/* replaces OfflineBackend::init(w,h) + BufferManager::init (OfflineBackend.h:30, BufferManager.cpp:107) */
+int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out);
+/* replaces OfflineBackend::clear (OfflineBackend.h:31) */
+void vxpt_destroy(vxpt_ctx *ctx);
+const char *vxpt_last_error(const vxpt_ctx *ctx);
+
+/* GlobalSettings::LoadFromYAML + AssetRegistry/MaterialManager (mainOffline.cpp:142-198):
+ * reads data_dir/settings/global_settings.yaml, assets/{materials,blocks}.yaml */
+int vxpt_load_settings(vxpt_ctx *ctx);
+/* SceneConfigParser::LoadFromFile (SceneConfig.cpp:6-) -> camera */
+int vxpt_load_scene_camera(vxpt_ctx *ctx, const char *scene_yaml, vxpt_camera *out);
+
+/* VoxelEngine::init -> initVoxelsMultiChunk (VoxelSceneGen.cu:341-388): Perlin terrain.
+ * height_scale = 32 and freq_den = 32*chunks_x reproduce the reference.  flags:
+ * VXPT_TERRAIN_SHADER_BALLS keeps the 10 instanced shader balls (their mesh is missing, so
+ * parity scenes drop them); VXPT_TERRAIN_GLOBAL_Y compares world y instead of the chunk-local
+ * y the reference uses (the reference repeats the terrain in every chunk layer; identical
+ * when chunks_y == 1) -- used for the synthetic 256^3 benchmark world. */
+#define VXPT_TERRAIN_SHADER_BALLS 1
+#define VXPT_TERRAIN_GLOBAL_Y 2
+int vxpt_generate_terrain(vxpt_ctx *ctx, int chunks_x, int chunks_y, int chunks_z, float height_scale,
+                          float freq_den, int flags);
+/* upload an explicit grid: chunk-major, 32^3 per chunk, x + 32*(z + 32*y) (VoxelChunk.h:12-55) */
+int vxpt_upload_voxels(vxpt_ctx *ctx, const uint8_t *ids, int chunks_x, int chunks_y, int chunks_z);
+/* MaterialManager GPU table (MaterialManager.cpp:60-170) for block ids 1..12 */
+int vxpt_upload_materials(vxpt_ctx *ctx, const vxpt_material *mats, int n_block_ids);
+/* SkyModel::update (Sky.cu:355-396): sky + sun maps on the GPU, alias tables on the host */
+int vxpt_set_sky(vxpt_ctx *ctx, float time_of_day, float sun_axis_angle_deg, float sun_axis_rotate_deg,
+                 float brightness);
+/* RenderCamera camera/historyCamera (mainOffline.cpp:227-251) */
+int vxpt_set_camera(vxpt_ctx *ctx, const vxpt_camera *cur, const vxpt_camera *prev);
+/* Camera matrices as the kernels see them: pos3 dir3 uvToWorld9 worldToUv9 res2 invRes2 tanHalfFov2 yaw pitch */
+int vxpt_get_camera(vxpt_ctx *ctx, int which, float out32[32]);
+
+/* OptixRenderer::render (OptixRenderer.cpp:411-485): one 1-spp trace pass with the given
+ * iterationIndex.  flags: VXPT_TRACE_PRIMARY_ONLY = C2 bring-up mode (DDA + sky + G-buffer). */
+#define VXPT_TRACE_PRIMARY_ONLY 1u
+int vxpt_trace(vxpt_ctx *ctx, int32_t iteration_index, uint32_t flags);
+/* Denoiser::run (Denoiser.cu:24-408); iteration_index = value after render() incremented it */
+int vxpt_denoise(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame_num, int32_t iteration_index);
+/* one denoiser pass on the current buffers (parity hooks): pass ids as orc_pass */
+int vxpt_denoise_pass(vxpt_ctx *ctx, const vxpt_denoise_params *p, int pass, int arg, int arg2);
+/* OfflineBackend::renderFrame: spp trace passes (radiance averaged) + denoise.  frame_num as
+ * OfflineBackend::m_frameNum; iteration indices frame_num*spp .. +spp-1. */
+int vxpt_render_frame(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame_num, int32_t spp);
+
+/* multi-GPU: exchange `rows` border rows of the planes in buffer_mask with band
+ * neighbours (RCCL when linked by the host process; no-op for a single band) */
+int vxpt_exchange_halo(vxpt_ctx *ctx, uint32_t buffer_mask, int rows);
+
+/* copy any logical buffer to/from host memory (parity hooks, PNG output) */
+int vxpt_readback(vxpt_ctx *ctx, int which, void *host, size_t bytes);
+int vxpt_upload(vxpt_ctx *ctx, int which, const void *host, size_t bytes);
+/* sky alias table (Vose, AliasTable.cu:66-153): q,p floats and alias ints, 1024*512 each */
+int vxpt_get_sky_alias(vxpt_ctx *ctx, float *q, float *p, int32_t *alias, float sun_dir[3]);
+int vxpt_timings(vxpt_ctx *ctx, vxpt_timing *out);
+int vxpt_sync(vxpt_ctx *ctx);
+/* raw stream handle (hipStream_t) for hosts that enqueue their own work */
+void *vxpt_stream(vxpt_ctx *ctx);
+/* DDA probe: n rays (o3 d3 tmin tmax) -> n x (hit x y z face id) + t; mode 0 closest, 2 occluded */
+int vxpt_probe_rays(vxpt_ctx *ctx, int n, const float *rays, int32_t *out6, float *t, int mode);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VXPT_H */

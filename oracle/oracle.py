@@ -1,0 +1,203 @@
+"""ORACLE (test infrastructure only) -- ctypes binding of liboracle.so, the CPU
+restatement of the reference's offline hot path (see oracle/*.cpp headers for
+the reference file:line each function follows).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / CPU baseline; the product never does.
+
+Pinning: Perlin noise KATs from the reference's PerlinNoise.hpp (SURVEY.md
+§8c: octave2D_01(0,0,4)=0.890182078, (10/64,5/64)=0.961326897, 64x64 map
+min/max/mean) and the reference camera KATs (renderer/test/camera/test.cpp:
+145-257) are checked in tests/test_oracle.py; the voxel DDA is pinned against a
+brute-force culled-triangle caster over the face mesh the reference builds.
+Shading and denoising have no reference golden vectors --
+their parity is against this restatement only.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "liboracle.so")
+TABLES = os.path.join(REPO, "data", "tables")
+
+RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
+                            ("M", "<f4")])
+FLOAT1 = {1, 5, 12, 13, 19, 20}
+# default cube materials (data/assets/materials.yaml order): (block id, roughness, material id)
+TERRAIN_ROUGHNESS = [0.8, 0.9, 0.85, 0.9, 0.8, 0.7, 0.85, 0.6, 0.7, 0.65, 0.75, 0.75]
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        sig = {
+            "orc_create": (P, [I, I, ctypes.c_char_p]),
+            "orc_destroy": (None, [P]),
+            "orc_set_bounces": (None, [P, I, I]),
+            "orc_terrain": (I, [P, I, I, I, F, F, I, I]),
+            "orc_set_voxels": (I, [P, P, I, I, I]),
+            "orc_get_voxels": (I, [P, P]),
+            "orc_set_material": (None, [P, I, F, F, F, F, I, F, I]),
+            "orc_set_sky": (I, [P, F, F, F, F]),
+            "orc_set_sky_maps": (None, [P, P, P, P]),
+            "orc_get_sky": (None, [P, P, P, P, P, P, P]),
+            "orc_set_camera": (None, [P, P, P, F, I]),
+            "orc_get_camera": (None, [P, I, P]),
+            "orc_camera_kat": (None, [I, I, F, F, P, I, P, P]),
+            "orc_copy_camera_to_prev": (None, [P]),
+            "orc_trace": (None, [P, I, I, I, I]),
+            "orc_post_trace": (None, [P]),
+            "orc_set_denoise_params": (None, [P, P, P]),
+            "orc_denoise": (None, [P, I, I]),
+            "orc_pass": (None, [P, I, I, I]),
+            "orc_buffer": (I, [P, I, P, I]),
+            "orc_rand": (F, [P, I, I, I, I]),
+            "orc_perlin": (F, [F, F, I]),
+            "orc_dda": (None, [P, I, P, P, P, I]),
+        }
+        for k, (r, a) in sig.items():
+            fn = getattr(L, k)
+            fn.restype = r
+            fn.argtypes = a
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def perlin(x, y, octaves=4):
+    return lib().orc_perlin(x, y, octaves)
+
+
+def camera_kat(w, h, yaw, pitch, uvs):
+    uvs = np.ascontiguousarray(uvs, np.float32).reshape(-1, 2)
+    n = uvs.shape[0]
+    d, b = np.zeros((n, 3), np.float32), np.zeros((n, 2), np.float32)
+    lib().orc_camera_kat(w, h, yaw, pitch, _p(uvs), n, _p(d), _p(b))
+    return d, b
+
+
+class Oracle:
+    def __init__(self, width, height, bounces=(3, 1)):
+        self.L = lib()
+        self.W, self.H = width, height
+        self.h = self.L.orc_create(width, height, TABLES.encode())
+        if not self.h:
+            raise RuntimeError("oracle tables missing under " + TABLES)
+        self.L.orc_set_bounces(self.h, bounces[0], bounces[1])
+        for b, r in enumerate(TERRAIN_ROUGHNESS, start=1):
+            self.L.orc_set_material(self.h, b, 1.0, 1.0, 1.0, r, 0, 0.0, b - 1)
+        self.chunks = None
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.orc_destroy(self.h)
+            self.h = None
+
+    def terrain(self, chunks=(2, 1, 2), height_scale=32.0, freq_den=None, use_fma=True, keep_balls=False,
+                global_y=False):
+        if freq_den is None:
+            freq_den = 32.0 * chunks[0]
+        self.L.orc_terrain(self.h, chunks[0], chunks[1], chunks[2], height_scale, freq_den, int(use_fma),
+                           (1 if keep_balls else 0) | (2 if global_y else 0))
+        self.chunks = tuple(chunks)
+
+    def voxels(self):
+        cx, cy, cz = self.chunks
+        out = np.zeros(cx * cy * cz * 32768, np.uint8)
+        self.L.orc_get_voxels(self.h, _p(out))
+        return out
+
+    def set_voxels(self, ids, chunks):
+        ids = np.ascontiguousarray(ids, np.uint8)
+        self.L.orc_set_voxels(self.h, _p(ids), *chunks)
+        self.chunks = tuple(chunks)
+
+    def set_sky(self, tod=0.25, axis=45.0, rot=0.0, bright=1.0):
+        self.L.orc_set_sky(self.h, tod, axis, rot, bright)
+
+    def set_sky_maps(self, sky, sun, sun_dir):
+        sky = np.ascontiguousarray(sky, np.float32)
+        sun = np.ascontiguousarray(sun, np.float32)
+        sd = np.ascontiguousarray(sun_dir, np.float32)
+        self.L.orc_set_sky_maps(self.h, _p(sky), _p(sun), _p(sd))
+
+    def sky(self):
+        sky, sun, sd = np.zeros((512, 1024, 4), np.float32), np.zeros((32, 32, 4), np.float32), np.zeros(3, np.float32)
+        n = 1024 * 512
+        q, p, a = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.int32)
+        self.L.orc_get_sky(self.h, _p(sky), _p(sun), _p(sd), _p(q), _p(p), _p(a))
+        return dict(sky=sky, sun=sun, sun_dir=sd, q=q, p=p, alias=a)
+
+    def set_camera(self, pos, direction, fov=90.0, which=0):
+        pos = np.asarray(pos, np.float32)
+        d = np.asarray(direction, np.float32)
+        self.L.orc_set_camera(self.h, _p(pos), _p(d), fov, which)
+
+    def camera_info(self, which=0):
+        out = np.zeros(32, np.float32)
+        self.L.orc_get_camera(self.h, which, _p(out))
+        return out
+
+    def trace(self, it, y0=0, y1=None, primary_only=False):
+        self.L.orc_trace(self.h, it, y0, self.H if y1 is None else y1, int(primary_only))
+
+    def post_trace(self):
+        self.L.orc_post_trace(self.h)
+
+    def set_denoise_params(self, fl, ints):
+        fl = np.asarray(fl, np.float32)
+        ints = np.asarray(ints, np.int32)
+        self.L.orc_set_denoise_params(self.h, _p(fl), _p(ints))
+
+    def denoise(self, frame, it):
+        self.L.orc_denoise(self.h, frame, it)
+
+    def run_pass(self, which, arg=0, arg2=0):
+        self.L.orc_pass(self.h, which, arg, arg2)
+
+    def _alloc(self, which):
+        n = self.W * self.H
+        if which == 14:
+            return np.zeros(2 * n, RESERVOIR_DTYPE)
+        if which in FLOAT1:
+            return np.zeros((self.H, self.W), np.float32)
+        return np.zeros((self.H, self.W, 4), np.float32)
+
+    def read(self, which):
+        out = self._alloc(which)
+        self.L.orc_buffer(self.h, which, _p(out), 0)
+        return out
+
+    def write(self, which, data):
+        ref = self._alloc(which)
+        data = np.ascontiguousarray(data, dtype=ref.dtype).reshape(ref.shape)
+        self.L.orc_buffer(self.h, which, _p(data), 1)
+
+    def rand(self, i, j, s, d):
+        return self.L.orc_rand(self.h, i, j, s, d)
+
+    def rays(self, rays, mode=0):
+        """mode 0: DDA closest, 1: brute-force mesh caster, 2: DDA occluded."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        out = np.zeros((n, 6), np.int32)
+        t = np.zeros(n, np.float32)
+        self.L.orc_dda(self.h, n, _p(rays), _p(out), _p(t), mode)
+        return out, t

@@ -1,0 +1,79 @@
+// ORACLE (test infrastructure only): frame state + path tracer + denoiser.
+#pragma once
+#include <cstdint>
+#include <vector>
+#include "orc_math.h"
+#include "orc_scene.h"
+#include "orc_sky.h"
+
+namespace orc {
+
+struct Reservoir {  // DIReservoir (RestirCommon.h:6-12)
+    uint32_t lightData = 0, uvData = 0;
+    float weightSum = 0, targetPdf = 0, M = 0;
+};
+static_assert(sizeof(Reservoir) == 20, "reservoir is 20 B");
+
+struct Material {  // MaterialParameter subset (SystemParameter.h:11-38), untextured
+    F3 albedo{1, 1, 1};
+    float roughness = 0.5f;
+    bool metallic = false;
+    float translucency = 0.0f;
+    int materialId = -1;
+    bool isEmissive = false, isThinfilm = false;
+};
+
+struct DenoiseParams {  // DenoisingParams (GlobalSettings.h:82-141) with yaml values
+    bool enableTemporalAccumulation = true, enableHistoryFix = true, enableHistoryClamping = true;
+    bool enableSpatialFiltering = true, enableFireflyFilter = true;
+    float maxAccumulatedFrameNum = 30, maxFastAccumulatedFrameNum = 6, phiLuminance = 2;
+    float lobeAngleFraction = 0.5f, roughnessFraction = 0.15f, depthThreshold = 0.003f;
+    int atrousIterationNum = 1;
+    float disocclusionThreshold = 0.01f, disocclusionThresholdAlternate = 0.05f, denoisingRange = 500000.0f;
+};
+
+// All per-pixel surfaces of BufferManager.cpp:150-206 that the hot path touches.
+struct Frame {
+    int W = 0, H = 0;
+    std::vector<F4> illum, normalRough, geoNormalThin, albedo, matParam, motion;
+    std::vector<float> depth, material;
+    std::vector<F4> prevNormalRough, prevGeoNormalThin, prevAlbedo, prevMatParam;
+    std::vector<float> prevDepth, prevMaterial;
+    std::vector<Reservoir> reservoir;  // 2*W*H, ping-pong on iterationIndex parity
+    std::vector<F4> ping, pong, prevIllum, prevFast, output;
+    std::vector<float> histLen, prevHistLen;
+    void alloc(int w, int h);
+};
+
+struct Scene {
+    World world;
+    Sky sky;
+    BlueNoise bn;
+    Material mats[13];   // index = block id (1..12); 0 unused
+    Camera cam, prevCam;
+    int totalBounceLimit = 3, diffuseBounceLimit = 1;  // RayGen.cu:146-147
+};
+
+// One 1-spp trace pass (OptixRenderer::render, OptixRenderer.cpp:411-485),
+// rows [y0, y1).  primaryOnly: C2 bring-up mode (no shading; G-buffer + sky).
+void trace_frame(const Scene &s, Frame &f, int iterationIndex, int y0, int y1, bool primaryOnly);
+// Post-trace copies GeoNormal/Albedo/MaterialParameter -> Prev* (OptixRenderer.cpp:476-478)
+void post_trace_copies(Frame &f);
+
+// Denoiser::run (Denoiser.cu:24-408); frameNum = OfflineBackend frame counter,
+// iterationIndex = value after render() incremented it.
+void denoise_frame(const Scene &s, Frame &f, const DenoiseParams &p, int frameNum, int iterationIndex);
+
+// individual passes (exposed for pass-level parity tests)
+void pass_firefly(const Scene &s, Frame &f, int reservoirParity, float phiLuminance);
+void pass_copy_sky(Frame &f);
+void pass_temporal(const Scene &s, Frame &f, const DenoiseParams &p);
+void pass_history_fix(const Scene &s, Frame &f);
+void pass_history_clamp(Frame &f);
+void pass_atrous_smem(const Scene &s, Frame &f, const DenoiseParams &p);
+void pass_atrous(const Scene &s, Frame &f, const std::vector<F4> &in, std::vector<F4> &out, const DenoiseParams &p,
+                 unsigned frameIndex, unsigned step);
+void pass_copy_nonsky(Frame &f, const std::vector<F4> &in);
+void pass_history_copies(Frame &f);
+
+}  // namespace orc

@@ -1,0 +1,702 @@
+// vxpt -- ReLAX-style diffuse denoiser on gfx950.
+//
+// Passes and their reference anchors (renderer/denoising/*):
+//   firefly  FireflyBoilingFilter (FireflyFilter.h:9-251): detect + filter into a
+//            compact list, applied by a second launch so every read sees the
+//            pre-filter illumination (the reference's in-place write races).
+//   TA       TemporalAccumulation<8,1> (TemporalAccumulation.h:8-449)
+//   HF       HistoryFix (HistoryFix.h:6-119)
+//   HC       HistoryClamping<8,2> (HistoryClamping.h:6-219)
+//   ASmem    AtrousSmem<8,2> (AtrousSmem.h:9-302)
+//   Atrous   Atrous (Atrous.h:6-158), x3; the last one also writes the output
+//            (BufferCopySky + BufferCopyNonSky, BufferCopy.h:6-116 fused in).
+// Buffers are SoA float4/float planes, W*H row-major, 16-B lanes (dwordx4).
+// The reference's Float4 operator behaviour (w taken from z) is reproduced
+// because the variance / second-moment channel depends on it.
+#include "vx_internal.hpp"
+
+namespace vx {
+namespace {
+
+constexpr float kRange = 500000.0f;
+
+VX_D int cl(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
+VX_D V4 f4(float4 v) { return V4(v.x, v.y, v.z, v.w); }
+VX_D float4 tf(V4 v) { return make_float4(v.x, v.y, v.z, v.w); }
+VX_D V4 ld4(const float4 *b, int W, int H, int x, int y) { return f4(b[(size_t)cl(y, H) * W + cl(x, W)]); }
+VX_D float ld1(const float *b, int W, int H, int x, int y) { return b[(size_t)cl(y, H) * W + cl(x, W)]; }
+// 16-bit read of the R32F material plane at byte offset 2x (Load2DUshort1 semantics)
+VX_D float ld_ushort(const float *b, int W, int H, int x, int y) {
+    const int ux = clampi(x, 0, 2 * W - 1);
+    const uint16_t *row = reinterpret_cast<const uint16_t *>(b + (size_t)cl(y, H) * W);
+    return (float)row[ux];
+}
+VX_D V3 world_pos(const CamDev &c, int x, int y, float depth) {
+    const V2 uv = (V2((float)x, (float)y) + 0.5f) * c.invRes;
+    return c.pos + c.uv_to_dir(uv) * depth;
+}
+VX_D float smooth_step10(float x) {  // SmoothStep(1, 0, x)
+    const float t = saturate((x - 1.0f) / (0.0f - 1.0f));
+    return t * t * (3.0f - 2.0f * t);
+}
+VX_D float acos_approx(float x) { return sqrtf(2.0f) * sqrtf(saturate(1.0f - x)); }
+VX_D float nonexp_w(float x, float px) { return smooth_step10(fabsf(x * px + 0.0f)); }
+VX_D float normal_weight_param(float roughness, float af) {
+    const float r = saturate(roughness), p = saturate(af);
+    const float angle = atanf(r * r * p / (1.0f - p + 1e-6f));
+    return 1.0f / fmaxf(angle, 1e-6f);
+}
+VX_D float plane_w(V3 c, V3 n, V3 s, float thr) { return fabsf(dot(s - c, n)) < thr ? 1.0f : 0.0f; }
+VX_D V3 rgb_to_ycocg(V3 c) { return V3(0.25f * (c.x + 2.0f * c.y + c.z), c.x - c.z, c.y - 0.5f * (c.x + c.z)); }
+VX_D V3 ycocg_to_rgb(V3 c) { return V3(c.x + 0.5f * (c.y - c.z), c.x + 0.5f * c.z, c.x - 0.5f * (c.y + c.z)); }
+VX_D uint32_t seq_hash(uint32_t x) {
+    x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+    return x;
+}
+VX_D uint32_t explode(uint32_t x) {
+    x = (x | (x << 8)) & 0x00FF00FFu; x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u; x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
+// ---------------------------------------------------------------- firefly
+// 64-thread workgroups = two 8x4 tiles (one per 32-lane half of the wave).
+__global__ __launch_bounds__(64) void k_firefly(DenoiseArgs a, int parity) {
+    const int W = a.W, H = a.H;
+    const int lane = threadIdx.x;
+    const int l32 = lane & 31;
+    const int x = blockIdx.x * 8 + (l32 & 7);
+    const int y = blockIdx.y * 8 + (lane >> 5) * 4 + (l32 >> 3);
+    const bool inb = x < W && y < H;
+    const size_t i = (size_t)y * W + x;
+    const float cd = inb ? a.depth[i] : 0.0f;
+    const bool sky = inb && cd > kRange;
+    Reservoir r = Reservoir{0u, 0u, 0.f, 0.f, 0.f};
+    if (inb && !sky) r = a.reservoir[i];
+    const bool valid = inb && !sky && r.lightData != 0 && isfinite(r.weightSum) && r.weightSum > 0.0f;
+    float v = valid ? r.weightSum : 0.0f;
+    unsigned cnt = valid ? 1u : 0u;
+    for (int off = 16; off > 0; off >>= 1) {
+        v += __shfl_down(v, off, 32);
+        cnt += __shfl_down(cnt, off, 32);
+    }
+    const float tileSum = __shfl(v, 0, 32);
+    const unsigned tileCnt = __shfl(cnt, 0, 32);
+    if (!valid) return;
+    const float cw = r.weightSum;
+    const float nSum = tileSum - cw;
+    const int nCnt = (int)tileCnt - 1;
+    const float minWeight = 5.0f, wThr = 80.0f, nThr = 0.8f, depthSigma = 0.02f;
+    bool firefly = false;
+    if (cw >= minWeight) {
+        if (nCnt <= 0) firefly = true;
+        else {
+            const float avg = nSum / float(nCnt);
+            if (avg > 0.0f && cw > avg * wThr) firefly = true;
+        }
+    }
+    if (!firefly) return;
+    const V4 cc4 = f4(a.illum[i]);
+    const float cLum = luminance(cc4.xyz());
+    V3 cN = f4(a.normalRough[i]).xyz();
+    const float cl_ = length(cN);
+    if (cl_ > 0.0f) cN /= cl_; else cN = V3(0.0f, 1.0f, 0.0f);
+    const float cMat = a.material[i];
+    const V3 cWP = world_pos(a.cam, x, y, cd);
+    const float g[3] = {1.0f, 2.0f, 1.0f};
+    V4 filt = cc4;
+    float filtW = 1.0f;
+    V4 fb = cc4 * (g[0] * g[0]);
+    float fbW = g[0] * g[0];
+    const float depthScale = fmaxf(fabsf(cd), 1.0f);
+    const float nwp = normal_weight_param(1.0f, 0.25f);
+    Reservoir best = r;
+    float bestScore = 3.402823466e+38f;
+    bool repl = false;
+    for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+            if (dx == 0 && dy == 0) continue;
+            const int sx = x + dx, sy = y + dy;
+            if (sx < 0 || sy < 0 || sx >= W || sy >= H) continue;
+            const float gw = g[abs(dx)] * g[abs(dy)];
+            const size_t j = (size_t)sy * W + sx;
+            const V4 sc4 = f4(a.illum[j]);
+            fb += sc4 * gw;
+            fbW += gw;
+            const float sd = a.depth[j];
+            if (sd > kRange) continue;
+            V3 sN = f4(a.normalRough[j]).xyz();
+            const float sl = length(sN);
+            if (sl <= 0.0f) continue;
+            sN /= sl;
+            const float nd = dot(cN, sN);
+            if (nd < nThr) continue;
+            if (fabsf(a.material[j] - cMat) > 0.5f) continue;
+            const V3 sWP = world_pos(a.cam, sx, sy, sd);
+            if (plane_w(cWP, cN, sWP, depthSigma * depthScale) <= 0.0f) continue;
+            const float nw = nonexp_w(acos_approx(clampf(nd, -1.0f, 1.0f)), nwp);
+            const float dw = expf(-fabsf(sd - cd) / (depthScale * depthSigma + 1e-6f));
+            const float lw = expf(-fabsf(luminance(sc4.xyz()) - cLum) * a.p.phiL);
+            const float tw = gw * 1.0f * nw * dw * lw;
+            if (tw > 1e-5f) {
+                filt += sc4 * tw;
+                filtW += tw;
+            }
+            const Reservoir nr = a.reservoir[j];
+            if (nr.lightData != 0 && isfinite(nr.weightSum) && nr.weightSum > 0.0f && nr.weightSum < cw) {
+                const float score = fabsf(sd - cd) / (depthScale + 1e-6f) + (1.0f - clampf(nd, 0.0f, 1.0f)) +
+                                    0.25f * fabsf(nr.weightSum - cw);
+                if (score < bestScore) { bestScore = score; best = nr; repl = true; }
+            }
+        }
+    V4 outc;
+    if (filtW > 0.0f) outc = filt / filtW;
+    else if (fbW > 0.0f) outc = fb / fbW;
+    else outc = cc4;
+    Reservoir dst;
+    if (repl) dst = best;
+    else {
+        dst = r;
+        const float avg = (nCnt > 0) ? (nSum / float(nCnt)) : minWeight;
+        float tgt = (nCnt > 0) ? (avg * wThr) : minWeight;
+        tgt = fmaxf(tgt, minWeight);
+        dst.weightSum = fminf(dst.weightSum, tgt);
+    }
+    const uint32_t slot = atomicAdd(a.ffCount, 1u);
+    a.ffIndex[slot] = (uint32_t)i;
+    a.ffColor[slot] = tf(outc);
+    a.ffRes[slot] = dst;
+}
+
+__global__ __launch_bounds__(256) void k_firefly_apply(DenoiseArgs a) {
+    const uint32_t n = *a.ffCount;
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
+        const uint32_t i = a.ffIndex[s];
+        a.illum[i] = a.ffColor[s];
+        a.reservoir[i] = a.ffRes[s];
+    }
+}
+
+// ---------------------------------------------------------------- frame 0
+__global__ __launch_bounds__(256) void k_frame0(DenoiseArgs a) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)a.W * a.H) return;
+    const float4 v = a.illum[i];
+    a.prevIllum[i] = v;
+    a.prevFast[i] = v;
+    a.histLen[i] = 0.0f;
+    a.prevHistLen[i] = 0.0f;
+}
+
+// ---------------------------------------------------------------- TA
+template <bool kQuirk>
+VX_D V4 bicubic12(const float4 *b, int W, int H, V2 uv) {
+    const V2 UV(uv.x * (float)W, uv.y * (float)H);
+    const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
+    const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
+    const V2 w0 = f2 - 0.5f * (f3 + fr);
+    const V2 w1 = 1.5f * f3 - 2.5f * f2 + 1.0f;
+    const V2 w3 = 0.5f * (f3 - f2);
+    const V2 w2 = 1.0f - w0 - w1 - w3;
+    const int x1 = (int)fx, y1 = (int)fy;
+    const int sx[12] = {x1, x1 + 1, x1 - 1, x1, x1 + 1, x1 + 2, x1 - 1, x1, x1 + 1, x1 + 2, x1, x1 + 1};
+    const int sy[12] = {y1 - 1, y1 - 1, y1, y1, y1, y1, y1 + 1, y1 + 1, y1 + 1, y1 + 1, y1 + 2, y1 + 2};
+    const float wt[12] = {w1.x * w0.y, w2.x * w0.y, w0.x * w1.y, w1.x * w1.y, w2.x * w1.y, w3.x * w1.y,
+                          w0.x * w2.y, w1.x * w2.y, w2.x * w2.y, w3.x * w2.y, w1.x * w3.y, w2.x * w3.y};
+    V4 out;
+    V3 out3(0.0f);
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        sum += wt[k];
+        const V4 v = ld4(b, W, H, sx[k], sy[k]);
+        if (kQuirk) out += v * wt[k];
+        else out3 += v.xyz() * wt[k];
+    }
+    if (kQuirk) { out /= sum; return out; }
+    out3 /= sum;
+    return V4(out3, 0.0f);
+}
+VX_D void bilinear_taps(int W, int H, V2 uv, int &x0, int &y0, float w[4]) {
+    const V2 UV(uv.x * (float)W, uv.y * (float)H);
+    const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
+    const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f);
+    const V2 w1 = fr, w0 = 1.0f - fr;
+    x0 = (int)fx;
+    y0 = (int)fy;
+    w[0] = w0.x * w0.y; w[1] = w1.x * w0.y; w[2] = w0.x * w1.y; w[3] = w1.x * w1.y;
+}
+VX_D V4 bilinear_custom4(const float4 *b, int W, int H, V2 uv, const float cw[4]) {
+    int x0, y0;
+    float w[4];
+    bilinear_taps(W, H, uv, x0, y0, w);
+    V4 out;
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float wt = w[k] * cw[k];
+        const float weight = (wt < 1e-6f) ? 1e-6f : wt;
+        sum += weight;
+        out += ld4(b, W, H, x0 + (k & 1), y0 + (k >> 1)) * weight;
+    }
+    out /= sum;
+    return out;
+}
+VX_D float bilinear_custom1(const float *b, int W, int H, V2 uv, const float cw[4]) {
+    int x0, y0;
+    float w[4];
+    bilinear_taps(W, H, uv, x0, y0, w);
+    float out = 0.0f, sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float wt = w[k] * cw[k];
+        const float weight = (wt < 1e-6f) ? 1e-6f : wt;
+        sum += weight;
+        out += ld1(b, W, H, x0 + (k & 1), y0 + (k >> 1)) * weight;
+    }
+    return out / sum;
+}
+VX_D V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
+    const V2 UV(uv.x * (float)W, uv.y * (float)H);
+    const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
+    const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
+    const V2 w1 = -2.0f * f3 + 3.0f * f2;
+    const V2 w0 = 1.0f - w1;
+    const int x0 = (int)fx, y0 = (int)fy;
+    const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
+    V3 out(0.0f);
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        sum += wt[k];
+        out += ld4(b, W, H, x0 + (k & 1), y0 + (k >> 1)).xyz() * wt[k];
+    }
+    out /= sum;
+    return out;
+}
+
+__global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
+    const int W = a.W, H = a.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t i = (size_t)y * W + x;
+    const float z = a.depth[i];
+    if (z > a.p.denoisingRange) return;
+    const CamDev &cam = a.cam, &pc = a.prevCam;
+    const V3 cN = f4(a.normalRough[i]).xyz();
+    V3 avgN = cN;
+    for (int ax = -1; ax <= 1; ++ax)
+        for (int by = -1; by <= 1; ++by) {
+            if (ax == 0 && by == 0) continue;
+            avgN += ld4(a.normalRough, W, H, x + ax, y + by).xyz();
+        }
+    avgN /= 9.0f;
+    const V2 pixelUv = (V2((float)x, (float)y) + 0.5f) * V2(1.0f / (float)W, 1.0f / (float)H);
+    const V2 curUV = (V2((float)x, (float)y) + 0.5f) * cam.invRes;
+    const V3 view = cam.uv_to_dir(curUV);
+    const V3 cWP = world_pos(cam, x, y, z);
+    const V3 Vv = -normalize(view);
+    const float NoV = fabsf(dot(cN, Vv));
+    const V3 prevWP = cWP + f4(a.motion[i]).xyz();
+    const V2 prevUV = pc.dir_to_uv(normalize(prevWP - pc.pos));
+    const V3 illum = f4(a.illum[i]).xyz();
+    const float m1 = luminance(illum), m2 = m1 * m1;
+    const V3 camDelta = pc.pos - cam.pos;
+    float par1, par2;
+    {
+        const V2 u1 = pc.dir_to_uv(normalize((prevWP + camDelta) - pc.pos));
+        const V2 d1 = (u1 - pixelUv) * V2((float)W, (float)H);
+        par1 = sqrtf(d1.x * d1.x + d1.y * d1.y);
+        const V2 u2 = cam.dir_to_uv(normalize((prevWP - camDelta) - cam.pos));
+        const V2 d2 = (u2 - prevUV) * V2((float)W, (float)H);
+        par2 = sqrtf(d2.x * d2.x + d2.y * d2.y);
+    }
+    const float parMax = fmaxf(par1, par2);
+    const float thrB = a.p.disocclusionThreshold + (1.5f / (float)H);
+    const float thrA = a.p.disocclusionThresholdAlternate + (1.5f / (float)H);
+    const float thr = lerpf(thrB, thrA, 0.0f);
+    // loadSurfaceMotionBasedPrevData
+    const V3 nIn = normalize(avgN);
+    const float estDepth = length(prevWP - pc.pos);
+    const V2 ppf(prevUV.x * (float)W, prevUV.y * (float)H);
+    const int ox = (int)floorf(ppf.x - 0.5f), oy = (int)floorf(ppf.y - 0.5f);
+    const float frustum = (cam.tanHalfFov.x / (cam.res.x / 2)) * z * (float)(W < H ? W : H);
+    const double slope = 1.0 / (double)lerpf(lerpf(0.05f, 1.0f, NoV), 1.0f, saturate(parMax / 30.0f));
+    const float t0 = saturate((float)((double)thr * slope)) * frustum;
+    V4 thr4(t0);
+    {
+        float r[4] = {ox >= 0 ? 1.f : 0.f, oy >= 0 ? 1.f : 0.f, ox + 1 >= 0 ? 1.f : 0.f, oy + 1 >= 0 ? 1.f : 0.f};
+        const float cmp[4] = {ox < W ? 1.f : 0.f, oy < H ? 1.f : 0.f, ox + 1 < W ? 1.f : 0.f, oy + 1 < H ? 1.f : 0.f};
+        for (int k = 0; k < 4; ++k) r[k] *= cmp[k];
+        thr4 *= (V4(r[0], r[2], r[0], r[2]) * V4(r[1], r[1], r[3], r[3]));
+    }
+    thr4 -= 1e-6f;
+    const float thrv[4] = {thr4.x, thr4.y, thr4.z, thr4.w};
+    const int bcx[8] = {0, -1, 1, 2, -1, 0, 2, 1}, bcy[8] = {-1, 0, -1, 0, 1, 2, 1, 2};
+    float bicValid = 1.0f;
+    float taps[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float pz = ld1(a.prevDepth, W, H, ox + bcx[k], oy + bcy[k]);
+        bicValid *= fabsf(pz - estDepth) > thrv[k >> 1] ? 0.0f : 1.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float pz = ld1(a.prevDepth, W, H, ox + (k & 1), oy + (k >> 1));
+        const float v = fabsf(pz - estDepth) > thrv[k] ? 0.0f : 1.0f;
+        bicValid *= v;
+        taps[k] = v;
+    }
+    const V3 pnf = normalize(bicubic_smoothstep3(a.prevNormalRough, W, H, prevUV));
+    const V3 pnr = normalize(q_rotate(rot, pnf));
+    if (dot(nIn, pnr) < 0.0f) {
+        taps[0] = taps[1] = taps[2] = taps[3] = 0.0f;
+        bicValid = 0.0f;
+    }
+    const bool useBic = bicValid > 0;
+    V4 prevI = useBic ? bicubic12<true>(a.prevIllum, W, H, prevUV) : bilinear_custom4(a.prevIllum, W, H, prevUV, taps);
+    V3 prevF = useBic ? bicubic12<false>(a.prevFast, W, H, prevUV).xyz()
+                      : bilinear_custom4(a.prevFast, W, H, prevUV, taps).xyz();
+    prevI = V4(fmaxf(prevI.x, 0.0f), fmaxf(prevI.y, 0.0f), fmaxf(prevI.z, 0.0f), fmaxf(prevI.w, 0.0f));
+    prevF = max3(prevF, V3(0.0f));
+    float found = (bicValid > 0.0f) ? 2.0f : 1.0f;
+    int bx0, by0;
+    float bw[4];
+    bilinear_taps(W, H, prevUV, bx0, by0, bw);
+    float quality = (bicValid > 0) ? 1.0f : (bw[0] * 1.0f + bw[1] * 1.0f + bw[2] * 1.0f + bw[3] * 1.0f);
+    float hist;
+    if ((taps[0] * 1.0f + taps[1] * 1.0f + taps[2] * 1.0f + taps[3] * 1.0f) == 0.0f) {
+        found = 0.0f; quality = 0.0f; hist = 0.0f;
+    } else {
+        hist = bilinear_custom1(a.prevHistLen, W, H, prevUV, taps);
+    }
+    hist = hist + 1.0f;
+    const V3 Vp = normalize(prevWP - pc.pos);
+    const float NoVp = fabsf(dot(cN, Vp));
+    float sq = (NoVp + 1e-3f) / (NoV + 1e-3f);
+    sq *= sq;
+    sq *= sq;
+    quality *= lerpf(0.1f, 1.0f, saturate(sq));
+    if (quality < 1.0f) {
+        hist *= sqrtf(quality);
+        hist = fmaxf(hist, 1.0f);
+    }
+    hist = fminf(hist, a.p.maxAcc);
+    const float alpha = (found > 0) ? fmaxf(1.0f / (a.p.maxAcc + 1.0f), 1.0f / hist) : 1.0f;
+    const float alphaR = (found > 0) ? fmaxf(1.0f / (a.p.maxFast + 1.0f), 1.0f / hist) : 1.0f;
+    const V4 acc = lerp4(prevI, V4(illum, m2), alpha);
+    const V3 accR = lerp3(prevF, illum, alphaR);
+    a.ping[i] = tf(acc);
+    a.pong[i] = make_float4(accR.x, accR.y, accR.z, 0.0f);
+    a.histLen[i] = hist;
+}
+
+// ---------------------------------------------------------------- HF
+__global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
+    const int W = a.W, H = a.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t i = (size_t)y * W + x;
+    const float z = a.depth[i], hist = a.histLen[i];
+    if (z > kRange || hist > 4.0f) return;
+    const float cMat = ld_ushort(a.material, W, H, x, y);
+    const V3 cN = f4(a.normalRough[i]).xyz();
+    const V3 cWP = world_pos(a.cam, x, y, z);
+    const float dthr = 0.003f * z;
+    V4 sum = f4(a.ping[i]);
+    float wsum = 1.0f;
+    const float r = exp2f(4.0f - hist) + 1.0f;
+    for (int j = -2; j <= 2; ++j)
+        for (int k = -2; k <= 2; ++k) {
+            const int sx = x + (int)(k * r), sy = y + (int)(j * r);
+            const bool inside = sx >= 0 && sy >= 0 && sx < W && sy < H;
+            if (k == 0 && j == 0) continue;
+            const float sMat = ld_ushort(a.material, W, H, sx, sy);
+            const V3 sN = ld4(a.normalRough, W, H, sx, sy).xyz();
+            const float sz = ld1(a.depth, W, H, sx, sy);
+            const V3 sWP = world_pos(a.cam, sx, sy, sz);
+            float w = plane_w(cWP, cN, sWP, dthr);
+            w *= powf(fmaxf(0.01f, dot(cN, sN)), 8.0f);
+            w = inside ? w : 0;
+            w *= (float)(sMat == cMat);
+            if (w > 1e-4f) {
+                sum += ld4(a.ping, W, H, sx, sy) * w;
+                wsum += w;
+            }
+        }
+    a.pong[i] = tf(sum / wsum);
+}
+
+// ---------------------------------------------------------------- HC
+__global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
+    const int W = a.W, H = a.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t i = (size_t)y * W + x;
+    if (a.depth[i] > kRange) return;
+    const float hist = a.histLen[i];
+    V3 m1(0.0f), m2(0.0f), nm1(0.0f);
+    float nm2 = 0.0f;
+    for (int dx = -2; dx <= 2; ++dx)
+        for (int dy = -2; dy <= 2; ++dy) {
+            const V3 s = rgb_to_ycocg(ld4(a.pong, W, H, x + dx, y + dy).xyz());
+            m1 += s;
+            m2 += s * s;
+            const V3 nz = ld4(a.illum, W, H, x + dx, y + dy).xyz();
+            const float nl = luminance(nz);
+            nm1 += nz;
+            nm2 += nl * nl;
+        }
+    m1 /= 25.0f; m2 /= 25.0f; nm1 /= 25.0f; nm2 /= 25.0f;
+    const V3 sigma(sqrtf(fmaxf(0.0f, m2.x - m1.x * m1.x)), sqrtf(fmaxf(0.0f, m2.y - m1.y * m1.y)),
+                   sqrtf(fmaxf(0.0f, m2.z - m1.z * m1.z)));
+    V3 cmin = m1 - 2.0f * sigma, cmax = m1 + 2.0f * sigma;
+    const V3 center = rgb_to_ycocg(f4(a.pong[i]).xyz());
+    cmin = (cmin.x < center.x) ? cmin : center;  // LinearMath.h template min on Float3 (x-compare)
+    cmax = (cmax.x > center.x) ? cmax : center;
+    const V4 pi = f4(a.ping[i]);
+    const V3 dY = rgb_to_ycocg(pi.xyz());
+    const V3 cY(clampf(dY.x, cmin.x, cmax.x), clampf(dY.y, cmin.y, cmax.y), clampf(dY.z, cmin.z, cmax.z));
+    V4 outD(ycocg_to_rgb(cY), pi.w);
+    const V3 respC = ycocg_to_rgb(center);
+    V4 outR(respC, 0.0f);
+    if (hist <= 4.0f) outD.set_xyz(outR.xyz());
+    float factor = (cY.x - dY.x) == 0.0f ? 0.0f : saturate((cY.x - dY.x) / (center.x - dY.x));
+    if (hist <= 4.0f) factor = 1.0f;
+    float hdl = 10.0f * 0.3f * luminance(abs3(respC - pi.xyz()));
+    hdl *= factor;
+    if (hist <= 4.0f) hdl = 0.0f;
+    const V3 dist = nm1 - respC;
+    const float distL = luminance(abs3(dist));
+    V3 acc = (distL == 0.0f) ? V3(0.0f) : dist * hdl / distL;
+    const float accL = luminance(abs3(acc));
+    const float ratio = (accL == 0.0f) ? 0.0f : distL / accL;
+    if (ratio < 1.0f) acc *= ratio;
+    if (ratio <= 0.0f) acc = V3(0.0f);
+    outD.set_xyz(outD.xyz() + acc);
+    outR.set_xyz(outR.xyz() + acc);
+    const float dL = luminance(pi.xyz()), nL = luminance(nm1);
+    const float tSig = 0.5f * sqrtf(fmaxf(0.0f, nm2 - nL * nL));
+    const float sSig = 4.5f * sigma.x;
+    float reset = 0.5f * fmaxf(0.0f, fabsf(dL - nL) - sSig - tSig) / (1.0e-6f + fmaxf(dL, nL) + sSig + tSig);
+    reset = saturate(reset);
+    const V3 noisyC = f4(a.illum[i]).xyz();
+    outD.set_xyz(lerp3(outD.xyz(), noisyC, reset));
+    outR.set_xyz(lerp3(outR.xyz(), noisyC, reset));
+    const float oL = luminance(outD.xyz());
+    outD.w += (oL * oL - dL * dL);
+    outD.w = fmaxf(0.0f, outD.w);
+    a.prevIllum[i] = tf(outD);
+    a.prevFast[i] = tf(outR);
+    a.prevHistLen[i] = hist;
+}
+
+// ---------------------------------------------------------------- A-trous (LDS variant)
+__global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
+    const int W = a.W, H = a.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t i = (size_t)y * W + x;
+    const float z = a.depth[i];
+    if (z > 500000.0f) return;
+    const V3 cN = f4(a.normalRough[i]).xyz();
+    const V3 cWP = world_pos(a.cam, x, y, z);
+    const float cMat = a.material[i];
+    const float hist = a.histLen[i];
+    const float k3[2] = {0.44198f, 0.27901f};
+    if (hist >= 3.0f) {
+        V4 vs;
+        const float kern[4] = {1.0f / 4.0f, 1.0f / 8.0f, 1.0f / 8.0f, 1.0f / 16.0f};
+        for (int dx = -1; dx <= 1; ++dx)
+            for (int dy = -1; dy <= 1; ++dy)
+                vs += ld4(a.prevIllum, W, H, x + dx, y + dy) * kern[abs(dx) * 2 + abs(dy)];
+        const float vm1 = luminance(vs.xyz());
+        const float var = fmaxf(0.0f, vs.w - vm1 * vm1);
+        const float cLum = luminance(f4(a.prevIllum[i]).xyz());
+        const float phiInv = 1.0f / fmaxf(1.0e-4f, a.p.phiL * sqrtf(var));
+        const float nwp = normal_weight_param(1.0f, a.p.lobeAngleFraction);
+        float sumW = 0.0f;
+        V4 sum;
+        const float dthr = a.p.depthThreshold * z;
+        for (int cx = -1; cx <= 1; ++cx)
+            for (int cy = -1; cy <= 1; ++cy) {
+                const int px = x + cx, py = y + cy;
+                const bool isC = cx == 0 && cy == 0;
+                const bool inside = px >= 0 && py >= 0 && px < W && py < H;
+                const float kernel = inside ? k3[abs(cx)] * k3[abs(cy)] : 0.0f;
+                const int qx = cl(px, W), qy = cl(py, H);
+                const size_t j = (size_t)qy * W + qx;
+                const V3 sN = f4(a.normalRough[j]).xyz();
+                const V3 sWP = world_pos(a.cam, qx, qy, a.depth[j]);
+                const float sMat = a.material[j];
+                float geo = plane_w(cWP, cN, sWP, dthr) * kernel;
+                const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
+                const V4 si = f4(a.prevIllum[j]);
+                const float lw = fabsf(cLum - luminance(si.xyz())) * phiInv;
+                float w = geo * nw * expf(-lw);
+                w = isC ? kernel : w;
+                w *= (float)(sMat == cMat);
+                sumW += w;
+                sum += w * si;
+            }
+        sumW = fmaxf(sumW, 1e-6f);
+        sum /= sumW;
+        const float o1 = luminance(sum.xyz());
+        a.ping[i] = make_float4(sum.x, sum.y, sum.z, fmaxf(0.0f, sum.w - o1 * o1));
+    } else {
+        float sw = 0.0f, s1 = 0.0f, s2 = 0.0f;
+        V3 si(0.0f);
+        const float nwp = normal_weight_param(1.0f, a.p.lobeAngleFraction);
+        for (int cx = -2; cx <= 2; ++cx)
+            for (int cy = -2; cy <= 2; ++cy) {
+                const size_t j = (size_t)cl(y + cy, H) * W + cl(x + cx, W);
+                const V3 sN = f4(a.normalRough[j]).xyz();
+                const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
+                const V4 smp = f4(a.prevIllum[j]);
+                const V3 sill = smp.xyz();
+                float w = nw * 1.0f;
+                w *= (float)(a.material[j] == cMat);
+                sw += w;
+                si += sill * w;
+                s1 += luminance(sill) * w;
+                s2 += smp.w * w;
+            }
+        const float boost = fmaxf(1.0f, 4.0f / (hist + 1.0f));
+        sw = fmaxf(sw, 1e-6f);
+        si /= sw;
+        s1 /= sw;
+        s2 /= sw;
+        const float var = fmaxf(0.0f, s2 - s1 * s1) * boost;
+        a.ping[i] = make_float4(si.x, si.y, si.z, var);
+    }
+}
+
+// ---------------------------------------------------------------- A-trous
+__global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
+                                                unsigned frameIndex, int final) {
+    const int W = a.W, H = a.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t i = (size_t)y * W + x;
+    const float z = a.depth[i];
+    if (z > 500000.0f) {
+        if (final) a.output[i] = a.illum[i];  // BufferCopySky
+        return;
+    }
+    const float cMat = ld_ushort(a.material, W, H, x, y);
+    const V3 cN = f4(a.normalRough[i]).xyz();
+    const V3 cWP = world_pos(a.cam, x, y, z);
+    const float hist = a.histLen[i];
+    float lobe = a.p.lobeAngleFraction / sqrtf((float)step);
+    lobe = lerpf(0.99f, lobe, saturate(hist / 5.0f));
+    const V4 c = f4(in[i]);
+    const float cLum = luminance(c.xyz());
+    const float phiInv = 1.0f / fmaxf(1.0e-4f, a.p.phiL * sqrtf(c.w));
+    const float nwp = normal_weight_param(1.0f, lobe);
+    float sumW = 0.44198f * 0.44198f;
+    V4 sum = c * V4(V3(sumW), sumW * sumW);
+    const float dthr = a.p.depthThreshold * z;
+    int ofx = 0, ofy = 0;
+    if (step > 4) {
+        const uint32_t lin = explode((uint32_t)x) | (explode((uint32_t)y) << 1);
+        const uint32_t seed = seq_hash(frameIndex + 0x035F9F29u);
+        uint32_t st = seed ^ (seq_hash(lin) + 0x9E3779B9u + (seed << 6) + (seed >> 2));
+        st = seq_hash(st);
+        const uint32_t u0 = st;
+        st = seq_hash(st);
+        const uint32_t u1 = st;
+        const V2 r(u0 / 4294967295.0f, u1 / 4294967295.0f);
+        const V2 o = V2((float)step) * 0.5f * (r - 0.5f);
+        ofx = (int)o.x;
+        ofy = (int)o.y;
+    }
+    const float k3[2] = {0.44198f, 0.27901f};
+    for (int yy = -1; yy <= 1; ++yy)
+        for (int xx = -1; xx <= 1; ++xx) {
+            if (xx == 0 && yy == 0) continue;
+            const int px = x + ofx + xx * (int)step, py = y + ofy + yy * (int)step;
+            const bool inside = px >= 0 && py >= 0 && px < W && py < H;
+            const float kernel = k3[abs(xx)] * k3[abs(yy)];
+            const float sMat = ld_ushort(a.material, W, H, px, py);
+            const V3 sN = ld4(a.normalRough, W, H, px, py).xyz();
+            const float sz = ld1(a.depth, W, H, px, py);
+            const V3 sWP = world_pos(a.cam, px, py, sz);
+            float geo = plane_w(cWP, cN, sWP, dthr);
+            geo *= kernel;
+            geo *= float(inside && sz < 500000.0f);
+            const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
+            float w = geo * nw;
+            w *= (float)(sMat == cMat);
+            if (w > 1e-4f) {
+                const V4 sv = ld4(in, W, H, px, py);
+                float lw = fabsf(cLum - luminance(sv.xyz())) * phiInv;
+                lw = fminf(INFINITY, lw);
+                w *= expf(-lw);
+                sumW += w;
+                sum += V4(V3(w), w * w) * sv;
+            }
+        }
+    const V4 res = sum / V4(V3(sumW), sumW * sumW);
+    out[i] = tf(res);
+    if (final) {
+        const float4 al = a.albedo[i];
+        a.output[i] = make_float4(res.x * al.x, res.y * al.y, res.z * al.z, 0.0f);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_copy_output(DenoiseArgs a, const float4 *in) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)a.W * a.H) return;
+    if (a.depth[i] > kRange) {
+        a.output[i] = a.illum[i];
+    } else {
+        const float4 v = in[i], al = a.albedo[i];
+        a.output[i] = make_float4(v.x * al.x, v.y * al.y, v.z * al.z, 0.0f);
+    }
+}
+
+inline dim3 grid16(int W, int H) { return dim3((W + 15) / 16, (H + 15) / 16); }
+
+}  // namespace
+
+hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st) {
+    const int used = 0;
+    (void)used;
+    hipMemsetAsync(a.ffCount, 0, 16, st);
+    // parity is baked into a.reservoir by the host
+    hipLaunchKernelGGL(k_firefly, dim3((a.W + 7) / 8, (a.H + 7) / 8), dim3(64), 0, st, a, 0);
+    hipLaunchKernelGGL(k_firefly_apply, dim3(64), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_frame0, dim3((unsigned)(((size_t)a.W * a.H + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
+    const Qt rot = q_rotation_between(a.prevCam.dir, a.cam.dir);
+    hipLaunchKernelGGL(k_temporal, grid16(a.W, a.H), dim3(256), 0, st, a, rot);
+    return hipGetLastError();
+}
+hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_history_fix, grid16(a.W, a.H), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_history_clamp, grid16(a.W, a.H), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_atrous_smem, grid16(a.W, a.H), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex,
+                         bool final, hipStream_t st) {
+    hipLaunchKernelGGL(k_atrous, grid16(a.W, a.H), dim3(256), 0, st, a, in, out, step, frameIndex, final ? 1 : 0);
+    return hipGetLastError();
+}
+hipError_t launch_copy_output(const DenoiseArgs &a, const float4 *in, hipStream_t st) {
+    hipLaunchKernelGGL(k_copy_output, dim3((unsigned)(((size_t)a.W * a.H + 255) / 256)), dim3(256), 0, st, a, in);
+    return hipGetLastError();
+}
+
+}  // namespace vx

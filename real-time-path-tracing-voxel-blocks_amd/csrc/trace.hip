@@ -1,0 +1,915 @@
+// vxpt -- the per-pixel path-tracing pass on gfx950.
+//
+// One thread per pixel, 256-thread workgroups covering 16x16 pixels (each
+// 64-lane wave an 8x8 tile, so a wave's primary rays are coherent and its
+// G-buffer stores are whole 128-byte row segments).  Hardware BVH traversal
+// of the reference (optixTraverse over one triangle mesh per chunk x block
+// type, renderer/shaders/RayGen.cu:49, closesthit.cu:458/616/745/801) is
+// replaced by an exact voxel DDA over the u8 grid with a 1-bit-per-4^3-brick
+// occupancy mask: empty bricks are crossed without touching the grid.  The
+// DDA returns what the face mesh + CULL_BACK would (SURVEY.md §8a A3/A4').
+//
+// Shading follows closesthit.cu:10-852 / miss.cu:9-82 / Restir.h / Bsdf.h:
+// Disney BSDF, NEE over sun + sky (+ BRDF sample), RIS, ReSTIR-DI temporal
+// reuse with bias correction, 3-segment / 1-diffuse path limit.
+#include "vx_internal.hpp"
+
+namespace vx {
+namespace {
+
+constexpr uint32_t kValidBit = 0x80000000u, kIndexMask = 0x7FFFFFFFu;
+constexpr uint32_t kInvalidLight = 0x7FFFFFFFu, kSkyLight = 0x7FFFFFFEu, kSunLight = 0x7FFFFFFDu;
+enum { LtInvalid = 0, LtSky = 1, LtSun = 2 };
+constexpr float kRoughThresh = 0.00001f, kTranslThresh = 0.001f;
+constexpr float kMinPdf = 1e-5f, kMaxThroughput = 32.0f, kMinLobe = 0.05f;
+
+// ----------------------------------------------------------------- voxel DDA
+VX_D bool is_cube(int id) { return id >= 1 && id <= 12; }
+
+VX_D int voxel(const WorldDev &w, int x, int y, int z) {
+    const int c = (x >> 5) + w.cx * ((z >> 5) + w.cz * (y >> 5));
+    return w.ids[(size_t)c * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
+}
+VX_D bool brick_occupied(const WorldDev &w, int x, int y, int z) {
+    const int b = (x >> 2) + w.bx * ((z >> 2) + w.bz * (y >> 2));
+    return (w.occ[b >> 5] >> (b & 31)) & 1u;
+}
+
+struct Hit { int hit, x, y, z, face, id; float t; };
+
+VX_D int entry_face(int a, int s) {
+    return a == 0 ? (s > 0 ? 2 : 3) : (a == 1 ? (s > 0 ? 1 : 0) : (s > 0 ? 5 : 4));
+}
+
+struct Walk {
+    V3 o;
+    int c[3], st[3];
+    float inv[3], t[3];
+    bool mv[3];
+};
+
+VX_D float plane_t(const Walk &k, int a, float oa) {
+    if (!k.mv[a]) return INFINITY;
+    const float plane = (float)(k.st[a] > 0 ? k.c[a] + 1 : k.c[a]);
+    return (plane - oa) * k.inv[a];
+}
+
+// Start a walk; returns false if the ray never meets the world box.  `entered`
+// reports a start outside the box (the entry crossing is then already taken
+// and handled by the caller through `ax`/`tEnter`).
+VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Walk &k, bool &outside, int &ax, float &tEnter) {
+    const float dd[3] = {d.x, d.y, d.z}, oo[3] = {o.x, o.y, o.z};
+    const int W[3] = {w.wx, w.wy, w.wz};
+    k.o = o;
+    for (int a = 0; a < 3; ++a) {
+        k.mv[a] = dd[a] != 0.0f;
+        k.st[a] = dd[a] > 0.0f ? 1 : -1;
+        k.inv[a] = k.mv[a] ? 1.0f / dd[a] : 0.0f;
+        k.c[a] = (int)floorf(oo[a]);
+    }
+    outside = !(k.c[0] >= 0 && k.c[0] < W[0] && k.c[1] >= 0 && k.c[1] < W[1] && k.c[2] >= 0 && k.c[2] < W[2]);
+    if (outside) {
+        float t0 = -INFINITY, t1 = INFINITY;
+        ax = -1;
+        for (int a = 0; a < 3; ++a) {
+            if (dd[a] == 0.0f) {
+                if (oo[a] < 0.0f || oo[a] >= (float)W[a]) return false;
+                continue;
+            }
+            const float inv = 1.0f / dd[a];
+            const float ta = (0.0f - oo[a]) * inv, tb = ((float)W[a] - oo[a]) * inv;
+            const float lo = ta < tb ? ta : tb, hi = ta < tb ? tb : ta;
+            if (lo > t0) { t0 = lo; ax = a; }
+            if (hi < t1) t1 = hi;
+        }
+        if (ax < 0 || t0 > t1 || t1 <= 0.0f) return false;
+        for (int a = 0; a < 3; ++a) {
+            if (a == ax) k.c[a] = dd[a] > 0.0f ? 0 : W[a] - 1;
+            else k.c[a] = clampi((int)floorf(oo[a] + t0 * dd[a]), 0, W[a] - 1);
+        }
+        tEnter = t0;
+    }
+    k.t[0] = plane_t(k, 0, oo[0]);
+    k.t[1] = plane_t(k, 1, oo[1]);
+    k.t[2] = plane_t(k, 2, oo[2]);
+    return true;
+}
+
+VX_D int walk_pick(const Walk &k) {
+    if (k.t[0] < k.t[1]) return k.t[0] < k.t[2] ? 0 : 2;
+    return k.t[1] < k.t[2] ? 1 : 2;
+}
+
+VX_D float comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+// Closest front-facing cube face along the ray, t <= tmax (radiance rays).
+VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
+    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+    Walk k;
+    bool outside;
+    int ax = -1;
+    float tEnter = 0;
+    if (!walk_begin(w, o, d, k, outside, ax, tEnter)) return h;
+    int prevId = 0;
+    if (outside) {
+        if (tEnter > tmax) return h;
+        const int b = voxel(w, k.c[0], k.c[1], k.c[2]);
+        if (is_cube(b) && tEnter >= 0.0f) {
+            h = {1, k.c[0], k.c[1], k.c[2], entry_face(ax, k.st[ax]), b, tEnter};
+            return h;
+        }
+        prevId = b;
+    } else if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) {
+        prevId = voxel(w, k.c[0], k.c[1], k.c[2]);
+    }
+    const int W[3] = {w.wx, w.wy, w.wz};
+    const int maxSteps = W[0] + W[1] + W[2] + 3;
+    for (int s = 0; s < maxSteps; ++s) {
+        const int a = walk_pick(k);
+        const float t = k.t[a];
+        if (!(t <= tmax)) return h;
+        const int planeCoord = k.st[a] > 0 ? k.c[a] + 1 : k.c[a];
+        k.c[a] += k.st[a];
+        if (k.c[a] < 0 || k.c[a] >= W[a]) return h;
+        k.t[a] = plane_t(k, a, comp(o, a));
+        int b = 0;
+        if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) b = voxel(w, k.c[0], k.c[1], k.c[2]);
+        if (is_cube(b) && (b != prevId || (planeCoord & 31) == 0)) {
+            h = {1, k.c[0], k.c[1], k.c[2], entry_face(a, k.st[a]), b, t};
+            return h;
+        }
+        prevId = b;
+    }
+    return h;
+}
+
+// Any face crossing with tmin <= t <= tmax (visibility rays: no culling).
+VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
+    Walk k;
+    bool outside;
+    int ax = -1;
+    float tEnter = 0;
+    if (!walk_begin(w, o, d, k, outside, ax, tEnter)) return false;
+    int prevId = 0;
+    if (outside) {
+        if (tEnter > tmax) return false;
+        const int b = voxel(w, k.c[0], k.c[1], k.c[2]);
+        if (is_cube(b) && tEnter >= tmin) return true;
+        prevId = b;
+    } else if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) {
+        prevId = voxel(w, k.c[0], k.c[1], k.c[2]);
+    }
+    const int W[3] = {w.wx, w.wy, w.wz};
+    const int maxSteps = W[0] + W[1] + W[2] + 3;
+    for (int s = 0; s < maxSteps; ++s) {
+        const int a = walk_pick(k);
+        const float t = k.t[a];
+        if (!(t <= tmax)) return false;
+        const int planeCoord = k.st[a] > 0 ? k.c[a] + 1 : k.c[a];
+        const bool chunkPlane = (planeCoord & 31) == 0;
+        const int aId = prevId;
+        k.c[a] += k.st[a];
+        const bool out = k.c[a] < 0 || k.c[a] >= W[a];
+        int b = 0;
+        if (!out) {
+            k.t[a] = plane_t(k, a, comp(o, a));
+            if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) b = voxel(w, k.c[0], k.c[1], k.c[2]);
+        }
+        if (t >= tmin) {
+            const bool frontB = is_cube(b) && (b != aId || chunkPlane);
+            const bool backA = is_cube(aId) && (aId != b || chunkPlane || out);
+            if (frontB || backA) return true;
+        }
+        if (out) return false;
+        prevId = b;
+    }
+    return false;
+}
+
+VX_D V3 face_normal(int f) {
+    return f == 0 ? V3(0, 1, 0) : f == 1 ? V3(0, -1, 0) : f == 2 ? V3(-1, 0, 0) : f == 3 ? V3(1, 0, 0)
+         : f == 4 ? V3(0, 0, 1) : V3(0, 0, -1);
+}
+
+// Hit point on the face plane + self-intersection-safe spawn points
+// (SelfHit.h:539-656 specialised to unit quads under one translation instance).
+VX_D void hit_frame(const Hit &h, V3 o, V3 d, V3 &front, V3 &back, V3 &ng) {
+    V3 p = o + d * h.t;
+    const int axis = (h.face < 2) ? 1 : (h.face < 4 ? 0 : 2);
+    const int cell = axis == 0 ? h.x : (axis == 1 ? h.y : h.z);
+    const bool high = (h.face == 0 || h.face == 3 || h.face == 4);
+    const int plane = cell + (high ? 1 : 0);
+    p.set(axis, (float)plane);
+    ng = face_normal(h.face);
+    const int T = (cell >> 5) * 32;
+    const float planeLocal = (float)(plane - T), planeWorld = (float)plane, Tf = (float)T;
+    const float c0t = 5.9604648328104529e-08f, c1t = 1.1920930376163769e-07f;
+    const float eps = mul_ru(c1t, 2.0f);
+    const float triErr = fma_ru(c0t, planeLocal, eps);
+    const float cI = 1.19209317972490680404007434844970703125E-7f;
+    const float wldErr = fma_ru(cI, planeLocal, mul_ru(cI, Tf));
+    const float objErr = fma_ru(cI, planeWorld, mul_ru(cI, Tf));
+    float off = add_ru(objErr, triErr);
+    off = off + wldErr;
+    front = p;
+    back = p;
+    const float n = ng.get(axis), pa = p.get(axis);
+    if (n > 0.f) {
+        front.set(axis, fma_ru(off, n, pa));
+        back.set(axis, fma_rd(-off, n, pa));
+    } else {
+        front.set(axis, fma_rd(off, n, pa));
+        back.set(axis, fma_ru(-off, n, pa));
+    }
+}
+
+// ----------------------------------------------------------------- BSDF
+VX_D V3 clamp_throughput(V3 v) {
+    const float l = luminance(v), a = fabsf(l);
+    if (a > kMaxThroughput && a > 0.0f) return v * (kMaxThroughput / a);
+    return v;
+}
+VX_D float disney_diffuse_fresnel(float cwo, float cwi, float r) {
+    const float eb = lerpf(0.0f, 0.5f, r), ef = lerpf(1.0f, 1.0f / 1.51f, r);
+    const float fd90 = eb + 2.0f * r * cwi * cwi;
+    const float ls = 1.0f + (fd90 - 1.0f) * pow5(1.0f - cwo);
+    const float vs = 1.0f + (fd90 - 1.0f) * pow5(1.0f - cwi);
+    return ls * vs * ef;
+}
+VX_D float gtr2(float ch, float sh, float a) {  // GTR2Aniso(ch, sh, 0, 1, a, a)
+    const float a2 = a * a;
+    const float s = (1.0f * 1.0f) / a2 + (0.0f * 0.0f) / a2;
+    const float t = sh * sh * s + ch * ch;
+    return 1.0f / (kPi * a * a * t * t);
+}
+VX_D float smith_g(float c, float a) {
+    const float a2 = a * a, c2 = c * c;
+    return 2.0f / (1.0f + sqrtf(1.0f + a2 * (1.0f - c2) / c2));
+}
+
+struct Lobes { V3 C0; float sp, dp; };
+VX_D bool lobes(V3 albedo, float metalness, float cosForF, Lobes &L) {
+    const float lum = 0.299f * albedo.x + 0.587f * albedo.y + 0.114f * albedo.z;
+    const V3 tint = lum > 0.0f ? albedo / lum : V3(1.0f);
+    const V3 specColor = lerp3(V3(1.0f), tint, 0.0f);
+    L.C0 = lerp3(0.08f * 0.5f * specColor, albedo, metalness);
+    const V3 F = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cosForF);
+    const float avgF = (F.x + F.y + F.z) / 3.0f;
+    const float sw = avgF, dw = (1.0f - metalness) * (1.0f - avgF), tw = sw + dw;
+    if (tw < kSafeCos) return false;
+    float sp = sw / tw;
+    if (dw > kSafeCos && sw > kSafeCos) sp = clampf(sp, kMinLobe, 1.0f - kMinLobe);
+    L.sp = clampf(sp, 0.0f, 1.0f);
+    L.dp = fmaxf(0.0f, 1.0f - L.sp);
+    return true;
+}
+
+// DisneyBSDFSample for rough surfaces (Bsdf.h:401-534); specular branch of
+// the reference only for roughness < 1e-5 (:403-425).
+VX_D void disney_sample(float u0, float u1, float u2, float u3, V3 n, V3 ng, V3 wo, V3 albedo, bool metallic,
+                        float translucency, float roughness, V3 &wi, V3 &bop, float &pdf) {
+    if (roughness < kRoughThresh) {
+        if (translucency < kTranslThresh) {
+            wi = reflect3(-wo, n);
+            if (dot(wi, n) <= 0.0f || dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; }
+            else { bop = albedo; pdf = 1.0f; }
+            pdf = fmaxf(pdf, kMinPdf);
+            bop = clamp_throughput(bop);
+        } else {
+            bop = V3(0.0f);  // refractive specular: not in the cube material table
+            pdf = 0.0f;
+        }
+        return;
+    }
+    const float metalness = metallic ? 1.0f : 0.0f;
+    const float alpha = fmaxf(roughness * roughness, kRoughThresh);
+    const float cwo = fmaxf(kSafeCos, dot(n, wo));
+    Lobes L;
+    if (!lobes(albedo, metalness, cwo, L)) { bop = V3(0.0f); pdf = 0.0f; return; }
+    if (u3 < L.sp) {
+        float ct = sqrtf((1.0f - u0) / (1.0f + (alpha * alpha - 1.0f) * u0));
+        ct = clampf(ct, kSafeCos, 1.0f);
+        const float st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+        const float phi = kTwoPi * u1;
+        V3 wh(st * cosf(phi), st * sinf(phi), ct);
+        align_vector(n, wh);
+        wi = normalize(reflect3(-wo, wh));
+        if (dot(wi, n) <= 0.0f || dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; return; }
+        const float cwi = dot(wi, n);
+        const float cwh = fmaxf(kSafeCos, fabsf(dot(wh, n)));
+        const float cwowh = fmaxf(kSafeCos, fabsf(dot(wo, wh)));
+        const float swh = sqrtf(fmaxf(0.0f, 1.0f - cwh * cwh));
+        const float D = gtr2(cwh, swh, alpha);
+        const V3 Fs = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cwowh);
+        const float G = smith_g(cwo, alpha) * smith_g(cwi, alpha);
+        const V3 brdf = Fs * D * G / (4.0f * cwo * cwi);
+        float mpdf = fmaxf(D * cwh / (4.0f * cwowh), kMinPdf);
+        pdf = fmaxf(mpdf * fmaxf(L.sp, kMinPdf), kMinPdf);
+        bop = clamp_throughput(brdf * cwi / pdf);
+    } else {
+        const float ct = sqrtf(u0);
+        const float st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+        const float phi = kTwoPi * u1;
+        wi = V3(st * cosf(phi), st * sinf(phi), ct);
+        align_vector(n, wi);
+        if (dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; return; }
+        const float cwi = fmaxf(kSafeCos, dot(wi, n));
+        const float fl = disney_diffuse_fresnel(cwo, cwi, roughness);
+        const V3 db = albedo * (1.0f - metalness) * fl / kPi;
+        float dpdf = fmaxf(cwi / kPi, kMinPdf);
+        pdf = fmaxf(dpdf * fmaxf(L.dp, kMinPdf), kMinPdf);
+        bop = clamp_throughput(db * cwi / pdf);
+    }
+}
+
+VX_D void disney_eval(V3 n, V3 ng, V3 wi, V3 wo, V3 albedo, bool metallic, float roughness, V3 &bsdf, float &pdf) {
+    bsdf = V3(0.0f);
+    if (roughness < kRoughThresh) { pdf = 0.0f; return; }
+    if (dot(wo, n) <= 0.0f || dot(wi, n) <= 0.0f || dot(wo, ng) <= 0.0f || dot(wi, ng) <= 0.0f) { pdf = 0.0f; return; }
+    const float metalness = metallic ? 1.0f : 0.0f;
+    const float alpha = fmaxf(roughness * roughness, kRoughThresh);
+    const float cwo = dot(wo, n), cwi = dot(wi, n);
+    const V3 wh = normalize(wi + wo);
+    const float cwh = fmaxf(kSafeCos, fabsf(dot(wh, n)));
+    const float cwowh = fmaxf(kSafeCos, fabsf(dot(wo, wh)));
+    Lobes L;
+    const bool ok = lobes(albedo, metalness, cwowh, L);
+    const V3 F = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cwowh);
+    V3 diffuse(0.0f);
+    if (!metallic) diffuse = albedo * (1.0f - metalness) * disney_diffuse_fresnel(cwo, cwi, roughness) / kPi;
+    const float swh = sqrtf(fmaxf(0.0f, 1.0f - cwh * cwh));
+    const float D = gtr2(cwh, swh, alpha);
+    const float G = smith_g(cwo, alpha) * smith_g(cwi, alpha);
+    const V3 spec = F * D * G / (4.0f * cwo * cwi);
+    bsdf = clamp_throughput(diffuse + spec);
+    if (!ok) { pdf = 0.0f; return; }
+    const float dpdf = fmaxf(cwi / kPi, kMinPdf);
+    const float spdf = fmaxf(D * cwh / (4.0f * cwowh), kMinPdf);
+    pdf = fmaxf(dpdf * fmaxf(L.dp, kMinPdf) + spdf * fmaxf(L.sp, kMinPdf), kMinPdf);
+}
+
+// ----------------------------------------------------------------- sampling
+struct Rng {
+    const BlueNoiseDev *bn;
+    int px, py, it, idx;
+    VX_D float next() {  // BlueNoiseRandGenerator::rand (RandGen.h:21-45)
+        const int i = px & 127, j = py & 127, s = it & 255, d = idx++;
+        const int rk = s ^ bn->rank[(d + (i + j * 128) * 8) & (128 * 128 * 8 - 1)];
+        int v = bn->sobol[d + rk * 256];
+        v ^= bn->scramble[(d % 8) + (i + j * 128) * 8];
+        return v / 256.0f;
+    }
+};
+VX_D float bn_rand(const BlueNoiseDev &bn, int px, int py, int it, int d) {
+    const int i = px & 127, j = py & 127, s = it & 255;
+    const int rk = s ^ bn.rank[(d + (i + j * 128) * 8) & (128 * 128 * 8 - 1)];
+    int v = bn.sobol[d + rk * 256];
+    v ^= bn.scramble[(d % 8) + (i + j * 128) * 8];
+    return v / 256.0f;
+}
+
+VX_D unsigned alias_sample(const AliasBin *b, int len, float u, float &pmf) {
+    const int offset = min(int(u * len), int(len - 1));
+    const float up = fminf(u * len - offset, 0.999999f);
+    const AliasBin e = b[offset];
+    if (up < e.q) { pmf = e.p; return offset; }
+    pmf = b[e.alias].p;
+    return e.alias;
+}
+
+struct LSample { V3 position, radiance; float solidAnglePdf; int type; };
+
+VX_D V3 ld3(const float4 *p, size_t i) { const float4 v = p[i]; return V3(v.x, v.y, v.z); }
+
+VX_D LSample sun_ls(const SkyDev &k, int idx) {
+    const int sx = idx % k.sunW, sy = idx / k.sunW;
+    LSample s;
+    s.solidAnglePdf = (k.sunW * k.sunH) / (kTwoPi * (1.0f - k.sunCosMax));
+    s.position = eq_area_cone_dir(k.sunDir, (sx + 0.5f) / float(k.sunW), (sy + 0.5f) / float(k.sunH), k.sunCosMax);
+    s.radiance = ld3(k.sun, (size_t)clampi(sy, 0, k.sunH - 1) * k.sunW + clampi(sx, 0, k.sunW - 1));
+    s.type = LtSun;
+    return s;
+}
+VX_D LSample sky_ls(const SkyDev &k, int idx) {
+    const int sx = idx % k.skyW, sy = idx / k.skyW;
+    LSample s;
+    s.solidAnglePdf = (k.skyW * k.skyH) / (4.0f * kPi);
+    s.position = eq_area_sphere_dir((sx + 0.5f) / float(k.skyW), (sy + 0.5f) / float(k.skyH));
+    s.radiance = ld3(k.sky, (size_t)sy * k.skyW + sx);
+    s.type = LtSky;
+    return s;
+}
+
+struct SurfS {
+    V3 pos, normal, geoNormal, albedo, wo;
+    float depth, roughness, translucency;
+    bool metallic;
+};
+
+VX_D float target_pdf(const LSample &ls, const SurfS &sf) {
+    if (ls.solidAnglePdf <= 0 || ls.type == LtInvalid) return 0.0f;
+    V3 fr;
+    float pdf;
+    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, pdf);
+    return luminance(ls.radiance * fr * fabsf(dot(ls.position, sf.normal)) / ls.solidAnglePdf);
+}
+VX_D float mis_weight(const SurfS &sf, const LSample &ls, float selPdf, float lightMis, float brdfMis) {
+    const float sa = ls.solidAnglePdf;
+    if (brdfMis == 0.0f || sa <= 0.0f || isinf(sa) || isnan(sa)) return lightMis * selPdf;
+    V3 fr;
+    float bp;
+    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, bp);
+    return (lightMis * (selPdf * sa) + brdfMis * bp) / sa;
+}
+VX_D bool stream_sample(Reservoir &r, uint32_t light, V2 uv, float rnd, float target, float invSrc) {
+    const float w = target * invSrc;
+    r.M += 1;
+    r.weightSum += w;
+    const bool sel = (rnd * r.weightSum < w);
+    if (sel) {
+        r.lightData = light | kValidBit;
+        r.uvData = (uint32_t)(saturate(uv.x) * 0xffff) | ((uint32_t)(saturate(uv.y) * 0xffff) << 16);
+        r.targetPdf = target;
+    }
+    return sel;
+}
+VX_D bool combine(Reservoir &r, const Reservoir &n, float rnd, float target) {
+    const float w = target * (n.weightSum * n.M);
+    r.M += n.M;
+    r.weightSum += w;
+    const bool sel = (rnd * r.weightSum < w);
+    if (sel) { r.lightData = n.lightData; r.uvData = n.uvData; r.targetPdf = target; }
+    return sel;
+}
+VX_D void finalize(Reservoir &r, float num, float den) {
+    const float d = r.targetPdf * den;
+    r.weightSum = (d == 0.0f) ? 0.0f : (r.weightSum * num) / d;
+}
+VX_D Reservoir empty_res() { return Reservoir{0u, 0u, 0.0f, 0.0f, 0.0f}; }
+
+VX_D bool light_from_res(const SkyDev &k, LSample &ls, const Reservoir &r) {
+    const uint32_t li = r.lightData & kIndexMask;
+    const float ux = (float)(r.uvData & 0xffff) / float(0xffff), uy = (float)(r.uvData >> 16) / float(0xffff);
+    if (li == kSkyLight) {
+        const int x = clampi(int(ux * k.skyW), 0, k.skyW - 1), y = clampi(int(uy * k.skyH), 0, k.skyH - 1);
+        ls = sky_ls(k, y * k.skyW + x);
+    } else if (li == kSunLight) {
+        const int x = clampi(int(ux * k.sunW), 0, k.sunW - 1), y = clampi(int(uy * k.sunH), 0, k.sunH - 1);
+        ls = sun_ls(k, y * k.sunW + x);
+    }
+    return li < kInvalidLight;
+}
+
+VX_D int reflect_view(int p, int n) {
+    if (p < 0) p = -p;
+    if (p >= n) p = 2 * n - p - 1;
+    return p;
+}
+
+VX_D bool prev_surface(const TraceArgs &a, int px, int py, SurfS &sf, int x, int y) {
+    if (x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y) return false;
+    const size_t i = (size_t)y * a.W + x;
+    sf.depth = a.prev.depth[i];
+    if (sf.depth == kRayMax) return false;
+    const float4 nr = a.prev.normalRough[i], gt = a.prev.geoNormalThin[i], mp = a.prev.matParam[i];
+    const float j0 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 0);
+    const float j1 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 1);
+    const V2 uv = (V2((float)x, (float)y) + V2(j0, j1)) * a.prevCam.invRes;
+    const V3 vd = a.prevCam.uv_to_dir(uv);
+    sf.pos = a.prevCam.pos + vd * sf.depth;
+    sf.wo = -vd;
+    sf.normal = V3(nr.x, nr.y, nr.z);
+    sf.geoNormal = V3(gt.x, gt.y, gt.z);
+    sf.albedo = ld3(a.prev.albedo, i);
+    sf.roughness = nr.w;
+    sf.metallic = (mp.x == 1.0f);
+    sf.translucency = mp.y;
+    return true;
+}
+
+VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
+    V3 emission(0.0f);
+    V2 uv = eq_area_sphere_uv(dir);
+    {
+        const V2 UV(uv.x * (float)k.skyW, uv.y * (float)k.skyH);
+        const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
+        const V2 fr = UV - V2(fx0 + 0.5f, fy0 + 0.5f);
+        const V2 f2 = fr * fr, f3 = f2 * fr;
+        const V2 w1 = -2.0f * f3 + 3.0f * f2;
+        const V2 w0 = 1.0f - w1;
+        const int tx0 = (int)fx0, ty0 = (int)fy0;
+        const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
+        V3 out(0.0f);
+        float sum = 0.0f;
+        for (int i = 0; i < 4; ++i) {
+            int x = tx0 + (i & 1), y = ty0 + (i >> 1);
+            if (x >= k.skyW) x %= k.skyW;
+            if (x < 0) x = k.skyW - (-x) % k.skyW;
+            y = clampi(y, 0, k.skyH - 1);
+            sum += wt[i];
+            out += ld3(k.sky, (size_t)y * k.skyW + x) * wt[i];
+        }
+        out /= sum;
+        emission += out;
+    }
+    if (eq_area_cone_uv(uv, k.sunDir, dir, k.sunCosMax)) {
+        int x = (int)(uv.x * k.sunW), y = (int)(uv.y * k.sunH);
+        if (x >= k.sunW) x %= k.sunW;
+        if (x < 0) x = k.sunW - (-x) % k.sunW;
+        emission += ld3(k.sun, (size_t)clampi(y, 0, k.sunH - 1) * k.sunW + clampi(x, 0, k.sunW - 1));
+    }
+    return emission;
+}
+
+struct PathState {
+    V3 pos, wi, radiance, bop;
+    float distance, pdf;
+    int depth;
+    bool hitFirstDiffuse, terminate, curDiffuse;
+};
+
+VX_D void store_res(const TraceArgs &a, size_t pi, const Reservoir &r) { a.resCur[pi] = r; }
+
+// closesthit for a cube face (closesthit.cu:10-852)
+VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps, const Hit &h) {
+    const size_t pi = (size_t)py * a.W + px;
+    const V3 wo = -ps.wi;
+    ps.distance = h.t;
+    V3 frontPos, backPos, ng;
+    hit_frame(h, ps.pos, ps.wi, frontPos, backPos, ng);
+    if (ps.depth == 0) a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const MatDev &m = a.mats[h.id];
+    SurfS sf;
+    sf.geoNormal = ng;
+    sf.wo = wo;
+    sf.albedo = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
+    sf.roughness = m.roughness;
+    if (ps.hitFirstDiffuse) sf.roughness = fminf(sf.roughness * 2.0f + 0.1f, 1.0f);
+    const bool isDiffuse = sf.roughness > kRoughThresh;
+    sf.metallic = m.metallic != 0;
+    sf.translucency = m.translucency;
+    sf.normal = lerp3(ng, ng, 0.2f);
+    ps.curDiffuse = isDiffuse;
+    if (ps.depth == 0) {
+        a.cur.material[pi] = (float)m.materialId;
+        a.cur.normalRough[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, sf.roughness);
+        a.cur.geoNormalThin[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, m.thin ? 1.0f : 0.0f);
+        a.cur.matParam[pi] = make_float4(sf.metallic ? 1.0f : 0.0f, sf.translucency, 0.0f, 0.0f);
+    }
+    {
+        const float u0 = rng.next(), u1 = rng.next(), u2 = rng.next(), u3 = rng.next();
+        V3 swi, sbop;
+        float spdf;
+        disney_sample(u0, u1, u2, u3, sf.normal, sf.geoNormal, wo, sf.albedo, sf.metallic, sf.translucency,
+                      sf.roughness, swi, sbop, spdf);
+        if (spdf <= 0.0f) ps.terminate = true;
+        ps.pos = frontPos;
+        ps.wi = swi;
+        ps.bop = sbop;
+        ps.pdf = spdf;
+    }
+    bool skipAlbedo = false;
+    if (ps.depth == 0) {
+        ps.hitFirstDiffuse = true;
+        a.cur.albedo[pi] = make_float4(sf.albedo.x, sf.albedo.y, sf.albedo.z, 1.0f);
+        skipAlbedo = true;
+    }
+    const bool restir = ps.depth == 0;
+    if (!isDiffuse) {
+        if (restir) store_res(a, pi, empty_res());
+        return;
+    }
+    sf.pos = frontPos;
+    sf.depth = h.t;
+    const SkyDev &k = a.sky;
+    const bool skipSun = (dot(sf.normal, k.sunDir) < 0.0f || dot(sf.geoNormal, k.sunDir) < 0.0f);
+    const int nSun = skipSun ? 0 : 1;
+    const int nMis = nSun + 2;
+    const float sunMis = float(nSun) / nMis, skyMis = 1.0f / nMis, brdfMis = 1.0f / nMis;
+
+    Reservoir localRes = empty_res();
+    finalize(localRes, 1.0f, (float)nMis);
+    localRes.M = 1;
+
+    Reservoir sunRes = empty_res();
+    LSample sunLs{V3(0.f), V3(0.f), 0.f, LtInvalid};
+    if (nSun) {
+        float src;
+        const int idx = (int)alias_sample(k.sunAlias, k.sunW * k.sunH, rng.next(), src);
+        const LSample cand = sun_ls(k, idx);
+        const int sx = idx % k.sunW, sy = idx / k.sunW;
+        const V2 uv((sx + 0.5f) / float(k.sunW), (sy + 0.5f) / float(k.sunH));
+        const float blended = mis_weight(sf, cand, src, sunMis, brdfMis);
+        const float tp = target_pdf(cand, sf);
+        const float rr = rng.next();
+        if (stream_sample(sunRes, kSunLight, uv, rr, tp, 1.0f / blended)) sunLs = cand;
+    }
+    finalize(sunRes, 1.0f, (float)nMis);
+    sunRes.M = 1;
+
+    Reservoir skyRes = empty_res();
+    LSample skyLs{V3(0.f), V3(0.f), 0.f, LtInvalid};
+    {
+        float src;
+        const float r0 = rng.next(), r1 = rng.next();
+        const int idx = (int)alias_sample(k.skyAlias, k.skyW * k.skyH, r0 + r1 / 256.0f, src);
+        const LSample cand = sky_ls(k, idx);
+        const int sx = idx % k.skyW, sy = idx / k.skyW;
+        const V2 uv((sx + 0.5f) / float(k.skyW), (sy + 0.5f) / float(k.skyH));
+        const float blended = mis_weight(sf, cand, src, skyMis, brdfMis);
+        const float tp = target_pdf(cand, sf);
+        const float rr = rng.next();
+        if (stream_sample(skyRes, kSkyLight, uv, rr, tp, 1.0f / blended)) skyLs = cand;
+    }
+    finalize(skyRes, 1.0f, (float)nMis);
+    skyRes.M = 1;
+
+    Reservoir brdfRes = empty_res();
+    LSample brdfLs{V3(0.f), V3(0.f), 0.f, LtInvalid};
+    {
+        float lightSrcPdf = 0.0f;
+        uint32_t li = kInvalidLight;
+        V2 uv(0.0f, 0.0f);
+        LSample cand{V3(0.f), V3(0.f), 0.f, LtInvalid};
+        const float u0 = rng.next(), u1 = rng.next(), u2 = rng.next(), u3 = rng.next();
+        V3 sd, bop;
+        float bp;
+        disney_sample(u0, u1, u2, u3, sf.normal, sf.geoNormal, wo, sf.albedo, sf.metallic, sf.translucency,
+                      sf.roughness, sd, bop, bp);
+        if (bp > 0.0f) {
+            const Hit bh = dda_closest(a.world, frontPos, sd, 3.402823466e+38f);
+            if (!bh.hit) {
+                if (eq_area_cone_uv(uv, k.sunDir, sd, k.sunCosMax)) {
+                    li = kSunLight;
+                    int x = (int)(uv.x * k.sunW - 0.5f), y = (int)(uv.y * k.sunH - 0.5f);
+                    if (x >= k.sunW) x %= k.sunW;
+                    if (x < 0) x = k.sunW - ((-x) % k.sunW);
+                    y = clampi(y, 0, k.sunH - 1);
+                    const int idx = y * k.sunW + x;
+                    cand = sun_ls(k, idx);
+                    cand.position = sd;
+                    lightSrcPdf = k.sunAlias[idx].p;
+                } else {
+                    li = kSkyLight;
+                    uv = eq_area_sphere_uv(sd);
+                    const int x = (int)(uv.x * k.skyW - 0.5f), y = (int)(uv.y * k.skyH - 0.5f);
+                    const int idx = y * k.skyW + x;
+                    cand = sky_ls(k, idx);
+                    cand.position = sd;
+                    lightSrcPdf = k.skyAlias[idx].p;
+                }
+            }
+        }
+        if (lightSrcPdf != 0.0f) {
+            const float tp = target_pdf(cand, sf);
+            const float misW = (li == kSkyLight) ? skyMis : ((li == kSunLight) ? sunMis : 0.0f);
+            const float blended = mis_weight(sf, cand, lightSrcPdf, misW, brdfMis);
+            const float rr = rng.next();
+            if (stream_sample(brdfRes, li, uv, rr, tp, 1.0f / blended)) brdfLs = cand;
+        }
+    }
+    finalize(brdfRes, 1.0f, (float)nMis);
+    brdfRes.M = 1;
+
+    Reservoir ris = empty_res();
+    combine(ris, localRes, 0.5f, localRes.targetPdf);
+    const bool selSun = combine(ris, sunRes, rng.next(), sunRes.targetPdf);
+    const bool selSky = combine(ris, skyRes, rng.next(), skyRes.targetPdf);
+    const bool selBrdf = combine(ris, brdfRes, rng.next(), brdfRes.targetPdf);
+    finalize(ris, 1.0f, 1.0f);
+    ris.M = 1;
+    LSample ls = selBrdf ? brdfLs : (selSky ? skyLs : (selSun ? sunLs : LSample{V3(0.f), V3(0.f), 0.f, LtInvalid}));
+
+    bool visible = false;
+    if (ls.type != LtInvalid && ris.lightData != 0) {
+        visible = !dda_occluded(a.world, frontPos, ls.position, 0.0f, kRayMax);
+        if (!visible) { ris.lightData = 0; ris.weightSum = 0; }
+    }
+
+    Reservoir rr = empty_res();
+    if (restir) {
+        combine(rr, ris, 0.5f, ris.targetPdf);
+        const CamDev &pc = a.prevCam;
+        const V3 prevW = sf.pos;  // + motion (static geometry: 0)
+        const V2 puv = pc.dir_to_uv(normalize(prevW - pc.pos));
+        const int ppx = (int)(puv.x * pc.res.x), ppy = (int)(puv.y * pc.res.y);
+        const V3 dd = prevW - pc.pos;
+        const float expDepth = sqrtf(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z);
+        int ox[3], oy[3];
+        ox[0] = ppx - px; oy[0] = ppy - py;
+        {
+            const float r0 = rng.next(), r1 = rng.next();
+            V2 u = V2(r0 * 2.0f - 1.0f, r1 * 2.0f - 1.0f);
+            V2 dsk(0.0f, 0.0f);
+            if (!(fabsf(u.x) < 1e-10f && fabsf(u.y) < 1e-10f)) {
+                float th, r;
+                if (fabsf(u.x) > fabsf(u.y)) { r = u.x; th = kPiOver4 * (u.y / u.x); }
+                else { r = u.y; th = kPiOver2 - kPiOver4 * (u.x / u.y); }
+                dsk = V2(cosf(th) * r, sinf(th) * r);
+            }
+            dsk = dsk * 64.0f;
+            ox[1] = ppx - px + (int)dsk.x; oy[1] = ppy - py + (int)dsk.y;
+        }
+        {
+            const float r0 = rng.next(), r1 = rng.next();
+            V2 u = V2(r0 * 2.0f - 1.0f, r1 * 2.0f - 1.0f);
+            V2 dsk(0.0f, 0.0f);
+            if (!(fabsf(u.x) < 1e-10f && fabsf(u.y) < 1e-10f)) {
+                float th, r;
+                if (fabsf(u.x) > fabsf(u.y)) { r = u.x; th = kPiOver4 * (u.y / u.x); }
+                else { r = u.y; th = kPiOver2 - kPiOver4 * (u.x / u.y); }
+                dsk = V2(cosf(th) * r, sinf(th) * r);
+            }
+            dsk = dsk * 64.0f;
+            ox[2] = (int)dsk.x; oy[2] = (int)dsk.y;
+        }
+        unsigned cached = 0;
+        int selLoop = -1;
+        for (int i = 0; i < 3; ++i) {
+            const int x = reflect_view(px + ox[i], a.W), y = reflect_view(py + oy[i], a.H);
+            SurfS ts;
+            if (!prev_surface(a, px, py, ts, x, y)) continue;
+            const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
+            const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
+            const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
+            if (!(nOk && dOk && rOk)) continue;
+            cached |= (1u << i);
+            Reservoir pr = a.resPrev[(size_t)y * a.W + x];
+            if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
+            if (pr.M > 20.0f) pr.M = 20.0f;
+            float nw = 0.0f;
+            LSample cand{V3(0.f), V3(0.f), 0.f, LtInvalid};
+            if (pr.lightData != 0) {
+                if (!light_from_res(k, cand, pr)) pr = empty_res();
+                nw = target_pdf(cand, sf);
+            }
+            if (combine(rr, pr, rng.next(), nw)) { ls = cand; selLoop = i; }
+        }
+        if (rr.lightData != 0) {
+            float piv = rr.targetPdf, piSum = rr.targetPdf * 1;
+            for (int i = 0; i < 3; ++i) {
+                if ((cached & (1u << i)) == 0) continue;
+                const int x = reflect_view(px + ox[i], a.W), y = reflect_view(py + oy[i], a.H);
+                SurfS ts;
+                prev_surface(a, px, py, ts, x, y);
+                LSample sel{V3(0.f), V3(0.f), 0.f, LtInvalid};
+                light_from_res(k, sel, rr);
+                float psv = target_pdf(sel, ts);
+                if (psv > 0 && !(i == 0 && i == selLoop)) {
+                    const float extra = 0.01f + 0.01f * ts.depth;
+                    if (dda_occluded(a.world, ts.pos, ls.position, extra, kRayMax)) psv = 0.0f;
+                }
+                Reservoir pr = a.resPrev[(size_t)y * a.W + x];
+                if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
+                if (pr.M > 20.0f) pr.M = 20.0f;
+                if (selLoop == i) piv = psv;
+                piSum += psv * pr.M;
+            }
+            finalize(rr, piv, piSum);
+        }
+        if (ls.type != LtInvalid) {
+            visible = !dda_occluded(a.world, frontPos, ls.position, 0.0f, kRayMax);
+            if (!visible) { rr.lightData = 0; rr.weightSum = 0; }
+        }
+    }
+    const Reservoir &shade = restir ? rr : ris;
+    if (ls.type != LtInvalid && shade.lightData != 0 && visible) {
+        const V3 alb = skipAlbedo ? V3(1.0f) : sf.albedo;
+        V3 bsdf;
+        float pdf;
+        disney_eval(sf.normal, sf.geoNormal, ls.position, wo, alb, sf.metallic, sf.roughness, bsdf, pdf);
+        const float cosT = fmaxf(0.0f, dot(ls.position, sf.normal));
+        ps.radiance += bsdf * cosT * ls.radiance * shade.weightSum / ls.solidAnglePdf;
+    }
+    if (restir) store_res(a, pi, rr);
+}
+
+VX_D void shade_miss(const TraceArgs &a, int px, int py, PathState &ps) {
+    const size_t pi = (size_t)py * a.W + px;
+    if (ps.depth == 0) {
+        store_res(a, pi, empty_res());
+        a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        a.cur.material[pi] = (float)0xFFFF;
+        a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+        a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+        a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    ps.radiance = sky_emission(a.sky, ps.wi);
+    ps.distance = kRayMax;
+    ps.terminate = true;
+}
+
+__global__ __launch_bounds__(256) void k_trace(TraceArgs a) {
+    // 16x16 pixel workgroup; wave w owns the 8x8 quadrant (w&1, w>>1)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int py = a.y0 + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (px >= a.W || py >= a.y1) return;
+    Rng rng{&a.bn, px, py, a.iterationIndex, 0};
+    const size_t pi = (size_t)py * a.W + px;
+    const float j0 = rng.next(), j1 = rng.next();
+    const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
+    PathState ps;
+    ps.pos = a.cam.pos;
+    ps.wi = a.cam.uv_to_dir(uv);
+    ps.depth = 0;
+    ps.hitFirstDiffuse = false;
+    ps.curDiffuse = false;
+    V3 radiance(0.0f), throughput(1.0f);
+    float primaryDist = kRayMax;
+
+    if (a.primaryOnly) {
+        const Hit h = dda_closest(a.world, ps.pos, ps.wi, kRayMax);
+        if (!h.hit) {
+            shade_miss(a, px, py, ps);
+            a.cur.depth[pi] = kRayMax;
+            a.illum[pi] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, kRayMax);
+            return;
+        }
+        V3 fp, bp, ng;
+        hit_frame(h, ps.pos, ps.wi, fp, bp, ng);
+        const MatDev &m = a.mats[h.id];
+        const V3 alb = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
+        a.cur.material[pi] = (float)m.materialId;
+        a.cur.normalRough[pi] = make_float4(ng.x, ng.y, ng.z, m.roughness);
+        a.cur.geoNormalThin[pi] = make_float4(ng.x, ng.y, ng.z, 0.0f);
+        a.cur.matParam[pi] = make_float4(m.metallic ? 1.0f : 0.0f, m.translucency, 0.0f, 0.0f);
+        a.cur.albedo[pi] = make_float4(alb.x, alb.y, alb.z, 1.0f);
+        a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        a.cur.depth[pi] = h.t;
+        a.illum[pi] = make_float4(0.0f, 0.0f, 0.0f, h.t);
+        return;
+    }
+
+    int total = 0, diffuse = 0;
+    bool done = false;
+    while (!done) {
+        // TraceNextPath (RayGen.cu:8-100)
+        ps.bop = V3(1.0f);
+        ps.pdf = 0.0f;
+        ps.radiance = V3(0.0f);
+        ps.distance = kRayMax;
+        ps.terminate = false;
+        ps.curDiffuse = false;
+        const Hit h = dda_closest(a.world, ps.pos, ps.wi, kRayMax);
+        if (h.hit) shade_hit(a, px, py, rng, ps, h);
+        else shade_miss(a, px, py, ps);
+        radiance += throughput * ps.radiance;
+        bool cont = !(ps.terminate || ps.pdf <= 0.0f || is_null(ps.bop));
+        if (cont) throughput *= ps.bop;
+        done = !cont;
+        ++total;
+        if (ps.curDiffuse) ++diffuse;
+        if (total == a.totalBounceLimit || diffuse == a.diffuseBounceLimit) done = true;
+        if (ps.depth == 0) primaryDist = ps.distance;
+        ++ps.depth;
+    }
+    if (isnan(radiance.x) || isnan(radiance.y) || isnan(radiance.z)) radiance = V3(0.5f);
+    a.cur.depth[pi] = primaryDist;
+    if (a.accum) {
+        // spp > 1: average the passes' radiance, depth from the last pass
+        float4 acc = a.accumFirst ? make_float4(0.f, 0.f, 0.f, 0.f) : a.accum[pi];
+        acc.x += radiance.x * a.accumScale;
+        acc.y += radiance.y * a.accumScale;
+        acc.z += radiance.z * a.accumScale;
+        acc.w = primaryDist;
+        a.accum[pi] = acc;
+    }
+    a.illum[pi] = make_float4(radiance.x, radiance.y, radiance.z, primaryDist);
+}
+
+__global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *rays, int *out, float *t, int mode) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float *r = rays + 8 * i;
+    const V3 o(r[0], r[1], r[2]), d(r[3], r[4], r[5]);
+    int *q = out + 6 * i;
+    if (mode == 2) {
+        q[0] = dda_occluded(w, o, d, r[6], r[7]) ? 1 : 0;
+        q[1] = q[2] = q[3] = q[4] = q[5] = 0;
+        t[i] = 0.0f;
+        return;
+    }
+    const Hit h = dda_closest(w, o, d, r[7]);
+    q[0] = h.hit; q[1] = h.x; q[2] = h.y; q[3] = h.z; q[4] = h.face; q[5] = h.id;
+    t[i] = h.t;
+}
+
+}  // namespace
+
+hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, float *t, int mode, hipStream_t st) {
+    hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, st, w, n, rays, out, t, mode);
+    return hipGetLastError();
+}
+
+namespace {
+}  // namespace
+
+hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
+    const int rows = a.y1 - a.y0;
+    dim3 g((a.W + 15) / 16, (rows + 15) / 16);
+    hipLaunchKernelGGL(k_trace, g, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace vx

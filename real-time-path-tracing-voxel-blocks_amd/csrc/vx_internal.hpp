@@ -1,0 +1,127 @@
+// vxpt -- internal types shared by the host runtime and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+#include "vx_math.hpp"
+
+namespace vx {
+
+// camera as the kernels see it (shaders/Camera.h:6-150, host-computed matrices)
+struct CamDev {
+    V3 pos, dir;
+    V2 res, invRes, tanHalfFov;
+    M3 uvToWorld, worldToUv;
+    VX_HD V3 uv_to_dir(V2 uv) const { return normalize(m3_apply(uvToWorld, V3(uv.x, uv.y, 1.0f))); }
+    VX_HD V2 dir_to_uv(V3 d) const {
+        V3 n = m3_apply(worldToUv, d);
+        return {n.x / n.z, n.y / n.z};
+    }
+};
+
+struct MatDev {  // per block id, untextured MaterialParameter subset
+    float albedo[3];
+    float roughness;
+    float translucency;
+    int metallic;
+    int materialId;
+    int thin;
+};
+
+struct AliasBin { float q, p; int alias; };
+
+struct Reservoir { uint32_t lightData, uvData; float weightSum, targetPdf, M; };
+
+// Voxel world on the device.  ids: chunk-major u8 (32^3 per chunk, x + 32*(z + 32*y));
+// occ: one bit per 4^3 brick, bricks ordered bx + BX*(bz + BZ*by).
+struct WorldDev {
+    const uint8_t *ids;
+    const uint32_t *occ;
+    int cx, cy, cz;       // chunks
+    int wx, wy, wz;       // cells
+    int bx, by, bz;       // bricks
+};
+
+struct SkyDev {
+    const float4 *sky;    // 1024 x 512
+    const float4 *sun;    // 32 x 32
+    const AliasBin *skyAlias, *sunAlias;
+    V3 sunDir;
+    int skyW, skyH, sunW, sunH;
+    float sunCosMax;
+};
+
+struct BlueNoiseDev { const uint8_t *sobol, *scramble, *rank; };
+
+// Per-frame G-buffer planes, SoA, row-major W*H each (BufferManager.cpp:150-186)
+struct GBuf {
+    float4 *normalRough, *geoNormalThin, *albedo, *matParam;
+    float *depth, *material;
+};
+
+struct TraceArgs {
+    WorldDev world;
+    SkyDev sky;
+    BlueNoiseDev bn;
+    MatDev mats[13];
+    CamDev cam, prevCam;
+    GBuf cur, prev;
+    float4 *illum, *motion;
+    Reservoir *resCur;          // written this pass (iterationIndex parity)
+    const Reservoir *resPrev;   // read by temporal reuse
+    float4 *accum;              // spp accumulation target (nullptr when spp == 1)
+    int W, H, y0, y1;
+    int iterationIndex;
+    int totalBounceLimit, diffuseBounceLimit;
+    int primaryOnly;
+    float accumScale;           // 1/spp
+    int accumFirst;
+};
+
+// kernel launchers (defined in the .hip translation units)
+hipError_t launch_sky(const float *cfg90, const float *rad10, const float *solar, const float *limb, V3 sunDir,
+                      float brightness, float4 *sky, float4 *sun, float *skyPdf, float *sunPdf, int skyW, int skyH,
+                      int sunW, int sunH, hipStream_t st);
+hipError_t launch_sky_lower(float4 *sky, float *skyPdf, int skyW, int skyH, float sumUpper, hipStream_t st);
+hipError_t launch_trace(const TraceArgs &a, hipStream_t st);
+
+struct DenoiseParamsDev {
+    float maxAcc, maxFast, phiL, lobeAngleFraction, roughnessFraction, depthThreshold;
+    float disocclusionThreshold, disocclusionThresholdAlternate, denoisingRange;
+    int enableTA, enableHF, enableHC, enableSpatial, enableFirefly, atrousIterations;
+};
+
+struct DenoiseArgs {
+    int W, H;
+    CamDev cam, prevCam;
+    DenoiseParamsDev p;
+    // inputs of this frame
+    float4 *illum;
+    const float4 *normalRough, *albedo, *motion;
+    const float *depth, *material;
+    const float4 *prevNormalRough;
+    const float *prevDepth;
+    Reservoir *reservoir;       // the pass's reservoirs (parity usedIteration&1)
+    // persistent denoiser state
+    float4 *ping, *pong, *prevIllum, *prevFast, *output;
+    float *histLen, *prevHistLen;
+    // firefly scratch
+    uint32_t *ffCount;
+    uint32_t *ffIndex;
+    float4 *ffColor;
+    Reservoir *ffRes;
+};
+
+hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st);
+// final: also writes output (sky pixels copy illum, others illum*albedo)
+hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex,
+                         bool final, hipStream_t st);
+hipError_t launch_copy_output(const DenoiseArgs &a, const float4 *in, hipStream_t st);
+
+}  // namespace vx

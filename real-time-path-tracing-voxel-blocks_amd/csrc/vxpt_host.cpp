@@ -1,0 +1,942 @@
+// vxpt -- host runtime behind the C ABI (include/vxpt.h).
+//
+// Owns the device memory of one GPU (the reference's BufferManager /
+// SkyModel / MaterialManager singletons), sets up the camera and the sky the
+// way the reference does on its host (mainOffline.cpp:201-251, Sky.cu:355-396,
+// AliasTable.cu:66-153), generates the Perlin terrain (VoxelSceneGen.cu:341-388)
+// and sequences the kernels of one frame (OfflineBackend.cpp:46-89).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <queue>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/vxpt.h"
+#include "vx_internal.hpp"
+
+using namespace vx;
+
+namespace {
+
+// ---------------------------------------------------------------- helpers
+template <class T>
+struct DBuf {
+    T *p = nullptr;
+    size_t n = 0;
+};
+
+struct GSlot {
+    float4 *normalRough = nullptr, *geoNormalThin = nullptr, *albedo = nullptr, *matParam = nullptr;
+    float *depth = nullptr, *material = nullptr;
+};
+
+// Perlin noise (siv::BasicPerlinNoise<float>, voxelengine/ext/PerlinNoise.hpp:229-494, 565-568)
+struct Perlin {
+    uint8_t p[256];
+    explicit Perlin(uint32_t seed) {
+        for (int i = 0; i < 256; ++i) p[i] = (uint8_t)i;
+        std::mt19937 g(seed);
+        for (int i = 1; i < 256; ++i) {
+            const uint64_t r = (uint64_t)g() % (uint64_t)(i + 1);
+            std::swap(p[i], p[r]);
+        }
+    }
+    static float fade(float t) { return t * t * t * (t * (t * 6 - 15) + 10); }
+    static float lerp(float a, float b, float t) { return a + (b - a) * t; }
+    static float grad(uint8_t hash, float x, float y, float z) {
+        const uint8_t h = hash & 15;
+        const float u = h < 8 ? x : y;
+        const float v = h < 4 ? y : (h == 12 || h == 14 ? x : z);
+        return ((h & 1) == 0 ? u : -u) + ((h & 2) == 0 ? v : -v);
+    }
+    float noise(float x, float y, float z) const {
+        const float X = std::floor(x), Y = std::floor(y), Z = std::floor(z);
+        const int ix = (int)X & 255, iy = (int)Y & 255, iz = (int)Z & 255;
+        const float fx = x - X, fy = y - Y, fz = z - Z;
+        const float u = fade(fx), v = fade(fy), w = fade(fz);
+        const uint8_t A = (p[ix] + iy) & 255, B = (p[(ix + 1) & 255] + iy) & 255;
+        const uint8_t AA = (p[A] + iz) & 255, AB = (p[(A + 1) & 255] + iz) & 255;
+        const uint8_t BA = (p[B] + iz) & 255, BB = (p[(B + 1) & 255] + iz) & 255;
+        const float q0 = lerp(grad(p[AA], fx, fy, fz), grad(p[BA], fx - 1, fy, fz), u);
+        const float q1 = lerp(grad(p[AB], fx, fy - 1, fz), grad(p[BB], fx - 1, fy - 1, fz), u);
+        const float q2 = lerp(grad(p[(AA + 1) & 255], fx, fy, fz - 1), grad(p[(BA + 1) & 255], fx - 1, fy, fz - 1), u);
+        const float q3 = lerp(grad(p[(AB + 1) & 255], fx, fy - 1, fz - 1), grad(p[(BB + 1) & 255], fx - 1, fy - 1, fz - 1), u);
+        return lerp(lerp(q0, q1, v), lerp(q2, q3, v), w);
+    }
+    float octave01(float x, float y, int oct) const {
+        float r = 0, a = 1;
+        for (int i = 0; i < oct; ++i) {
+            r += noise(x, y, (float)0.34567) * a;
+            x *= 2;
+            y *= 2;
+            a *= 0.5f;
+        }
+        if (r <= -1.0f) return 0.0f;
+        if (1.0f <= r) return 1.0f;
+        return r * 0.5f + 0.5f;
+    }
+};
+
+// minimal YAML reader for the reference's settings / scene / asset files:
+// `section:` headers, `key: value` pairs, `- {k: v, ...}` / `properties: {...}` flow maps
+std::string trim(const std::string &s) {
+    size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
+    return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+}
+std::map<std::string, std::string> parse_flow_map(const std::string &s) {
+    std::map<std::string, std::string> m;
+    size_t a = s.find('{'), b = s.rfind('}');
+    if (a == std::string::npos || b == std::string::npos) return m;
+    std::string body = s.substr(a + 1, b - a - 1);
+    int depth = 0;
+    std::string cur;
+    std::vector<std::string> items;
+    for (char c : body) {
+        if (c == '[') depth++;
+        if (c == ']') depth--;
+        if (c == ',' && depth == 0) { items.push_back(cur); cur.clear(); continue; }
+        cur += c;
+    }
+    if (!trim(cur).empty()) items.push_back(cur);
+    for (auto &it : items) {
+        size_t c = it.find(':');
+        if (c == std::string::npos) continue;
+        m[trim(it.substr(0, c))] = trim(it.substr(c + 1));
+    }
+    return m;
+}
+std::vector<float> parse_list(const std::string &s) {
+    std::vector<float> v;
+    std::string t = s;
+    for (char &c : t)
+        if (c == '[' || c == ']' || c == ',') c = ' ';
+    std::istringstream is(t);
+    float f;
+    while (is >> f) v.push_back(f);
+    return v;
+}
+bool as_bool(const std::string &s) { return s == "true" || s == "1" || s == "True"; }
+
+}  // namespace
+
+struct vxpt_ctx {
+    int W = 0, H = 0, dev = 0, rowBegin = 0, rowEnd = 0;
+    int totalBounce = 3, diffuseBounce = 1;
+    std::string dataDir;
+    std::string err;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8] = {};
+    vxpt_timing timing{};
+
+    // scene
+    int cx = 0, cy = 0, cz = 0;
+    DBuf<uint8_t> voxels;
+    DBuf<uint32_t> occ;
+    MatDev mats[13] = {};
+    CamDev cam{}, prevCam{};
+    float camYaw = 0, camPitch = 0;
+
+    // sky
+    DBuf<float4> sky, sun;
+    DBuf<float> skyPdf, sunPdf;
+    DBuf<AliasBin> skyAlias, sunAlias;
+    std::vector<AliasBin> hSkyAlias;
+    V3 sunDir;
+    float tabSky[540], tabSkyRad[60];
+    DBuf<float> solar, limb;
+    bool skyReady = false;
+
+    // blue noise
+    DBuf<uint8_t> bnSobol, bnScramble, bnRank;
+
+    // frame buffers
+    GSlot gb[2];
+    int last = 0;              // slot of the most recent trace output
+    float4 *illum = nullptr, *accum = nullptr, *motion = nullptr;
+    Reservoir *res = nullptr;  // 2*W*H
+    float4 *ping = nullptr, *pong = nullptr, *prevIllum = nullptr, *prevFast = nullptr, *output = nullptr;
+    float *histLen = nullptr, *prevHistLen = nullptr;
+    float4 *dnPrevNormalRough = nullptr;
+    float *dnPrevDepth = nullptr, *dnPrevMaterial = nullptr;
+    uint32_t *ffCount = nullptr, *ffIndex = nullptr;
+    float4 *ffColor = nullptr;
+    Reservoir *ffRes = nullptr;
+    bool denoiseInputIsAccum = false;
+    std::vector<void *> allocs;
+
+    vxpt_denoise_params yamlDenoise{};
+    float skyParams[4] = {0.25f, 45.0f, 0.0f, 1.0f};
+    vxpt_material yamlMats[13] = {};
+};
+
+namespace {
+
+int fail(vxpt_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+#define HIPCHK(c, expr)                                                                          \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) return fail((c), VXPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+int dalloc(vxpt_ctx *c, T *&p, size_t n) {
+    void *q = nullptr;
+    HIPCHK(c, hipMalloc(&q, n * sizeof(T) + 16));
+    HIPCHK(c, hipMemset(q, 0, n * sizeof(T) + 16));
+    c->allocs.push_back(q);
+    p = (T *)q;
+    return 0;
+}
+
+bool read_file(const std::string &p, std::vector<uint8_t> &out) {
+    std::ifstream f(p, std::ios::binary);
+    if (!f) return false;
+    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return true;
+}
+
+template <class T>
+int upload_vec(vxpt_ctx *c, DBuf<T> &d, const T *h, size_t n) {
+    if (d.n < n) {
+        if (dalloc(c, d.p, n)) return VXPT_ERR_HIP;
+        d.n = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
+// Camera set-up exactly as mainOffline.cpp:227-246 + Camera::update (Camera.h:44-100)
+V3 yaw_pitch_to_dir(float yaw, float pitch) {
+    if (std::isnan(yaw) || std::isnan(pitch)) return {0, 0, 1};
+    pitch = clampf(pitch, -kPiOver2 + 0.01f, kPiOver2 - 0.01f);
+    const float sy = std::sin(yaw), cyw = std::cos(yaw), sp = std::sin(pitch), cp = std::cos(pitch);
+    return normalize(V3(sy * cp, sp, cyw * cp));
+}
+CamDev make_camera(int W, int H, const vxpt_camera &in, float *yawOut, float *pitchOut) {
+    CamDev c{};
+    c.res = V2((float)W, (float)H);
+    c.invRes = V2(1.0f / c.res.x, 1.0f / c.res.y);
+    c.pos = V3(in.pos[0], in.pos[1], in.pos[2]);
+    const V3 d = normalized_c(normalize(V3(in.dir[0], in.dir[1], in.dir[2])));
+    const float yaw = std::atan2(d.x, d.z), pitch = std::asin(d.y);
+    const float fovX = in.fov_deg * kPiOver180;
+    const float fovY = fovX * (c.res.y / c.res.x);
+    c.tanHalfFov = V2(std::tan(fovX * 0.5f), std::tan(fovY * 0.5f));
+    c.dir = yaw_pitch_to_dir(yaw, pitch);
+    const V3 worldUp(0.0f, 1.0f, 0.0f);
+    const V3 left = normalize(cross(worldUp, c.dir));
+    const V3 up = normalize(cross(c.dir, left));
+    const M3 uvToNdc = m3_cols(V3(2.0f, 0.0f, 0.0f), V3(0.0f, 2.0f, 0.0f), V3(-1.0f, -1.0f, 1.0f));
+    M3 ndcToView = m3_zero();
+    ndcToView.m00 = c.tanHalfFov.x;
+    ndcToView.m11 = c.tanHalfFov.y;
+    ndcToView.m22 = 1.0f;
+    const M3 viewToWorld = m3_cols(-left, up, c.dir);
+    c.uvToWorld = m3_mul(m3_mul(viewToWorld, ndcToView), uvToNdc);
+    const M3 ndcToUv = m3_cols(V3(0.5f, 0.0f, 0.0f), V3(0.0f, 0.5f, 0.0f), V3(0.5f, 0.5f, 1.0f));
+    const M3 worldToView = m3_transpose(viewToWorld);
+    M3 viewToNdc = m3_zero();
+    viewToNdc.m00 = 1.0f / c.tanHalfFov.x;
+    viewToNdc.m11 = 1.0f / c.tanHalfFov.y;
+    viewToNdc.m22 = 1.0f;
+    c.worldToUv = m3_mul(m3_mul(ndcToUv, viewToNdc), worldToView);
+    if (yawOut) *yawOut = yaw;
+    if (pitchOut) *pitchOut = pitch;
+    return c;
+}
+
+std::vector<AliasBin> build_alias(const std::vector<float> &w, float &sumOut) {
+    const unsigned n = (unsigned)w.size();
+    double acc = 0.0;
+    for (unsigned i = 0; i < n; ++i) acc += (double)w[i];
+    const float sum = (float)acc;
+    sumOut = sum;
+    std::vector<float> prob(n), scaled(n);
+    std::vector<int> alias(n, -1);
+    for (unsigned i = 0; i < n; ++i) {
+        prob[i] = w[i] / sum;
+        scaled[i] = prob[i] * n;
+    }
+    std::queue<int> small, large;
+    for (unsigned i = 0; i < n; ++i) (scaled[i] < 1.0f ? small : large).push((int)i);
+    while (!small.empty() && !large.empty()) {
+        const int s = small.front(); small.pop();
+        const int l = large.front(); large.pop();
+        alias[s] = l;
+        scaled[l] -= (1.0f - scaled[s]);
+        (scaled[l] < 1.0f ? small : large).push(l);
+    }
+    while (!small.empty()) { scaled[small.front()] = 1.0f; small.pop(); }
+    while (!large.empty()) { scaled[large.front()] = 1.0f; large.pop(); }
+    std::vector<AliasBin> b(n);
+    for (unsigned i = 0; i < n; ++i) b[i] = {scaled[i], prob[i], alias[i]};
+    return b;
+}
+
+float fit6(const float *M, float t, int i, int stride) {  // Sky.cu:19-47
+    return (std::pow(1.0f - t, 5.0f) * M[i] + 5.0f * std::pow(1.0f - t, 4.0f) * t * M[i + stride] +
+            10.0f * std::pow(1.0f - t, 3.0f) * std::pow(t, 2.0f) * M[i + 2 * stride] +
+            10.0f * std::pow(1.0f - t, 2.0f) * std::pow(t, 3.0f) * M[i + 3 * stride] +
+            5.0f * (1.0f - t) * std::pow(t, 4.0f) * M[i + 4 * stride] + std::pow(t, 5.0f) * M[i + 5 * stride]);
+}
+
+V3 q_rotate3(V3 axis, float angle, V3 v) {  // rotate3f (LinearMath.h:1368)
+    const Qt q{normalized_c(axis) * std::sin(angle / 2), std::cos(angle / 2)};
+    return q_mul(q_mul(q, {v, 0.f}), q_conj(q)).v;
+}
+
+void fill_world(vxpt_ctx *c, WorldDev &w) {
+    w.ids = c->voxels.p;
+    w.occ = c->occ.p;
+    w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
+    w.wx = c->cx * 32; w.wy = c->cy * 32; w.wz = c->cz * 32;
+    w.bx = w.wx / 4; w.by = w.wy / 4; w.bz = w.wz / 4;
+}
+
+void fill_sky(vxpt_ctx *c, SkyDev &s) {
+    s.sky = c->sky.p;
+    s.sun = c->sun.p;
+    s.skyAlias = c->skyAlias.p;
+    s.sunAlias = c->sunAlias.p;
+    s.sunDir = c->sunDir;
+    s.skyW = 1024; s.skyH = 512; s.sunW = 32; s.sunH = 32;
+    s.sunCosMax = std::cos(0.51f * kPi / 180.0f / 2.0f);
+}
+
+void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int parity) {
+    a.W = c->W; a.H = c->H;
+    a.cam = c->cam; a.prevCam = c->prevCam;
+    a.p = {p->max_accumulated_frame_num, p->max_fast_accumulated_frame_num, p->phi_luminance,
+           p->lobe_angle_fraction, p->roughness_fraction, p->depth_threshold, p->disocclusion_threshold,
+           p->disocclusion_threshold_alternate, p->denoising_range, p->enable_temporal_accumulation,
+           p->enable_history_fix, p->enable_history_clamping, p->enable_spatial_filtering,
+           p->enable_firefly_filter, p->atrous_iteration_num};
+    const GSlot &g = c->gb[c->last];
+    a.illum = c->denoiseInputIsAccum ? c->accum : c->illum;
+    a.normalRough = g.normalRough;
+    a.albedo = g.albedo;
+    a.motion = c->motion;
+    a.depth = g.depth;
+    a.material = g.material;
+    a.prevNormalRough = c->dnPrevNormalRough;
+    a.prevDepth = c->dnPrevDepth;
+    a.reservoir = c->res + (size_t)parity * c->W * c->H;
+    a.ping = c->ping; a.pong = c->pong; a.prevIllum = c->prevIllum; a.prevFast = c->prevFast;
+    a.output = c->output;
+    a.histLen = c->histLen; a.prevHistLen = c->prevHistLen;
+    a.ffCount = c->ffCount; a.ffIndex = c->ffIndex; a.ffColor = c->ffColor; a.ffRes = c->ffRes;
+}
+
+const vxpt_denoise_params &default_denoise() {
+    static vxpt_denoise_params d{30.f, 6.f, 2.f, 0.5f, 0.15f, 0.003f, 0.01f, 0.05f, 500000.f, 1, 1, 1, 1, 1, 1};
+    return d;
+}
+
+// pointer + byte size of a logical buffer
+bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, void **mirror) {
+    const size_t n = (size_t)c->W * c->H;
+    // current = the slot the last trace wrote; previous = the other ring slot,
+    // which the next trace reads as its history (ReSTIR prev surface) and then overwrites
+    const GSlot &g = c->gb[c->last];
+    const GSlot &gp = c->gb[1 - c->last];
+    *mirror = nullptr;
+    switch (which) {
+        case VXPT_BUF_ILLUM: p = c->denoiseInputIsAccum ? c->accum : c->illum; bytes = n * 16; return true;
+        case VXPT_BUF_DEPTH: p = g.depth; bytes = n * 4; return true;
+        case VXPT_BUF_NORMAL_ROUGH: p = g.normalRough; bytes = n * 16; return true;
+        case VXPT_BUF_GEO_NORMAL_THIN: p = g.geoNormalThin; bytes = n * 16; return true;
+        case VXPT_BUF_PREV_GEO_NORMAL_THIN: p = gp.geoNormalThin; bytes = n * 16; return true;
+        case VXPT_BUF_ALBEDO: p = g.albedo; bytes = n * 16; return true;
+        case VXPT_BUF_PREV_ALBEDO: p = gp.albedo; bytes = n * 16; return true;
+        case VXPT_BUF_MATERIAL: p = g.material; bytes = n * 4; return true;
+        case VXPT_BUF_MAT_PARAM: p = g.matParam; bytes = n * 16; return true;
+        case VXPT_BUF_PREV_MAT_PARAM: p = gp.matParam; bytes = n * 16; return true;
+        case VXPT_BUF_MOTION: p = c->motion; bytes = n * 16; return true;
+        case VXPT_BUF_PREV_NORMAL_ROUGH:
+            p = c->dnPrevNormalRough; bytes = n * 16; if (forWrite) *mirror = gp.normalRough; return true;
+        case VXPT_BUF_PREV_DEPTH: p = c->dnPrevDepth; bytes = n * 4; if (forWrite) *mirror = gp.depth; return true;
+        case VXPT_BUF_PREV_MATERIAL:
+            p = c->dnPrevMaterial; bytes = n * 4; if (forWrite) *mirror = gp.material; return true;
+        case VXPT_BUF_RESERVOIRS: p = c->res; bytes = 2 * n * sizeof(Reservoir); return true;
+        case VXPT_BUF_PING: p = c->ping; bytes = n * 16; return true;
+        case VXPT_BUF_PONG: p = c->pong; bytes = n * 16; return true;
+        case VXPT_BUF_PREV_ILLUM: p = c->prevIllum; bytes = n * 16; return true;
+        case VXPT_BUF_PREV_FAST: p = c->prevFast; bytes = n * 16; return true;
+        case VXPT_BUF_HIST_LEN: p = c->histLen; bytes = n * 4; return true;
+        case VXPT_BUF_PREV_HIST_LEN: p = c->prevHistLen; bytes = n * 4; return true;
+        case VXPT_BUF_OUTPUT: p = c->output; bytes = n * 16; return true;
+        case VXPT_BUF_SKY: p = c->sky.p; bytes = 1024 * 512 * 16; return c->sky.p != nullptr;
+        case VXPT_BUF_SUN: p = c->sun.p; bytes = 32 * 32 * 16; return c->sun.p != nullptr;
+        case VXPT_BUF_VOXELS: p = c->voxels.p; bytes = (size_t)c->cx * c->cy * c->cz * 32768; return c->voxels.p != nullptr;
+        default: return false;
+    }
+}
+
+int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
+    const int wx = c->cx * 32, wy = c->cy * 32, wz = c->cz * 32;
+    const int bx = wx / 4, by = wy / 4, bz = wz / 4;
+    std::vector<uint32_t> occ(((size_t)bx * by * bz + 31) / 32, 0u);
+    for (int y = 0; y < wy; ++y)
+        for (int z = 0; z < wz; ++z)
+            for (int x = 0; x < wx; ++x) {
+                const int ch = (x >> 5) + c->cx * ((z >> 5) + c->cz * (y >> 5));
+                const uint8_t id = ids[(size_t)ch * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
+                if (id >= 1 && id <= 12) {
+                    const size_t b = (size_t)(x >> 2) + (size_t)bx * ((z >> 2) + (size_t)bz * (y >> 2));
+                    occ[b >> 5] |= 1u << (b & 31);
+                }
+            }
+    return upload_vec(c, c->occ, occ.data(), occ.size());
+}
+
+int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale) {
+    if (!c->voxels.p) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
+    if (!c->skyReady) return fail(c, VXPT_ERR_STATE, "sky not set");
+    TraceArgs a{};
+    fill_world(c, a.world);
+    fill_sky(c, a.sky);
+    a.bn = {c->bnSobol.p, c->bnScramble.p, c->bnRank.p};
+    for (int i = 0; i < 13; ++i) a.mats[i] = c->mats[i];
+    a.cam = c->cam;
+    a.prevCam = c->prevCam;
+    const int next = 1 - c->last;
+    const GSlot &cur = c->gb[next], &prev = c->gb[c->last];
+    a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material};
+    a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material};
+    a.illum = c->illum;
+    a.motion = c->motion;
+    const size_t n = (size_t)c->W * c->H;
+    a.resCur = c->res + (size_t)(((it % 2) + 2) % 2) * n;
+    a.resPrev = c->res + (size_t)((((it + 1) % 2) + 2) % 2) * n;
+    a.accum = accumulate ? c->accum : nullptr;
+    a.accumScale = accumScale;
+    a.accumFirst = accumFirst ? 1 : 0;
+    a.W = c->W; a.H = c->H;
+    a.y0 = c->rowBegin; a.y1 = c->rowEnd;
+    a.iterationIndex = it;
+    a.totalBounceLimit = c->totalBounce;
+    a.diffuseBounceLimit = c->diffuseBounce;
+    a.primaryOnly = (flags & VXPT_TRACE_PRIMARY_ONLY) ? 1 : 0;
+    HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(c, launch_trace(a, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    c->last = next;
+    return 0;
+}
+
+int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) {
+    if (!p) p = &default_denoise();
+    const int used = it > 0 ? it - 1 : 0;
+    DenoiseArgs a{};
+    fill_denoise(c, p, a, used & 1);
+    HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    if (p->enable_firefly_filter) HIPCHK(c, launch_firefly(a, c->stream));
+    if (frameNum == 0) HIPCHK(c, launch_frame0_init(a, c->stream));
+    int fin = 0;  // 0 illum, 1 ping, 2 pong, 3 prevIllum
+    if (p->enable_temporal_accumulation && frameNum > 0) {
+        HIPCHK(c, launch_temporal(a, c->stream));
+        fin = 1;
+        if (p->enable_history_fix) { HIPCHK(c, launch_history_fix(a, c->stream)); fin = 2; }
+        if (p->enable_history_clamping) { HIPCHK(c, launch_history_clamp(a, c->stream)); fin = 3; }
+    }
+    bool outputDone = false;
+    if (p->enable_spatial_filtering) {
+        HIPCHK(c, launch_atrous_smem(a, c->stream));
+        fin = 1;
+        if (p->atrous_iteration_num > 0) {
+            int idx = 1;
+            unsigned step = 1u << idx;
+            const int maxIt = p->atrous_iteration_num * 2;
+            while (idx < maxIt) {
+                HIPCHK(c, launch_atrous(a, a.ping, a.pong, step, (unsigned)it, false, c->stream));
+                ++idx; step = 1u << idx;
+                HIPCHK(c, launch_atrous(a, a.pong, a.ping, step, (unsigned)it, false, c->stream));
+                ++idx; step = 1u << idx;
+            }
+            HIPCHK(c, launch_atrous(a, a.ping, a.pong, step, (unsigned)it, true, c->stream));
+            fin = 2;
+            outputDone = true;
+        }
+    }
+    if (!outputDone) {
+        const float4 *src = fin == 1 ? a.ping : (fin == 2 ? a.pong : (fin == 3 ? a.prevIllum : a.illum));
+        HIPCHK(c, launch_copy_output(a, src, c->stream));
+    }
+    // history copies NormalRough/Depth/Material -> Prev (Denoiser.cu:394-407)
+    const size_t n = (size_t)c->W * c->H;
+    const GSlot &g = c->gb[c->last];
+    HIPCHK(c, hipMemcpyAsync(c->dnPrevNormalRough, g.normalRough, n * 16, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->dnPrevDepth, g.depth, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->dnPrevMaterial, g.material, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+    return 0;
+}
+
+}  // namespace
+
+// =====================================================================  C ABI
+extern "C" {
+
+const char *vxpt_last_error(const vxpt_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
+    if (!cfg || !out) return VXPT_ERR_ARG;
+    *out = nullptr;
+    if (cfg->width <= 0 || cfg->height <= 0 || cfg->width % 8 || cfg->height % 8) return VXPT_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return VXPT_ERR_NODEV;
+    auto *c = new vxpt_ctx();
+    c->W = cfg->width; c->H = cfg->height; c->dev = cfg->device;
+    c->rowBegin = cfg->row_begin; c->rowEnd = cfg->row_end;
+    if (c->rowEnd <= c->rowBegin) { c->rowBegin = 0; c->rowEnd = c->H; }
+    if (cfg->total_bounce_limit > 0) c->totalBounce = cfg->total_bounce_limit;
+    if (cfg->diffuse_bounce_limit > 0) c->diffuseBounce = cfg->diffuse_bounce_limit;
+    c->dataDir = cfg->data_dir ? cfg->data_dir : "data";
+    *out = c;
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto &e : c->ev) HIPCHK(c, hipEventCreate(&e));
+    const size_t n = (size_t)c->W * c->H;
+    for (auto &g : c->gb) {
+        if (dalloc(c, g.normalRough, n) || dalloc(c, g.geoNormalThin, n) || dalloc(c, g.albedo, n) ||
+            dalloc(c, g.matParam, n) || dalloc(c, g.depth, n) || dalloc(c, g.material, n))
+            return VXPT_ERR_HIP;
+    }
+    if (dalloc(c, c->illum, n) || dalloc(c, c->accum, n) || dalloc(c, c->motion, n) || dalloc(c, c->res, 2 * n) ||
+        dalloc(c, c->ping, n) || dalloc(c, c->pong, n) || dalloc(c, c->prevIllum, n) || dalloc(c, c->prevFast, n) ||
+        dalloc(c, c->output, n) || dalloc(c, c->histLen, n) || dalloc(c, c->prevHistLen, n) ||
+        dalloc(c, c->dnPrevNormalRough, n) || dalloc(c, c->dnPrevDepth, n) || dalloc(c, c->dnPrevMaterial, n) ||
+        dalloc(c, c->ffCount, 4) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n))
+        return VXPT_ERR_HIP;
+    // tables
+    const std::string t = c->dataDir + "/tables/";
+    std::vector<uint8_t> so, sc, rk, f0, f1, f2, f3;
+    if (!read_file(t + "bn_sobol.u8", so) || !read_file(t + "bn_scramble.u8", sc) || !read_file(t + "bn_rank.u8", rk) ||
+        !read_file(t + "sky_datasets.f32", f0) || !read_file(t + "sky_datasets_rad.f32", f1) ||
+        !read_file(t + "solar_datasets.f32", f2) || !read_file(t + "limb_darkening.f32", f3) ||
+        so.size() != 65536 || sc.size() != 131072 || rk.size() != 131072 || f0.size() != 2160 || f1.size() != 240 ||
+        f2.size() != 7200 || f3.size() != 240)
+        return fail(c, VXPT_ERR_IO, "cannot read tables from " + t);
+    if (upload_vec(c, c->bnSobol, so.data(), so.size()) || upload_vec(c, c->bnScramble, sc.data(), sc.size()) ||
+        upload_vec(c, c->bnRank, rk.data(), rk.size()) ||
+        upload_vec(c, c->solar, (const float *)f2.data(), 1800) || upload_vec(c, c->limb, (const float *)f3.data(), 60))
+        return VXPT_ERR_HIP;
+    std::memcpy(c->tabSky, f0.data(), sizeof(c->tabSky));
+    std::memcpy(c->tabSkyRad, f1.data(), sizeof(c->tabSkyRad));
+    // default material table: terrain materials of data/assets/materials.yaml
+    const float rough[13] = {0.5f, 0.8f, 0.9f, 0.85f, 0.9f, 0.8f, 0.7f, 0.85f, 0.6f, 0.7f, 0.65f, 0.75f, 0.75f};
+    for (int b = 1; b <= 12; ++b) c->mats[b] = MatDev{{1.f, 1.f, 1.f}, rough[b], 0.0f, 0, b - 1, 0};
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+void vxpt_destroy(vxpt_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->dev);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (void *p : c->allocs) hipFree(p);
+    for (auto &e : c->ev)
+        if (e) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int vxpt_load_settings(vxpt_ctx *c) {
+    if (!c) return VXPT_ERR_ARG;
+    // global_settings.yaml: denoising + sky sections (GlobalSettings.cpp:69-492)
+    std::ifstream f(c->dataDir + "/settings/global_settings.yaml");
+    if (!f) return fail(c, VXPT_ERR_IO, "missing settings/global_settings.yaml");
+    vxpt_denoise_params d = default_denoise();
+    std::string line, section;
+    while (std::getline(f, line)) {
+        const size_t hash = line.find('#');
+        if (hash != std::string::npos) line = line.substr(0, hash);
+        if (trim(line).empty()) continue;
+        const bool indented = line[0] == ' ' || line[0] == '\t';
+        const size_t col = line.find(':');
+        if (col == std::string::npos) continue;
+        const std::string key = trim(line.substr(0, col)), val = trim(line.substr(col + 1));
+        if (!indented) { section = key; continue; }
+        if (section == "denoising") {
+            const float v = (float)std::atof(val.c_str());
+            if (key == "enableTemporalAccumulation") d.enable_temporal_accumulation = as_bool(val);
+            else if (key == "enableHistoryFix") d.enable_history_fix = as_bool(val);
+            else if (key == "enableHistoryClamping") d.enable_history_clamping = as_bool(val);
+            else if (key == "enableSpatialFiltering") d.enable_spatial_filtering = as_bool(val);
+            else if (key == "enableFireflyFilter") d.enable_firefly_filter = as_bool(val);
+            else if (key == "maxAccumulatedFrameNum") d.max_accumulated_frame_num = v;
+            else if (key == "maxFastAccumulatedFrameNum") d.max_fast_accumulated_frame_num = v;
+            else if (key == "phiLuminance") d.phi_luminance = v;
+            else if (key == "lobeAngleFraction") d.lobe_angle_fraction = v;
+            else if (key == "roughnessFraction") d.roughness_fraction = v;
+            else if (key == "depthThreshold") d.depth_threshold = v;
+            else if (key == "atrousIterationNum") d.atrous_iteration_num = (int)v;
+            else if (key == "disocclusionThreshold") d.disocclusion_threshold = v;
+            else if (key == "disocclusionThresholdAlternate") d.disocclusion_threshold_alternate = v;
+            else if (key == "denoisingRange") d.denoising_range = v;
+        } else if (section == "sky") {
+            const float v = (float)std::atof(val.c_str());
+            if (key == "timeOfDay") c->skyParams[0] = v;
+            else if (key == "sunAxisAngle") c->skyParams[1] = v;
+            else if (key == "sunAxisRotate") c->skyParams[2] = v;
+            else if (key == "skyBrightness") c->skyParams[3] = v;
+        }
+    }
+    c->yamlDenoise = d;
+    // materials.yaml (order == material index, MaterialManager.cpp:84-97) + blocks.yaml
+    std::ifstream fm(c->dataDir + "/assets/materials.yaml");
+    if (!fm) return fail(c, VXPT_ERR_IO, "missing assets/materials.yaml");
+    std::vector<std::string> ids;
+    std::vector<std::map<std::string, std::string>> props;
+    while (std::getline(fm, line)) {
+        const std::string tl = trim(line);
+        if (tl.rfind("- id:", 0) == 0) { ids.push_back(trim(tl.substr(5))); props.emplace_back(); }
+        else if (tl.rfind("properties:", 0) == 0 && !props.empty()) props.back() = parse_flow_map(tl);
+    }
+    std::ifstream fb(c->dataDir + "/assets/blocks.yaml");
+    if (!fb) return fail(c, VXPT_ERR_IO, "missing assets/blocks.yaml");
+    while (std::getline(fb, line)) {
+        const std::string tl = trim(line);
+        if (tl.rfind("- {", 0) != 0) continue;
+        auto m = parse_flow_map(tl);
+        const int bid = std::atoi(m["id"].c_str());
+        if (bid < 1 || bid > 12) continue;
+        const auto it = std::find(ids.begin(), ids.end(), m["material"]);
+        if (it == ids.end()) continue;
+        const int mi = (int)(it - ids.begin());
+        auto &p = props[mi];
+        MatDev md{{1.f, 1.f, 1.f}, 0.5f, 0.0f, 0, mi, 0};  // MaterialProperties defaults (MaterialDefinition.h:18-28)
+        if (p.count("roughness")) md.roughness = (float)std::atof(p["roughness"].c_str());
+        if (p.count("metallic")) md.metallic = std::atof(p["metallic"].c_str()) != 0.0;
+        if (p.count("translucency")) md.translucency = (float)std::atof(p["translucency"].c_str());
+        if (p.count("is_thinfilm")) md.thin = as_bool(p["is_thinfilm"]);
+        if (p.count("albedo")) {
+            auto v = parse_list(p["albedo"]);
+            if (v.size() == 3) { md.albedo[0] = v[0]; md.albedo[1] = v[1]; md.albedo[2] = v[2]; }
+        }
+        c->mats[bid] = md;
+    }
+    return VXPT_OK;
+}
+
+int vxpt_load_scene_camera(vxpt_ctx *c, const char *path, vxpt_camera *out) {
+    if (!c || !out) return VXPT_ERR_ARG;
+    std::string p = path ? path : (c->dataDir + "/scene/scene_export.yaml");
+    std::ifstream f(p);
+    if (!f) return fail(c, VXPT_ERR_IO, "cannot open " + p);
+    std::string line, section;
+    vxpt_camera cam{{35.6184f, 11.8733f, 42.0387f}, {-0.321564f, -0.0129988f, -0.946799f}, 90.0f};
+    while (std::getline(f, line)) {
+        const size_t hash = line.find('#');
+        if (hash != std::string::npos) line = line.substr(0, hash);
+        if (trim(line).empty()) continue;
+        const size_t col = line.find(':');
+        if (col == std::string::npos) continue;
+        const std::string key = trim(line.substr(0, col)), val = trim(line.substr(col + 1));
+        if (line[0] != ' ') { section = key; continue; }
+        if (section != "camera") continue;
+        auto v = parse_list(val);
+        if (key == "position" && v.size() == 3) std::copy(v.begin(), v.end(), cam.pos);
+        else if (key == "direction" && v.size() == 3) std::copy(v.begin(), v.end(), cam.dir);
+        else if (key == "fov" && v.size() == 1) cam.fov_deg = v[0];
+    }
+    *out = cam;
+    return VXPT_OK;
+}
+
+int vxpt_generate_terrain(vxpt_ctx *c, int cxn, int cyn, int czn, float heightScale, float freqDen, int flags) {
+    if (!c || cxn <= 0 || cyn <= 0 || czn <= 0) return VXPT_ERR_ARG;
+    const bool keepBalls = (flags & VXPT_TERRAIN_SHADER_BALLS) != 0, globalY = (flags & VXPT_TERRAIN_GLOBAL_Y) != 0;
+    std::vector<uint8_t> ids((size_t)cxn * cyn * czn * 32768, 0);
+    const Perlin noise(124);
+    const float freq = 1.0f / freqDen, width = heightScale;
+    for (int ch = 0; ch < cxn * cyn * czn; ++ch) {
+        const int gox = (ch % cxn) * 32, goz = ((ch / cxn) % czn) * 32, goy = globalY ? (ch / (cxn * czn)) * 32 : 0;
+        float hmap[32][32];
+        for (int z = 0; z < 32; ++z)
+            for (int x = 0; x < 32; ++x) {
+                const float n = noise.octave01((float)(gox + x) * freq, (float)(goz + z) * freq, 4);
+                float h = std::fmaf(n, 1.4f, -0.7f);  // nvcc --fmad=true contraction of n*1.4f-0.7f
+                h = std::fmax(0.1f, (h + 0.25f) * width);
+                hmap[z][x] = std::fmin(h, width * 0.9f);
+            }
+        for (int y = 0; y < 32; ++y)
+            for (int z = 0; z < 32; ++z)
+                for (int x = 0; x < 32; ++x) {
+                    const float h = hmap[z][x];
+                    uint8_t id = 0;
+                    const float yy = (float)(goy + y);
+                    if (yy < h) {
+                        const float d = h - yy;
+                        if (h < width * (0.25f + 0.05f)) id = d < 3.5f ? 1 : 7;
+                        else if (h < width * (0.25f + 0.6f) && h > width * (0.25f + 0.3f)) id = d < 5.5f ? 3 : 7;
+                        else id = d < 1.5f ? 2 : (d < 5.5f ? 3 : 7);
+                    }
+                    const int gx = gox + x, gz = goz + z;
+                    if (keepBalls && y == 7 && gz == 43 && gx >= 30 && gx <= 39) {
+                        static const uint8_t ball[10] = {17, 21, 22, 23, 24, 25, 26, 27, 28, 29};
+                        id = ball[gx - 30];
+                    }
+                    ids[(size_t)ch * 32768 + x + 32 * (z + 32 * y)] = id;
+                }
+    }
+    return vxpt_upload_voxels(c, ids.data(), cxn, cyn, czn);
+}
+
+int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int czn) {
+    if (!c || !ids || cxn <= 0 || cyn <= 0 || czn <= 0) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    c->cx = cxn; c->cy = cyn; c->cz = czn;
+    const size_t n = (size_t)cxn * cyn * czn * 32768;
+    if (int r = upload_vec(c, c->voxels, ids, n)) return r;
+    if (int r = build_occupancy(c, ids)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+int vxpt_upload_materials(vxpt_ctx *c, const vxpt_material *m, int n) {
+    if (!c || !m || n < 1 || n > 12) return VXPT_ERR_ARG;
+    for (int b = 1; b <= n; ++b) {
+        const vxpt_material &s = m[b - 1];
+        c->mats[b] = MatDev{{s.albedo[0], s.albedo[1], s.albedo[2]}, s.roughness, s.translucency, s.metallic,
+                            s.material_id, s.thinfilm};
+    }
+    return VXPT_OK;
+}
+
+int vxpt_set_sky(vxpt_ctx *c, float tod, float axisAngle, float axisRotate, float brightness) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    // sun direction (Sky.cu:363-368)
+    V3 axis(1.0f, std::cos(axisAngle * kPiOver180), std::sin(axisAngle * kPiOver180));
+    axis *= V3(std::sin(axisRotate * kPiOver180), 1.0f, std::cos(axisRotate * kPiOver180));
+    axis = normalize(axis);
+    const float angle = std::fmod(tod * kPi, kTwoPi);
+    c->sunDir = normalized_c(q_rotate3(axis, angle, cross(V3(0, 1, 0), axis)));
+    // updateSkyState (Sky.cu:57-83), CPU fit
+    float cfg[90], rad[10];
+    const float elevation = (kPi / 2.0f) - std::acos(c->sunDir.y);
+    const float se = std::pow(elevation / (kPi / 2.0f), (1.0f / 3.0f));
+    for (int ch = 0; ch < 10; ++ch) {
+        for (int i = 0; i < 9; ++i) cfg[ch * 9 + i] = fit6(c->tabSky + ch * 54, se, i, 9);
+        rad[ch] = fit6(c->tabSkyRad + ch * 6, se, 0, 1);
+    }
+    const int sw = 1024, sh = 512, uw = 32, uh = 32;
+    if (!c->sky.p) {
+        if (dalloc(c, c->sky.p, (size_t)sw * sh) || dalloc(c, c->sun.p, (size_t)uw * uh) ||
+            dalloc(c, c->skyPdf.p, (size_t)sw * sh) || dalloc(c, c->sunPdf.p, (size_t)uw * uh))
+            return VXPT_ERR_HIP;
+        c->sky.n = (size_t)sw * sh; c->sun.n = (size_t)uw * uh;
+    }
+    HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+    HIPCHK(c, launch_sky(cfg, rad, c->solar.p, c->limb.p, c->sunDir, brightness, c->sky.p, c->sun.p, c->skyPdf.p,
+                         c->sunPdf.p, sw, sh, uw, uh, c->stream));
+    std::vector<float> pdf((size_t)sw * sh), spdf((size_t)uw * uh);
+    HIPCHK(c, hipMemcpyAsync(pdf.data() + (size_t)sw * (sh / 2), c->skyPdf.p + (size_t)sw * (sh / 2),
+                             (size_t)sw * (sh / 2) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double upper = 0.0;
+    for (size_t i = (size_t)sw * (sh / 2); i < (size_t)sw * sh; ++i) upper += (double)pdf[i];
+    HIPCHK(c, launch_sky_lower(c->sky.p, c->skyPdf.p, sw, sh, (float)upper, c->stream));
+    HIPCHK(c, hipMemcpyAsync(pdf.data(), c->skyPdf.p, pdf.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(spdf.data(), c->sunPdf.p, spdf.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float s1, s2;
+    c->hSkyAlias = build_alias(pdf, s1);
+    const std::vector<AliasBin> sunA = build_alias(spdf, s2);
+    if (upload_vec(c, c->skyAlias, c->hSkyAlias.data(), c->hSkyAlias.size()) ||
+        upload_vec(c, c->sunAlias, sunA.data(), sunA.size()))
+        return VXPT_ERR_HIP;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[4], c->ev[5]);
+    c->timing.sky_ms = ms;
+    c->skyReady = true;
+    return VXPT_OK;
+}
+
+int vxpt_set_camera(vxpt_ctx *c, const vxpt_camera *cur, const vxpt_camera *prev) {
+    if (!c || !cur) return VXPT_ERR_ARG;
+    c->cam = make_camera(c->W, c->H, *cur, &c->camYaw, &c->camPitch);
+    c->prevCam = make_camera(c->W, c->H, prev ? *prev : *cur, nullptr, nullptr);
+    return VXPT_OK;
+}
+
+int vxpt_get_camera(vxpt_ctx *c, int which, float *o) {
+    if (!c || !o) return VXPT_ERR_ARG;
+    const CamDev &k = which ? c->prevCam : c->cam;
+    const float v[32] = {k.pos.x, k.pos.y, k.pos.z, k.dir.x, k.dir.y, k.dir.z,
+                         k.uvToWorld.m00, k.uvToWorld.m10, k.uvToWorld.m20, k.uvToWorld.m01, k.uvToWorld.m11,
+                         k.uvToWorld.m21, k.uvToWorld.m02, k.uvToWorld.m12, k.uvToWorld.m22,
+                         k.worldToUv.m00, k.worldToUv.m10, k.worldToUv.m20, k.worldToUv.m01, k.worldToUv.m11,
+                         k.worldToUv.m21, k.worldToUv.m02, k.worldToUv.m12, k.worldToUv.m22,
+                         k.res.x, k.res.y, k.invRes.x, k.invRes.y, k.tanHalfFov.x, k.tanHalfFov.y, c->camYaw, c->camPitch};
+    std::memcpy(o, v, sizeof(v));
+    return VXPT_OK;
+}
+
+int vxpt_trace(vxpt_ctx *c, int32_t it, uint32_t flags) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    c->denoiseInputIsAccum = false;
+    int r = do_trace(c, it, flags, false, false, 1.0f);
+    if (r) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+    c->timing.trace_ms = ms;
+    return VXPT_OK;
+}
+
+int vxpt_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNum, int32_t it) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    int r = do_denoise(c, p, frameNum, it);
+    if (r) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+    c->timing.denoise_ms = ms;
+    return VXPT_OK;
+}
+
+int vxpt_denoise_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int arg2) {
+    if (!c) return VXPT_ERR_ARG;
+    if (!p) p = &default_denoise();
+    HIPCHK(c, hipSetDevice(c->dev));
+    DenoiseArgs a{};
+    fill_denoise(c, p, a, pass == 0 ? (arg & 1) : 0);
+    switch (pass) {
+        case 0: HIPCHK(c, launch_firefly(a, c->stream)); break;
+        case 2: HIPCHK(c, launch_temporal(a, c->stream)); break;
+        case 3: HIPCHK(c, launch_history_fix(a, c->stream)); break;
+        case 4: HIPCHK(c, launch_history_clamp(a, c->stream)); break;
+        case 5: HIPCHK(c, launch_atrous_smem(a, c->stream)); break;
+        case 6: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
+        case 7: HIPCHK(c, launch_atrous(a, a.pong, a.ping, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
+        case 10: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, true, c->stream)); break;
+        default: return fail(c, VXPT_ERR_ARG, "unknown pass");
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNum, int32_t spp) {
+    if (!c || spp < 1) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    const int it0 = frameNum * spp;
+    HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+    for (int s = 0; s < spp; ++s) {
+        int r = do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp);
+        if (r) return r;
+        if (s == 0) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    c->denoiseInputIsAccum = spp > 1;
+    int r = do_denoise(c, p, frameNum, it0 + spp);
+    if (r) return r;
+    HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0, d = 0, f = 0;
+    hipEventElapsedTime(&t, c->ev[6], c->ev[1]);
+    hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
+    c->timing.trace_ms = t;
+    c->timing.denoise_ms = d;
+    c->timing.frame_ms = f;
+    return VXPT_OK;
+}
+
+int vxpt_exchange_halo(vxpt_ctx *c, uint32_t, int) { return c ? VXPT_OK : VXPT_ERR_ARG; }
+
+int vxpt_readback(vxpt_ctx *c, int which, void *host, size_t bytes) {
+    if (!c || !host) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    void *p, *mirror;
+    size_t n;
+    if (!buffer_ptr(c, which, p, n, false, &mirror)) return fail(c, VXPT_ERR_ARG, "unknown buffer");
+    if (bytes < n) return fail(c, VXPT_ERR_ARG, "host buffer too small");
+    HIPCHK(c, hipMemcpyAsync(host, p, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+int vxpt_upload(vxpt_ctx *c, int which, const void *host, size_t bytes) {
+    if (!c || !host) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    void *p, *mirror;
+    size_t n;
+    if (!buffer_ptr(c, which, p, n, true, &mirror) || which >= 32) return fail(c, VXPT_ERR_ARG, "unknown buffer");
+    if (bytes < n) return fail(c, VXPT_ERR_ARG, "host buffer too small");
+    HIPCHK(c, hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
+    if (mirror) HIPCHK(c, hipMemcpyAsync(mirror, host, n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+int vxpt_get_sky_alias(vxpt_ctx *c, float *q, float *p, int32_t *alias, float *sunDir) {
+    if (!c || !c->skyReady) return VXPT_ERR_STATE;
+    for (size_t i = 0; i < c->hSkyAlias.size(); ++i) {
+        if (q) q[i] = c->hSkyAlias[i].q;
+        if (p) p[i] = c->hSkyAlias[i].p;
+        if (alias) alias[i] = c->hSkyAlias[i].alias;
+    }
+    if (sunDir) { sunDir[0] = c->sunDir.x; sunDir[1] = c->sunDir.y; sunDir[2] = c->sunDir.z; }
+    return VXPT_OK;
+}
+
+int vxpt_timings(vxpt_ctx *c, vxpt_timing *out) {
+    if (!c || !out) return VXPT_ERR_ARG;
+    *out = c->timing;
+    return VXPT_OK;
+}
+
+int vxpt_sync(vxpt_ctx *c) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+void *vxpt_stream(vxpt_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+}  // extern "C"
+
+// probe kernel lives in trace.hip
+namespace vx {
+hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, float *t, int mode, hipStream_t st);
+}
+
+extern "C" int vxpt_probe_rays(vxpt_ctx *c, int n, const float *rays, int32_t *out6, float *t, int mode) {
+    if (!c || n <= 0 || !rays || !out6 || !t) return VXPT_ERR_ARG;
+    if (!c->voxels.p) return fail(c, VXPT_ERR_STATE, "no voxels");
+    HIPCHK(c, hipSetDevice(c->dev));
+    float *dr;
+    int *dout;
+    float *dt;
+    HIPCHK(c, hipMalloc(&dr, (size_t)n * 8 * 4));
+    HIPCHK(c, hipMalloc(&dout, (size_t)n * 6 * 4));
+    HIPCHK(c, hipMalloc(&dt, (size_t)n * 4));
+    HIPCHK(c, hipMemcpyAsync(dr, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    WorldDev w;
+    fill_world(c, w);
+    HIPCHK(c, launch_probe(w, n, dr, dout, dt, mode, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out6, dout, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(t, dt, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(dr);
+    hipFree(dout);
+    hipFree(dt);
+    return VXPT_OK;
+}

@@ -1,0 +1,273 @@
+"""vxpt -- Python host mirror of the reference's offline render interface.
+
+The product is libvxpt.so (HIP kernels for gfx950 + C++ host runtime, C ABI in
+include/vxpt.h).  This module only binds that ABI with ctypes and mirrors the
+reference's OfflineBackend / mainOffline call order
+(renderer/core/OfflineBackend.cpp:46-89, mainOffline.cpp:142-251) so host
+programs and tests read like the reference's own driver.  It never computes
+pixels itself: if libvxpt.so is missing or cannot reach a GPU every entry
+point raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_HERE, "libvxpt.so")
+DATA_DIR = os.path.join(REPO, "data")
+
+# logical buffers (include/vxpt.h enum vxpt_buffer)
+BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERIAL=5, MAT_PARAM=6, MOTION=7,
+           PREV_NORMAL_ROUGH=8, PREV_GEO_NORMAL_THIN=9, PREV_ALBEDO=10, PREV_MAT_PARAM=11, PREV_DEPTH=12,
+           PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
+           PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34)
+FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
+RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
+                            ("M", "<f4")])
+TRACE_PRIMARY_ONLY = 1
+
+
+class VxptError(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("row_begin", ctypes.c_int32), ("row_end", ctypes.c_int32),
+                ("total_bounce_limit", ctypes.c_int32), ("diffuse_bounce_limit", ctypes.c_int32),
+                ("data_dir", ctypes.c_char_p)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_float * 3), ("dir", ctypes.c_float * 3), ("fov_deg", ctypes.c_float)]
+
+
+class Material(ctypes.Structure):
+    _fields_ = [("albedo", ctypes.c_float * 3), ("roughness", ctypes.c_float), ("translucency", ctypes.c_float),
+                ("metallic", ctypes.c_int32), ("material_id", ctypes.c_int32), ("thinfilm", ctypes.c_int32)]
+
+
+class DenoiseParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in (
+        "max_accumulated_frame_num", "max_fast_accumulated_frame_num", "phi_luminance", "lobe_angle_fraction",
+        "roughness_fraction", "depth_threshold", "disocclusion_threshold", "disocclusion_threshold_alternate",
+        "denoising_range")] + [(n, ctypes.c_int32) for n in (
+            "enable_temporal_accumulation", "enable_history_fix", "enable_history_clamping",
+            "enable_spatial_filtering", "enable_firefly_filter", "atrous_iteration_num")]
+
+    @classmethod
+    def defaults(cls):
+        """global_settings.yaml denoising section (atrousIterationNum: 1)."""
+        return cls(30.0, 6.0, 2.0, 0.5, 0.15, 0.003, 0.01, 0.05, 500000.0, 1, 1, 1, 1, 1, 1)
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("trace_ms", ctypes.c_float), ("denoise_ms", ctypes.c_float), ("sky_ms", ctypes.c_float),
+                ("frame_ms", ctypes.c_float)]
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libvxpt.so; raises (no fallback) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise VxptError("libvxpt.so not built (%s); run __graft_entry__.build()" % path)
+    lib = ctypes.CDLL(path)
+    P, I, F, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint32
+    sigs = {
+        "vxpt_create": (I, [ctypes.POINTER(Config), ctypes.POINTER(P)]),
+        "vxpt_destroy": (None, [P]),
+        "vxpt_last_error": (ctypes.c_char_p, [P]),
+        "vxpt_load_settings": (I, [P]),
+        "vxpt_load_scene_camera": (I, [P, ctypes.c_char_p, ctypes.POINTER(Camera)]),
+        "vxpt_generate_terrain": (I, [P, I, I, I, F, F, I]),
+        "vxpt_upload_voxels": (I, [P, P, I, I, I]),
+        "vxpt_upload_materials": (I, [P, ctypes.POINTER(Material), I]),
+        "vxpt_set_sky": (I, [P, F, F, F, F]),
+        "vxpt_set_camera": (I, [P, ctypes.POINTER(Camera), ctypes.POINTER(Camera)]),
+        "vxpt_get_camera": (I, [P, I, P]),
+        "vxpt_trace": (I, [P, ctypes.c_int32, U32]),
+        "vxpt_denoise": (I, [P, ctypes.POINTER(DenoiseParams), ctypes.c_int32, ctypes.c_int32]),
+        "vxpt_denoise_pass": (I, [P, ctypes.POINTER(DenoiseParams), I, I, I]),
+        "vxpt_render_frame": (I, [P, ctypes.POINTER(DenoiseParams), ctypes.c_int32, ctypes.c_int32]),
+        "vxpt_exchange_halo": (I, [P, U32, I]),
+        "vxpt_readback": (I, [P, I, P, ctypes.c_size_t]),
+        "vxpt_upload": (I, [P, I, P, ctypes.c_size_t]),
+        "vxpt_get_sky_alias": (I, [P, P, P, P, P]),
+        "vxpt_timings": (I, [P, ctypes.POINTER(Timing)]),
+        "vxpt_sync": (I, [P]),
+        "vxpt_stream": (P, [P]),
+        "vxpt_probe_rays": (I, [P, I, P, P, P, I]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Renderer:
+    """One GPU's share of the offline renderer (OfflineBackend + OptixRenderer +
+    Denoiser + SkyModel singletons of the reference, as one context)."""
+
+    def __init__(self, width, height, device=0, rows=None, bounces=(3, 1), data_dir=DATA_DIR):
+        self.lib = load_library()
+        self.W, self.H = int(width), int(height)
+        r0, r1 = rows if rows else (0, 0)
+        cfg = Config(self.W, self.H, device, r0, r1, bounces[0], bounces[1], data_dir.encode())
+        ctx = ctypes.c_void_p()
+        rc = self.lib.vxpt_create(ctypes.byref(cfg), ctypes.byref(ctx))
+        self.ctx = ctx
+        if rc != 0:
+            msg = self.lib.vxpt_last_error(ctx).decode() if ctx.value else ""
+            if ctx.value:
+                self.lib.vxpt_destroy(ctx)
+            self.ctx = None
+            raise VxptError("vxpt_create failed (%d) %s" % (rc, msg))
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise VxptError("%s failed (%d): %s" % (what, rc, self.lib.vxpt_last_error(self.ctx).decode()))
+
+    def close(self):
+        if self.ctx:
+            self.lib.vxpt_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- scene set-up (mainOffline.cpp:142-251) ---
+    def load_settings(self):
+        self._chk(self.lib.vxpt_load_settings(self.ctx), "vxpt_load_settings")
+
+    def scene_camera(self, path=None):
+        cam = Camera()
+        self._chk(self.lib.vxpt_load_scene_camera(self.ctx, path.encode() if path else None, ctypes.byref(cam)),
+                  "vxpt_load_scene_camera")
+        return cam
+
+    def generate_terrain(self, chunks=(2, 1, 2), height_scale=32.0, freq_den=None, keep_shader_balls=False,
+                         global_y=False):
+        if freq_den is None:
+            freq_den = 32.0 * chunks[0]
+        flags = (1 if keep_shader_balls else 0) | (2 if global_y else 0)
+        self._chk(self.lib.vxpt_generate_terrain(self.ctx, chunks[0], chunks[1], chunks[2], float(height_scale),
+                                                 float(freq_den), flags), "vxpt_generate_terrain")
+        self.chunks = tuple(chunks)
+
+    def upload_voxels(self, ids, chunks):
+        ids = np.ascontiguousarray(ids, dtype=np.uint8)
+        self._chk(self.lib.vxpt_upload_voxels(self.ctx, _ptr(ids), chunks[0], chunks[1], chunks[2]),
+                  "vxpt_upload_voxels")
+        self.chunks = tuple(chunks)
+
+    def set_sky(self, time_of_day=0.25, axis_angle=45.0, axis_rotate=0.0, brightness=1.0):
+        self._chk(self.lib.vxpt_set_sky(self.ctx, time_of_day, axis_angle, axis_rotate, brightness), "vxpt_set_sky")
+
+    def set_camera(self, pos, direction, fov=90.0, prev=None):
+        cur = Camera((ctypes.c_float * 3)(*pos), (ctypes.c_float * 3)(*direction), fov)
+        pv = None
+        if prev is not None:
+            pv = ctypes.byref(Camera((ctypes.c_float * 3)(*prev[0]), (ctypes.c_float * 3)(*prev[1]), prev[2]))
+        self._chk(self.lib.vxpt_set_camera(self.ctx, ctypes.byref(cur), pv), "vxpt_set_camera")
+
+    def camera_info(self, which=0):
+        out = np.zeros(32, np.float32)
+        self._chk(self.lib.vxpt_get_camera(self.ctx, which, _ptr(out)), "vxpt_get_camera")
+        return out
+
+    # --- frame (OfflineBackend::renderFrame) ---
+    def trace(self, iteration_index, primary_only=False):
+        self._chk(self.lib.vxpt_trace(self.ctx, iteration_index, TRACE_PRIMARY_ONLY if primary_only else 0),
+                  "vxpt_trace")
+
+    def denoise(self, frame_num, iteration_index, params=None):
+        p = params or DenoiseParams.defaults()
+        self._chk(self.lib.vxpt_denoise(self.ctx, ctypes.byref(p), frame_num, iteration_index), "vxpt_denoise")
+
+    def denoise_pass(self, which, arg=0, arg2=0, params=None):
+        p = params or DenoiseParams.defaults()
+        self._chk(self.lib.vxpt_denoise_pass(self.ctx, ctypes.byref(p), which, arg, arg2), "vxpt_denoise_pass")
+
+    def render_frame(self, frame_num, spp=1, params=None):
+        p = params or DenoiseParams.defaults()
+        self._chk(self.lib.vxpt_render_frame(self.ctx, ctypes.byref(p), frame_num, spp), "vxpt_render_frame")
+
+    def timings(self):
+        t = Timing()
+        self._chk(self.lib.vxpt_timings(self.ctx, ctypes.byref(t)), "vxpt_timings")
+        return dict(trace_ms=t.trace_ms, denoise_ms=t.denoise_ms, sky_ms=t.sky_ms, frame_ms=t.frame_ms)
+
+    def sync(self):
+        self._chk(self.lib.vxpt_sync(self.ctx), "vxpt_sync")
+
+    # --- buffers ---
+    def _shape(self, which):
+        n = self.W * self.H
+        if which == BUF["RESERVOIRS"]:
+            return np.zeros(2 * n, RESERVOIR_DTYPE)
+        if which == BUF["SKY"]:
+            return np.zeros((512, 1024, 4), np.float32)
+        if which == BUF["SUN"]:
+            return np.zeros((32, 32, 4), np.float32)
+        if which == BUF["VOXELS"]:
+            cx, cy, cz = self.chunks
+            return np.zeros(cx * cy * cz * 32768, np.uint8)
+        if which in FLOAT1_BUFS:
+            return np.zeros((self.H, self.W), np.float32)
+        return np.zeros((self.H, self.W, 4), np.float32)
+
+    def read(self, name):
+        which = BUF[name] if isinstance(name, str) else int(name)
+        out = self._shape(which)
+        self._chk(self.lib.vxpt_readback(self.ctx, which, _ptr(out), out.nbytes), "vxpt_readback")
+        return out
+
+    def write(self, name, data):
+        which = BUF[name] if isinstance(name, str) else int(name)
+        ref = self._shape(which)
+        data = np.ascontiguousarray(data, dtype=ref.dtype).reshape(ref.shape)
+        self._chk(self.lib.vxpt_upload(self.ctx, which, _ptr(data), data.nbytes), "vxpt_upload")
+
+    def sky_alias(self):
+        n = 1024 * 512
+        q, p = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        a, sd = np.zeros(n, np.int32), np.zeros(3, np.float32)
+        self._chk(self.lib.vxpt_get_sky_alias(self.ctx, _ptr(q), _ptr(p), _ptr(a), _ptr(sd)), "vxpt_get_sky_alias")
+        return q, p, a, sd
+
+    def probe_rays(self, rays, mode=0):
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        out = np.zeros((n, 6), np.int32)
+        t = np.zeros(n, np.float32)
+        self._chk(self.lib.vxpt_probe_rays(self.ctx, n, _ptr(rays), _ptr(out), _ptr(t), mode), "vxpt_probe_rays")
+        return out, t
+
+
+def render_offline(width, height, frames, spp=1, chunks=(2, 1, 2), height_scale=32.0, device=0):
+    """mainOffline.cpp flow: settings, terrain, camera from the scene yaml, sky, frame loop."""
+    r = Renderer(width, height, device=device)
+    r.load_settings()
+    r.generate_terrain(chunks, height_scale=height_scale)
+    cam = r.scene_camera()
+    r.set_camera(list(cam.pos), list(cam.dir), cam.fov_deg)
+    r.set_sky()
+    for f in range(frames):
+        r.render_frame(f, spp)
+    return r
