@@ -151,6 +151,8 @@ def main():
     else:
         alg_bytes, dur_ms, kern = B_ALG_PER_PX * a.width * a.height, avg_dn, "denoiser chain"
     achieved = alg_bytes / (dur_ms * 1e-3) / 1e9
+    depth = r.read("DEPTH")
+    hit_frac = float((depth < 1e26).mean())  # scene sanity: fraction of primary rays that hit voxels
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, a.cpu_seconds)
@@ -167,7 +169,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "alg_bytes_per_launch": alg_bytes, "avg_duration_ms": round(dur_ms, 4)},
-            "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4),
+            "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4), "primary_hit_frac": round(hit_frac, 4),
+            "trace_mpaths_s": round(paths / (avg_trace * 1e-3) / 1e6, 3),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

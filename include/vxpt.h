@@ -147,6 +147,9 @@ int vxpt_sync(vxpt_ctx *ctx);
 void *vxpt_stream(vxpt_ctx *ctx);
 /* DDA probe: n rays (o3 d3 tmin tmax) -> n x (hit x y z face id) + t; mode 0 closest, 2 occluded */
 int vxpt_probe_rays(vxpt_ctx *ctx, int n, const float *rays, int32_t *out6, float *t, int mode);
+/* blue-noise sampler probe: n queries (pixel x, pixel y, iterationIndex, dimension) ->
+ * BlueNoiseRandGenerator::rand (RandGen.h:21-45) as the trace kernel evaluates it */
+int vxpt_probe_rng(vxpt_ctx *ctx, int n, const int32_t *q4, float *out);
 
 #ifdef __cplusplus
 }

@@ -895,7 +895,18 @@ __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *r
     t[i] = h.t;
 }
 
+__global__ __launch_bounds__(256) void k_probe_rng(BlueNoiseDev bn, int n, const int *q, float *out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out[i] = bn_rand(bn, q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
+}
+
 }  // namespace
+
+hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_probe_rng, dim3((n + 255) / 256), dim3(256), 0, st, bn, n, q, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, float *t, int mode, hipStream_t st) {
     hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, st, w, n, rays, out, t, mode);

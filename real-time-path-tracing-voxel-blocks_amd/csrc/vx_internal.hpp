@@ -85,6 +85,7 @@ hipError_t launch_sky(const float *cfg90, const float *rad10, const float *solar
                       int sunW, int sunH, hipStream_t st);
 hipError_t launch_sky_lower(float4 *sky, float *skyPdf, int skyW, int skyH, float sumUpper, hipStream_t st);
 hipError_t launch_trace(const TraceArgs &a, hipStream_t st);
+hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st);
 
 struct DenoiseParamsDev {
     float maxAcc, maxFast, phiL, lobeAngleFraction, roughnessFraction, depthThreshold;

