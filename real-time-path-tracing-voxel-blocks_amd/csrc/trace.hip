@@ -26,116 +26,185 @@ constexpr float kMinPdf = 1e-5f, kMaxThroughput = 32.0f, kMinLobe = 0.05f;
 // ----------------------------------------------------------------- voxel DDA
 VX_D bool is_cube(int id) { return id >= 1 && id <= 12; }
 
-VX_D int voxel(const WorldDev &w, int x, int y, int z) {
-    const int c = (x >> 5) + w.cx * ((z >> 5) + w.cz * (y >> 5));
-    return w.ids[(size_t)c * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
-}
-VX_D bool brick_occupied(const WorldDev &w, int x, int y, int z) {
-    const int b = (x >> 2) + w.bx * ((z >> 2) + w.bz * (y >> 2));
-    return (w.occ[b >> 5] >> (b & 31)) & 1u;
-}
-
 struct Hit { int hit, x, y, z, face, id; float t; };
 
 VX_D int entry_face(int a, int s) {
     return a == 0 ? (s > 0 ? 2 : 3) : (a == 1 ? (s > 0 ? 1 : 0) : (s > 0 ? 5 : 4));
 }
 
-struct Walk {
-    V3 o;
-    int c[3], st[3];
-    float inv[3], t[3];
-    bool mv[3];
+// The walk keeps every per-axis quantity in named scalars (no runtime-indexed
+// arrays: those would live in scratch on gfx950).
+struct Ray3 {
+    float ox, oy, oz, dx, dy, dz, ix, iy, iz;
+    int sx, sy, sz;
+    bool mx, my, mz;
+};
+struct Cell {
+    int x, y, z;
+    float tx, ty, tz;  // t of the next plane crossing on each axis (INF if the axis does not move)
 };
 
-VX_D float plane_t(const Walk &k, int a, float oa) {
-    if (!k.mv[a]) return INFINITY;
-    const float plane = (float)(k.st[a] > 0 ? k.c[a] + 1 : k.c[a]);
-    return (plane - oa) * k.inv[a];
+// t of the next plane after cell c along one axis; the only formula for plane t,
+// so skipped and stepped walks produce identical values.
+VX_D float next_t(int c, int s, float o, float inv, bool mv) {
+    if (!mv) return INFINITY;
+    return ((float)(s > 0 ? c + 1 : c) - o) * inv;
+}
+// axis order of the reference tie rule (VoxelEngine.cu:1040-1166 strict '<'):
+// smallest t first, ties to Z, then Y, then X
+VX_D int pick3(float tx, float ty, float tz) {
+    if (tx < ty) return tx < tz ? 0 : 2;
+    return ty < tz ? 1 : 2;
+}
+VX_D bool before(float t1, int a1, float t2, int a2) { return t1 < t2 || (t1 == t2 && a1 > a2); }
+
+VX_D int macro_of(const WorldDev &w, int x, int y, int z) { return (x >> 4) + w.mx * ((z >> 4) + w.mz * (y >> 4)); }
+VX_D int brick_bit(int x, int y, int z) { return ((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3)); }
+VX_D int cell_id(const WorldDev &w, int m, uint64_t mw, int x, int y, int z, bool &brickOcc) {
+    const int lb = brick_bit(x, y, z);
+    brickOcc = (mw >> lb) & 1ull;
+    if (!brickOcc) return 0;
+    const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
+    return w.bricks[((size_t)m * 64 + lb) * 64 + lc];
 }
 
-// Start a walk; returns false if the ray never meets the world box.  `entered`
-// reports a start outside the box (the entry crossing is then already taken
-// and handled by the caller through `ax`/`tEnter`).
-VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Walk &k, bool &outside, int &ax, float &tEnter) {
-    const float dd[3] = {d.x, d.y, d.z}, oo[3] = {o.x, o.y, o.z};
-    const int W[3] = {w.wx, w.wy, w.wz};
-    k.o = o;
-    for (int a = 0; a < 3; ++a) {
-        k.mv[a] = dd[a] != 0.0f;
-        k.st[a] = dd[a] > 0.0f ? 1 : -1;
-        k.inv[a] = k.mv[a] ? 1.0f / dd[a] : 0.0f;
-        k.c[a] = (int)floorf(oo[a]);
+// Advance one axis to the cell it occupies when the walk leaves the box through
+// the crossing (Te, ea): exactly the planes the cell-by-cell walk would cross first.
+VX_D void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int lo, int hi, int ab, float Te, int ea) {
+    int est = clampi((int)floorf(o + Te * d), lo, hi);
+    est = s > 0 ? max(est, cb) : min(est, cb);
+    while (est != cb) {
+        const float te = ((float)(s > 0 ? est : est + 1) - o) * inv;  // plane entering est
+        if (before(te, ab, Te, ea)) break;
+        est -= s;
     }
-    outside = !(k.c[0] >= 0 && k.c[0] < W[0] && k.c[1] >= 0 && k.c[1] < W[1] && k.c[2] >= 0 && k.c[2] < W[2]);
-    if (outside) {
-        float t0 = -INFINITY, t1 = INFINITY;
-        ax = -1;
-        for (int a = 0; a < 3; ++a) {
-            if (dd[a] == 0.0f) {
-                if (oo[a] < 0.0f || oo[a] >= (float)W[a]) return false;
-                continue;
-            }
-            const float inv = 1.0f / dd[a];
-            const float ta = (0.0f - oo[a]) * inv, tb = ((float)W[a] - oo[a]) * inv;
-            const float lo = ta < tb ? ta : tb, hi = ta < tb ? tb : ta;
-            if (lo > t0) { t0 = lo; ax = a; }
-            if (hi < t1) t1 = hi;
-        }
-        if (ax < 0 || t0 > t1 || t1 <= 0.0f) return false;
-        for (int a = 0; a < 3; ++a) {
-            if (a == ax) k.c[a] = dd[a] > 0.0f ? 0 : W[a] - 1;
-            else k.c[a] = clampi((int)floorf(oo[a] + t0 * dd[a]), 0, W[a] - 1);
-        }
-        tEnter = t0;
+    float tn = ((float)(s > 0 ? est + 1 : est) - o) * inv;
+    while (before(tn, ab, Te, ea)) {
+        est += s;
+        tn = ((float)(s > 0 ? est + 1 : est) - o) * inv;
     }
-    k.t[0] = plane_t(k, 0, oo[0]);
-    k.t[1] = plane_t(k, 1, oo[1]);
-    k.t[2] = plane_t(k, 2, oo[2]);
+    cb = est;
+    tb = tn;
+}
+// Jump from the current cell to the last cell of an empty box [lo, lo+size) the
+// ray visits; the box exit crossing is then the walk's next step.
+VX_D void skip_box(const Ray3 &r, Cell &c, int size) {
+    const int lx = c.x & ~(size - 1), ly = c.y & ~(size - 1), lz = c.z & ~(size - 1);
+    const int hx = lx + size - 1, hy = ly + size - 1, hz = lz + size - 1;
+    const float Tx = r.mx ? ((float)(r.sx > 0 ? hx + 1 : lx) - r.ox) * r.ix : INFINITY;
+    const float Ty = r.my ? ((float)(r.sy > 0 ? hy + 1 : ly) - r.oy) * r.iy : INFINITY;
+    const float Tz = r.mz ? ((float)(r.sz > 0 ? hz + 1 : lz) - r.oz) * r.iz : INFINITY;
+    const int ea = pick3(Tx, Ty, Tz);
+    const float Te = ea == 0 ? Tx : (ea == 1 ? Ty : Tz);
+    if (ea == 0) { c.x = r.sx > 0 ? hx : lx; c.tx = Tx; }
+    else if (r.mx) skip_axis(c.x, c.tx, r.sx, r.ox, r.dx, r.ix, lx, hx, 0, Te, ea);
+    if (ea == 1) { c.y = r.sy > 0 ? hy : ly; c.ty = Ty; }
+    else if (r.my) skip_axis(c.y, c.ty, r.sy, r.oy, r.dy, r.iy, ly, hy, 1, Te, ea);
+    if (ea == 2) { c.z = r.sz > 0 ? hz : lz; c.tz = Tz; }
+    else if (r.mz) skip_axis(c.z, c.tz, r.sz, r.oz, r.dz, r.iz, lz, hz, 2, Te, ea);
+}
+
+VX_D bool slab(float o, float d, float W, int a, float &t0, float &t1, int &ax) {
+    if (d == 0.0f) return !(o < 0.0f || o >= W);
+    const float inv = 1.0f / d;
+    const float ta = (0.0f - o) * inv, tb = (W - o) * inv;
+    const float lo = ta < tb ? ta : tb, hi = ta < tb ? tb : ta;
+    if (lo > t0) { t0 = lo; ax = a; }
+    if (hi < t1) t1 = hi;
     return true;
 }
 
-VX_D int walk_pick(const Walk &k) {
-    if (k.t[0] < k.t[1]) return k.t[0] < k.t[2] ? 0 : 2;
-    return k.t[1] < k.t[2] ? 1 : 2;
+// Start a walk; returns false if the ray never meets the world box.  For an
+// origin outside the box, `outside` is set and the entry crossing (axis `ax`,
+// t `tEnter`) is already taken.
+VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outside, int &ax, float &tEnter) {
+    r.ox = o.x; r.oy = o.y; r.oz = o.z;
+    r.dx = d.x; r.dy = d.y; r.dz = d.z;
+    r.mx = d.x != 0.0f; r.my = d.y != 0.0f; r.mz = d.z != 0.0f;
+    r.sx = d.x > 0.0f ? 1 : -1; r.sy = d.y > 0.0f ? 1 : -1; r.sz = d.z > 0.0f ? 1 : -1;
+    r.ix = r.mx ? 1.0f / d.x : 0.0f; r.iy = r.my ? 1.0f / d.y : 0.0f; r.iz = r.mz ? 1.0f / d.z : 0.0f;
+    c.x = (int)floorf(o.x); c.y = (int)floorf(o.y); c.z = (int)floorf(o.z);
+    outside = !(c.x >= 0 && c.x < w.wx && c.y >= 0 && c.y < w.wy && c.z >= 0 && c.z < w.wz);
+    if (outside) {
+        // slab test against the world box, axes in x, y, z order
+        float t0 = -INFINITY, t1 = INFINITY;
+        ax = -1;
+        if (!slab(o.x, d.x, (float)w.wx, 0, t0, t1, ax) || !slab(o.y, d.y, (float)w.wy, 1, t0, t1, ax) ||
+            !slab(o.z, d.z, (float)w.wz, 2, t0, t1, ax))
+            return false;
+        if (ax < 0 || t0 > t1 || t1 <= 0.0f) return false;
+        c.x = ax == 0 ? (d.x > 0.0f ? 0 : w.wx - 1) : clampi((int)floorf(o.x + t0 * d.x), 0, w.wx - 1);
+        c.y = ax == 1 ? (d.y > 0.0f ? 0 : w.wy - 1) : clampi((int)floorf(o.y + t0 * d.y), 0, w.wy - 1);
+        c.z = ax == 2 ? (d.z > 0.0f ? 0 : w.wz - 1) : clampi((int)floorf(o.z + t0 * d.z), 0, w.wz - 1);
+        tEnter = t0;
+    }
+    c.tx = next_t(c.x, r.sx, r.ox, r.ix, r.mx);
+    c.ty = next_t(c.y, r.sy, r.oy, r.iy, r.my);
+    c.tz = next_t(c.z, r.sz, r.oz, r.iz, r.mz);
+    return true;
 }
 
-VX_D float comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+// One step of the walk: cross the nearest plane.  Returns the crossed plane's
+// t and coordinate and the face of the entered cell the crossing goes through.
+VX_D void walk_step(const Ray3 &r, Cell &c, float &t, int &planeCoord, int &face) {
+    const int a = pick3(c.tx, c.ty, c.tz);
+    if (a == 0) {
+        t = c.tx; planeCoord = r.sx > 0 ? c.x + 1 : c.x; face = r.sx > 0 ? 2 : 3;
+        c.x += r.sx; c.tx = next_t(c.x, r.sx, r.ox, r.ix, true);
+    } else if (a == 1) {
+        t = c.ty; planeCoord = r.sy > 0 ? c.y + 1 : c.y; face = r.sy > 0 ? 1 : 0;
+        c.y += r.sy; c.ty = next_t(c.y, r.sy, r.oy, r.iy, true);
+    } else {
+        t = c.tz; planeCoord = r.sz > 0 ? c.z + 1 : c.z; face = r.sz > 0 ? 5 : 4;
+        c.z += r.sz; c.tz = next_t(c.z, r.sz, r.oz, r.iz, true);
+    }
+}
+VX_D bool in_world(const WorldDev &w, const Cell &c) {
+    return (unsigned)c.x < (unsigned)w.wx && (unsigned)c.y < (unsigned)w.wy && (unsigned)c.z < (unsigned)w.wz;
+}
+// face through which a ray entering the world box along axis ax enters the cell
+VX_D int entry_face_of(int ax, V3 d) {
+    return ax == 0 ? (d.x > 0.0f ? 2 : 3) : (ax == 1 ? (d.y > 0.0f ? 1 : 0) : (d.z > 0.0f ? 5 : 4));
+}
 
 // Closest front-facing cube face along the ray, t <= tmax (radiance rays).
+// Contract A4': entering cube cell b from a hits iff b != a, or the crossed
+// plane is a chunk boundary, or a is outside the world.
 VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
-    Walk k;
+    Ray3 r;
+    Cell c;
     bool outside;
     int ax = -1;
     float tEnter = 0;
-    if (!walk_begin(w, o, d, k, outside, ax, tEnter)) return h;
-    int prevId = 0;
+    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return h;
+    int m = macro_of(w, c.x, c.y, c.z);
+    uint64_t mw = w.macro[m];
+    bool occ;
+    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
     if (outside) {
         if (tEnter > tmax) return h;
-        const int b = voxel(w, k.c[0], k.c[1], k.c[2]);
-        if (is_cube(b) && tEnter >= 0.0f) {
-            h = {1, k.c[0], k.c[1], k.c[2], entry_face(ax, k.st[ax]), b, tEnter};
+        if (is_cube(prevId) && tEnter >= 0.0f) {
+            h = {1, c.x, c.y, c.z, entry_face_of(ax, d), prevId, tEnter};
             return h;
         }
-        prevId = b;
-    } else if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) {
-        prevId = voxel(w, k.c[0], k.c[1], k.c[2]);
     }
-    const int W[3] = {w.wx, w.wy, w.wz};
-    const int maxSteps = W[0] + W[1] + W[2] + 3;
+    const int maxSteps = w.wx + w.wy + w.wz + 3;
     for (int s = 0; s < maxSteps; ++s) {
-        const int a = walk_pick(k);
-        const float t = k.t[a];
+        if (prevId == 0) {
+            if (mw == 0) skip_box(r, c, 16);
+            else if (!occ) skip_box(r, c, 4);
+        }
+        float t;
+        int planeCoord, face;
+        walk_step(r, c, t, planeCoord, face);
         if (!(t <= tmax)) return h;
-        const int planeCoord = k.st[a] > 0 ? k.c[a] + 1 : k.c[a];
-        k.c[a] += k.st[a];
-        if (k.c[a] < 0 || k.c[a] >= W[a]) return h;
-        k.t[a] = plane_t(k, a, comp(o, a));
-        int b = 0;
-        if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) b = voxel(w, k.c[0], k.c[1], k.c[2]);
+        if (!in_world(w, c)) return h;
+        const int nm = macro_of(w, c.x, c.y, c.z);
+        if (nm != m) { m = nm; mw = w.macro[m]; }
+        const int b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
         if (is_cube(b) && (b != prevId || (planeCoord & 31) == 0)) {
-            h = {1, k.c[0], k.c[1], k.c[2], entry_face(a, k.st[a]), b, t};
+            h = {1, c.x, c.y, c.z, face, b, t};
             return h;
         }
         prevId = b;
@@ -143,41 +212,44 @@ VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
     return h;
 }
 
-// Any face crossing with tmin <= t <= tmax (visibility rays: no culling).
+// Any face crossing with tmin <= t <= tmax (visibility rays: no culling, so
+// leaving a cube cell counts too).
 VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
-    Walk k;
+    Ray3 r;
+    Cell c;
     bool outside;
     int ax = -1;
     float tEnter = 0;
-    if (!walk_begin(w, o, d, k, outside, ax, tEnter)) return false;
-    int prevId = 0;
+    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return false;
+    int m = macro_of(w, c.x, c.y, c.z);
+    uint64_t mw = w.macro[m];
+    bool occ;
+    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
     if (outside) {
         if (tEnter > tmax) return false;
-        const int b = voxel(w, k.c[0], k.c[1], k.c[2]);
-        if (is_cube(b) && tEnter >= tmin) return true;
-        prevId = b;
-    } else if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) {
-        prevId = voxel(w, k.c[0], k.c[1], k.c[2]);
+        if (is_cube(prevId) && tEnter >= tmin) return true;
     }
-    const int W[3] = {w.wx, w.wy, w.wz};
-    const int maxSteps = W[0] + W[1] + W[2] + 3;
+    const int maxSteps = w.wx + w.wy + w.wz + 3;
     for (int s = 0; s < maxSteps; ++s) {
-        const int a = walk_pick(k);
-        const float t = k.t[a];
+        if (prevId == 0) {
+            if (mw == 0) skip_box(r, c, 16);
+            else if (!occ) skip_box(r, c, 4);
+        }
+        float t;
+        int planeCoord, face;
+        walk_step(r, c, t, planeCoord, face);
         if (!(t <= tmax)) return false;
-        const int planeCoord = k.st[a] > 0 ? k.c[a] + 1 : k.c[a];
         const bool chunkPlane = (planeCoord & 31) == 0;
-        const int aId = prevId;
-        k.c[a] += k.st[a];
-        const bool out = k.c[a] < 0 || k.c[a] >= W[a];
+        const bool out = !in_world(w, c);
         int b = 0;
         if (!out) {
-            k.t[a] = plane_t(k, a, comp(o, a));
-            if (brick_occupied(w, k.c[0], k.c[1], k.c[2])) b = voxel(w, k.c[0], k.c[1], k.c[2]);
+            const int nm = macro_of(w, c.x, c.y, c.z);
+            if (nm != m) { m = nm; mw = w.macro[m]; }
+            b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
         }
         if (t >= tmin) {
-            const bool frontB = is_cube(b) && (b != aId || chunkPlane);
-            const bool backA = is_cube(aId) && (aId != b || chunkPlane || out);
+            const bool frontB = is_cube(b) && (b != prevId || chunkPlane);
+            const bool backA = is_cube(prevId) && (prevId != b || chunkPlane || out);
             if (frontB || backA) return true;
         }
         if (out) return false;
@@ -195,11 +267,12 @@ VX_D V3 face_normal(int f) {
 // (SelfHit.h:539-656 specialised to unit quads under one translation instance).
 VX_D void hit_frame(const Hit &h, V3 o, V3 d, V3 &front, V3 &back, V3 &ng) {
     V3 p = o + d * h.t;
-    const int axis = (h.face < 2) ? 1 : (h.face < 4 ? 0 : 2);
-    const int cell = axis == 0 ? h.x : (axis == 1 ? h.y : h.z);
+    const bool ax0 = h.face == 2 || h.face == 3, ax1 = h.face < 2;  // else z (faces 4, 5)
+    // blend instead of selecting a field by index: keeps h and p in registers
+    const int cell = (ax0 ? h.x : 0) + (ax1 ? h.y : 0) + ((!ax0 && !ax1) ? h.z : 0);
     const bool high = (h.face == 0 || h.face == 3 || h.face == 4);
     const int plane = cell + (high ? 1 : 0);
-    p.set(axis, (float)plane);
+    const float pa = (float)plane;
     ng = face_normal(h.face);
     const int T = (cell >> 5) * 32;
     const float planeLocal = (float)(plane - T), planeWorld = (float)plane, Tf = (float)T;
@@ -211,16 +284,12 @@ VX_D void hit_frame(const Hit &h, V3 o, V3 d, V3 &front, V3 &back, V3 &ng) {
     const float objErr = fma_ru(cI, planeWorld, mul_ru(cI, Tf));
     float off = add_ru(objErr, triErr);
     off = off + wldErr;
-    front = p;
-    back = p;
-    const float n = ng.get(axis), pa = p.get(axis);
-    if (n > 0.f) {
-        front.set(axis, fma_ru(off, n, pa));
-        back.set(axis, fma_rd(-off, n, pa));
-    } else {
-        front.set(axis, fma_rd(off, n, pa));
-        back.set(axis, fma_ru(-off, n, pa));
-    }
+    // outward normal component along the axis is +1 for the high faces, -1 otherwise
+    const float n = high ? 1.0f : -1.0f;
+    const float fa = high ? fma_ru(off, n, pa) : fma_rd(off, n, pa);
+    const float ba = high ? fma_rd(-off, n, pa) : fma_ru(-off, n, pa);
+    front = V3(ax0 ? fa : p.x, ax1 ? fa : p.y, (!ax0 && !ax1) ? fa : p.z);
+    back = V3(ax0 ? ba : p.x, ax1 ? ba : p.y, (!ax0 && !ax1) ? ba : p.z);
 }
 
 // ----------------------------------------------------------------- BSDF
@@ -501,6 +570,7 @@ VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
         const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
         V3 out(0.0f);
         float sum = 0.0f;
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
             int x = tx0 + (i & 1), y = ty0 + (i >> 1);
             if (x >= k.skyW) x %= k.skyW;
@@ -695,8 +765,9 @@ VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps,
         const int ppx = (int)(puv.x * pc.res.x), ppy = (int)(puv.y * pc.res.y);
         const V3 dd = prevW - pc.pos;
         const float expDepth = sqrtf(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z);
-        int ox[3], oy[3];
-        ox[0] = ppx - px; oy[0] = ppy - py;
+        // three temporal taps (scalars, not arrays: no runtime-indexed private memory)
+        int ox0, oy0, ox1, oy1, ox2, oy2;
+        ox0 = ppx - px; oy0 = ppy - py;
         {
             const float r0 = rng.next(), r1 = rng.next();
             V2 u = V2(r0 * 2.0f - 1.0f, r1 * 2.0f - 1.0f);
@@ -708,7 +779,7 @@ VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps,
                 dsk = V2(cosf(th) * r, sinf(th) * r);
             }
             dsk = dsk * 64.0f;
-            ox[1] = ppx - px + (int)dsk.x; oy[1] = ppy - py + (int)dsk.y;
+            ox1 = ppx - px + (int)dsk.x; oy1 = ppy - py + (int)dsk.y;
         }
         {
             const float r0 = rng.next(), r1 = rng.next();
@@ -721,12 +792,13 @@ VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps,
                 dsk = V2(cosf(th) * r, sinf(th) * r);
             }
             dsk = dsk * 64.0f;
-            ox[2] = (int)dsk.x; oy[2] = (int)dsk.y;
+            ox2 = (int)dsk.x; oy2 = (int)dsk.y;
         }
         unsigned cached = 0;
         int selLoop = -1;
         for (int i = 0; i < 3; ++i) {
-            const int x = reflect_view(px + ox[i], a.W), y = reflect_view(py + oy[i], a.H);
+            const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+            const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
             SurfS ts;
             if (!prev_surface(a, px, py, ts, x, y)) continue;
             const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
@@ -749,7 +821,8 @@ VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps,
             float piv = rr.targetPdf, piSum = rr.targetPdf * 1;
             for (int i = 0; i < 3; ++i) {
                 if ((cached & (1u << i)) == 0) continue;
-                const int x = reflect_view(px + ox[i], a.W), y = reflect_view(py + oy[i], a.H);
+                const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+            const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
                 SurfS ts;
                 prev_surface(a, px, py, ts, x, y);
                 LSample sel{V3(0.f), V3(0.f), 0.f, LtInvalid};

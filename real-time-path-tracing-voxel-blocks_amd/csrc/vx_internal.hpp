@@ -33,14 +33,19 @@ struct AliasBin { float q, p; int alias; };
 
 struct Reservoir { uint32_t lightData, uvData; float weightSum, targetPdf, M; };
 
-// Voxel world on the device.  ids: chunk-major u8 (32^3 per chunk, x + 32*(z + 32*y));
-// occ: one bit per 4^3 brick, bricks ordered bx + BX*(bz + BZ*by).
+// Voxel world on the device, laid out for the DDA:
+//   macro[m]  one 64-bit occupancy word per 16^3 macro cell (bit = one 4^3 brick,
+//             (bx&3) + 4*((bz&3) + 4*(by&3))); m = mx + MX*(mz + MZ*my); 0 = empty macro
+//   bricks    u8 block ids, macro-major then brick then cell: a brick is 64
+//             contiguous bytes, a macro 4 KiB ((m*64 + brick)*64 + (x&3) + 4*((z&3) + 4*(y&3)))
+//   ids       the chunk-major upload layout (x + 32*(z + 32*y) per 32^3 chunk), kept for readback
 struct WorldDev {
     const uint8_t *ids;
-    const uint32_t *occ;
+    const uint8_t *bricks;
+    const uint64_t *macro;
     int cx, cy, cz;       // chunks
     int wx, wy, wz;       // cells
-    int bx, by, bz;       // bricks
+    int mx, my, mz;       // 16^3 macro cells
 };
 
 struct SkyDev {

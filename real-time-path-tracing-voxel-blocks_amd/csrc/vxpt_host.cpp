@@ -139,7 +139,8 @@ struct vxpt_ctx {
     // scene
     int cx = 0, cy = 0, cz = 0;
     DBuf<uint8_t> voxels;
-    DBuf<uint32_t> occ;
+    DBuf<uint8_t> bricks;
+    DBuf<uint64_t> macro;
     MatDev mats[13] = {};
     CamDev cam{}, prevCam{};
     float camYaw = 0, camPitch = 0;
@@ -298,10 +299,11 @@ V3 q_rotate3(V3 axis, float angle, V3 v) {  // rotate3f (LinearMath.h:1368)
 
 void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.ids = c->voxels.p;
-    w.occ = c->occ.p;
+    w.bricks = c->bricks.p;
+    w.macro = c->macro.p;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
     w.wx = c->cx * 32; w.wy = c->cy * 32; w.wz = c->cz * 32;
-    w.bx = w.wx / 4; w.by = w.wy / 4; w.bz = w.wz / 4;
+    w.mx = w.wx / 16; w.my = w.wy / 16; w.mz = w.wz / 16;
 }
 
 void fill_sky(vxpt_ctx *c, SkyDev &s) {
@@ -383,21 +385,29 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
     }
 }
 
+// DDA acceleration layout (WorldDev): macro occupancy words + brick-major ids
 int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     const int wx = c->cx * 32, wy = c->cy * 32, wz = c->cz * 32;
-    const int bx = wx / 4, by = wy / 4, bz = wz / 4;
-    std::vector<uint32_t> occ(((size_t)bx * by * bz + 31) / 32, 0u);
+    const int mx = wx / 16, my = wy / 16, mz = wz / 16;
+    std::vector<uint64_t> macro((size_t)mx * my * mz, 0ull);
+    std::vector<uint8_t> bricks((size_t)wx * wy * wz, 0);
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
                 const int ch = (x >> 5) + c->cx * ((z >> 5) + c->cz * (y >> 5));
                 const uint8_t id = ids[(size_t)ch * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
-                if (id >= 1 && id <= 12) {
-                    const size_t b = (size_t)(x >> 2) + (size_t)bx * ((z >> 2) + (size_t)bz * (y >> 2));
-                    occ[b >> 5] |= 1u << (b & 31);
-                }
+                if (!id) continue;
+                const size_t m = (size_t)(x >> 4) + (size_t)mx * ((z >> 4) + (size_t)mz * (y >> 4));
+                const int lb = ((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3));
+                const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
+                bricks[(m * 64 + lb) * 64 + lc] = id;
+                // only cube ids (1..12) make a brick visible to the DDA; other ids are empty for it
+                if (id >= 1 && id <= 12) macro[m] |= 1ull << lb;
             }
-    return upload_vec(c, c->occ, occ.data(), occ.size());
+    if (int r = upload_vec(c, c->bricks, bricks.data(), bricks.size())) return r;
+    if (int r = upload_vec(c, c->macro, macro.data(), macro.size())) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors die on return
+    return 0;
 }
 
 int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale) {
