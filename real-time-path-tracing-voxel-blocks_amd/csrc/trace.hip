@@ -1,668 +1,288 @@
-// vxpt -- the per-pixel path-tracing pass on gfx950.
+// vxpt -- the path-tracing pass on gfx950, as a wavefront of small kernels.
 //
-// One thread per pixel, 256-thread workgroups covering 16x16 pixels (each
-// 64-lane wave an 8x8 tile, so a wave's primary rays are coherent and its
-// G-buffer stores are whole 128-byte row segments).  Hardware BVH traversal
-// of the reference (optixTraverse over one triangle mesh per chunk x block
-// type, renderer/shaders/RayGen.cu:49, closesthit.cu:458/616/745/801) is
-// replaced by an exact voxel DDA over the u8 grid with a 1-bit-per-4^3-brick
-// occupancy mask: empty bricks are crossed without touching the grid.  The
-// DDA returns what the face mesh + CULL_BACK would (SURVEY.md §8a A3/A4').
+// The reference runs one OptiX raygen program per pixel that traces the
+// camera ray, shades the hit (closesthit.cu:10-852) and traces up to six more
+// rays for NEE and ReSTIR-DI inside the shader (RayGen.cu:8-182).  A single
+// HIP kernel doing the same needs all of that state live across every DDA
+// loop: 256 VGPRs, one wave per SIMD, nothing to hide memory latency.  Here
+// the pass is split at every ray: traversal kernels (k_closest, k_occluded)
+// hold only the DDA state and run at high occupancy; shading kernels hold no
+// traversal loop.  Per-pixel state between stages lives in HBM (WaveBufs),
+// one slot per pixel in 8x8-tile order so every wave works on one tile.
 //
-// Shading follows closesthit.cu:10-852 / miss.cu:9-82 / Restir.h / Bsdf.h:
-// Disney BSDF, NEE over sun + sky (+ BRDF sample), RIS, ReSTIR-DI temporal
-// reuse with bias correction, 3-segment / 1-diffuse path limit.
-#include "vx_internal.hpp"
+// Per path segment (seg = 0 .. totalBounceLimit-1):
+//   k_closest   camera ray (seg 0) / continuing path ray        -> hit
+//   k_shade     miss: sky; hit: G-buffer, BSDF sample, sun/sky candidates,
+//               BRDF candidate ray                               (closesthit.cu:10-414)
+//   k_closest   BRDF candidate rays                              (closesthit.cu:415-520)
+//   k_nee       BRDF candidate + RIS -> visibility ray           (closesthit.cu:520-625)
+//   k_occluded  visibility rays
+//   k_restir    seg 0: ReSTIR temporal taps -> bias-correction + final visibility rays
+//               seg > 0: shade with the RIS sample               (closesthit.cu:626-851)
+//   k_occluded  (seg 0) bias-correction + final visibility rays
+//   k_finish    (seg 0) bias correction, final shading, reservoir store
+// Every stage consumes the blue-noise dimensions in the reference's order
+// (the sampler dimension travels in the path state), so results equal the
+// one-thread-per-pixel program bit for bit.
+#include "vx_device.hpp"
 
 namespace vx {
 namespace {
 
-constexpr uint32_t kValidBit = 0x80000000u, kIndexMask = 0x7FFFFFFFu;
-constexpr uint32_t kInvalidLight = 0x7FFFFFFFu, kSkyLight = 0x7FFFFFFEu, kSunLight = 0x7FFFFFFDu;
-enum { LtInvalid = 0, LtSky = 1, LtSun = 2 };
-constexpr float kRoughThresh = 0.00001f, kTranslThresh = 0.001f;
-constexpr float kMinPdf = 1e-5f, kMaxThroughput = 32.0f, kMinLobe = 0.05f;
+constexpr int F_ALIVE = 1, F_HFD = 2, F_NEE = 4, F_RESTIR = 8;
+constexpr float kFltMax = 3.402823466e+38f;
 
-// ----------------------------------------------------------------- voxel DDA
-VX_D bool is_cube(int id) { return id >= 1 && id <= 12; }
-
-struct Hit { int hit, x, y, z, face, id; float t; };
-
-VX_D int entry_face(int a, int s) {
-    return a == 0 ? (s > 0 ? 2 : 3) : (a == 1 ? (s > 0 ? 1 : 0) : (s > 0 ? 5 : 4));
+VX_D bool slot_pixel(const TraceArgs &a, int s, int &px, int &py) {
+    const int tile = s >> 6, lane = s & 63;
+    px = (tile % a.tilesX) * 8 + (lane & 7);
+    py = a.y0 + (tile / a.tilesX) * 8 + (lane >> 3);
+    return s < a.nSlots && px < a.W && py < a.y1;
 }
 
-// The walk keeps every per-axis quantity in named scalars (no runtime-indexed
-// arrays: those would live in scratch on gfx950).
-struct Ray3 {
-    float ox, oy, oz, dx, dy, dz, ix, iy, iz;
-    int sx, sy, sz;
-    bool mx, my, mz;
-};
-struct Cell {
-    int x, y, z;
-    float tx, ty, tz;  // t of the next plane crossing on each axis (INF if the axis does not move)
-};
-
-// t of the next plane after cell c along one axis; the only formula for plane t,
-// so skipped and stepped walks produce identical values.
-VX_D float next_t(int c, int s, float o, float inv, bool mv) {
-    if (!mv) return INFINITY;
-    return ((float)(s > 0 ? c + 1 : c) - o) * inv;
-}
-// axis order of the reference tie rule (VoxelEngine.cu:1040-1166 strict '<'):
-// smallest t first, ties to Z, then Y, then X
-VX_D int pick3(float tx, float ty, float tz) {
-    if (tx < ty) return tx < tz ? 0 : 2;
-    return ty < tz ? 1 : 2;
-}
-VX_D bool before(float t1, int a1, float t2, int a2) { return t1 < t2 || (t1 == t2 && a1 > a2); }
-
-VX_D int macro_of(const WorldDev &w, int x, int y, int z) { return (x >> 4) + w.mx * ((z >> 4) + w.mz * (y >> 4)); }
-VX_D int brick_bit(int x, int y, int z) { return ((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3)); }
-VX_D int cell_id(const WorldDev &w, int m, uint64_t mw, int x, int y, int z, bool &brickOcc) {
-    const int lb = brick_bit(x, y, z);
-    brickOcc = (mw >> lb) & 1ull;
-    if (!brickOcc) return 0;
-    const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
-    return w.bricks[((size_t)m * 64 + lb) * 64 + lc];
-}
-
-// Advance one axis to the cell it occupies when the walk leaves the box through
-// the crossing (Te, ea): exactly the planes the cell-by-cell walk would cross first.
-VX_D void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int lo, int hi, int ab, float Te, int ea) {
-    int est = clampi((int)floorf(o + Te * d), lo, hi);
-    est = s > 0 ? max(est, cb) : min(est, cb);
-    while (est != cb) {
-        const float te = ((float)(s > 0 ? est : est + 1) - o) * inv;  // plane entering est
-        if (before(te, ab, Te, ea)) break;
-        est -= s;
-    }
-    float tn = ((float)(s > 0 ? est + 1 : est) - o) * inv;
-    while (before(tn, ab, Te, ea)) {
-        est += s;
-        tn = ((float)(s > 0 ? est + 1 : est) - o) * inv;
-    }
-    cb = est;
-    tb = tn;
-}
-// Jump from the current cell to the last cell of an empty box [lo, lo+size) the
-// ray visits; the box exit crossing is then the walk's next step.
-VX_D void skip_box(const Ray3 &r, Cell &c, int size) {
-    const int lx = c.x & ~(size - 1), ly = c.y & ~(size - 1), lz = c.z & ~(size - 1);
-    const int hx = lx + size - 1, hy = ly + size - 1, hz = lz + size - 1;
-    const float Tx = r.mx ? ((float)(r.sx > 0 ? hx + 1 : lx) - r.ox) * r.ix : INFINITY;
-    const float Ty = r.my ? ((float)(r.sy > 0 ? hy + 1 : ly) - r.oy) * r.iy : INFINITY;
-    const float Tz = r.mz ? ((float)(r.sz > 0 ? hz + 1 : lz) - r.oz) * r.iz : INFINITY;
-    const int ea = pick3(Tx, Ty, Tz);
-    const float Te = ea == 0 ? Tx : (ea == 1 ? Ty : Tz);
-    if (ea == 0) { c.x = r.sx > 0 ? hx : lx; c.tx = Tx; }
-    else if (r.mx) skip_axis(c.x, c.tx, r.sx, r.ox, r.dx, r.ix, lx, hx, 0, Te, ea);
-    if (ea == 1) { c.y = r.sy > 0 ? hy : ly; c.ty = Ty; }
-    else if (r.my) skip_axis(c.y, c.ty, r.sy, r.oy, r.dy, r.iy, ly, hy, 1, Te, ea);
-    if (ea == 2) { c.z = r.sz > 0 ? hz : lz; c.tz = Tz; }
-    else if (r.mz) skip_axis(c.z, c.tz, r.sz, r.oz, r.dz, r.iz, lz, hz, 2, Te, ea);
-}
-
-VX_D bool slab(float o, float d, float W, int a, float &t0, float &t1, int &ax) {
-    if (d == 0.0f) return !(o < 0.0f || o >= W);
-    const float inv = 1.0f / d;
-    const float ta = (0.0f - o) * inv, tb = (W - o) * inv;
-    const float lo = ta < tb ? ta : tb, hi = ta < tb ? tb : ta;
-    if (lo > t0) { t0 = lo; ax = a; }
-    if (hi < t1) t1 = hi;
-    return true;
-}
-
-// Start a walk; returns false if the ray never meets the world box.  For an
-// origin outside the box, `outside` is set and the entry crossing (axis `ax`,
-// t `tEnter`) is already taken.
-VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outside, int &ax, float &tEnter) {
-    r.ox = o.x; r.oy = o.y; r.oz = o.z;
-    r.dx = d.x; r.dy = d.y; r.dz = d.z;
-    r.mx = d.x != 0.0f; r.my = d.y != 0.0f; r.mz = d.z != 0.0f;
-    r.sx = d.x > 0.0f ? 1 : -1; r.sy = d.y > 0.0f ? 1 : -1; r.sz = d.z > 0.0f ? 1 : -1;
-    r.ix = r.mx ? 1.0f / d.x : 0.0f; r.iy = r.my ? 1.0f / d.y : 0.0f; r.iz = r.mz ? 1.0f / d.z : 0.0f;
-    c.x = (int)floorf(o.x); c.y = (int)floorf(o.y); c.z = (int)floorf(o.z);
-    outside = !(c.x >= 0 && c.x < w.wx && c.y >= 0 && c.y < w.wy && c.z >= 0 && c.z < w.wz);
-    if (outside) {
-        // slab test against the world box, axes in x, y, z order
-        float t0 = -INFINITY, t1 = INFINITY;
-        ax = -1;
-        if (!slab(o.x, d.x, (float)w.wx, 0, t0, t1, ax) || !slab(o.y, d.y, (float)w.wy, 1, t0, t1, ax) ||
-            !slab(o.z, d.z, (float)w.wz, 2, t0, t1, ax))
-            return false;
-        if (ax < 0 || t0 > t1 || t1 <= 0.0f) return false;
-        c.x = ax == 0 ? (d.x > 0.0f ? 0 : w.wx - 1) : clampi((int)floorf(o.x + t0 * d.x), 0, w.wx - 1);
-        c.y = ax == 1 ? (d.y > 0.0f ? 0 : w.wy - 1) : clampi((int)floorf(o.y + t0 * d.y), 0, w.wy - 1);
-        c.z = ax == 2 ? (d.z > 0.0f ? 0 : w.wz - 1) : clampi((int)floorf(o.z + t0 * d.z), 0, w.wz - 1);
-        tEnter = t0;
-    }
-    c.tx = next_t(c.x, r.sx, r.ox, r.ix, r.mx);
-    c.ty = next_t(c.y, r.sy, r.oy, r.iy, r.my);
-    c.tz = next_t(c.z, r.sz, r.oz, r.iz, r.mz);
-    return true;
-}
-
-// One step of the walk: cross the nearest plane.  Returns the crossed plane's
-// t and coordinate and the face of the entered cell the crossing goes through.
-VX_D void walk_step(const Ray3 &r, Cell &c, float &t, int &planeCoord, int &face) {
-    const int a = pick3(c.tx, c.ty, c.tz);
-    if (a == 0) {
-        t = c.tx; planeCoord = r.sx > 0 ? c.x + 1 : c.x; face = r.sx > 0 ? 2 : 3;
-        c.x += r.sx; c.tx = next_t(c.x, r.sx, r.ox, r.ix, true);
-    } else if (a == 1) {
-        t = c.ty; planeCoord = r.sy > 0 ? c.y + 1 : c.y; face = r.sy > 0 ? 1 : 0;
-        c.y += r.sy; c.ty = next_t(c.y, r.sy, r.oy, r.iy, true);
-    } else {
-        t = c.tz; planeCoord = r.sz > 0 ? c.z + 1 : c.z; face = r.sz > 0 ? 5 : 4;
-        c.z += r.sz; c.tz = next_t(c.z, r.sz, r.oz, r.iz, true);
-    }
-}
-VX_D bool in_world(const WorldDev &w, const Cell &c) {
-    return (unsigned)c.x < (unsigned)w.wx && (unsigned)c.y < (unsigned)w.wy && (unsigned)c.z < (unsigned)w.wz;
-}
-// face through which a ray entering the world box along axis ax enters the cell
-VX_D int entry_face_of(int ax, V3 d) {
-    return ax == 0 ? (d.x > 0.0f ? 2 : 3) : (ax == 1 ? (d.y > 0.0f ? 1 : 0) : (d.z > 0.0f ? 5 : 4));
-}
-
-// Closest front-facing cube face along the ray, t <= tmax (radiance rays).
-// Contract A4': entering cube cell b from a hits iff b != a, or the crossed
-// plane is a chunk boundary, or a is outside the world.
-VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
-    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
-    Ray3 r;
-    Cell c;
-    bool outside;
-    int ax = -1;
-    float tEnter = 0;
-    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return h;
-    int m = macro_of(w, c.x, c.y, c.z);
-    uint64_t mw = w.macro[m];
-    bool occ;
-    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
-    if (outside) {
-        if (tEnter > tmax) return h;
-        if (is_cube(prevId) && tEnter >= 0.0f) {
-            h = {1, c.x, c.y, c.z, entry_face_of(ax, d), prevId, tEnter};
-            return h;
-        }
-    }
-    const int maxSteps = w.wx + w.wy + w.wz + 3;
-    for (int s = 0; s < maxSteps; ++s) {
-        if (prevId == 0) {
-            if (mw == 0) skip_box(r, c, 16);
-            else if (!occ) skip_box(r, c, 4);
-        }
-        float t;
-        int planeCoord, face;
-        walk_step(r, c, t, planeCoord, face);
-        if (!(t <= tmax)) return h;
-        if (!in_world(w, c)) return h;
-        const int nm = macro_of(w, c.x, c.y, c.z);
-        if (nm != m) { m = nm; mw = w.macro[m]; }
-        const int b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
-        if (is_cube(b) && (b != prevId || (planeCoord & 31) == 0)) {
-            h = {1, c.x, c.y, c.z, face, b, t};
-            return h;
-        }
-        prevId = b;
-    }
+VX_D int4 pack_hit(const Hit &h) { return make_int4(h.x, h.y, h.z, (h.face & 15) | (h.id << 4) | (h.hit << 12)); }
+VX_D Hit unpack_hit(int4 v, float t) {
+    Hit h;
+    h.x = v.x; h.y = v.y; h.z = v.z;
+    h.face = v.w & 15; h.id = (v.w >> 4) & 255; h.hit = (v.w >> 12) & 1;
+    h.t = t;
     return h;
 }
+VX_D V3 xyz(float4 v) { return V3(v.x, v.y, v.z); }
+VX_D float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
-// Any face crossing with tmin <= t <= tmax (visibility rays: no culling, so
-// leaving a cube cell counts too).
-VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
-    Ray3 r;
-    Cell c;
-    bool outside;
-    int ax = -1;
-    float tEnter = 0;
-    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return false;
-    int m = macro_of(w, c.x, c.y, c.z);
-    uint64_t mw = w.macro[m];
-    bool occ;
-    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
-    if (outside) {
-        if (tEnter > tmax) return false;
-        if (is_cube(prevId) && tEnter >= tmin) return true;
+// temporal-reuse disk offset (Restir.h: concentric square-to-disk, radius 64)
+VX_D V2 restir_disk(float r0, float r1) {
+    const V2 u = V2(r0 * 2.0f - 1.0f, r1 * 2.0f - 1.0f);
+    V2 dsk(0.0f, 0.0f);
+    if (!(fabsf(u.x) < 1e-10f && fabsf(u.y) < 1e-10f)) {
+        float th, r;
+        if (fabsf(u.x) > fabsf(u.y)) { r = u.x; th = kPiOver4 * (u.y / u.x); }
+        else { r = u.y; th = kPiOver2 - kPiOver4 * (u.x / u.y); }
+        dsk = V2(cosf(th) * r, sinf(th) * r);
     }
-    const int maxSteps = w.wx + w.wy + w.wz + 3;
-    for (int s = 0; s < maxSteps; ++s) {
-        if (prevId == 0) {
-            if (mw == 0) skip_box(r, c, 16);
-            else if (!occ) skip_box(r, c, 4);
-        }
-        float t;
-        int planeCoord, face;
-        walk_step(r, c, t, planeCoord, face);
-        if (!(t <= tmax)) return false;
-        const bool chunkPlane = (planeCoord & 31) == 0;
-        const bool out = !in_world(w, c);
-        int b = 0;
-        if (!out) {
-            const int nm = macro_of(w, c.x, c.y, c.z);
-            if (nm != m) { m = nm; mw = w.macro[m]; }
-            b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
-        }
-        if (t >= tmin) {
-            const bool frontB = is_cube(b) && (b != prevId || chunkPlane);
-            const bool backA = is_cube(prevId) && (prevId != b || chunkPlane || out);
-            if (frontB || backA) return true;
-        }
-        if (out) return false;
-        prevId = b;
+    return dsk * 64.0f;
+}
+
+// ----------------------------------------------------------------- traversal
+// mode 2: camera rays (RayGen.cu:102-126; initialises the path state);
+// mode 0: continuing path rays; mode 1: BRDF-candidate queue.
+__global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    V3 o, d;
+    float tmax = kRayMax;
+    if (mode == 2) {
+        Rng rng{&a.bn, px, py, a.iterationIndex, 0};
+        const float j0 = rng.next(), j1 = rng.next();
+        const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
+        o = a.cam.pos;
+        d = a.cam.uv_to_dir(uv);
+        w.pPos[s] = f4(o, kRayMax);
+        w.pDir[s] = f4(d, 0.0f);
+        w.pThr[s] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+        w.pRad[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        w.pMeta[s] = make_int4(F_ALIVE, rng.idx, 0, 0);
+    } else if (mode == 0) {
+        if (!(w.pMeta[s].x & F_ALIVE)) return;
+        o = xyz(w.pPos[s]);
+        d = xyz(w.pDir[s]);
+    } else {
+        if (!(w.pMeta[s].x & F_NEE)) return;
+        const float4 ro = w.cRayO[s];
+        if (!(ro.w >= 0.0f)) return;
+        o = xyz(ro);
+        d = xyz(w.cRayD[s]);
+        tmax = ro.w;
     }
-    return false;
+    const Hit h = dda_closest(a.world, o, d, tmax);
+    w.cHit[s] = pack_hit(h);
+    w.cT[s] = h.t;
 }
 
-VX_D V3 face_normal(int f) {
-    return f == 0 ? V3(0, 1, 0) : f == 1 ? V3(0, -1, 0) : f == 2 ? V3(-1, 0, 0) : f == 3 ? V3(1, 0, 0)
-         : f == 4 ? V3(0, 0, 1) : V3(0, 0, -1);
+// Visibility rays, 4 per slot; perSlot = 1 traces only ray 0 of each slot.
+__global__ __launch_bounds__(256) void k_occluded(TraceArgs a, int perSlot) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    const int s = perSlot == 4 ? (r >> 2) : r;
+    const int q = perSlot == 4 ? r : s * 4;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    if (!(w.pMeta[s].x & F_NEE)) return;
+    const float4 rd = w.oRayD[q];
+    if (!(rd.w >= 0.0f)) return;
+    const float4 ro = w.oRayO[q];
+    w.oHit[q] = dda_occluded(a.world, xyz(ro), xyz(rd), ro.w, rd.w) ? 1 : 0;
 }
 
-// Hit point on the face plane + self-intersection-safe spawn points
-// (SelfHit.h:539-656 specialised to unit quads under one translation instance).
-VX_D void hit_frame(const Hit &h, V3 o, V3 d, V3 &front, V3 &back, V3 &ng) {
-    V3 p = o + d * h.t;
-    const bool ax0 = h.face == 2 || h.face == 3, ax1 = h.face < 2;  // else z (faces 4, 5)
-    // blend instead of selecting a field by index: keeps h and p in registers
-    const int cell = (ax0 ? h.x : 0) + (ax1 ? h.y : 0) + ((!ax0 && !ax1) ? h.z : 0);
-    const bool high = (h.face == 0 || h.face == 3 || h.face == 4);
-    const int plane = cell + (high ? 1 : 0);
-    const float pa = (float)plane;
-    ng = face_normal(h.face);
-    const int T = (cell >> 5) * 32;
-    const float planeLocal = (float)(plane - T), planeWorld = (float)plane, Tf = (float)T;
-    const float c0t = 5.9604648328104529e-08f, c1t = 1.1920930376163769e-07f;
-    const float eps = mul_ru(c1t, 2.0f);
-    const float triErr = fma_ru(c0t, planeLocal, eps);
-    const float cI = 1.19209317972490680404007434844970703125E-7f;
-    const float wldErr = fma_ru(cI, planeLocal, mul_ru(cI, Tf));
-    const float objErr = fma_ru(cI, planeWorld, mul_ru(cI, Tf));
-    float off = add_ru(objErr, triErr);
-    off = off + wldErr;
-    // outward normal component along the axis is +1 for the high faces, -1 otherwise
-    const float n = high ? 1.0f : -1.0f;
-    const float fa = high ? fma_ru(off, n, pa) : fma_rd(off, n, pa);
-    const float ba = high ? fma_rd(-off, n, pa) : fma_ru(-off, n, pa);
-    front = V3(ax0 ? fa : p.x, ax1 ? fa : p.y, (!ax0 && !ax1) ? fa : p.z);
-    back = V3(ax0 ? ba : p.x, ax1 ? ba : p.y, (!ax0 && !ax1) ? ba : p.z);
+// ----------------------------------------------------------------- shading
+VX_D void path_end(const TraceArgs &a, int px, int py, V3 radiance, float primaryDist) {
+    if (isnan(radiance.x) || isnan(radiance.y) || isnan(radiance.z)) radiance = V3(0.5f);  // RayGen.cu:175-178
+    const size_t pi = (size_t)py * a.W + px;
+    a.cur.depth[pi] = primaryDist;
+    if (a.accum) {
+        // spp > 1: average the passes' radiance (DESIGN.md §5), depth from the last pass
+        float4 acc = a.accumFirst ? make_float4(0.f, 0.f, 0.f, 0.f) : a.accum[pi];
+        acc.x += radiance.x * a.accumScale;
+        acc.y += radiance.y * a.accumScale;
+        acc.z += radiance.z * a.accumScale;
+        acc.w = primaryDist;
+        a.accum[pi] = acc;
+    }
+    a.illum[pi] = make_float4(radiance.x, radiance.y, radiance.z, primaryDist);
 }
 
-// ----------------------------------------------------------------- BSDF
-VX_D V3 clamp_throughput(V3 v) {
-    const float l = luminance(v), a = fabsf(l);
-    if (a > kMaxThroughput && a > 0.0f) return v * (kMaxThroughput / a);
-    return v;
-}
-VX_D float disney_diffuse_fresnel(float cwo, float cwi, float r) {
-    const float eb = lerpf(0.0f, 0.5f, r), ef = lerpf(1.0f, 1.0f / 1.51f, r);
-    const float fd90 = eb + 2.0f * r * cwi * cwi;
-    const float ls = 1.0f + (fd90 - 1.0f) * pow5(1.0f - cwo);
-    const float vs = 1.0f + (fd90 - 1.0f) * pow5(1.0f - cwi);
-    return ls * vs * ef;
-}
-VX_D float gtr2(float ch, float sh, float a) {  // GTR2Aniso(ch, sh, 0, 1, a, a)
-    const float a2 = a * a;
-    const float s = (1.0f * 1.0f) / a2 + (0.0f * 0.0f) / a2;
-    const float t = sh * sh * s + ch * ch;
-    return 1.0f / (kPi * a * a * t * t);
-}
-VX_D float smith_g(float c, float a) {
-    const float a2 = a * a, c2 = c * c;
-    return 2.0f / (1.0f + sqrtf(1.0f + a2 * (1.0f - c2) / c2));
+// End of one TraceNextPath segment (RayGen.cu:146-173): accumulate, apply the
+// BSDF weight, bounce limits; writes the pass outputs when the path ends.
+VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segRad, V3 bop, float pdf, bool terminate,
+                  bool curDiffuse) {
+    const WaveBufs &w = a.wb;
+    V3 thr = xyz(w.pThr[s]), rad = xyz(w.pRad[s]);
+    rad += thr * segRad;
+    const bool cont = !(terminate || pdf <= 0.0f || is_null(bop));
+    if (cont) thr *= bop;
+    bool done = !cont;
+    meta.z += 1;
+    if (curDiffuse) meta.w += 1;
+    if (meta.z == a.totalBounceLimit || meta.w == a.diffuseBounceLimit) done = true;
+    if (done) {
+        path_end(a, px, py, rad, w.pPos[s].w);
+        meta.x &= ~(F_ALIVE | F_NEE | F_RESTIR);
+    } else {
+        w.pThr[s] = f4(thr, 0.0f);
+        w.pRad[s] = f4(rad, 0.0f);
+    }
 }
 
-struct Lobes { V3 C0; float sp, dp; };
-VX_D bool lobes(V3 albedo, float metalness, float cosForF, Lobes &L) {
-    const float lum = 0.299f * albedo.x + 0.587f * albedo.y + 0.114f * albedo.z;
-    const V3 tint = lum > 0.0f ? albedo / lum : V3(1.0f);
-    const V3 specColor = lerp3(V3(1.0f), tint, 0.0f);
-    L.C0 = lerp3(0.08f * 0.5f * specColor, albedo, metalness);
-    const V3 F = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cosForF);
-    const float avgF = (F.x + F.y + F.z) / 3.0f;
-    const float sw = avgF, dw = (1.0f - metalness) * (1.0f - avgF), tw = sw + dw;
-    if (tw < kSafeCos) return false;
-    float sp = sw / tw;
-    if (dw > kSafeCos && sw > kSafeCos) sp = clampf(sp, kMinLobe, 1.0f - kMinLobe);
-    L.sp = clampf(sp, 0.0f, 1.0f);
-    L.dp = fmaxf(0.0f, 1.0f - L.sp);
-    return true;
+VX_D SurfS load_surf(const WaveBufs &w, int s, bool &skipAlbedo) {
+    SurfS sf;
+    const float4 p = w.sPos[s], n = w.sNrm[s], g = w.sGeo[s], al = w.sAlb[s], wo = w.sWo[s];
+    sf.pos = xyz(p); sf.depth = p.w;
+    sf.normal = xyz(n); sf.roughness = n.w;
+    sf.geoNormal = xyz(g); sf.translucency = g.w;
+    sf.albedo = xyz(al); sf.metallic = al.w != 0.0f;
+    sf.wo = xyz(wo);
+    skipAlbedo = wo.w != 0.0f;
+    return sf;
 }
 
-// DisneyBSDFSample for rough surfaces (Bsdf.h:401-534); specular branch of
-// the reference only for roughness < 1e-5 (:403-425).
-VX_D void disney_sample(float u0, float u1, float u2, float u3, V3 n, V3 ng, V3 wo, V3 albedo, bool metallic,
-                        float translucency, float roughness, V3 &wi, V3 &bop, float &pdf) {
-    if (roughness < kRoughThresh) {
-        if (translucency < kTranslThresh) {
-            wi = reflect3(-wo, n);
-            if (dot(wi, n) <= 0.0f || dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; }
-            else { bop = albedo; pdf = 1.0f; }
-            pdf = fmaxf(pdf, kMinPdf);
-            bop = clamp_throughput(bop);
-        } else {
-            bop = V3(0.0f);  // refractive specular: not in the cube material table
-            pdf = 0.0f;
+VX_D void mis_params(const SkyDev &k, const SurfS &sf, int &nSun, int &nMis, float &sunMis, float &skyMis,
+                     float &brdfMis) {
+    const bool skipSun = (dot(sf.normal, k.sunDir) < 0.0f || dot(sf.geoNormal, k.sunDir) < 0.0f);
+    nSun = skipSun ? 0 : 1;
+    nMis = nSun + 2;
+    sunMis = float(nSun) / nMis;
+    skyMis = 1.0f / nMis;
+    brdfMis = 1.0f / nMis;
+}
+
+VX_D void store_ls(const WaveBufs &w, int s, const LSample &ls) {
+    w.ls0[s] = f4(ls.position, ls.solidAnglePdf);
+    w.ls1[s] = f4(ls.radiance, (float)ls.type);
+}
+VX_D LSample load_ls(const WaveBufs &w, int s) {
+    const float4 a = w.ls0[s], b = w.ls1[s];
+    return LSample{xyz(a), xyz(b), a.w, (int)b.w};
+}
+VX_D LSample invalid_ls() { return LSample{V3(0.f), V3(0.f), 0.f, LtInvalid}; }
+
+VX_D V3 shade_light(const SurfS &sf, bool skipAlbedo, const LSample &ls, const Reservoir &r) {
+    const V3 alb = skipAlbedo ? V3(1.0f) : sf.albedo;  // closesthit.cu:834
+    V3 bsdf;
+    float pdf;
+    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, alb, sf.metallic, sf.roughness, bsdf, pdf);
+    const float cosT = fmaxf(0.0f, dot(ls.position, sf.normal));
+    return bsdf * cosT * ls.radiance * r.weightSum / ls.solidAnglePdf;
+}
+
+// closesthit / miss for the segment's ray; candidate generation for NEE
+__global__ __launch_bounds__(256) void k_shade(TraceArgs a, int seg) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    int4 meta = w.pMeta[s];
+    if (!(meta.x & F_ALIVE)) return;
+    meta.x &= ~(F_NEE | F_RESTIR);
+    const size_t pi = (size_t)py * a.W + px;
+    const Hit h = unpack_hit(w.cHit[s], w.cT[s]);
+    const float4 p4 = w.pPos[s];
+    const V3 rayO = xyz(p4), rayD = xyz(w.pDir[s]);
+    float primaryDist = p4.w;
+    Rng rng{&a.bn, px, py, a.iterationIndex, meta.y};
+
+    if (!h.hit) {  // __miss__radiance (miss.cu:9-82)
+        if (seg == 0) {
+            a.resCur[pi] = empty_res();
+            a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            a.cur.material[pi] = (float)0xFFFF;
+            a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+            a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+            a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            w.pPos[s].w = kRayMax;
         }
+        seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false);
+        w.pMeta[s] = meta;
         return;
     }
-    const float metalness = metallic ? 1.0f : 0.0f;
-    const float alpha = fmaxf(roughness * roughness, kRoughThresh);
-    const float cwo = fmaxf(kSafeCos, dot(n, wo));
-    Lobes L;
-    if (!lobes(albedo, metalness, cwo, L)) { bop = V3(0.0f); pdf = 0.0f; return; }
-    if (u3 < L.sp) {
-        float ct = sqrtf((1.0f - u0) / (1.0f + (alpha * alpha - 1.0f) * u0));
-        ct = clampf(ct, kSafeCos, 1.0f);
-        const float st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
-        const float phi = kTwoPi * u1;
-        V3 wh(st * cosf(phi), st * sinf(phi), ct);
-        align_vector(n, wh);
-        wi = normalize(reflect3(-wo, wh));
-        if (dot(wi, n) <= 0.0f || dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; return; }
-        const float cwi = dot(wi, n);
-        const float cwh = fmaxf(kSafeCos, fabsf(dot(wh, n)));
-        const float cwowh = fmaxf(kSafeCos, fabsf(dot(wo, wh)));
-        const float swh = sqrtf(fmaxf(0.0f, 1.0f - cwh * cwh));
-        const float D = gtr2(cwh, swh, alpha);
-        const V3 Fs = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cwowh);
-        const float G = smith_g(cwo, alpha) * smith_g(cwi, alpha);
-        const V3 brdf = Fs * D * G / (4.0f * cwo * cwi);
-        float mpdf = fmaxf(D * cwh / (4.0f * cwowh), kMinPdf);
-        pdf = fmaxf(mpdf * fmaxf(L.sp, kMinPdf), kMinPdf);
-        bop = clamp_throughput(brdf * cwi / pdf);
-    } else {
-        const float ct = sqrtf(u0);
-        const float st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
-        const float phi = kTwoPi * u1;
-        wi = V3(st * cosf(phi), st * sinf(phi), ct);
-        align_vector(n, wi);
-        if (dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; return; }
-        const float cwi = fmaxf(kSafeCos, dot(wi, n));
-        const float fl = disney_diffuse_fresnel(cwo, cwi, roughness);
-        const V3 db = albedo * (1.0f - metalness) * fl / kPi;
-        float dpdf = fmaxf(cwi / kPi, kMinPdf);
-        pdf = fmaxf(dpdf * fmaxf(L.dp, kMinPdf), kMinPdf);
-        bop = clamp_throughput(db * cwi / pdf);
-    }
-}
 
-VX_D void disney_eval(V3 n, V3 ng, V3 wi, V3 wo, V3 albedo, bool metallic, float roughness, V3 &bsdf, float &pdf) {
-    bsdf = V3(0.0f);
-    if (roughness < kRoughThresh) { pdf = 0.0f; return; }
-    if (dot(wo, n) <= 0.0f || dot(wi, n) <= 0.0f || dot(wo, ng) <= 0.0f || dot(wi, ng) <= 0.0f) { pdf = 0.0f; return; }
-    const float metalness = metallic ? 1.0f : 0.0f;
-    const float alpha = fmaxf(roughness * roughness, kRoughThresh);
-    const float cwo = dot(wo, n), cwi = dot(wi, n);
-    const V3 wh = normalize(wi + wo);
-    const float cwh = fmaxf(kSafeCos, fabsf(dot(wh, n)));
-    const float cwowh = fmaxf(kSafeCos, fabsf(dot(wo, wh)));
-    Lobes L;
-    const bool ok = lobes(albedo, metalness, cwowh, L);
-    const V3 F = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cwowh);
-    V3 diffuse(0.0f);
-    if (!metallic) diffuse = albedo * (1.0f - metalness) * disney_diffuse_fresnel(cwo, cwi, roughness) / kPi;
-    const float swh = sqrtf(fmaxf(0.0f, 1.0f - cwh * cwh));
-    const float D = gtr2(cwh, swh, alpha);
-    const float G = smith_g(cwo, alpha) * smith_g(cwi, alpha);
-    const V3 spec = F * D * G / (4.0f * cwo * cwi);
-    bsdf = clamp_throughput(diffuse + spec);
-    if (!ok) { pdf = 0.0f; return; }
-    const float dpdf = fmaxf(cwi / kPi, kMinPdf);
-    const float spdf = fmaxf(D * cwh / (4.0f * cwowh), kMinPdf);
-    pdf = fmaxf(dpdf * fmaxf(L.dp, kMinPdf) + spdf * fmaxf(L.sp, kMinPdf), kMinPdf);
-}
-
-// ----------------------------------------------------------------- sampling
-struct Rng {
-    const BlueNoiseDev *bn;
-    int px, py, it, idx;
-    VX_D float next() {  // BlueNoiseRandGenerator::rand (RandGen.h:21-45)
-        const int i = px & 127, j = py & 127, s = it & 255, d = idx++;
-        const int rk = s ^ bn->rank[(d + (i + j * 128) * 8) & (128 * 128 * 8 - 1)];
-        int v = bn->sobol[d + rk * 256];
-        v ^= bn->scramble[(d % 8) + (i + j * 128) * 8];
-        return v / 256.0f;
-    }
-};
-VX_D float bn_rand(const BlueNoiseDev &bn, int px, int py, int it, int d) {
-    const int i = px & 127, j = py & 127, s = it & 255;
-    const int rk = s ^ bn.rank[(d + (i + j * 128) * 8) & (128 * 128 * 8 - 1)];
-    int v = bn.sobol[d + rk * 256];
-    v ^= bn.scramble[(d % 8) + (i + j * 128) * 8];
-    return v / 256.0f;
-}
-
-VX_D unsigned alias_sample(const AliasBin *b, int len, float u, float &pmf) {
-    const int offset = min(int(u * len), int(len - 1));
-    const float up = fminf(u * len - offset, 0.999999f);
-    const AliasBin e = b[offset];
-    if (up < e.q) { pmf = e.p; return offset; }
-    pmf = b[e.alias].p;
-    return e.alias;
-}
-
-struct LSample { V3 position, radiance; float solidAnglePdf; int type; };
-
-VX_D V3 ld3(const float4 *p, size_t i) { const float4 v = p[i]; return V3(v.x, v.y, v.z); }
-
-VX_D LSample sun_ls(const SkyDev &k, int idx) {
-    const int sx = idx % k.sunW, sy = idx / k.sunW;
-    LSample s;
-    s.solidAnglePdf = (k.sunW * k.sunH) / (kTwoPi * (1.0f - k.sunCosMax));
-    s.position = eq_area_cone_dir(k.sunDir, (sx + 0.5f) / float(k.sunW), (sy + 0.5f) / float(k.sunH), k.sunCosMax);
-    s.radiance = ld3(k.sun, (size_t)clampi(sy, 0, k.sunH - 1) * k.sunW + clampi(sx, 0, k.sunW - 1));
-    s.type = LtSun;
-    return s;
-}
-VX_D LSample sky_ls(const SkyDev &k, int idx) {
-    const int sx = idx % k.skyW, sy = idx / k.skyW;
-    LSample s;
-    s.solidAnglePdf = (k.skyW * k.skyH) / (4.0f * kPi);
-    s.position = eq_area_sphere_dir((sx + 0.5f) / float(k.skyW), (sy + 0.5f) / float(k.skyH));
-    s.radiance = ld3(k.sky, (size_t)sy * k.skyW + sx);
-    s.type = LtSky;
-    return s;
-}
-
-struct SurfS {
-    V3 pos, normal, geoNormal, albedo, wo;
-    float depth, roughness, translucency;
-    bool metallic;
-};
-
-VX_D float target_pdf(const LSample &ls, const SurfS &sf) {
-    if (ls.solidAnglePdf <= 0 || ls.type == LtInvalid) return 0.0f;
-    V3 fr;
-    float pdf;
-    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, pdf);
-    return luminance(ls.radiance * fr * fabsf(dot(ls.position, sf.normal)) / ls.solidAnglePdf);
-}
-VX_D float mis_weight(const SurfS &sf, const LSample &ls, float selPdf, float lightMis, float brdfMis) {
-    const float sa = ls.solidAnglePdf;
-    if (brdfMis == 0.0f || sa <= 0.0f || isinf(sa) || isnan(sa)) return lightMis * selPdf;
-    V3 fr;
-    float bp;
-    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, bp);
-    return (lightMis * (selPdf * sa) + brdfMis * bp) / sa;
-}
-VX_D bool stream_sample(Reservoir &r, uint32_t light, V2 uv, float rnd, float target, float invSrc) {
-    const float w = target * invSrc;
-    r.M += 1;
-    r.weightSum += w;
-    const bool sel = (rnd * r.weightSum < w);
-    if (sel) {
-        r.lightData = light | kValidBit;
-        r.uvData = (uint32_t)(saturate(uv.x) * 0xffff) | ((uint32_t)(saturate(uv.y) * 0xffff) << 16);
-        r.targetPdf = target;
-    }
-    return sel;
-}
-VX_D bool combine(Reservoir &r, const Reservoir &n, float rnd, float target) {
-    const float w = target * (n.weightSum * n.M);
-    r.M += n.M;
-    r.weightSum += w;
-    const bool sel = (rnd * r.weightSum < w);
-    if (sel) { r.lightData = n.lightData; r.uvData = n.uvData; r.targetPdf = target; }
-    return sel;
-}
-VX_D void finalize(Reservoir &r, float num, float den) {
-    const float d = r.targetPdf * den;
-    r.weightSum = (d == 0.0f) ? 0.0f : (r.weightSum * num) / d;
-}
-VX_D Reservoir empty_res() { return Reservoir{0u, 0u, 0.0f, 0.0f, 0.0f}; }
-
-VX_D bool light_from_res(const SkyDev &k, LSample &ls, const Reservoir &r) {
-    const uint32_t li = r.lightData & kIndexMask;
-    const float ux = (float)(r.uvData & 0xffff) / float(0xffff), uy = (float)(r.uvData >> 16) / float(0xffff);
-    if (li == kSkyLight) {
-        const int x = clampi(int(ux * k.skyW), 0, k.skyW - 1), y = clampi(int(uy * k.skyH), 0, k.skyH - 1);
-        ls = sky_ls(k, y * k.skyW + x);
-    } else if (li == kSunLight) {
-        const int x = clampi(int(ux * k.sunW), 0, k.sunW - 1), y = clampi(int(uy * k.sunH), 0, k.sunH - 1);
-        ls = sun_ls(k, y * k.sunW + x);
-    }
-    return li < kInvalidLight;
-}
-
-VX_D int reflect_view(int p, int n) {
-    if (p < 0) p = -p;
-    if (p >= n) p = 2 * n - p - 1;
-    return p;
-}
-
-VX_D bool prev_surface(const TraceArgs &a, int px, int py, SurfS &sf, int x, int y) {
-    if (x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y) return false;
-    const size_t i = (size_t)y * a.W + x;
-    sf.depth = a.prev.depth[i];
-    if (sf.depth == kRayMax) return false;
-    const float4 nr = a.prev.normalRough[i], gt = a.prev.geoNormalThin[i], mp = a.prev.matParam[i];
-    const float j0 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 0);
-    const float j1 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 1);
-    const V2 uv = (V2((float)x, (float)y) + V2(j0, j1)) * a.prevCam.invRes;
-    const V3 vd = a.prevCam.uv_to_dir(uv);
-    sf.pos = a.prevCam.pos + vd * sf.depth;
-    sf.wo = -vd;
-    sf.normal = V3(nr.x, nr.y, nr.z);
-    sf.geoNormal = V3(gt.x, gt.y, gt.z);
-    sf.albedo = ld3(a.prev.albedo, i);
-    sf.roughness = nr.w;
-    sf.metallic = (mp.x == 1.0f);
-    sf.translucency = mp.y;
-    return true;
-}
-
-VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
-    V3 emission(0.0f);
-    V2 uv = eq_area_sphere_uv(dir);
-    {
-        const V2 UV(uv.x * (float)k.skyW, uv.y * (float)k.skyH);
-        const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
-        const V2 fr = UV - V2(fx0 + 0.5f, fy0 + 0.5f);
-        const V2 f2 = fr * fr, f3 = f2 * fr;
-        const V2 w1 = -2.0f * f3 + 3.0f * f2;
-        const V2 w0 = 1.0f - w1;
-        const int tx0 = (int)fx0, ty0 = (int)fy0;
-        const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
-        V3 out(0.0f);
-        float sum = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            int x = tx0 + (i & 1), y = ty0 + (i >> 1);
-            if (x >= k.skyW) x %= k.skyW;
-            if (x < 0) x = k.skyW - (-x) % k.skyW;
-            y = clampi(y, 0, k.skyH - 1);
-            sum += wt[i];
-            out += ld3(k.sky, (size_t)y * k.skyW + x) * wt[i];
-        }
-        out /= sum;
-        emission += out;
-    }
-    if (eq_area_cone_uv(uv, k.sunDir, dir, k.sunCosMax)) {
-        int x = (int)(uv.x * k.sunW), y = (int)(uv.y * k.sunH);
-        if (x >= k.sunW) x %= k.sunW;
-        if (x < 0) x = k.sunW - (-x) % k.sunW;
-        emission += ld3(k.sun, (size_t)clampi(y, 0, k.sunH - 1) * k.sunW + clampi(x, 0, k.sunW - 1));
-    }
-    return emission;
-}
-
-struct PathState {
-    V3 pos, wi, radiance, bop;
-    float distance, pdf;
-    int depth;
-    bool hitFirstDiffuse, terminate, curDiffuse;
-};
-
-VX_D void store_res(const TraceArgs &a, size_t pi, const Reservoir &r) { a.resCur[pi] = r; }
-
-// closesthit for a cube face (closesthit.cu:10-852)
-VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps, const Hit &h) {
-    const size_t pi = (size_t)py * a.W + px;
-    const V3 wo = -ps.wi;
-    ps.distance = h.t;
+    // __closesthit__radiance (closesthit.cu:10-316)
+    const V3 wo = -rayD;
     V3 frontPos, backPos, ng;
-    hit_frame(h, ps.pos, ps.wi, frontPos, backPos, ng);
-    if (ps.depth == 0) a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    hit_frame(h, rayO, rayD, frontPos, backPos, ng);
+    if (seg == 0) a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const MatDev &m = a.mats[h.id];
     SurfS sf;
     sf.geoNormal = ng;
     sf.wo = wo;
     sf.albedo = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
     sf.roughness = m.roughness;
-    if (ps.hitFirstDiffuse) sf.roughness = fminf(sf.roughness * 2.0f + 0.1f, 1.0f);
+    if (meta.x & F_HFD) sf.roughness = fminf(sf.roughness * 2.0f + 0.1f, 1.0f);
     const bool isDiffuse = sf.roughness > kRoughThresh;
     sf.metallic = m.metallic != 0;
     sf.translucency = m.translucency;
     sf.normal = lerp3(ng, ng, 0.2f);
-    ps.curDiffuse = isDiffuse;
-    if (ps.depth == 0) {
+    if (seg == 0) {
         a.cur.material[pi] = (float)m.materialId;
         a.cur.normalRough[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, sf.roughness);
         a.cur.geoNormalThin[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, m.thin ? 1.0f : 0.0f);
         a.cur.matParam[pi] = make_float4(sf.metallic ? 1.0f : 0.0f, sf.translucency, 0.0f, 0.0f);
     }
+    V3 swi, sbop;
+    float spdf;
     {
         const float u0 = rng.next(), u1 = rng.next(), u2 = rng.next(), u3 = rng.next();
-        V3 swi, sbop;
-        float spdf;
         disney_sample(u0, u1, u2, u3, sf.normal, sf.geoNormal, wo, sf.albedo, sf.metallic, sf.translucency,
                       sf.roughness, swi, sbop, spdf);
-        if (spdf <= 0.0f) ps.terminate = true;
-        ps.pos = frontPos;
-        ps.wi = swi;
-        ps.bop = sbop;
-        ps.pdf = spdf;
     }
+    const bool terminate = spdf <= 0.0f;
     bool skipAlbedo = false;
-    if (ps.depth == 0) {
-        ps.hitFirstDiffuse = true;
+    if (seg == 0) {
+        meta.x |= F_HFD;
         a.cur.albedo[pi] = make_float4(sf.albedo.x, sf.albedo.y, sf.albedo.z, 1.0f);
         skipAlbedo = true;
+        primaryDist = h.t;
     }
-    const bool restir = ps.depth == 0;
+    w.pPos[s] = f4(frontPos, primaryDist);
+    w.pDir[s] = f4(swi, spdf);
     if (!isDiffuse) {
-        if (restir) store_res(a, pi, empty_res());
+        if (seg == 0) a.resCur[pi] = empty_res();
+        seg_end(a, s, px, py, meta, V3(0.0f), sbop, spdf, terminate, false);
+        meta.y = rng.idx;
+        w.pMeta[s] = meta;
         return;
     }
+
+    // NEE candidates: sun and sky from their alias tables (closesthit.cu:318-414)
     sf.pos = frontPos;
     sf.depth = h.t;
     const SkyDev &k = a.sky;
-    const bool skipSun = (dot(sf.normal, k.sunDir) < 0.0f || dot(sf.geoNormal, k.sunDir) < 0.0f);
-    const int nSun = skipSun ? 0 : 1;
-    const int nMis = nSun + 2;
-    const float sunMis = float(nSun) / nMis, skyMis = 1.0f / nMis, brdfMis = 1.0f / nMis;
-
-    Reservoir localRes = empty_res();
-    finalize(localRes, 1.0f, (float)nMis);
-    localRes.M = 1;
-
+    int nSun, nMis;
+    float sunMis, skyMis, brdfMis;
+    mis_params(k, sf, nSun, nMis, sunMis, skyMis, brdfMis);
     Reservoir sunRes = empty_res();
-    LSample sunLs{V3(0.f), V3(0.f), 0.f, LtInvalid};
+    int sunSel = -1;
     if (nSun) {
         float src;
         const int idx = (int)alias_sample(k.sunAlias, k.sunW * k.sunH, rng.next(), src);
@@ -672,13 +292,12 @@ VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps,
         const float blended = mis_weight(sf, cand, src, sunMis, brdfMis);
         const float tp = target_pdf(cand, sf);
         const float rr = rng.next();
-        if (stream_sample(sunRes, kSunLight, uv, rr, tp, 1.0f / blended)) sunLs = cand;
+        if (stream_sample(sunRes, kSunLight, uv, rr, tp, 1.0f / blended)) sunSel = idx;
     }
     finalize(sunRes, 1.0f, (float)nMis);
     sunRes.M = 1;
-
     Reservoir skyRes = empty_res();
-    LSample skyLs{V3(0.f), V3(0.f), 0.f, LtInvalid};
+    int skySel = -1;
     {
         float src;
         const float r0 = rng.next(), r1 = rng.next();
@@ -689,44 +308,87 @@ VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps,
         const float blended = mis_weight(sf, cand, src, skyMis, brdfMis);
         const float tp = target_pdf(cand, sf);
         const float rr = rng.next();
-        if (stream_sample(skyRes, kSkyLight, uv, rr, tp, 1.0f / blended)) skyLs = cand;
+        if (stream_sample(skyRes, kSkyLight, uv, rr, tp, 1.0f / blended)) skySel = idx;
     }
     finalize(skyRes, 1.0f, (float)nMis);
     skyRes.M = 1;
-
-    Reservoir brdfRes = empty_res();
-    LSample brdfLs{V3(0.f), V3(0.f), 0.f, LtInvalid};
+    // BRDF candidate direction; its ray is traced by the next k_closest
     {
-        float lightSrcPdf = 0.0f;
-        uint32_t li = kInvalidLight;
-        V2 uv(0.0f, 0.0f);
-        LSample cand{V3(0.f), V3(0.f), 0.f, LtInvalid};
         const float u0 = rng.next(), u1 = rng.next(), u2 = rng.next(), u3 = rng.next();
         V3 sd, bop;
         float bp;
         disney_sample(u0, u1, u2, u3, sf.normal, sf.geoNormal, wo, sf.albedo, sf.metallic, sf.translucency,
                       sf.roughness, sd, bop, bp);
-        if (bp > 0.0f) {
-            const Hit bh = dda_closest(a.world, frontPos, sd, 3.402823466e+38f);
-            if (!bh.hit) {
+        w.cRayO[s] = f4(frontPos, bp > 0.0f ? kFltMax : -1.0f);
+        w.cRayD[s] = f4(sd, 0.0f);
+    }
+    w.sPos[s] = f4(frontPos, h.t);
+    w.sNrm[s] = f4(sf.normal, sf.roughness);
+    w.sGeo[s] = f4(sf.geoNormal, sf.translucency);
+    w.sAlb[s] = f4(sf.albedo, sf.metallic ? 1.0f : 0.0f);
+    w.sWo[s] = f4(wo, skipAlbedo ? 1.0f : 0.0f);
+    w.pBop[s] = f4(sbop, terminate ? 1.0f : 0.0f);
+    w.rSun[s] = sunRes;
+    w.rSky[s] = skyRes;
+    w.nIdx[s] = make_int4(sunSel, skySel, -1, 0);
+    meta.x |= F_NEE | (seg == 0 ? F_RESTIR : 0);
+    meta.y = rng.idx;
+    w.pMeta[s] = meta;
+}
+
+// BRDF candidate from its traced ray, RIS over {local, sun, sky, BRDF}, visibility ray
+__global__ __launch_bounds__(256) void k_nee(TraceArgs a) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    int4 meta = w.pMeta[s];
+    if (!(meta.x & F_NEE)) return;
+    bool skipAlbedo;
+    const SurfS sf = load_surf(w, s, skipAlbedo);
+    const SkyDev &k = a.sky;
+    Rng rng{&a.bn, px, py, a.iterationIndex, meta.y};
+    int nSun, nMis;
+    float sunMis, skyMis, brdfMis;
+    mis_params(k, sf, nSun, nMis, sunMis, skyMis, brdfMis);
+
+    Reservoir localRes = empty_res();
+    finalize(localRes, 1.0f, (float)nMis);
+    localRes.M = 1;
+    const Reservoir sunRes = w.rSun[s], skyRes = w.rSky[s];
+    const int4 idx = w.nIdx[s];
+    const LSample sunLs = idx.x >= 0 ? sun_ls(k, idx.x) : invalid_ls();
+    const LSample skyLs = idx.y >= 0 ? sky_ls(k, idx.y) : invalid_ls();
+
+    Reservoir brdfRes = empty_res();
+    LSample brdfLs = invalid_ls();
+    {
+        float lightSrcPdf = 0.0f;
+        uint32_t li = kInvalidLight;
+        V2 uv(0.0f, 0.0f);
+        LSample cand = invalid_ls();
+        if (w.cRayO[s].w >= 0.0f) {
+            const V3 sd = xyz(w.cRayD[s]);
+            const Hit bh = unpack_hit(w.cHit[s], w.cT[s]);
+            if (!bh.hit) {  // __miss__bsdf_light
                 if (eq_area_cone_uv(uv, k.sunDir, sd, k.sunCosMax)) {
                     li = kSunLight;
                     int x = (int)(uv.x * k.sunW - 0.5f), y = (int)(uv.y * k.sunH - 0.5f);
                     if (x >= k.sunW) x %= k.sunW;
                     if (x < 0) x = k.sunW - ((-x) % k.sunW);
                     y = clampi(y, 0, k.sunH - 1);
-                    const int idx = y * k.sunW + x;
-                    cand = sun_ls(k, idx);
+                    const int l = y * k.sunW + x;
+                    cand = sun_ls(k, l);
                     cand.position = sd;
-                    lightSrcPdf = k.sunAlias[idx].p;
+                    lightSrcPdf = k.sunAlias[l].p;
                 } else {
                     li = kSkyLight;
                     uv = eq_area_sphere_uv(sd);
                     const int x = (int)(uv.x * k.skyW - 0.5f), y = (int)(uv.y * k.skyH - 0.5f);
-                    const int idx = y * k.skyW + x;
-                    cand = sky_ls(k, idx);
+                    const int l = y * k.skyW + x;
+                    cand = sky_ls(k, l);
                     cand.position = sd;
-                    lightSrcPdf = k.skyAlias[idx].p;
+                    lightSrcPdf = k.skyAlias[l].p;
                 }
             }
         }
@@ -748,207 +410,205 @@ VX_D void shade_hit(const TraceArgs &a, int px, int py, Rng &rng, PathState &ps,
     const bool selBrdf = combine(ris, brdfRes, rng.next(), brdfRes.targetPdf);
     finalize(ris, 1.0f, 1.0f);
     ris.M = 1;
-    LSample ls = selBrdf ? brdfLs : (selSky ? skyLs : (selSun ? sunLs : LSample{V3(0.f), V3(0.f), 0.f, LtInvalid}));
+    const LSample ls = selBrdf ? brdfLs : (selSky ? skyLs : (selSun ? sunLs : invalid_ls()));
+    const bool trace = ls.type != LtInvalid && ris.lightData != 0;
+    w.oRayO[4 * s] = f4(sf.pos, 0.0f);
+    w.oRayD[4 * s] = f4(ls.position, trace ? kRayMax : -1.0f);
+    w.rRis[s] = ris;
+    store_ls(w, s, ls);
+    meta.y = rng.idx;
+    w.pMeta[s] = meta;
+}
 
+// visibility of the RIS sample; seg 0: ReSTIR temporal reuse (Restir.h:11-415,
+// closesthit.cu:626-851) up to its visibility rays; seg > 0: final shading.
+__global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    int4 meta = w.pMeta[s];
+    if (!(meta.x & F_NEE)) return;
+    bool skipAlbedo;
+    const SurfS sf = load_surf(w, s, skipAlbedo);
+    const SkyDev &k = a.sky;
+    Reservoir ris = w.rRis[s];
+    LSample ls = load_ls(w, s);
     bool visible = false;
     if (ls.type != LtInvalid && ris.lightData != 0) {
-        visible = !dda_occluded(a.world, frontPos, ls.position, 0.0f, kRayMax);
+        visible = !w.oHit[4 * s];
         if (!visible) { ris.lightData = 0; ris.weightSum = 0; }
     }
+    if (!(meta.x & F_RESTIR)) {
+        V3 segRad(0.0f);
+        if (ls.type != LtInvalid && ris.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, ris);
+        const float4 b = w.pBop[s];
+        seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true);
+        w.pMeta[s] = meta;
+        return;
+    }
 
+    Rng rng{&a.bn, px, py, a.iterationIndex, meta.y};
     Reservoir rr = empty_res();
-    if (restir) {
-        combine(rr, ris, 0.5f, ris.targetPdf);
-        const CamDev &pc = a.prevCam;
-        const V3 prevW = sf.pos;  // + motion (static geometry: 0)
-        const V2 puv = pc.dir_to_uv(normalize(prevW - pc.pos));
-        const int ppx = (int)(puv.x * pc.res.x), ppy = (int)(puv.y * pc.res.y);
-        const V3 dd = prevW - pc.pos;
-        const float expDepth = sqrtf(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z);
-        // three temporal taps (scalars, not arrays: no runtime-indexed private memory)
-        int ox0, oy0, ox1, oy1, ox2, oy2;
-        ox0 = ppx - px; oy0 = ppy - py;
-        {
-            const float r0 = rng.next(), r1 = rng.next();
-            V2 u = V2(r0 * 2.0f - 1.0f, r1 * 2.0f - 1.0f);
-            V2 dsk(0.0f, 0.0f);
-            if (!(fabsf(u.x) < 1e-10f && fabsf(u.y) < 1e-10f)) {
-                float th, r;
-                if (fabsf(u.x) > fabsf(u.y)) { r = u.x; th = kPiOver4 * (u.y / u.x); }
-                else { r = u.y; th = kPiOver2 - kPiOver4 * (u.x / u.y); }
-                dsk = V2(cosf(th) * r, sinf(th) * r);
-            }
-            dsk = dsk * 64.0f;
-            ox1 = ppx - px + (int)dsk.x; oy1 = ppy - py + (int)dsk.y;
+    combine(rr, ris, 0.5f, ris.targetPdf);
+    const CamDev &pc = a.prevCam;
+    const V3 prevW = sf.pos;  // + motion (static geometry: 0)
+    const V2 puv = pc.dir_to_uv(normalize(prevW - pc.pos));
+    const int ppx = (int)(puv.x * pc.res.x), ppy = (int)(puv.y * pc.res.y);
+    const V3 dd = prevW - pc.pos;
+    const float expDepth = sqrtf(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z);
+    // three temporal taps (scalars, not arrays: no runtime-indexed private memory)
+    const int ox0 = ppx - px, oy0 = ppy - py;
+    int ox1, oy1, ox2, oy2;
+    {
+        const float r0 = rng.next(), r1 = rng.next();
+        const V2 dsk = restir_disk(r0, r1);
+        ox1 = ppx - px + (int)dsk.x; oy1 = ppy - py + (int)dsk.y;
+    }
+    {
+        const float r0 = rng.next(), r1 = rng.next();
+        const V2 dsk = restir_disk(r0, r1);
+        ox2 = (int)dsk.x; oy2 = (int)dsk.y;
+    }
+    unsigned cached = 0;
+    int selLoop = -1;
+    float tapM0 = 0, tapM1 = 0, tapM2 = 0;
+    for (int i = 0; i < 3; ++i) {
+        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
+        SurfS ts;
+        if (!prev_surface(a, px, py, ts, x, y)) continue;
+        const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
+        const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
+        const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
+        if (!(nOk && dOk && rOk)) continue;
+        cached |= (1u << i);
+        Reservoir pr = a.resPrev[(size_t)y * a.W + x];
+        if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
+        if (pr.M > 20.0f) pr.M = 20.0f;
+        if (i == 0) tapM0 = pr.M; else if (i == 1) tapM1 = pr.M; else tapM2 = pr.M;
+        float nw = 0.0f;
+        LSample cand = invalid_ls();
+        if (pr.lightData != 0) {
+            if (!light_from_res(k, cand, pr)) pr = empty_res();
+            nw = target_pdf(cand, sf);
         }
-        {
-            const float r0 = rng.next(), r1 = rng.next();
-            V2 u = V2(r0 * 2.0f - 1.0f, r1 * 2.0f - 1.0f);
-            V2 dsk(0.0f, 0.0f);
-            if (!(fabsf(u.x) < 1e-10f && fabsf(u.y) < 1e-10f)) {
-                float th, r;
-                if (fabsf(u.x) > fabsf(u.y)) { r = u.x; th = kPiOver4 * (u.y / u.x); }
-                else { r = u.y; th = kPiOver2 - kPiOver4 * (u.x / u.y); }
-                dsk = V2(cosf(th) * r, sinf(th) * r);
-            }
-            dsk = dsk * 64.0f;
-            ox2 = (int)dsk.x; oy2 = (int)dsk.y;
-        }
-        unsigned cached = 0;
-        int selLoop = -1;
-        for (int i = 0; i < 3; ++i) {
+        if (combine(rr, pr, rng.next(), nw)) { ls = cand; selLoop = i; }
+    }
+    // bias-correction rays: the selected light seen from each accepted tap's surface
+    float psv0 = 0, psv1 = 0, psv2 = 0;
+    for (int i = 0; i < 3; ++i) {
+        float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = make_float4(0.f, 0.f, 0.f, -1.0f);
+        if (rr.lightData != 0 && (cached & (1u << i))) {
             const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
             const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
             SurfS ts;
-            if (!prev_surface(a, px, py, ts, x, y)) continue;
-            const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
-            const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
-            const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
-            if (!(nOk && dOk && rOk)) continue;
-            cached |= (1u << i);
-            Reservoir pr = a.resPrev[(size_t)y * a.W + x];
-            if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
-            if (pr.M > 20.0f) pr.M = 20.0f;
-            float nw = 0.0f;
-            LSample cand{V3(0.f), V3(0.f), 0.f, LtInvalid};
-            if (pr.lightData != 0) {
-                if (!light_from_res(k, cand, pr)) pr = empty_res();
-                nw = target_pdf(cand, sf);
+            prev_surface(a, px, py, ts, x, y);
+            LSample sel = invalid_ls();
+            light_from_res(k, sel, rr);
+            const float psv = target_pdf(sel, ts);
+            if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;
+            if (psv > 0 && !(i == 0 && i == selLoop)) {
+                ro = f4(ts.pos, 0.01f + 0.01f * ts.depth);
+                rd = f4(ls.position, kRayMax);
             }
-            if (combine(rr, pr, rng.next(), nw)) { ls = cand; selLoop = i; }
         }
-        if (rr.lightData != 0) {
-            float piv = rr.targetPdf, piSum = rr.targetPdf * 1;
-            for (int i = 0; i < 3; ++i) {
-                if ((cached & (1u << i)) == 0) continue;
-                const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
-            const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
-                SurfS ts;
-                prev_surface(a, px, py, ts, x, y);
-                LSample sel{V3(0.f), V3(0.f), 0.f, LtInvalid};
-                light_from_res(k, sel, rr);
-                float psv = target_pdf(sel, ts);
-                if (psv > 0 && !(i == 0 && i == selLoop)) {
-                    const float extra = 0.01f + 0.01f * ts.depth;
-                    if (dda_occluded(a.world, ts.pos, ls.position, extra, kRayMax)) psv = 0.0f;
-                }
-                Reservoir pr = a.resPrev[(size_t)y * a.W + x];
-                if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
-                if (pr.M > 20.0f) pr.M = 20.0f;
-                if (selLoop == i) piv = psv;
-                piSum += psv * pr.M;
-            }
-            finalize(rr, piv, piSum);
-        }
-        if (ls.type != LtInvalid) {
-            visible = !dda_occluded(a.world, frontPos, ls.position, 0.0f, kRayMax);
-            if (!visible) { rr.lightData = 0; rr.weightSum = 0; }
-        }
+        w.oRayO[4 * s + 1 + i] = ro;
+        w.oRayD[4 * s + 1 + i] = rd;
+        w.oHit[4 * s + 1 + i] = 0;
     }
-    const Reservoir &shade = restir ? rr : ris;
-    if (ls.type != LtInvalid && shade.lightData != 0 && visible) {
-        const V3 alb = skipAlbedo ? V3(1.0f) : sf.albedo;
-        V3 bsdf;
-        float pdf;
-        disney_eval(sf.normal, sf.geoNormal, ls.position, wo, alb, sf.metallic, sf.roughness, bsdf, pdf);
-        const float cosT = fmaxf(0.0f, dot(ls.position, sf.normal));
-        ps.radiance += bsdf * cosT * ls.radiance * shade.weightSum / ls.solidAnglePdf;
+    // final visibility: with no tap selected the sample is the RIS one and the
+    // ray equals the RIS visibility ray, whose result is already in oHit[4s]
+    if (ls.type != LtInvalid && selLoop >= 0) {
+        w.oRayO[4 * s] = f4(sf.pos, 0.0f);
+        w.oRayD[4 * s] = f4(ls.position, kRayMax);
+    } else {
+        w.oRayD[4 * s] = make_float4(0.f, 0.f, 0.f, -1.0f);
     }
-    if (restir) store_res(a, pi, rr);
+    w.rRR[s] = rr;
+    store_ls(w, s, ls);
+    w.nIdx[s] = make_int4(0, 0, selLoop, (int)cached);
+    w.tapPsv[s] = make_float4(psv0, psv1, psv2, 0.0f);
+    w.tapM[s] = make_float4(tapM0, tapM1, tapM2, 0.0f);
+    meta.y = rng.idx;
+    w.pMeta[s] = meta;
 }
 
-VX_D void shade_miss(const TraceArgs &a, int px, int py, PathState &ps) {
+// seg 0: bias-corrected ReSTIR weight, final visibility, shading, reservoir store
+__global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    int4 meta = w.pMeta[s];
+    if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
     const size_t pi = (size_t)py * a.W + px;
-    if (ps.depth == 0) {
-        store_res(a, pi, empty_res());
+    bool skipAlbedo;
+    const SurfS sf = load_surf(w, s, skipAlbedo);
+    Reservoir rr = w.rRR[s];
+    const LSample ls = load_ls(w, s);
+    const int4 idx = w.nIdx[s];
+    const int selLoop = idx.z;
+    const unsigned cached = (unsigned)idx.w;
+    if (rr.lightData != 0) {
+        const float4 psv4 = w.tapPsv[s], m4 = w.tapM[s];
+        float piv = rr.targetPdf, piSum = rr.targetPdf * 1;
+        for (int i = 0; i < 3; ++i) {
+            if ((cached & (1u << i)) == 0) continue;
+            float psv = i == 0 ? psv4.x : (i == 1 ? psv4.y : psv4.z);
+            const float M = i == 0 ? m4.x : (i == 1 ? m4.y : m4.z);
+            if (w.oHit[4 * s + 1 + i]) psv = 0.0f;
+            if (selLoop == i) piv = psv;
+            piSum += psv * M;
+        }
+        finalize(rr, piv, piSum);
+    }
+    bool visible = false;
+    if (ls.type != LtInvalid) {
+        visible = !w.oHit[4 * s];
+        if (!visible) { rr.lightData = 0; rr.weightSum = 0; }
+    }
+    V3 segRad(0.0f);
+    if (ls.type != LtInvalid && rr.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, rr);
+    a.resCur[pi] = rr;
+    const float4 b = w.pBop[s];
+    seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true);
+    w.pMeta[s] = meta;
+}
+
+// C2 bring-up mode: primary hit G-buffer + sky, no NEE
+__global__ __launch_bounds__(256) void k_primary_gbuffer(TraceArgs a) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    const size_t pi = (size_t)py * a.W + px;
+    const Hit h = unpack_hit(w.cHit[s], w.cT[s]);
+    const V3 o = xyz(w.pPos[s]), d = xyz(w.pDir[s]);
+    if (!h.hit) {
+        a.resCur[pi] = empty_res();
         a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         a.cur.material[pi] = (float)0xFFFF;
         a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
         a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
         a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
-    ps.radiance = sky_emission(a.sky, ps.wi);
-    ps.distance = kRayMax;
-    ps.terminate = true;
-}
-
-__global__ __launch_bounds__(256) void k_trace(TraceArgs a) {
-    // 16x16 pixel workgroup; wave w owns the 8x8 quadrant (w&1, w>>1)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int py = a.y0 + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    if (px >= a.W || py >= a.y1) return;
-    Rng rng{&a.bn, px, py, a.iterationIndex, 0};
-    const size_t pi = (size_t)py * a.W + px;
-    const float j0 = rng.next(), j1 = rng.next();
-    const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
-    PathState ps;
-    ps.pos = a.cam.pos;
-    ps.wi = a.cam.uv_to_dir(uv);
-    ps.depth = 0;
-    ps.hitFirstDiffuse = false;
-    ps.curDiffuse = false;
-    V3 radiance(0.0f), throughput(1.0f);
-    float primaryDist = kRayMax;
-
-    if (a.primaryOnly) {
-        const Hit h = dda_closest(a.world, ps.pos, ps.wi, kRayMax);
-        if (!h.hit) {
-            shade_miss(a, px, py, ps);
-            a.cur.depth[pi] = kRayMax;
-            a.illum[pi] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, kRayMax);
-            return;
-        }
-        V3 fp, bp, ng;
-        hit_frame(h, ps.pos, ps.wi, fp, bp, ng);
-        const MatDev &m = a.mats[h.id];
-        const V3 alb = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
-        a.cur.material[pi] = (float)m.materialId;
-        a.cur.normalRough[pi] = make_float4(ng.x, ng.y, ng.z, m.roughness);
-        a.cur.geoNormalThin[pi] = make_float4(ng.x, ng.y, ng.z, 0.0f);
-        a.cur.matParam[pi] = make_float4(m.metallic ? 1.0f : 0.0f, m.translucency, 0.0f, 0.0f);
-        a.cur.albedo[pi] = make_float4(alb.x, alb.y, alb.z, 1.0f);
-        a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        a.cur.depth[pi] = h.t;
-        a.illum[pi] = make_float4(0.0f, 0.0f, 0.0f, h.t);
+        const V3 e = sky_emission(a.sky, d);
+        a.cur.depth[pi] = kRayMax;
+        a.illum[pi] = make_float4(e.x, e.y, e.z, kRayMax);
         return;
     }
-
-    int total = 0, diffuse = 0;
-    bool done = false;
-    while (!done) {
-        // TraceNextPath (RayGen.cu:8-100)
-        ps.bop = V3(1.0f);
-        ps.pdf = 0.0f;
-        ps.radiance = V3(0.0f);
-        ps.distance = kRayMax;
-        ps.terminate = false;
-        ps.curDiffuse = false;
-        const Hit h = dda_closest(a.world, ps.pos, ps.wi, kRayMax);
-        if (h.hit) shade_hit(a, px, py, rng, ps, h);
-        else shade_miss(a, px, py, ps);
-        radiance += throughput * ps.radiance;
-        bool cont = !(ps.terminate || ps.pdf <= 0.0f || is_null(ps.bop));
-        if (cont) throughput *= ps.bop;
-        done = !cont;
-        ++total;
-        if (ps.curDiffuse) ++diffuse;
-        if (total == a.totalBounceLimit || diffuse == a.diffuseBounceLimit) done = true;
-        if (ps.depth == 0) primaryDist = ps.distance;
-        ++ps.depth;
-    }
-    if (isnan(radiance.x) || isnan(radiance.y) || isnan(radiance.z)) radiance = V3(0.5f);
-    a.cur.depth[pi] = primaryDist;
-    if (a.accum) {
-        // spp > 1: average the passes' radiance (SURVEY.md §8d), depth from the last pass
-        float4 acc = a.accumFirst ? make_float4(0.f, 0.f, 0.f, 0.f) : a.accum[pi];
-        acc.x += radiance.x * a.accumScale;
-        acc.y += radiance.y * a.accumScale;
-        acc.z += radiance.z * a.accumScale;
-        acc.w = primaryDist;
-        a.accum[pi] = acc;
-    }
-    a.illum[pi] = make_float4(radiance.x, radiance.y, radiance.z, primaryDist);
+    V3 fp, bp, ng;
+    hit_frame(h, o, d, fp, bp, ng);
+    const MatDev &m = a.mats[h.id];
+    const V3 alb = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
+    a.cur.material[pi] = (float)m.materialId;
+    a.cur.normalRough[pi] = make_float4(ng.x, ng.y, ng.z, m.roughness);
+    a.cur.geoNormalThin[pi] = make_float4(ng.x, ng.y, ng.z, 0.0f);
+    a.cur.matParam[pi] = make_float4(m.metallic ? 1.0f : 0.0f, m.translucency, 0.0f, 0.0f);
+    a.cur.albedo[pi] = make_float4(alb.x, alb.y, alb.z, 1.0f);
+    a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    a.cur.depth[pi] = h.t;
+    a.illum[pi] = make_float4(0.0f, 0.0f, 0.0f, h.t);
 }
 
 __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *rays, int *out, float *t, int mode) {
@@ -986,13 +646,25 @@ hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, f
     return hipGetLastError();
 }
 
-namespace {
-}  // namespace
-
 hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
-    const int rows = a.y1 - a.y0;
-    dim3 g((a.W + 15) / 16, (rows + 15) / 16);
-    hipLaunchKernelGGL(k_trace, g, dim3(256), 0, st, a);
+    const dim3 g((a.nSlots + 255) / 256), g4((4 * a.nSlots + 255) / 256), b(256);
+    hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 2);
+    if (a.primaryOnly) {
+        hipLaunchKernelGGL(k_primary_gbuffer, g, b, 0, st, a);
+        return hipGetLastError();
+    }
+    for (int seg = 0; seg < a.totalBounceLimit; ++seg) {
+        if (seg > 0) hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
+        hipLaunchKernelGGL(k_shade, g, b, 0, st, a, seg);
+        hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 1);
+        hipLaunchKernelGGL(k_nee, g, b, 0, st, a);
+        hipLaunchKernelGGL(k_occluded, g, b, 0, st, a, 1);
+        hipLaunchKernelGGL(k_restir, g, b, 0, st, a, seg);
+        if (seg == 0) {
+            hipLaunchKernelGGL(k_occluded, g4, b, 0, st, a, 4);
+            hipLaunchKernelGGL(k_finish, g, b, 0, st, a);
+        }
+    }
     return hipGetLastError();
 }
 

@@ -1,0 +1,585 @@
+// vxpt -- device-side building blocks of the trace pass (included by trace.hip only):
+// voxel DDA, safe spawn, Disney BSDF, blue-noise sampler, light sampling,
+// reservoirs, sky lookup.  See trace.hip for the pass structure.
+#pragma once
+#include "vx_internal.hpp"
+
+namespace vx {
+namespace {
+
+constexpr uint32_t kValidBit = 0x80000000u, kIndexMask = 0x7FFFFFFFu;
+constexpr uint32_t kInvalidLight = 0x7FFFFFFFu, kSkyLight = 0x7FFFFFFEu, kSunLight = 0x7FFFFFFDu;
+enum { LtInvalid = 0, LtSky = 1, LtSun = 2 };
+constexpr float kRoughThresh = 0.00001f, kTranslThresh = 0.001f;
+constexpr float kMinPdf = 1e-5f, kMaxThroughput = 32.0f, kMinLobe = 0.05f;
+
+// ----------------------------------------------------------------- voxel DDA
+VX_D bool is_cube(int id) { return id >= 1 && id <= 12; }
+
+struct Hit { int hit, x, y, z, face, id; float t; };
+
+VX_D int entry_face(int a, int s) {
+    return a == 0 ? (s > 0 ? 2 : 3) : (a == 1 ? (s > 0 ? 1 : 0) : (s > 0 ? 5 : 4));
+}
+
+// The walk keeps every per-axis quantity in named scalars (no runtime-indexed
+// arrays: those would live in scratch on gfx950).
+struct Ray3 {
+    float ox, oy, oz, dx, dy, dz, ix, iy, iz;
+    int sx, sy, sz;
+    bool mx, my, mz;
+};
+struct Cell {
+    int x, y, z;
+    float tx, ty, tz;  // t of the next plane crossing on each axis (INF if the axis does not move)
+};
+
+// t of the next plane after cell c along one axis; the only formula for plane t,
+// so skipped and stepped walks produce identical values.
+VX_D float next_t(int c, int s, float o, float inv, bool mv) {
+    if (!mv) return INFINITY;
+    return ((float)(s > 0 ? c + 1 : c) - o) * inv;
+}
+// axis order of the reference tie rule (VoxelEngine.cu:1040-1166 strict '<'):
+// smallest t first, ties to Z, then Y, then X
+VX_D int pick3(float tx, float ty, float tz) {
+    if (tx < ty) return tx < tz ? 0 : 2;
+    return ty < tz ? 1 : 2;
+}
+VX_D bool before(float t1, int a1, float t2, int a2) { return t1 < t2 || (t1 == t2 && a1 > a2); }
+
+VX_D int macro_of(const WorldDev &w, int x, int y, int z) { return (x >> 4) + w.mx * ((z >> 4) + w.mz * (y >> 4)); }
+VX_D int brick_bit(int x, int y, int z) { return ((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3)); }
+VX_D int cell_id(const WorldDev &w, int m, uint64_t mw, int x, int y, int z, bool &brickOcc) {
+    const int lb = brick_bit(x, y, z);
+    brickOcc = (mw >> lb) & 1ull;
+    if (!brickOcc) return 0;
+    const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
+    return w.bricks[((size_t)m * 64 + lb) * 64 + lc];
+}
+
+// Advance one axis to the cell it occupies when the walk leaves the box through
+// the crossing (Te, ea): exactly the planes the cell-by-cell walk would cross first.
+VX_D void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int lo, int hi, int ab, float Te, int ea) {
+    int est = clampi((int)floorf(o + Te * d), lo, hi);
+    est = s > 0 ? max(est, cb) : min(est, cb);
+    while (est != cb) {
+        const float te = ((float)(s > 0 ? est : est + 1) - o) * inv;  // plane entering est
+        if (before(te, ab, Te, ea)) break;
+        est -= s;
+    }
+    float tn = ((float)(s > 0 ? est + 1 : est) - o) * inv;
+    while (before(tn, ab, Te, ea)) {
+        est += s;
+        tn = ((float)(s > 0 ? est + 1 : est) - o) * inv;
+    }
+    cb = est;
+    tb = tn;
+}
+// Jump from the current cell to the last cell of an empty box [lo, lo+size) the
+// ray visits; the box exit crossing is then the walk's next step.
+VX_D void skip_box(const Ray3 &r, Cell &c, int size) {
+    const int lx = c.x & ~(size - 1), ly = c.y & ~(size - 1), lz = c.z & ~(size - 1);
+    const int hx = lx + size - 1, hy = ly + size - 1, hz = lz + size - 1;
+    const float Tx = r.mx ? ((float)(r.sx > 0 ? hx + 1 : lx) - r.ox) * r.ix : INFINITY;
+    const float Ty = r.my ? ((float)(r.sy > 0 ? hy + 1 : ly) - r.oy) * r.iy : INFINITY;
+    const float Tz = r.mz ? ((float)(r.sz > 0 ? hz + 1 : lz) - r.oz) * r.iz : INFINITY;
+    const int ea = pick3(Tx, Ty, Tz);
+    const float Te = ea == 0 ? Tx : (ea == 1 ? Ty : Tz);
+    if (ea == 0) { c.x = r.sx > 0 ? hx : lx; c.tx = Tx; }
+    else if (r.mx) skip_axis(c.x, c.tx, r.sx, r.ox, r.dx, r.ix, lx, hx, 0, Te, ea);
+    if (ea == 1) { c.y = r.sy > 0 ? hy : ly; c.ty = Ty; }
+    else if (r.my) skip_axis(c.y, c.ty, r.sy, r.oy, r.dy, r.iy, ly, hy, 1, Te, ea);
+    if (ea == 2) { c.z = r.sz > 0 ? hz : lz; c.tz = Tz; }
+    else if (r.mz) skip_axis(c.z, c.tz, r.sz, r.oz, r.dz, r.iz, lz, hz, 2, Te, ea);
+}
+
+VX_D bool slab(float o, float d, float W, int a, float &t0, float &t1, int &ax) {
+    if (d == 0.0f) return !(o < 0.0f || o >= W);
+    const float inv = 1.0f / d;
+    const float ta = (0.0f - o) * inv, tb = (W - o) * inv;
+    const float lo = ta < tb ? ta : tb, hi = ta < tb ? tb : ta;
+    if (lo > t0) { t0 = lo; ax = a; }
+    if (hi < t1) t1 = hi;
+    return true;
+}
+
+// Start a walk; returns false if the ray never meets the world box.  For an
+// origin outside the box, `outside` is set and the entry crossing (axis `ax`,
+// t `tEnter`) is already taken.
+VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outside, int &ax, float &tEnter) {
+    r.ox = o.x; r.oy = o.y; r.oz = o.z;
+    r.dx = d.x; r.dy = d.y; r.dz = d.z;
+    r.mx = d.x != 0.0f; r.my = d.y != 0.0f; r.mz = d.z != 0.0f;
+    r.sx = d.x > 0.0f ? 1 : -1; r.sy = d.y > 0.0f ? 1 : -1; r.sz = d.z > 0.0f ? 1 : -1;
+    r.ix = r.mx ? 1.0f / d.x : 0.0f; r.iy = r.my ? 1.0f / d.y : 0.0f; r.iz = r.mz ? 1.0f / d.z : 0.0f;
+    c.x = (int)floorf(o.x); c.y = (int)floorf(o.y); c.z = (int)floorf(o.z);
+    outside = !(c.x >= 0 && c.x < w.wx && c.y >= 0 && c.y < w.wy && c.z >= 0 && c.z < w.wz);
+    if (outside) {
+        // slab test against the world box, axes in x, y, z order
+        float t0 = -INFINITY, t1 = INFINITY;
+        ax = -1;
+        if (!slab(o.x, d.x, (float)w.wx, 0, t0, t1, ax) || !slab(o.y, d.y, (float)w.wy, 1, t0, t1, ax) ||
+            !slab(o.z, d.z, (float)w.wz, 2, t0, t1, ax))
+            return false;
+        if (ax < 0 || t0 > t1 || t1 <= 0.0f) return false;
+        c.x = ax == 0 ? (d.x > 0.0f ? 0 : w.wx - 1) : clampi((int)floorf(o.x + t0 * d.x), 0, w.wx - 1);
+        c.y = ax == 1 ? (d.y > 0.0f ? 0 : w.wy - 1) : clampi((int)floorf(o.y + t0 * d.y), 0, w.wy - 1);
+        c.z = ax == 2 ? (d.z > 0.0f ? 0 : w.wz - 1) : clampi((int)floorf(o.z + t0 * d.z), 0, w.wz - 1);
+        tEnter = t0;
+    }
+    c.tx = next_t(c.x, r.sx, r.ox, r.ix, r.mx);
+    c.ty = next_t(c.y, r.sy, r.oy, r.iy, r.my);
+    c.tz = next_t(c.z, r.sz, r.oz, r.iz, r.mz);
+    return true;
+}
+
+// One step of the walk: cross the nearest plane.  Returns the crossed plane's
+// t and coordinate and the face of the entered cell the crossing goes through.
+VX_D void walk_step(const Ray3 &r, Cell &c, float &t, int &planeCoord, int &face) {
+    const int a = pick3(c.tx, c.ty, c.tz);
+    if (a == 0) {
+        t = c.tx; planeCoord = r.sx > 0 ? c.x + 1 : c.x; face = r.sx > 0 ? 2 : 3;
+        c.x += r.sx; c.tx = next_t(c.x, r.sx, r.ox, r.ix, true);
+    } else if (a == 1) {
+        t = c.ty; planeCoord = r.sy > 0 ? c.y + 1 : c.y; face = r.sy > 0 ? 1 : 0;
+        c.y += r.sy; c.ty = next_t(c.y, r.sy, r.oy, r.iy, true);
+    } else {
+        t = c.tz; planeCoord = r.sz > 0 ? c.z + 1 : c.z; face = r.sz > 0 ? 5 : 4;
+        c.z += r.sz; c.tz = next_t(c.z, r.sz, r.oz, r.iz, true);
+    }
+}
+VX_D bool in_world(const WorldDev &w, const Cell &c) {
+    return (unsigned)c.x < (unsigned)w.wx && (unsigned)c.y < (unsigned)w.wy && (unsigned)c.z < (unsigned)w.wz;
+}
+// face through which a ray entering the world box along axis ax enters the cell
+VX_D int entry_face_of(int ax, V3 d) {
+    return ax == 0 ? (d.x > 0.0f ? 2 : 3) : (ax == 1 ? (d.y > 0.0f ? 1 : 0) : (d.z > 0.0f ? 5 : 4));
+}
+
+// Closest front-facing cube face along the ray, t <= tmax (radiance rays).
+// Contract A4': entering cube cell b from a hits iff b != a, or the crossed
+// plane is a chunk boundary, or a is outside the world.
+VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
+    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+    Ray3 r;
+    Cell c;
+    bool outside;
+    int ax = -1;
+    float tEnter = 0;
+    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return h;
+    int m = macro_of(w, c.x, c.y, c.z);
+    uint64_t mw = w.macro[m];
+    bool occ;
+    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
+    if (outside) {
+        if (tEnter > tmax) return h;
+        if (is_cube(prevId) && tEnter >= 0.0f) {
+            h = {1, c.x, c.y, c.z, entry_face_of(ax, d), prevId, tEnter};
+            return h;
+        }
+    }
+    const int maxSteps = w.wx + w.wy + w.wz + 3;
+    for (int s = 0; s < maxSteps; ++s) {
+        if (prevId == 0) {
+            if (mw == 0) skip_box(r, c, 16);
+            else if (!occ) skip_box(r, c, 4);
+        }
+        float t;
+        int planeCoord, face;
+        walk_step(r, c, t, planeCoord, face);
+        if (!(t <= tmax)) return h;
+        if (!in_world(w, c)) return h;
+        const int nm = macro_of(w, c.x, c.y, c.z);
+        if (nm != m) { m = nm; mw = w.macro[m]; }
+        const int b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
+        if (is_cube(b) && (b != prevId || (planeCoord & 31) == 0)) {
+            h = {1, c.x, c.y, c.z, face, b, t};
+            return h;
+        }
+        prevId = b;
+    }
+    return h;
+}
+
+// Any face crossing with tmin <= t <= tmax (visibility rays: no culling, so
+// leaving a cube cell counts too).
+VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
+    Ray3 r;
+    Cell c;
+    bool outside;
+    int ax = -1;
+    float tEnter = 0;
+    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return false;
+    int m = macro_of(w, c.x, c.y, c.z);
+    uint64_t mw = w.macro[m];
+    bool occ;
+    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
+    if (outside) {
+        if (tEnter > tmax) return false;
+        if (is_cube(prevId) && tEnter >= tmin) return true;
+    }
+    const int maxSteps = w.wx + w.wy + w.wz + 3;
+    for (int s = 0; s < maxSteps; ++s) {
+        if (prevId == 0) {
+            if (mw == 0) skip_box(r, c, 16);
+            else if (!occ) skip_box(r, c, 4);
+        }
+        float t;
+        int planeCoord, face;
+        walk_step(r, c, t, planeCoord, face);
+        if (!(t <= tmax)) return false;
+        const bool chunkPlane = (planeCoord & 31) == 0;
+        const bool out = !in_world(w, c);
+        int b = 0;
+        if (!out) {
+            const int nm = macro_of(w, c.x, c.y, c.z);
+            if (nm != m) { m = nm; mw = w.macro[m]; }
+            b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
+        }
+        if (t >= tmin) {
+            const bool frontB = is_cube(b) && (b != prevId || chunkPlane);
+            const bool backA = is_cube(prevId) && (prevId != b || chunkPlane || out);
+            if (frontB || backA) return true;
+        }
+        if (out) return false;
+        prevId = b;
+    }
+    return false;
+}
+
+VX_D V3 face_normal(int f) {
+    return f == 0 ? V3(0, 1, 0) : f == 1 ? V3(0, -1, 0) : f == 2 ? V3(-1, 0, 0) : f == 3 ? V3(1, 0, 0)
+         : f == 4 ? V3(0, 0, 1) : V3(0, 0, -1);
+}
+
+// Hit point on the face plane + self-intersection-safe spawn points
+// (SelfHit.h:539-656 specialised to unit quads under one translation instance).
+VX_D void hit_frame(const Hit &h, V3 o, V3 d, V3 &front, V3 &back, V3 &ng) {
+    V3 p = o + d * h.t;
+    const bool ax0 = h.face == 2 || h.face == 3, ax1 = h.face < 2;  // else z (faces 4, 5)
+    // blend instead of selecting a field by index: keeps h and p in registers
+    const int cell = (ax0 ? h.x : 0) + (ax1 ? h.y : 0) + ((!ax0 && !ax1) ? h.z : 0);
+    const bool high = (h.face == 0 || h.face == 3 || h.face == 4);
+    const int plane = cell + (high ? 1 : 0);
+    const float pa = (float)plane;
+    ng = face_normal(h.face);
+    const int T = (cell >> 5) * 32;
+    const float planeLocal = (float)(plane - T), planeWorld = (float)plane, Tf = (float)T;
+    const float c0t = 5.9604648328104529e-08f, c1t = 1.1920930376163769e-07f;
+    const float eps = mul_ru(c1t, 2.0f);
+    const float triErr = fma_ru(c0t, planeLocal, eps);
+    const float cI = 1.19209317972490680404007434844970703125E-7f;
+    const float wldErr = fma_ru(cI, planeLocal, mul_ru(cI, Tf));
+    const float objErr = fma_ru(cI, planeWorld, mul_ru(cI, Tf));
+    float off = add_ru(objErr, triErr);
+    off = off + wldErr;
+    // outward normal component along the axis is +1 for the high faces, -1 otherwise
+    const float n = high ? 1.0f : -1.0f;
+    const float fa = high ? fma_ru(off, n, pa) : fma_rd(off, n, pa);
+    const float ba = high ? fma_rd(-off, n, pa) : fma_ru(-off, n, pa);
+    front = V3(ax0 ? fa : p.x, ax1 ? fa : p.y, (!ax0 && !ax1) ? fa : p.z);
+    back = V3(ax0 ? ba : p.x, ax1 ? ba : p.y, (!ax0 && !ax1) ? ba : p.z);
+}
+
+// ----------------------------------------------------------------- BSDF
+VX_D V3 clamp_throughput(V3 v) {
+    const float l = luminance(v), a = fabsf(l);
+    if (a > kMaxThroughput && a > 0.0f) return v * (kMaxThroughput / a);
+    return v;
+}
+VX_D float disney_diffuse_fresnel(float cwo, float cwi, float r) {
+    const float eb = lerpf(0.0f, 0.5f, r), ef = lerpf(1.0f, 1.0f / 1.51f, r);
+    const float fd90 = eb + 2.0f * r * cwi * cwi;
+    const float ls = 1.0f + (fd90 - 1.0f) * pow5(1.0f - cwo);
+    const float vs = 1.0f + (fd90 - 1.0f) * pow5(1.0f - cwi);
+    return ls * vs * ef;
+}
+VX_D float gtr2(float ch, float sh, float a) {  // GTR2Aniso(ch, sh, 0, 1, a, a)
+    const float a2 = a * a;
+    const float s = (1.0f * 1.0f) / a2 + (0.0f * 0.0f) / a2;
+    const float t = sh * sh * s + ch * ch;
+    return 1.0f / (kPi * a * a * t * t);
+}
+VX_D float smith_g(float c, float a) {
+    const float a2 = a * a, c2 = c * c;
+    return 2.0f / (1.0f + sqrtf(1.0f + a2 * (1.0f - c2) / c2));
+}
+
+struct Lobes { V3 C0; float sp, dp; };
+VX_D bool lobes(V3 albedo, float metalness, float cosForF, Lobes &L) {
+    const float lum = 0.299f * albedo.x + 0.587f * albedo.y + 0.114f * albedo.z;
+    const V3 tint = lum > 0.0f ? albedo / lum : V3(1.0f);
+    const V3 specColor = lerp3(V3(1.0f), tint, 0.0f);
+    L.C0 = lerp3(0.08f * 0.5f * specColor, albedo, metalness);
+    const V3 F = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cosForF);
+    const float avgF = (F.x + F.y + F.z) / 3.0f;
+    const float sw = avgF, dw = (1.0f - metalness) * (1.0f - avgF), tw = sw + dw;
+    if (tw < kSafeCos) return false;
+    float sp = sw / tw;
+    if (dw > kSafeCos && sw > kSafeCos) sp = clampf(sp, kMinLobe, 1.0f - kMinLobe);
+    L.sp = clampf(sp, 0.0f, 1.0f);
+    L.dp = fmaxf(0.0f, 1.0f - L.sp);
+    return true;
+}
+
+// DisneyBSDFSample for rough surfaces (Bsdf.h:401-534); specular branch of
+// the reference only for roughness < 1e-5 (:403-425).
+VX_D void disney_sample(float u0, float u1, float u2, float u3, V3 n, V3 ng, V3 wo, V3 albedo, bool metallic,
+                        float translucency, float roughness, V3 &wi, V3 &bop, float &pdf) {
+    if (roughness < kRoughThresh) {
+        if (translucency < kTranslThresh) {
+            wi = reflect3(-wo, n);
+            if (dot(wi, n) <= 0.0f || dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; }
+            else { bop = albedo; pdf = 1.0f; }
+            pdf = fmaxf(pdf, kMinPdf);
+            bop = clamp_throughput(bop);
+        } else {
+            bop = V3(0.0f);  // refractive specular: not in the cube material table
+            pdf = 0.0f;
+        }
+        return;
+    }
+    const float metalness = metallic ? 1.0f : 0.0f;
+    const float alpha = fmaxf(roughness * roughness, kRoughThresh);
+    const float cwo = fmaxf(kSafeCos, dot(n, wo));
+    Lobes L;
+    if (!lobes(albedo, metalness, cwo, L)) { bop = V3(0.0f); pdf = 0.0f; return; }
+    if (u3 < L.sp) {
+        float ct = sqrtf((1.0f - u0) / (1.0f + (alpha * alpha - 1.0f) * u0));
+        ct = clampf(ct, kSafeCos, 1.0f);
+        const float st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+        const float phi = kTwoPi * u1;
+        V3 wh(st * cosf(phi), st * sinf(phi), ct);
+        align_vector(n, wh);
+        wi = normalize(reflect3(-wo, wh));
+        if (dot(wi, n) <= 0.0f || dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; return; }
+        const float cwi = dot(wi, n);
+        const float cwh = fmaxf(kSafeCos, fabsf(dot(wh, n)));
+        const float cwowh = fmaxf(kSafeCos, fabsf(dot(wo, wh)));
+        const float swh = sqrtf(fmaxf(0.0f, 1.0f - cwh * cwh));
+        const float D = gtr2(cwh, swh, alpha);
+        const V3 Fs = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cwowh);
+        const float G = smith_g(cwo, alpha) * smith_g(cwi, alpha);
+        const V3 brdf = Fs * D * G / (4.0f * cwo * cwi);
+        float mpdf = fmaxf(D * cwh / (4.0f * cwowh), kMinPdf);
+        pdf = fmaxf(mpdf * fmaxf(L.sp, kMinPdf), kMinPdf);
+        bop = clamp_throughput(brdf * cwi / pdf);
+    } else {
+        const float ct = sqrtf(u0);
+        const float st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+        const float phi = kTwoPi * u1;
+        wi = V3(st * cosf(phi), st * sinf(phi), ct);
+        align_vector(n, wi);
+        if (dot(wi, ng) <= 0.0f) { bop = V3(0.0f); pdf = 0.0f; return; }
+        const float cwi = fmaxf(kSafeCos, dot(wi, n));
+        const float fl = disney_diffuse_fresnel(cwo, cwi, roughness);
+        const V3 db = albedo * (1.0f - metalness) * fl / kPi;
+        float dpdf = fmaxf(cwi / kPi, kMinPdf);
+        pdf = fmaxf(dpdf * fmaxf(L.dp, kMinPdf), kMinPdf);
+        bop = clamp_throughput(db * cwi / pdf);
+    }
+}
+
+VX_D void disney_eval(V3 n, V3 ng, V3 wi, V3 wo, V3 albedo, bool metallic, float roughness, V3 &bsdf, float &pdf) {
+    bsdf = V3(0.0f);
+    if (roughness < kRoughThresh) { pdf = 0.0f; return; }
+    if (dot(wo, n) <= 0.0f || dot(wi, n) <= 0.0f || dot(wo, ng) <= 0.0f || dot(wi, ng) <= 0.0f) { pdf = 0.0f; return; }
+    const float metalness = metallic ? 1.0f : 0.0f;
+    const float alpha = fmaxf(roughness * roughness, kRoughThresh);
+    const float cwo = dot(wo, n), cwi = dot(wi, n);
+    const V3 wh = normalize(wi + wo);
+    const float cwh = fmaxf(kSafeCos, fabsf(dot(wh, n)));
+    const float cwowh = fmaxf(kSafeCos, fabsf(dot(wo, wh)));
+    Lobes L;
+    const bool ok = lobes(albedo, metalness, cwowh, L);
+    const V3 F = L.C0 + (V3(1.0f) - L.C0) * pow5(1.0f - cwowh);
+    V3 diffuse(0.0f);
+    if (!metallic) diffuse = albedo * (1.0f - metalness) * disney_diffuse_fresnel(cwo, cwi, roughness) / kPi;
+    const float swh = sqrtf(fmaxf(0.0f, 1.0f - cwh * cwh));
+    const float D = gtr2(cwh, swh, alpha);
+    const float G = smith_g(cwo, alpha) * smith_g(cwi, alpha);
+    const V3 spec = F * D * G / (4.0f * cwo * cwi);
+    bsdf = clamp_throughput(diffuse + spec);
+    if (!ok) { pdf = 0.0f; return; }
+    const float dpdf = fmaxf(cwi / kPi, kMinPdf);
+    const float spdf = fmaxf(D * cwh / (4.0f * cwowh), kMinPdf);
+    pdf = fmaxf(dpdf * fmaxf(L.dp, kMinPdf) + spdf * fmaxf(L.sp, kMinPdf), kMinPdf);
+}
+
+// ----------------------------------------------------------------- sampling
+struct Rng {
+    const BlueNoiseDev *bn;
+    int px, py, it, idx;
+    VX_D float next() {  // BlueNoiseRandGenerator::rand (RandGen.h:21-45)
+        const int i = px & 127, j = py & 127, s = it & 255, d = idx++;
+        const int rk = s ^ bn->rank[(d + (i + j * 128) * 8) & (128 * 128 * 8 - 1)];
+        int v = bn->sobol[d + rk * 256];
+        v ^= bn->scramble[(d % 8) + (i + j * 128) * 8];
+        return v / 256.0f;
+    }
+};
+VX_D float bn_rand(const BlueNoiseDev &bn, int px, int py, int it, int d) {
+    const int i = px & 127, j = py & 127, s = it & 255;
+    const int rk = s ^ bn.rank[(d + (i + j * 128) * 8) & (128 * 128 * 8 - 1)];
+    int v = bn.sobol[d + rk * 256];
+    v ^= bn.scramble[(d % 8) + (i + j * 128) * 8];
+    return v / 256.0f;
+}
+
+VX_D unsigned alias_sample(const AliasBin *b, int len, float u, float &pmf) {
+    const int offset = min(int(u * len), int(len - 1));
+    const float up = fminf(u * len - offset, 0.999999f);
+    const AliasBin e = b[offset];
+    if (up < e.q) { pmf = e.p; return offset; }
+    pmf = b[e.alias].p;
+    return e.alias;
+}
+
+struct LSample { V3 position, radiance; float solidAnglePdf; int type; };
+
+VX_D V3 ld3(const float4 *p, size_t i) { const float4 v = p[i]; return V3(v.x, v.y, v.z); }
+
+VX_D LSample sun_ls(const SkyDev &k, int idx) {
+    const int sx = idx % k.sunW, sy = idx / k.sunW;
+    LSample s;
+    s.solidAnglePdf = (k.sunW * k.sunH) / (kTwoPi * (1.0f - k.sunCosMax));
+    s.position = eq_area_cone_dir(k.sunDir, (sx + 0.5f) / float(k.sunW), (sy + 0.5f) / float(k.sunH), k.sunCosMax);
+    s.radiance = ld3(k.sun, (size_t)clampi(sy, 0, k.sunH - 1) * k.sunW + clampi(sx, 0, k.sunW - 1));
+    s.type = LtSun;
+    return s;
+}
+VX_D LSample sky_ls(const SkyDev &k, int idx) {
+    const int sx = idx % k.skyW, sy = idx / k.skyW;
+    LSample s;
+    s.solidAnglePdf = (k.skyW * k.skyH) / (4.0f * kPi);
+    s.position = eq_area_sphere_dir((sx + 0.5f) / float(k.skyW), (sy + 0.5f) / float(k.skyH));
+    s.radiance = ld3(k.sky, (size_t)sy * k.skyW + sx);
+    s.type = LtSky;
+    return s;
+}
+
+struct SurfS {
+    V3 pos, normal, geoNormal, albedo, wo;
+    float depth, roughness, translucency;
+    bool metallic;
+};
+
+VX_D float target_pdf(const LSample &ls, const SurfS &sf) {
+    if (ls.solidAnglePdf <= 0 || ls.type == LtInvalid) return 0.0f;
+    V3 fr;
+    float pdf;
+    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, pdf);
+    return luminance(ls.radiance * fr * fabsf(dot(ls.position, sf.normal)) / ls.solidAnglePdf);
+}
+VX_D float mis_weight(const SurfS &sf, const LSample &ls, float selPdf, float lightMis, float brdfMis) {
+    const float sa = ls.solidAnglePdf;
+    if (brdfMis == 0.0f || sa <= 0.0f || isinf(sa) || isnan(sa)) return lightMis * selPdf;
+    V3 fr;
+    float bp;
+    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, bp);
+    return (lightMis * (selPdf * sa) + brdfMis * bp) / sa;
+}
+VX_D bool stream_sample(Reservoir &r, uint32_t light, V2 uv, float rnd, float target, float invSrc) {
+    const float w = target * invSrc;
+    r.M += 1;
+    r.weightSum += w;
+    const bool sel = (rnd * r.weightSum < w);
+    if (sel) {
+        r.lightData = light | kValidBit;
+        r.uvData = (uint32_t)(saturate(uv.x) * 0xffff) | ((uint32_t)(saturate(uv.y) * 0xffff) << 16);
+        r.targetPdf = target;
+    }
+    return sel;
+}
+VX_D bool combine(Reservoir &r, const Reservoir &n, float rnd, float target) {
+    const float w = target * (n.weightSum * n.M);
+    r.M += n.M;
+    r.weightSum += w;
+    const bool sel = (rnd * r.weightSum < w);
+    if (sel) { r.lightData = n.lightData; r.uvData = n.uvData; r.targetPdf = target; }
+    return sel;
+}
+VX_D void finalize(Reservoir &r, float num, float den) {
+    const float d = r.targetPdf * den;
+    r.weightSum = (d == 0.0f) ? 0.0f : (r.weightSum * num) / d;
+}
+VX_D Reservoir empty_res() { return Reservoir{0u, 0u, 0.0f, 0.0f, 0.0f}; }
+
+VX_D bool light_from_res(const SkyDev &k, LSample &ls, const Reservoir &r) {
+    const uint32_t li = r.lightData & kIndexMask;
+    const float ux = (float)(r.uvData & 0xffff) / float(0xffff), uy = (float)(r.uvData >> 16) / float(0xffff);
+    if (li == kSkyLight) {
+        const int x = clampi(int(ux * k.skyW), 0, k.skyW - 1), y = clampi(int(uy * k.skyH), 0, k.skyH - 1);
+        ls = sky_ls(k, y * k.skyW + x);
+    } else if (li == kSunLight) {
+        const int x = clampi(int(ux * k.sunW), 0, k.sunW - 1), y = clampi(int(uy * k.sunH), 0, k.sunH - 1);
+        ls = sun_ls(k, y * k.sunW + x);
+    }
+    return li < kInvalidLight;
+}
+
+VX_D int reflect_view(int p, int n) {
+    if (p < 0) p = -p;
+    if (p >= n) p = 2 * n - p - 1;
+    return p;
+}
+
+VX_D bool prev_surface(const TraceArgs &a, int px, int py, SurfS &sf, int x, int y) {
+    if (x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y) return false;
+    const size_t i = (size_t)y * a.W + x;
+    sf.depth = a.prev.depth[i];
+    if (sf.depth == kRayMax) return false;
+    const float4 nr = a.prev.normalRough[i], gt = a.prev.geoNormalThin[i], mp = a.prev.matParam[i];
+    const float j0 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 0);
+    const float j1 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 1);
+    const V2 uv = (V2((float)x, (float)y) + V2(j0, j1)) * a.prevCam.invRes;
+    const V3 vd = a.prevCam.uv_to_dir(uv);
+    sf.pos = a.prevCam.pos + vd * sf.depth;
+    sf.wo = -vd;
+    sf.normal = V3(nr.x, nr.y, nr.z);
+    sf.geoNormal = V3(gt.x, gt.y, gt.z);
+    sf.albedo = ld3(a.prev.albedo, i);
+    sf.roughness = nr.w;
+    sf.metallic = (mp.x == 1.0f);
+    sf.translucency = mp.y;
+    return true;
+}
+
+VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
+    V3 emission(0.0f);
+    V2 uv = eq_area_sphere_uv(dir);
+    {
+        const V2 UV(uv.x * (float)k.skyW, uv.y * (float)k.skyH);
+        const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
+        const V2 fr = UV - V2(fx0 + 0.5f, fy0 + 0.5f);
+        const V2 f2 = fr * fr, f3 = f2 * fr;
+        const V2 w1 = -2.0f * f3 + 3.0f * f2;
+        const V2 w0 = 1.0f - w1;
+        const int tx0 = (int)fx0, ty0 = (int)fy0;
+        const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
+        V3 out(0.0f);
+        float sum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int x = tx0 + (i & 1), y = ty0 + (i >> 1);
+            if (x >= k.skyW) x %= k.skyW;
+            if (x < 0) x = k.skyW - (-x) % k.skyW;
+            y = clampi(y, 0, k.skyH - 1);
+            sum += wt[i];
+            out += ld3(k.sky, (size_t)y * k.skyW + x) * wt[i];
+        }
+        out /= sum;
+        emission += out;
+    }
+    if (eq_area_cone_uv(uv, k.sunDir, dir, k.sunCosMax)) {
+        int x = (int)(uv.x * k.sunW), y = (int)(uv.y * k.sunH);
+        if (x >= k.sunW) x %= k.sunW;
+        if (x < 0) x = k.sunW - (-x) % k.sunW;
+        emission += ld3(k.sun, (size_t)clampi(y, 0, k.sunH - 1) * k.sunW + clampi(x, 0, k.sunW - 1));
+    }
+    return emission;
+}
+
+}  // namespace
+}  // namespace vx

@@ -65,6 +65,38 @@ struct GBuf {
     float *depth, *material;
 };
 
+// Per-pixel state of the wavefront trace pass (trace.hip).  One slot per
+// pixel in 8x8-tile order (slot = tile*64 + lane, tiles row-major over the
+// band), so each 64-lane wave owns one tile in every stage.
+struct WaveBufs {
+    // path state
+    float4 *pPos;   // ray origin xyz, primary distance
+    float4 *pDir;   // ray direction xyz, BSDF pdf
+    float4 *pThr;   // throughput xyz
+    float4 *pRad;   // accumulated radiance xyz
+    int4 *pMeta;    // flags, sampler dimension, total segments, diffuse segments
+    float4 *pBop;   // BSDF weight of the sampled continuation xyz, terminate flag
+    // closest-hit queue (camera / path / BRDF-candidate rays) and its results
+    float4 *cRayO, *cRayD;  // o xyz + tmax (< 0: inactive), d xyz
+    int4 *cHit;             // cell xyz, face | id << 4 | hit << 12
+    float *cT;
+    // the diffuse surface being shaded (NEE)
+    float4 *sPos;   // front spawn point xyz, hit t
+    float4 *sNrm;   // shading normal xyz, roughness
+    float4 *sGeo;   // geometric normal xyz, translucency
+    float4 *sAlb;   // albedo xyz, metallic
+    float4 *sWo;    // wo xyz, skip-albedo flag
+    Reservoir *rSun, *rSky, *rRis, *rRR;
+    int4 *nIdx;     // sun light index, sky light index, selected temporal tap, cached-tap mask
+    float4 *ls0;    // selected light sample: direction xyz, solid-angle pdf
+    float4 *ls1;    // radiance xyz, light type
+    float4 *tapPsv; // target pdf of the selection at the three temporal taps, first-visibility flag
+    float4 *tapM;   // the taps' clamped M
+    // visibility queue: 4 rays per slot (0: RIS/final visibility, 1-3: bias-correction taps)
+    float4 *oRayO, *oRayD;  // o xyz + tmin, d xyz + tmax (< 0: inactive)
+    uint8_t *oHit;
+};
+
 struct TraceArgs {
     WorldDev world;
     SkyDev sky;
@@ -82,6 +114,8 @@ struct TraceArgs {
     int primaryOnly;
     float accumScale;           // 1/spp
     int accumFirst;
+    WaveBufs wb;
+    int tilesX, nSlots;         // 8x8 tiles across the frame width; slots in the band
 };
 
 // kernel launchers (defined in the .hip translation units)

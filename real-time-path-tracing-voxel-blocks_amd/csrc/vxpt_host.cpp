@@ -171,6 +171,7 @@ struct vxpt_ctx {
     float4 *ffColor = nullptr;
     Reservoir *ffRes = nullptr;
     bool denoiseInputIsAccum = false;
+    WaveBufs wb{};
     std::vector<void *> allocs;
 
     vxpt_denoise_params yamlDenoise{};
@@ -438,6 +439,9 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.totalBounceLimit = c->totalBounce;
     a.diffuseBounceLimit = c->diffuseBounce;
     a.primaryOnly = (flags & VXPT_TRACE_PRIMARY_ONLY) ? 1 : 0;
+    a.wb = c->wb;
+    a.tilesX = (c->W + 7) / 8;
+    a.nSlots = a.tilesX * ((a.y1 - a.y0 + 7) / 8) * 64;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_trace(a, c->stream));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -529,6 +533,18 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         dalloc(c, c->dnPrevNormalRough, n) || dalloc(c, c->dnPrevDepth, n) || dalloc(c, c->dnPrevMaterial, n) ||
         dalloc(c, c->ffCount, 4) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n))
         return VXPT_ERR_HIP;
+    {   // wavefront trace state: one slot per pixel (8x8 tiles), 4 visibility rays per slot
+        const size_t ns = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64;
+        WaveBufs &w = c->wb;
+        if (dalloc(c, w.pPos, ns) || dalloc(c, w.pDir, ns) || dalloc(c, w.pThr, ns) || dalloc(c, w.pRad, ns) ||
+            dalloc(c, w.pMeta, ns) || dalloc(c, w.pBop, ns) || dalloc(c, w.cRayO, ns) || dalloc(c, w.cRayD, ns) ||
+            dalloc(c, w.cHit, ns) || dalloc(c, w.cT, ns) || dalloc(c, w.sPos, ns) || dalloc(c, w.sNrm, ns) ||
+            dalloc(c, w.sGeo, ns) || dalloc(c, w.sAlb, ns) || dalloc(c, w.sWo, ns) || dalloc(c, w.rSun, ns) ||
+            dalloc(c, w.rSky, ns) || dalloc(c, w.rRis, ns) || dalloc(c, w.rRR, ns) || dalloc(c, w.nIdx, ns) ||
+            dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
+            dalloc(c, w.oRayO, 4 * ns) || dalloc(c, w.oRayD, 4 * ns) || dalloc(c, w.oHit, 4 * ns))
+            return VXPT_ERR_HIP;
+    }
     // tables
     const std::string t = c->dataDir + "/tables/";
     std::vector<uint8_t> so, sc, rk, f0, f1, f2, f3;
