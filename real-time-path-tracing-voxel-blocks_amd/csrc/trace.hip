@@ -653,7 +653,7 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k_primary_gbuffer, g, b, 0, st, a);
         return hipGetLastError();
     }
-    for (int seg = 0; seg < a.totalBounceLimit; ++seg) {
+    for (int seg = 0; seg < a.segments; ++seg) {
         if (seg > 0) hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
         hipLaunchKernelGGL(k_shade, g, b, 0, st, a, seg);
         hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 1);

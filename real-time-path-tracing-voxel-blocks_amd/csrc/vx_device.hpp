@@ -50,12 +50,28 @@ VX_D bool before(float t1, int a1, float t2, int a2) { return t1 < t2 || (t1 == 
 
 VX_D int macro_of(const WorldDev &w, int x, int y, int z) { return (x >> 4) + w.mx * ((z >> 4) + w.mz * (y >> 4)); }
 VX_D int brick_bit(int x, int y, int z) { return ((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3)); }
-VX_D int cell_id(const WorldDev &w, int m, uint64_t mw, int x, int y, int z, bool &brickOcc) {
+// Cached occupancy words of the walk's current macro cell and brick.
+struct Look { int m; uint64_t mw; int nb; uint64_t cm; };
+// Block id of cell (x,y,z) for the DDA (0 = empty or not a cube) and the
+// largest empty box around it: lvl 0 = empty 64^3 block, 1 = empty 16^3 macro,
+// 2 = empty 4^3 brick, 3 = occupied brick.  The id byte is read only for cube
+// cells; all other tests are bit tests on cached words.
+VX_D int classify(const WorldDev &w, Look &L, int x, int y, int z, int &lvl) {
+    if (w.topValid) {
+        const int tb = (x >> 6) + w.tx * ((z >> 6) + w.tz * (y >> 6));
+        if (!((w.top >> tb) & 1ull)) { lvl = 0; return 0; }
+    }
+    const int m = macro_of(w, x, y, z);
+    if (m != L.m) { L.m = m; L.mw = w.macro[m]; }
+    if (L.mw == 0) { lvl = 1; return 0; }
     const int lb = brick_bit(x, y, z);
-    brickOcc = (mw >> lb) & 1ull;
-    if (!brickOcc) return 0;
+    if (!((L.mw >> lb) & 1ull)) { lvl = 2; return 0; }
+    lvl = 3;
+    const int nb = m * 64 + lb;
+    if (nb != L.nb) { L.nb = nb; L.cm = w.cellMask[nb]; }
     const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
-    return w.bricks[((size_t)m * 64 + lb) * 64 + lc];
+    if (!((L.cm >> lc) & 1ull)) return 0;
+    return w.bricks[(size_t)nb * 64 + lc];
 }
 
 // Advance one axis to the cell it occupies when the walk leaves the box through
@@ -78,9 +94,9 @@ VX_D void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int 
 }
 // Jump from the current cell to the last cell of an empty box [lo, lo+size) the
 // ray visits; the box exit crossing is then the walk's next step.
-VX_D void skip_box(const Ray3 &r, Cell &c, int size) {
+VX_D void skip_box(const WorldDev &w, const Ray3 &r, Cell &c, int size) {
     const int lx = c.x & ~(size - 1), ly = c.y & ~(size - 1), lz = c.z & ~(size - 1);
-    const int hx = lx + size - 1, hy = ly + size - 1, hz = lz + size - 1;
+    const int hx = min(lx + size - 1, w.wx - 1), hy = min(ly + size - 1, w.wy - 1), hz = min(lz + size - 1, w.wz - 1);
     const float Tx = r.mx ? ((float)(r.sx > 0 ? hx + 1 : lx) - r.ox) * r.ix : INFINITY;
     const float Ty = r.my ? ((float)(r.sy > 0 ? hy + 1 : ly) - r.oy) * r.iy : INFINITY;
     const float Tz = r.mz ? ((float)(r.sz > 0 ? hz + 1 : lz) - r.oz) * r.iz : INFINITY;
@@ -168,10 +184,9 @@ VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
     int ax = -1;
     float tEnter = 0;
     if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return h;
-    int m = macro_of(w, c.x, c.y, c.z);
-    uint64_t mw = w.macro[m];
-    bool occ;
-    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
+    Look L{-1, 0ull, -1, 0ull};
+    int lvl;
+    int prevId = classify(w, L, c.x, c.y, c.z, lvl);
     if (outside) {
         if (tEnter > tmax) return h;
         if (is_cube(prevId) && tEnter >= 0.0f) {
@@ -181,18 +196,13 @@ VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
     }
     const int maxSteps = w.wx + w.wy + w.wz + 3;
     for (int s = 0; s < maxSteps; ++s) {
-        if (prevId == 0) {
-            if (mw == 0) skip_box(r, c, 16);
-            else if (!occ) skip_box(r, c, 4);
-        }
+        if (prevId == 0 && lvl < 3) skip_box(w, r, c, lvl == 0 ? 64 : (lvl == 1 ? 16 : 4));
         float t;
         int planeCoord, face;
         walk_step(r, c, t, planeCoord, face);
         if (!(t <= tmax)) return h;
         if (!in_world(w, c)) return h;
-        const int nm = macro_of(w, c.x, c.y, c.z);
-        if (nm != m) { m = nm; mw = w.macro[m]; }
-        const int b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
+        const int b = classify(w, L, c.x, c.y, c.z, lvl);
         if (is_cube(b) && (b != prevId || (planeCoord & 31) == 0)) {
             h = {1, c.x, c.y, c.z, face, b, t};
             return h;
@@ -211,20 +221,16 @@ VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
     int ax = -1;
     float tEnter = 0;
     if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return false;
-    int m = macro_of(w, c.x, c.y, c.z);
-    uint64_t mw = w.macro[m];
-    bool occ;
-    int prevId = cell_id(w, m, mw, c.x, c.y, c.z, occ);
+    Look L{-1, 0ull, -1, 0ull};
+    int lvl;
+    int prevId = classify(w, L, c.x, c.y, c.z, lvl);
     if (outside) {
         if (tEnter > tmax) return false;
         if (is_cube(prevId) && tEnter >= tmin) return true;
     }
     const int maxSteps = w.wx + w.wy + w.wz + 3;
     for (int s = 0; s < maxSteps; ++s) {
-        if (prevId == 0) {
-            if (mw == 0) skip_box(r, c, 16);
-            else if (!occ) skip_box(r, c, 4);
-        }
+        if (prevId == 0 && lvl < 3) skip_box(w, r, c, lvl == 0 ? 64 : (lvl == 1 ? 16 : 4));
         float t;
         int planeCoord, face;
         walk_step(r, c, t, planeCoord, face);
@@ -233,9 +239,7 @@ VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
         const bool out = !in_world(w, c);
         int b = 0;
         if (!out) {
-            const int nm = macro_of(w, c.x, c.y, c.z);
-            if (nm != m) { m = nm; mw = w.macro[m]; }
-            b = mw ? cell_id(w, m, mw, c.x, c.y, c.z, occ) : (occ = false, 0);
+            b = classify(w, L, c.x, c.y, c.z, lvl);
         }
         if (t >= tmin) {
             const bool frontB = is_cube(b) && (b != prevId || chunkPlane);

@@ -39,13 +39,19 @@ struct Reservoir { uint32_t lightData, uvData; float weightSum, targetPdf, M; };
 //   bricks    u8 block ids, macro-major then brick then cell: a brick is 64
 //             contiguous bytes, a macro 4 KiB ((m*64 + brick)*64 + (x&3) + 4*((z&3) + 4*(y&3)))
 //   ids       the chunk-major upload layout (x + 32*(z + 32*y) per 32^3 chunk), kept for readback
+//   cellMask  one 64-bit word per brick: bit = cell holds a cube block (ids 1..12)
+//   top       one bit per 64^3 block (bx + TX*(bz + TZ*by)) when the world has <= 64 of them
 struct WorldDev {
     const uint8_t *ids;
     const uint8_t *bricks;
     const uint64_t *macro;
+    const uint64_t *cellMask;
+    uint64_t top;
+    int topValid;
     int cx, cy, cz;       // chunks
     int wx, wy, wz;       // cells
     int mx, my, mz;       // 16^3 macro cells
+    int tx, ty, tz;       // 64^3 blocks
 };
 
 struct SkyDev {
@@ -111,6 +117,7 @@ struct TraceArgs {
     int W, H, y0, y1;
     int iterationIndex;
     int totalBounceLimit, diffuseBounceLimit;
+    int segments;               // path segments that can occur (<= totalBounceLimit, see do_trace)
     int primaryOnly;
     float accumScale;           // 1/spp
     int accumFirst;

@@ -140,7 +140,9 @@ struct vxpt_ctx {
     int cx = 0, cy = 0, cz = 0;
     DBuf<uint8_t> voxels;
     DBuf<uint8_t> bricks;
-    DBuf<uint64_t> macro;
+    DBuf<uint64_t> macro, cellMask;
+    uint64_t top = 0;
+    int topValid = 0;
     MatDev mats[13] = {};
     CamDev cam{}, prevCam{};
     float camYaw = 0, camPitch = 0;
@@ -302,9 +304,13 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.ids = c->voxels.p;
     w.bricks = c->bricks.p;
     w.macro = c->macro.p;
+    w.cellMask = c->cellMask.p;
+    w.top = c->top;
+    w.topValid = c->topValid;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
     w.wx = c->cx * 32; w.wy = c->cy * 32; w.wz = c->cz * 32;
     w.mx = w.wx / 16; w.my = w.wy / 16; w.mz = w.wz / 16;
+    w.tx = (w.wx + 63) / 64; w.ty = (w.wy + 63) / 64; w.tz = (w.wz + 63) / 64;
 }
 
 void fill_sky(vxpt_ctx *c, SkyDev &s) {
@@ -392,6 +398,9 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     const int mx = wx / 16, my = wy / 16, mz = wz / 16;
     std::vector<uint64_t> macro((size_t)mx * my * mz, 0ull);
     std::vector<uint8_t> bricks((size_t)wx * wy * wz, 0);
+    std::vector<uint64_t> cellMask((size_t)mx * my * mz * 64, 0ull);
+    const int tx = (wx + 63) / 64, ty = (wy + 63) / 64, tz = (wz + 63) / 64;
+    uint64_t top = 0;
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -403,10 +412,18 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
                 const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
                 bricks[(m * 64 + lb) * 64 + lc] = id;
                 // only cube ids (1..12) make a brick visible to the DDA; other ids are empty for it
-                if (id >= 1 && id <= 12) macro[m] |= 1ull << lb;
+                if (id >= 1 && id <= 12) {
+                    macro[m] |= 1ull << lb;
+                    cellMask[m * 64 + lb] |= 1ull << lc;
+                    const int tb = (x >> 6) + tx * ((z >> 6) + tz * (y >> 6));
+                    if (tb < 64) top |= 1ull << tb;
+                }
             }
+    c->topValid = (tx * ty * tz <= 64) ? 1 : 0;
+    c->top = top;
     if (int r = upload_vec(c, c->bricks, bricks.data(), bricks.size())) return r;
     if (int r = upload_vec(c, c->macro, macro.data(), macro.size())) return r;
+    if (int r = upload_vec(c, c->cellMask, cellMask.data(), cellMask.size())) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors die on return
     return 0;
 }
@@ -438,6 +455,12 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.iterationIndex = it;
     a.totalBounceLimit = c->totalBounce;
     a.diffuseBounceLimit = c->diffuseBounce;
+    // A path outlives its first segment only through a specular hit (roughness
+    // <= 1e-5, closesthit.cu:224) or a diffuse limit above 1 (RayGen.cu:146-173);
+    // otherwise the later segments' kernels would find no live path.
+    bool anySpecular = false;
+    for (int b = 1; b <= 12; ++b) anySpecular |= !(c->mats[b].roughness > 0.00001f);
+    a.segments = (c->diffuseBounce == 1 && !anySpecular) ? 1 : c->totalBounce;
     a.primaryOnly = (flags & VXPT_TRACE_PRIMARY_ONLY) ? 1 : 0;
     a.wb = c->wb;
     a.tilesX = (c->W + 7) / 8;
