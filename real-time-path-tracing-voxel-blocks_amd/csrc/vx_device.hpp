@@ -173,83 +173,144 @@ VX_D int entry_face_of(int ax, V3 d) {
     return ax == 0 ? (d.x > 0.0f ? 2 : 3) : (ax == 1 ? (d.y > 0.0f ? 1 : 0) : (d.z > 0.0f ? 5 : 4));
 }
 
-// Closest front-facing cube face along the ray, t <= tmax (radiance rays).
-// Contract A4': entering cube cell b from a hits iff b != a, or the crossed
-// plane is a chunk boundary, or a is outside the world.
-VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
-    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
-    Ray3 r;
-    Cell c;
-    bool outside;
-    int ax = -1;
-    float tEnter = 0;
-    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return h;
-    Look L{-1, 0ull, -1, 0ull};
-    int lvl;
-    int prevId = classify(w, L, c.x, c.y, c.z, lvl);
-    if (outside) {
-        if (tEnter > tmax) return h;
-        if (is_cube(prevId) && tEnter >= 0.0f) {
-            h = {1, c.x, c.y, c.z, entry_face_of(ax, d), prevId, tEnter};
-            return h;
-        }
-    }
-    const int maxSteps = w.wx + w.wy + w.wz + 3;
-    for (int s = 0; s < maxSteps; ++s) {
-        if (prevId == 0 && lvl < 3) skip_box(w, r, c, lvl == 0 ? 64 : (lvl == 1 ? 16 : 4));
-        float t;
-        int planeCoord, face;
-        walk_step(r, c, t, planeCoord, face);
-        if (!(t <= tmax)) return h;
-        if (!in_world(w, c)) return h;
-        const int b = classify(w, L, c.x, c.y, c.z, lvl);
-        if (is_cube(b) && (b != prevId || (planeCoord & 31) == 0)) {
+// Walk the crossings that stay inside the current occupied 4^3 brick (the
+// cell bitmask is in L.cm), touching memory only for cube cells' ids.  Inside
+// a brick no crossing is a chunk plane or leaves the world, so with ids 0/cube:
+// radiance rays hit iff b != 0 && b != prevId, visibility rays iff b != prevId.
+// Returns 0 when the next crossing leaves the brick (state = last cell inside),
+// 1 on a hit / occlusion (h filled for radiance rays), 2 when t exceeds tmax.
+template <bool OCC>
+VX_D int brick_walk(const WorldDev &w, const Ray3 &r, Cell &c, const Look &L, int &prevId, float tmin, float tmax,
+                    Hit &h) {
+    int lc = (c.x & 3) + 4 * ((c.z & 3) + 4 * (c.y & 3));
+    const uint64_t cm = L.cm;
+    const uint8_t *cells = w.bricks + (size_t)L.nb * 64;
+    for (int k = 0; k < 10; ++k) {  // at most 9 crossings stay inside a 4^3 brick
+        const int a = pick3(c.tx, c.ty, c.tz);
+        // per-axis choices as bit blends, not selects between struct fields (a
+        // select of two loads becomes a load through a selected pointer, which
+        // pins the walk state in scratch)
+        const int mx = -(int)(a == 0), my = -(int)(a == 1), mz = -(int)(a == 2);
+        const int sa = (r.sx & mx) | (r.sy & my) | (r.sz & mz);
+        const int la = ((c.x & mx) | (c.y & my) | (c.z & mz)) & 3;
+        if (sa > 0 ? la == 3 : la == 0) return 0;
+        const float t = __int_as_float((__float_as_int(c.tx) & mx) | (__float_as_int(c.ty) & my) |
+                                       (__float_as_int(c.tz) & mz));
+        if (!(t <= tmax)) return 2;
+        c.x += sa & mx;
+        c.y += sa & my;
+        c.z += sa & mz;
+        const int ca = (c.x & mx) | (c.y & my) | (c.z & mz);
+        const float oa = __int_as_float((__float_as_int(r.ox) & mx) | (__float_as_int(r.oy) & my) |
+                                        (__float_as_int(r.oz) & mz));
+        const float ia = __int_as_float((__float_as_int(r.ix) & mx) | (__float_as_int(r.iy) & my) |
+                                        (__float_as_int(r.iz) & mz));
+        const float nt = ((float)(sa > 0 ? ca + 1 : ca) - oa) * ia;
+        c.tx = mx ? nt : c.tx;
+        c.ty = my ? nt : c.ty;
+        c.tz = mz ? nt : c.tz;
+        lc += sa * ((1 & mx) | (16 & my) | (4 & mz));
+        const int b = ((cm >> lc) & 1ull) ? (int)cells[lc] : 0;
+        if (OCC) {
+            if (t >= tmin && b != prevId) return 1;
+        } else if (b != 0 && b != prevId) {
+            const int face = (mx & (sa > 0 ? 2 : 3)) | (my & (sa > 0 ? 1 : 0)) | (mz & (sa > 0 ? 5 : 4));
             h = {1, c.x, c.y, c.z, face, b, t};
-            return h;
+            return 1;
         }
         prevId = b;
     }
+    return 0;
+}
+
+// Resumable walk state: dda_begin + dda_iter (one outer iteration: the
+// crossings inside an occupied brick or one empty-box jump, then one crossing
+// out of it).  The traversal kernels interleave many rays per lane with it.
+struct Dda {
+    Ray3 r;
+    Cell c;
+    Look L;
+    int lvl, prevId, steps;
+    float tmin, tmax;
+};
+enum { DdaRun = 0, DdaEvent = 1, DdaNone = 2 };
+
+// Radiance rays (OCC = false): closest front-facing cube face, t <= tmax.
+// Contract A4': entering cube cell b from a hits iff b != a, or the crossed
+// plane is a chunk boundary, or a is outside the world.
+// Visibility rays (OCC = true): any face crossing with tmin <= t <= tmax (no
+// culling, so leaving a cube cell counts too).
+template <bool OCC>
+VX_D int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s, Hit &h) {
+    bool outside;
+    int ax = -1;
+    float tEnter = 0;
+    s.tmin = tmin;
+    s.tmax = tmax;
+    s.steps = 0;
+    if (!walk_begin(w, o, d, s.r, s.c, outside, ax, tEnter)) return DdaNone;
+    s.L = Look{-1, 0ull, -1, 0ull};
+    s.prevId = classify(w, s.L, s.c.x, s.c.y, s.c.z, s.lvl);
+    if (outside) {
+        if (tEnter > tmax) return DdaNone;
+        if (is_cube(s.prevId) && tEnter >= (OCC ? tmin : 0.0f)) {
+            if (!OCC) h = {1, s.c.x, s.c.y, s.c.z, entry_face_of(ax, d), s.prevId, tEnter};
+            return DdaEvent;
+        }
+    }
+    return DdaRun;
+}
+
+template <bool OCC>
+VX_D int dda_iter(const WorldDev &w, Dda &s, Hit &h) {
+    if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;
+    if (s.lvl == 3) {
+        const int rc = brick_walk<OCC>(w, s.r, s.c, s.L, s.prevId, s.tmin, s.tmax, h);
+        if (rc == 1) return DdaEvent;
+        if (rc == 2) return DdaNone;
+    } else {
+        skip_box(w, s.r, s.c, s.lvl == 0 ? 64 : (s.lvl == 1 ? 16 : 4));
+    }
+    // the next crossing leaves the brick (or the skipped box)
+    float t;
+    int planeCoord, face;
+    walk_step(s.r, s.c, t, planeCoord, face);
+    if (!(t <= s.tmax)) return DdaNone;
+    const bool chunkPlane = (planeCoord & 31) == 0;
+    const bool out = !in_world(w, s.c);
+    if (!OCC && out) return DdaNone;
+    int b = 0;
+    if (!out) b = classify(w, s.L, s.c.x, s.c.y, s.c.z, s.lvl);
+    if (OCC) {
+        if (t >= s.tmin) {
+            const bool frontB = is_cube(b) && (b != s.prevId || chunkPlane);
+            const bool backA = is_cube(s.prevId) && (s.prevId != b || chunkPlane || out);
+            if (frontB || backA) return DdaEvent;
+        }
+        if (out) return DdaNone;
+    } else if (is_cube(b) && (b != s.prevId || chunkPlane)) {
+        h = {1, s.c.x, s.c.y, s.c.z, face, b, t};
+        return DdaEvent;
+    }
+    s.prevId = b;
+    return DdaRun;
+}
+
+VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
+    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+    Dda s;
+    int rc = dda_begin<false>(w, o, d, 0.0f, tmax, s, h);
+    while (rc == DdaRun) rc = dda_iter<false>(w, s, h);
+    if (rc != DdaEvent) h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
     return h;
 }
 
-// Any face crossing with tmin <= t <= tmax (visibility rays: no culling, so
-// leaving a cube cell counts too).
 VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
-    Ray3 r;
-    Cell c;
-    bool outside;
-    int ax = -1;
-    float tEnter = 0;
-    if (!walk_begin(w, o, d, r, c, outside, ax, tEnter)) return false;
-    Look L{-1, 0ull, -1, 0ull};
-    int lvl;
-    int prevId = classify(w, L, c.x, c.y, c.z, lvl);
-    if (outside) {
-        if (tEnter > tmax) return false;
-        if (is_cube(prevId) && tEnter >= tmin) return true;
-    }
-    const int maxSteps = w.wx + w.wy + w.wz + 3;
-    for (int s = 0; s < maxSteps; ++s) {
-        if (prevId == 0 && lvl < 3) skip_box(w, r, c, lvl == 0 ? 64 : (lvl == 1 ? 16 : 4));
-        float t;
-        int planeCoord, face;
-        walk_step(r, c, t, planeCoord, face);
-        if (!(t <= tmax)) return false;
-        const bool chunkPlane = (planeCoord & 31) == 0;
-        const bool out = !in_world(w, c);
-        int b = 0;
-        if (!out) {
-            b = classify(w, L, c.x, c.y, c.z, lvl);
-        }
-        if (t >= tmin) {
-            const bool frontB = is_cube(b) && (b != prevId || chunkPlane);
-            const bool backA = is_cube(prevId) && (prevId != b || chunkPlane || out);
-            if (frontB || backA) return true;
-        }
-        if (out) return false;
-        prevId = b;
-    }
-    return false;
+    Hit h;
+    Dda s;
+    int rc = dda_begin<true>(w, o, d, tmin, tmax, s, h);
+    while (rc == DdaRun) rc = dda_iter<true>(w, s, h);
+    return rc == DdaEvent;
 }
 
 VX_D V3 face_normal(int f) {

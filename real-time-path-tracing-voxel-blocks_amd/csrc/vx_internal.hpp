@@ -123,6 +123,7 @@ struct TraceArgs {
     int accumFirst;
     WaveBufs wb;
     int tilesX, nSlots;         // 8x8 tiles across the frame width; slots in the band
+    int numCU;                  // compute units of the device (traversal grid sizing)
 };
 
 // kernel launchers (defined in the .hip translation units)

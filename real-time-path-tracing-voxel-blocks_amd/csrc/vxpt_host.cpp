@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -174,6 +175,7 @@ struct vxpt_ctx {
     Reservoir *ffRes = nullptr;
     bool denoiseInputIsAccum = false;
     WaveBufs wb{};
+    int numCU = 256;
     std::vector<void *> allocs;
 
     vxpt_denoise_params yamlDenoise{};
@@ -465,6 +467,7 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.wb = c->wb;
     a.tilesX = (c->W + 7) / 8;
     a.nSlots = a.tilesX * ((a.y1 - a.y0 + 7) / 8) * 64;
+    a.numCU = c->numCU;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_trace(a, c->stream));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -543,6 +546,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(c, hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->dev));
     for (auto &e : c->ev) HIPCHK(c, hipEventCreate(&e));
     const size_t n = (size_t)c->W * c->H;
     for (auto &g : c->gb) {
