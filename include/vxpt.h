@@ -44,7 +44,10 @@ enum vxpt_buffer {
     VXPT_BUF_PREV_FAST = 18, VXPT_BUF_HIST_LEN = 19, VXPT_BUF_PREV_HIST_LEN = 20, VXPT_BUF_OUTPUT = 21,
     VXPT_BUF_SKY = 32,       /* 1024*512 float4 sky map (Sky.cu:259-303)      */
     VXPT_BUF_SUN = 33,       /* 32*32 float4 sun map (Sky.cu:305-327)          */
-    VXPT_BUF_VOXELS = 34     /* chunk-major u8 block ids                        */
+    VXPT_BUF_VOXELS = 34,    /* chunk-major u8 block ids                        */
+    VXPT_BUF_RES_EVEN = 35,  /* reservoirs of even iterationIndex (W*H*20 B)   */
+    VXPT_BUF_RES_ODD = 36,   /* reservoirs of odd iterationIndex               */
+    VXPT_BUF_WPOS = 37       /* per-pixel hit world position (denoiser)        */
 };
 
 typedef struct vxpt_config {
@@ -123,17 +126,37 @@ int vxpt_get_camera(vxpt_ctx *ctx, int which, float out32[32]);
 /* OptixRenderer::render (OptixRenderer.cpp:411-485): one 1-spp trace pass with the given
  * iterationIndex.  flags: VXPT_TRACE_PRIMARY_ONLY = C2 bring-up mode (DDA + sky + G-buffer). */
 #define VXPT_TRACE_PRIMARY_ONLY 1u
+/* spp > 1 passes of one frame (OfflineBackend::renderFrame via vxpt_render_frame does this
+ * itself): ACCUMULATE adds radiance/spp into the denoiser input, ACCUM_FIRST starts the sum,
+ * bits 8..15 carry spp */
+#define VXPT_TRACE_ACCUMULATE 2u
+#define VXPT_TRACE_ACCUM_FIRST 4u
+#define VXPT_TRACE_SPP(n) ((uint32_t)(n) << 8)
 int vxpt_trace(vxpt_ctx *ctx, int32_t iteration_index, uint32_t flags);
 /* Denoiser::run (Denoiser.cu:24-408); iteration_index = value after render() incremented it */
 int vxpt_denoise(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame_num, int32_t iteration_index);
-/* one denoiser pass on the current buffers (parity hooks): pass ids as orc_pass */
+/* one denoiser pass on the current buffers, over the context's band (multi-GPU schedule,
+ * parity hooks): 0 firefly (arg = reservoir parity), 2 temporal accumulation, 3 history fix,
+ * 4 history clamping, 5 a-trous smem, 6 a-trous ping->pong (arg step, arg2 frame index),
+ * 7 a-trous pong->ping, 10 final a-trous ping->pong + output, 11 world positions (band +/- 40
+ * rows; needed before 0, 3, 5, 6, 7, 10), 12 frame-0 history init, 13 output copy (arg: source
+ * 0 illum, 1 ping, 2 pong, 3 prev illum), 14 history copies */
 int vxpt_denoise_pass(vxpt_ctx *ctx, const vxpt_denoise_params *p, int pass, int arg, int arg2);
 /* OfflineBackend::renderFrame: spp trace passes (radiance averaged) + denoise.  frame_num as
  * OfflineBackend::m_frameNum; iteration indices frame_num*spp .. +spp-1. */
 int vxpt_render_frame(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame_num, int32_t spp);
 
-/* multi-GPU: exchange `rows` border rows of the planes in buffer_mask with band
- * neighbours (RCCL when linked by the host process; no-op for a single band) */
+/* multi-GPU band partition: the context traces and denoises only rows
+ * [row_begin, row_end) (8-aligned; 0,0 = whole frame) of full-frame buffers.  Rows
+ * outside the band are filled by the host from the neighbours' bands with
+ * vxpt_copy_rows (the transport -- RCCL over xGMI -- belongs to the host process). */
+int vxpt_set_band(vxpt_ctx *ctx, int row_begin, int row_end);
+/* bytes per row of a per-pixel buffer (negative if it has no row layout) */
+int vxpt_row_bytes(vxpt_ctx *ctx, int which);
+/* copy `rows` rows starting at row y between a buffer and device memory `dev`
+ * (to_buffer = 1: dev -> buffer), enqueued on the context stream */
+int vxpt_copy_rows(vxpt_ctx *ctx, int which, int y, int rows, void *dev, int to_buffer);
+/* kept for ABI compatibility: no-op (the host drives the exchange with vxpt_copy_rows) */
 int vxpt_exchange_halo(vxpt_ctx *ctx, uint32_t buffer_mask, int rows);
 
 /* copy any logical buffer to/from host memory (parity hooks, PNG output) */

@@ -35,6 +35,16 @@ VX_D V3 world_pos(const CamDev &c, int x, int y, float depth) {
     const V2 uv = (V2((float)x, (float)y) + 0.5f) * c.invRes;
     return c.pos + c.uv_to_dir(uv) * depth;
 }
+VX_D V3 xyz4(float4 v) { return V3(v.x, v.y, v.z); }
+// world position of the (edge-clamped) pixel's hit, from the per-frame plane
+VX_D V3 wp(const DenoiseArgs &a, int x, int y) { return xyz4(a.wpos[(size_t)cl(y, a.H) * a.W + cl(x, a.W)]); }
+__global__ __launch_bounds__(256) void k_world_pos(DenoiseArgs a) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.y1) return;
+    const size_t i = (size_t)y * a.W + x;
+    const V3 p = world_pos(a.cam, x, y, a.depth[i]);
+    a.wpos[i] = make_float4(p.x, p.y, p.z, 0.0f);
+}
 VX_D float smooth_step10(float x) {  // SmoothStep(1, 0, x)
     const float t = saturate((x - 1.0f) / (0.0f - 1.0f));
     return t * t * (3.0f - 2.0f * t);
@@ -66,8 +76,8 @@ __global__ __launch_bounds__(64) void k_firefly(DenoiseArgs a, int parity) {
     const int lane = threadIdx.x;
     const int l32 = lane & 31;
     const int x = blockIdx.x * 8 + (l32 & 7);
-    const int y = blockIdx.y * 8 + (lane >> 5) * 4 + (l32 >> 3);
-    const bool inb = x < W && y < H;
+    const int y = a.y0 + blockIdx.y * 8 + (lane >> 5) * 4 + (l32 >> 3);  // band starts on an 8-row boundary
+    const bool inb = x < W && y < a.y1;
     const size_t i = (size_t)y * W + x;
     const float cd = inb ? a.depth[i] : 0.0f;
     const bool sky = inb && cd > kRange;
@@ -102,7 +112,7 @@ __global__ __launch_bounds__(64) void k_firefly(DenoiseArgs a, int parity) {
     const float cl_ = length(cN);
     if (cl_ > 0.0f) cN /= cl_; else cN = V3(0.0f, 1.0f, 0.0f);
     const float cMat = a.material[i];
-    const V3 cWP = world_pos(a.cam, x, y, cd);
+    const V3 cWP = wp(a, x, y);
     const float g[3] = {1.0f, 2.0f, 1.0f};
     V4 filt = cc4;
     float filtW = 1.0f;
@@ -132,7 +142,7 @@ __global__ __launch_bounds__(64) void k_firefly(DenoiseArgs a, int parity) {
             const float nd = dot(cN, sN);
             if (nd < nThr) continue;
             if (fabsf(a.material[j] - cMat) > 0.5f) continue;
-            const V3 sWP = world_pos(a.cam, sx, sy, sd);
+            const V3 sWP = wp(a, sx, sy);
             if (plane_w(cWP, cN, sWP, depthSigma * depthScale) <= 0.0f) continue;
             const float nw = nonexp_w(acos_approx(clampf(nd, -1.0f, 1.0f)), nwp);
             const float dw = expf(-fabsf(sd - cd) / (depthScale * depthSigma + 1e-6f));
@@ -179,8 +189,8 @@ __global__ __launch_bounds__(256) void k_firefly_apply(DenoiseArgs a) {
 
 // ---------------------------------------------------------------- frame 0
 __global__ __launch_bounds__(256) void k_frame0(DenoiseArgs a) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (size_t)a.W * a.H) return;
+    const size_t i = (size_t)a.y0 * a.W + (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)a.y1 * a.W) return;
     const float4 v = a.illum[i];
     a.prevIllum[i] = v;
     a.prevFast[i] = v;
@@ -277,8 +287,8 @@ VX_D V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
 
 __global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
     const int W = a.W, H = a.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= a.y1) return;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
     if (z > a.p.denoisingRange) return;
@@ -294,7 +304,7 @@ __global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
     const V2 pixelUv = (V2((float)x, (float)y) + 0.5f) * V2(1.0f / (float)W, 1.0f / (float)H);
     const V2 curUV = (V2((float)x, (float)y) + 0.5f) * cam.invRes;
     const V3 view = cam.uv_to_dir(curUV);
-    const V3 cWP = world_pos(cam, x, y, z);
+    const V3 cWP = wp(a, x, y);
     const V3 Vv = -normalize(view);
     const float NoV = fabsf(dot(cN, Vv));
     const V3 prevWP = cWP + f4(a.motion[i]).xyz();
@@ -394,14 +404,14 @@ __global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
 // ---------------------------------------------------------------- HF
 __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
     const int W = a.W, H = a.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= a.y1) return;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i], hist = a.histLen[i];
     if (z > kRange || hist > 4.0f) return;
     const float cMat = ld_ushort(a.material, W, H, x, y);
     const V3 cN = f4(a.normalRough[i]).xyz();
-    const V3 cWP = world_pos(a.cam, x, y, z);
+    const V3 cWP = wp(a, x, y);
     const float dthr = 0.003f * z;
     V4 sum = f4(a.ping[i]);
     float wsum = 1.0f;
@@ -414,7 +424,7 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
             const float sMat = ld_ushort(a.material, W, H, sx, sy);
             const V3 sN = ld4(a.normalRough, W, H, sx, sy).xyz();
             const float sz = ld1(a.depth, W, H, sx, sy);
-            const V3 sWP = world_pos(a.cam, sx, sy, sz);
+            const V3 sWP = wp(a, sx, sy);  // out-of-frame taps get weight 0 below
             float w = plane_w(cWP, cN, sWP, dthr);
             w *= powf(fmaxf(0.01f, dot(cN, sN)), 8.0f);
             w = inside ? w : 0;
@@ -428,10 +438,24 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
 }
 
 // ---------------------------------------------------------------- HC
+// The 5x5 neighbourhood of the 16x16 tile (20x20 with edge clamp) is staged
+// once in LDS: YCoCg of the fast history and the noisy radiance.
 __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
     const int W = a.W, H = a.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int x0 = blockIdx.x * 16, y0 = a.y0 + blockIdx.y * 16;
+    const int x = x0 + tx, y = y0 + ty;
+    __shared__ float sY[3][400], sR[3][400];
+    for (int k = threadIdx.x; k < 400; k += 256) {
+        const int gx = cl(x0 + k % 20 - 2, W), gy = cl(y0 + k / 20 - 2, H);
+        const size_t j = (size_t)gy * W + gx;
+        const V3 yc = rgb_to_ycocg(f4(a.pong[j]).xyz());
+        const float4 n = a.illum[j];
+        sY[0][k] = yc.x; sY[1][k] = yc.y; sY[2][k] = yc.z;
+        sR[0][k] = n.x; sR[1][k] = n.y; sR[2][k] = n.z;
+    }
+    __syncthreads();
+    if (x >= W || y >= a.y1) return;
     const size_t i = (size_t)y * W + x;
     if (a.depth[i] > kRange) return;
     const float hist = a.histLen[i];
@@ -439,10 +463,11 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
     float nm2 = 0.0f;
     for (int dx = -2; dx <= 2; ++dx)
         for (int dy = -2; dy <= 2; ++dy) {
-            const V3 s = rgb_to_ycocg(ld4(a.pong, W, H, x + dx, y + dy).xyz());
+            const int k = (ty + 2 + dy) * 20 + (tx + 2 + dx);
+            const V3 s(sY[0][k], sY[1][k], sY[2][k]);
             m1 += s;
             m2 += s * s;
-            const V3 nz = ld4(a.illum, W, H, x + dx, y + dy).xyz();
+            const V3 nz(sR[0][k], sR[1][k], sR[2][k]);
             const float nl = luminance(nz);
             nm1 += nz;
             nm2 += nl * nl;
@@ -492,15 +517,32 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
 }
 
 // ---------------------------------------------------------------- A-trous (LDS variant)
+// The 16x16 tile's 5x5 neighbourhood (20x20, edge-clamped) of the history,
+// normals, material ids and world positions is staged in LDS (AtrousSmem.h
+// stages the same tile in shared memory).
 __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
     const int W = a.W, H = a.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int x0 = blockIdx.x * 16, y0 = a.y0 + blockIdx.y * 16;
+    const int x = x0 + tx, y = y0 + ty;
+    __shared__ float4 sI[400];
+    __shared__ float sNx[400], sNy[400], sNz[400], sM[400], sPx[400], sPy[400], sPz[400];
+    for (int k = threadIdx.x; k < 400; k += 256) {
+        const int gx = cl(x0 + k % 20 - 2, W), gy = cl(y0 + k / 20 - 2, H);
+        const size_t j = (size_t)gy * W + gx;
+        sI[k] = a.prevIllum[j];
+        const float4 n = a.normalRough[j], p = a.wpos[j];
+        sNx[k] = n.x; sNy[k] = n.y; sNz[k] = n.z;
+        sM[k] = a.material[j];
+        sPx[k] = p.x; sPy[k] = p.y; sPz[k] = p.z;
+    }
+    __syncthreads();
+    if (x >= W || y >= a.y1) return;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
     if (z > 500000.0f) return;
     const V3 cN = f4(a.normalRough[i]).xyz();
-    const V3 cWP = world_pos(a.cam, x, y, z);
+    const V3 cWP = wp(a, x, y);
     const float cMat = a.material[i];
     const float hist = a.histLen[i];
     const float k3[2] = {0.44198f, 0.27901f};
@@ -509,7 +551,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
         const float kern[4] = {1.0f / 4.0f, 1.0f / 8.0f, 1.0f / 8.0f, 1.0f / 16.0f};
         for (int dx = -1; dx <= 1; ++dx)
             for (int dy = -1; dy <= 1; ++dy)
-                vs += ld4(a.prevIllum, W, H, x + dx, y + dy) * kern[abs(dx) * 2 + abs(dy)];
+                vs += f4(sI[(ty + 2 + dy) * 20 + tx + 2 + dx]) * kern[abs(dx) * 2 + abs(dy)];
         const float vm1 = luminance(vs.xyz());
         const float var = fmaxf(0.0f, vs.w - vm1 * vm1);
         const float cLum = luminance(f4(a.prevIllum[i]).xyz());
@@ -524,14 +566,13 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
                 const bool isC = cx == 0 && cy == 0;
                 const bool inside = px >= 0 && py >= 0 && px < W && py < H;
                 const float kernel = inside ? k3[abs(cx)] * k3[abs(cy)] : 0.0f;
-                const int qx = cl(px, W), qy = cl(py, H);
-                const size_t j = (size_t)qy * W + qx;
-                const V3 sN = f4(a.normalRough[j]).xyz();
-                const V3 sWP = world_pos(a.cam, qx, qy, a.depth[j]);
-                const float sMat = a.material[j];
+                const int k = (ty + 2 + cy) * 20 + tx + 2 + cx;  // = edge-clamped (px, py)
+                const V3 sN(sNx[k], sNy[k], sNz[k]);
+                const V3 sWP(sPx[k], sPy[k], sPz[k]);
+                const float sMat = sM[k];
                 float geo = plane_w(cWP, cN, sWP, dthr) * kernel;
                 const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
-                const V4 si = f4(a.prevIllum[j]);
+                const V4 si = f4(sI[k]);
                 const float lw = fabsf(cLum - luminance(si.xyz())) * phiInv;
                 float w = geo * nw * expf(-lw);
                 w = isC ? kernel : w;
@@ -549,13 +590,13 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
         const float nwp = normal_weight_param(1.0f, a.p.lobeAngleFraction);
         for (int cx = -2; cx <= 2; ++cx)
             for (int cy = -2; cy <= 2; ++cy) {
-                const size_t j = (size_t)cl(y + cy, H) * W + cl(x + cx, W);
-                const V3 sN = f4(a.normalRough[j]).xyz();
+                const int k = (ty + 2 + cy) * 20 + tx + 2 + cx;
+                const V3 sN(sNx[k], sNy[k], sNz[k]);
                 const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
-                const V4 smp = f4(a.prevIllum[j]);
+                const V4 smp = f4(sI[k]);
                 const V3 sill = smp.xyz();
                 float w = nw * 1.0f;
-                w *= (float)(a.material[j] == cMat);
+                w *= (float)(sM[k] == cMat);
                 sw += w;
                 si += sill * w;
                 s1 += luminance(sill) * w;
@@ -575,8 +616,8 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
 __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
                                                 unsigned frameIndex, int final) {
     const int W = a.W, H = a.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= a.y1) return;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
     if (z > 500000.0f) {
@@ -585,7 +626,7 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
     }
     const float cMat = ld_ushort(a.material, W, H, x, y);
     const V3 cN = f4(a.normalRough[i]).xyz();
-    const V3 cWP = world_pos(a.cam, x, y, z);
+    const V3 cWP = wp(a, x, y);
     const float hist = a.histLen[i];
     float lobe = a.p.lobeAngleFraction / sqrtf((float)step);
     lobe = lerpf(0.99f, lobe, saturate(hist / 5.0f));
@@ -620,7 +661,7 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
             const float sMat = ld_ushort(a.material, W, H, px, py);
             const V3 sN = ld4(a.normalRough, W, H, px, py).xyz();
             const float sz = ld1(a.depth, W, H, px, py);
-            const V3 sWP = world_pos(a.cam, px, py, sz);
+            const V3 sWP = wp(a, px, py);  // out-of-frame taps get weight 0 below
             float geo = plane_w(cWP, cN, sWP, dthr);
             geo *= kernel;
             geo *= float(inside && sz < 500000.0f);
@@ -645,8 +686,8 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
 }
 
 __global__ __launch_bounds__(256) void k_copy_output(DenoiseArgs a, const float4 *in) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (size_t)a.W * a.H) return;
+    const size_t i = (size_t)a.y0 * a.W + (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)a.y1 * a.W) return;
     if (a.depth[i] > kRange) {
         a.output[i] = a.illum[i];
     } else {
@@ -655,47 +696,54 @@ __global__ __launch_bounds__(256) void k_copy_output(DenoiseArgs a, const float4
     }
 }
 
-inline dim3 grid16(int W, int H) { return dim3((W + 15) / 16, (H + 15) / 16); }
+// 16x16 tiles over the band rows [y0, y1)
+inline dim3 grid16(const DenoiseArgs &a) { return dim3((a.W + 15) / 16, (a.y1 - a.y0 + 15) / 16); }
+inline dim3 grid1d(const DenoiseArgs &a) { return dim3((unsigned)(((size_t)(a.y1 - a.y0) * a.W + 255) / 256)); }
 
 }  // namespace
+
+hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_world_pos, grid16(a), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st) {
     const int used = 0;
     (void)used;
     hipMemsetAsync(a.ffCount, 0, 16, st);
     // parity is baked into a.reservoir by the host
-    hipLaunchKernelGGL(k_firefly, dim3((a.W + 7) / 8, (a.H + 7) / 8), dim3(64), 0, st, a, 0);
+    hipLaunchKernelGGL(k_firefly, dim3((a.W + 7) / 8, (a.y1 - a.y0 + 7) / 8), dim3(64), 0, st, a, 0);
     hipLaunchKernelGGL(k_firefly_apply, dim3(64), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_frame0, dim3((unsigned)(((size_t)a.W * a.H + 255) / 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_frame0, grid1d(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
     const Qt rot = q_rotation_between(a.prevCam.dir, a.cam.dir);
-    hipLaunchKernelGGL(k_temporal, grid16(a.W, a.H), dim3(256), 0, st, a, rot);
+    hipLaunchKernelGGL(k_temporal, grid16(a), dim3(256), 0, st, a, rot);
     return hipGetLastError();
 }
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_history_fix, grid16(a.W, a.H), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_history_fix, grid16(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_history_clamp, grid16(a.W, a.H), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_history_clamp, grid16(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_atrous_smem, grid16(a.W, a.H), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_atrous_smem, grid16(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex,
                          bool final, hipStream_t st) {
-    hipLaunchKernelGGL(k_atrous, grid16(a.W, a.H), dim3(256), 0, st, a, in, out, step, frameIndex, final ? 1 : 0);
+    hipLaunchKernelGGL(k_atrous, grid16(a), dim3(256), 0, st, a, in, out, step, frameIndex, final ? 1 : 0);
     return hipGetLastError();
 }
 hipError_t launch_copy_output(const DenoiseArgs &a, const float4 *in, hipStream_t st) {
-    hipLaunchKernelGGL(k_copy_output, dim3((unsigned)(((size_t)a.W * a.H + 255) / 256)), dim3(256), 0, st, a, in);
+    hipLaunchKernelGGL(k_copy_output, grid1d(a), dim3(256), 0, st, a, in);
     return hipGetLastError();
 }
 

@@ -142,6 +142,7 @@ struct DenoiseParamsDev {
 
 struct DenoiseArgs {
     int W, H;
+    int y0, y1;                 // band of rows the passes compute (whole frame: 0, H)
     CamDev cam, prevCam;
     DenoiseParamsDev p;
     // inputs of this frame
@@ -154,6 +155,10 @@ struct DenoiseArgs {
     // persistent denoiser state
     float4 *ping, *pong, *prevIllum, *prevFast, *output;
     float *histLen, *prevHistLen;
+    // world position of every pixel's primary hit (world_pos of depth), built
+    // once per frame by k_world_pos: the stencil passes read it instead of
+    // re-deriving a camera ray per tap
+    float4 *wpos;
     // firefly scratch
     uint32_t *ffCount;
     uint32_t *ffIndex;
@@ -162,6 +167,7 @@ struct DenoiseArgs {
 };
 
 hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st);

@@ -170,6 +170,7 @@ struct vxpt_ctx {
     float *histLen = nullptr, *prevHistLen = nullptr;
     float4 *dnPrevNormalRough = nullptr;
     float *dnPrevDepth = nullptr, *dnPrevMaterial = nullptr;
+    float4 *wpos = nullptr;
     uint32_t *ffCount = nullptr, *ffIndex = nullptr;
     float4 *ffColor = nullptr;
     Reservoir *ffRes = nullptr;
@@ -327,6 +328,7 @@ void fill_sky(vxpt_ctx *c, SkyDev &s) {
 
 void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int parity) {
     a.W = c->W; a.H = c->H;
+    a.y0 = c->rowBegin; a.y1 = c->rowEnd;
     a.cam = c->cam; a.prevCam = c->prevCam;
     a.p = {p->max_accumulated_frame_num, p->max_fast_accumulated_frame_num, p->phi_luminance,
            p->lobe_angle_fraction, p->roughness_fraction, p->depth_threshold, p->disocclusion_threshold,
@@ -347,6 +349,7 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.output = c->output;
     a.histLen = c->histLen; a.prevHistLen = c->prevHistLen;
     a.ffCount = c->ffCount; a.ffIndex = c->ffIndex; a.ffColor = c->ffColor; a.ffRes = c->ffRes;
+    a.wpos = c->wpos;
 }
 
 const vxpt_denoise_params &default_denoise() {
@@ -380,6 +383,9 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_PREV_MATERIAL:
             p = c->dnPrevMaterial; bytes = n * 4; if (forWrite) *mirror = gp.material; return true;
         case VXPT_BUF_RESERVOIRS: p = c->res; bytes = 2 * n * sizeof(Reservoir); return true;
+        case VXPT_BUF_RES_EVEN: p = c->res; bytes = n * sizeof(Reservoir); return true;
+        case VXPT_BUF_RES_ODD: p = c->res + n; bytes = n * sizeof(Reservoir); return true;
+        case VXPT_BUF_WPOS: p = c->wpos; bytes = n * 16; return true;
         case VXPT_BUF_PING: p = c->ping; bytes = n * 16; return true;
         case VXPT_BUF_PONG: p = c->pong; bytes = n * 16; return true;
         case VXPT_BUF_PREV_ILLUM: p = c->prevIllum; bytes = n * 16; return true;
@@ -475,12 +481,34 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     return 0;
 }
 
+// history copies NormalRough/Depth/Material -> Prev (Denoiser.cu:394-407); whole
+// planes, so the rows a band received from its neighbours are carried along
+hipError_t history_copies(vxpt_ctx *c) {
+    const size_t n = (size_t)c->W * c->H;
+    const GSlot &g = c->gb[c->last];
+    hipError_t e = hipMemcpyAsync(c->dnPrevNormalRough, g.normalRough, n * 16, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->dnPrevDepth, g.depth, n * 4, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->dnPrevMaterial, g.material, n * 4, hipMemcpyDeviceToDevice, c->stream);
+    return e;
+}
+
+// world positions for the band and kWposHalo rows either side (the widest
+// stencil, HistoryFix at 2 x 17 rows, reads them there)
+constexpr int kWposHalo = 40;
+hipError_t world_pos_band(const DenoiseArgs &a, hipStream_t st) {
+    DenoiseArgs e = a;
+    e.y0 = std::max(0, a.y0 - kWposHalo);
+    e.y1 = std::min(a.H, a.y1 + kWposHalo);
+    return launch_world_pos(e, st);
+}
+
 int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) {
     if (!p) p = &default_denoise();
     const int used = it > 0 ? it - 1 : 0;
     DenoiseArgs a{};
     fill_denoise(c, p, a, used & 1);
     HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    HIPCHK(c, world_pos_band(a, c->stream));
     if (p->enable_firefly_filter) HIPCHK(c, launch_firefly(a, c->stream));
     if (frameNum == 0) HIPCHK(c, launch_frame0_init(a, c->stream));
     int fin = 0;  // 0 illum, 1 ping, 2 pong, 3 prevIllum
@@ -513,12 +541,7 @@ int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) 
         const float4 *src = fin == 1 ? a.ping : (fin == 2 ? a.pong : (fin == 3 ? a.prevIllum : a.illum));
         HIPCHK(c, launch_copy_output(a, src, c->stream));
     }
-    // history copies NormalRough/Depth/Material -> Prev (Denoiser.cu:394-407)
-    const size_t n = (size_t)c->W * c->H;
-    const GSlot &g = c->gb[c->last];
-    HIPCHK(c, hipMemcpyAsync(c->dnPrevNormalRough, g.normalRough, n * 16, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->dnPrevDepth, g.depth, n * 4, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->dnPrevMaterial, g.material, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, history_copies(c));
     HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
     return 0;
 }
@@ -558,7 +581,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         dalloc(c, c->ping, n) || dalloc(c, c->pong, n) || dalloc(c, c->prevIllum, n) || dalloc(c, c->prevFast, n) ||
         dalloc(c, c->output, n) || dalloc(c, c->histLen, n) || dalloc(c, c->prevHistLen, n) ||
         dalloc(c, c->dnPrevNormalRough, n) || dalloc(c, c->dnPrevDepth, n) || dalloc(c, c->dnPrevMaterial, n) ||
-        dalloc(c, c->ffCount, 4) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n))
+        dalloc(c, c->ffCount, 4) || dalloc(c, c->wpos, n) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n))
         return VXPT_ERR_HIP;
     {   // wavefront trace state: one slot per pixel (8x8 tiles), 4 visibility rays per slot
         const size_t ns = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64;
@@ -843,8 +866,11 @@ int vxpt_get_camera(vxpt_ctx *c, int which, float *o) {
 int vxpt_trace(vxpt_ctx *c, int32_t it, uint32_t flags) {
     if (!c) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
-    c->denoiseInputIsAccum = false;
-    int r = do_trace(c, it, flags, false, false, 1.0f);
+    const bool accum = (flags & VXPT_TRACE_ACCUMULATE) != 0;
+    const int spp = (int)((flags >> 8) & 0xFF);
+    if (accum && spp < 1) return fail(c, VXPT_ERR_ARG, "VXPT_TRACE_ACCUMULATE needs the spp in flag bits 8..15");
+    c->denoiseInputIsAccum = accum;
+    int r = do_trace(c, it, flags, accum, (flags & VXPT_TRACE_ACCUM_FIRST) != 0, accum ? 1.0f / (float)spp : 1.0f);
     if (r) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float ms = 0;
@@ -880,6 +906,13 @@ int vxpt_denoise_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int a
         case 6: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
         case 7: HIPCHK(c, launch_atrous(a, a.pong, a.ping, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
         case 10: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, true, c->stream)); break;
+        case 11: HIPCHK(c, world_pos_band(a, c->stream)); break;
+        case 12: HIPCHK(c, launch_frame0_init(a, c->stream)); break;
+        case 13: {
+            const float4 *src = arg == 1 ? a.ping : (arg == 2 ? a.pong : (arg == 3 ? a.prevIllum : a.illum));
+            HIPCHK(c, launch_copy_output(a, src, c->stream));
+        } break;
+        case 14: HIPCHK(c, history_copies(c)); break;
         default: return fail(c, VXPT_ERR_ARG, "unknown pass");
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -909,6 +942,39 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
     c->timing.trace_ms = t;
     c->timing.denoise_ms = d;
     c->timing.frame_ms = f;
+    return VXPT_OK;
+}
+
+int vxpt_set_band(vxpt_ctx *c, int row_begin, int row_end) {
+    if (!c) return VXPT_ERR_ARG;
+    if (row_end <= row_begin) { row_begin = 0; row_end = c->H; }
+    // bands start on an 8-row boundary: 8x8 trace tiles and the firefly filter's 8x4 tiles stay whole
+    if (row_begin < 0 || row_end > c->H || (row_begin & 7) || ((row_end & 7) && row_end != c->H))
+        return fail(c, VXPT_ERR_ARG, "band rows must be 8-aligned and inside the frame");
+    c->rowBegin = row_begin;
+    c->rowEnd = row_end;
+    return VXPT_OK;
+}
+
+int vxpt_row_bytes(vxpt_ctx *c, int which) {
+    void *p, *mirror;
+    size_t n;
+    if (!c || !buffer_ptr(c, which, p, n, false, &mirror) || which >= 32 || which == VXPT_BUF_RESERVOIRS)
+        return VXPT_ERR_ARG;
+    return (int)(n / (size_t)c->H);
+}
+
+int vxpt_copy_rows(vxpt_ctx *c, int which, int y, int rows, void *dev, int to_buffer) {
+    if (!c || !dev || rows < 0 || y < 0 || y + rows > c->H) return VXPT_ERR_ARG;
+    const int rb = vxpt_row_bytes(c, which);
+    if (rb <= 0) return fail(c, VXPT_ERR_ARG, "buffer has no row layout");
+    void *p, *mirror;
+    size_t n;
+    buffer_ptr(c, which, p, n, false, &mirror);
+    HIPCHK(c, hipSetDevice(c->dev));
+    char *row = static_cast<char *>(p) + (size_t)y * rb;
+    if (to_buffer) HIPCHK(c, hipMemcpyAsync(row, dev, (size_t)rows * rb, hipMemcpyDeviceToDevice, c->stream));
+    else HIPCHK(c, hipMemcpyAsync(dev, row, (size_t)rows * rb, hipMemcpyDeviceToDevice, c->stream));
     return VXPT_OK;
 }
 
