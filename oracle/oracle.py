@@ -64,6 +64,7 @@ def lib():
             "orc_set_denoise_params": (None, [P, P, P]),
             "orc_denoise": (None, [P, I, I]),
             "orc_pass": (None, [P, I, I, I]),
+            "orc_set_band": (None, [P, I, I]),
             "orc_buffer": (I, [P, I, P, I]),
             "orc_rand": (F, [P, I, I, I, I]),
             "orc_perlin": (F, [F, F, I]),
@@ -171,6 +172,9 @@ class Oracle:
 
     def run_pass(self, which, arg=0, arg2=0):
         self.L.orc_pass(self.h, which, arg, arg2)
+
+    def set_band(self, y0, y1):
+        self.L.orc_set_band(self.h, y0, y1)
 
     def _alloc(self, which):
         n = self.W * self.H

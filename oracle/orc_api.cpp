@@ -157,6 +157,12 @@ void orc_trace(void *p, int it, int y0, int y1, int primaryOnly) {
     trace_frame(c->s, c->f, it, y0, y1, primaryOnly != 0);
 }
 void orc_post_trace(void *p) { post_trace_copies(static_cast<Ctx *>(p)->f); }
+// rows [y0, y1) the denoiser passes compute (multi-GPU band schedule; 0,0 = whole frame)
+void orc_set_band(void *p, int y0, int y1) {
+    Frame &f = static_cast<Ctx *>(p)->f;
+    f.y0 = y0;
+    f.y1 = y1;
+}
 void orc_set_denoise_params(void *p, const float *fl, const int *in) {
     DenoiseParams &d = static_cast<Ctx *>(p)->dp;
     d.maxAccumulatedFrameNum = fl[0]; d.maxFastAccumulatedFrameNum = fl[1]; d.phiLuminance = fl[2];
@@ -186,6 +192,7 @@ void orc_pass(void *p, int which, int arg, int arg2) {
         case 7: pass_atrous(c->s, f, f.pong, f.ping, c->dp, (unsigned)arg2, (unsigned)arg); break;
         case 8: { auto *b = f4_buf(f, arg); if (b) pass_copy_nonsky(f, *b); } break;
         case 9: pass_history_copies(f); break;
+        case 10: pass_frame0(f); break;
         default: break;
     }
 }

@@ -166,16 +166,16 @@ void pass_firefly(const Scene &s, Frame &f, int parity, float phiL) {
     const std::vector<F4> illum0 = f.illum;
     const std::vector<Reservoir> res0(f.reservoir.begin() + parity * stride, f.reservoir.begin() + (parity + 1) * stride);
     const float weightThreshold = 80.0f, minWeight = 5.0f, normalThreshold = 0.8f, depthSigma = 0.02f;
-    const int tilesX = (W + 7) / 8, tilesY = (H + 3) / 4;
+    const int tilesX = (W + 7) / 8, tilesY = (f.by1() - f.by0() + 3) / 4;
 #pragma omp parallel for schedule(dynamic, 4)
     for (int t = 0; t < tilesX * tilesY; ++t) {
-        const int tx0 = (t % tilesX) * 8, ty0 = (t / tilesX) * 4;
+        const int tx0 = (t % tilesX) * 8, ty0 = f.by0() + (t / tilesX) * 4;
         float v[32];
         unsigned cnt[32];
         for (int l = 0; l < 32; ++l) {
             int x = tx0 + (l & 7), y = ty0 + (l >> 3);
             v[l] = 0.0f; cnt[l] = 0;
-            if (x >= W || y >= H) continue;
+            if (x >= W || y >= f.by1()) continue;
             size_t i = (size_t)y * W + x;
             if (f.depth[i] > kRange) continue;
             const Reservoir &r = res0[i];
@@ -189,7 +189,7 @@ void pass_firefly(const Scene &s, Frame &f, int parity, float phiL) {
         const unsigned tileCnt = cnt[0];
         for (int l = 0; l < 32; ++l) {
             int x = tx0 + (l & 7), y = ty0 + (l >> 3);
-            if (x >= W || y >= H) continue;
+            if (x >= W || y >= f.by1()) continue;
             size_t i = (size_t)y * W + x;
             const float cd = f.depth[i];
             if (cd > kRange) continue;
@@ -287,7 +287,7 @@ void pass_firefly(const Scene &s, Frame &f, int parity, float phiL) {
 
 // ---------------------------------------------------------------- D2
 void pass_copy_sky(Frame &f) {
-    for (size_t i = 0; i < (size_t)f.W * f.H; ++i)
+    for (size_t i = (size_t)f.by0() * f.W; i < (size_t)f.by1() * f.W; ++i)
         if (f.depth[i] > kRange) f.output[i] = f.illum[i];
 }
 
@@ -298,7 +298,7 @@ void pass_temporal(const Scene &s, Frame &f, const DenoiseParams &p) {
     const F2 invScreen(1.0f / (float)W, 1.0f / (float)H);
     const Q rot = rotation_between(Q(pc.dir, 0.f), Q(cam.dir, 0.f));
 #pragma omp parallel for schedule(dynamic, 4)
-    for (int y = 0; y < H; ++y)
+    for (int y = f.by0(); y < f.by1(); ++y)
         for (int x = 0; x < W; ++x) {
             const size_t i = (size_t)y * W + x;
             const float z = f.depth[i];
@@ -413,7 +413,7 @@ void pass_history_fix(const Scene &s, Frame &f) {
     const int W = f.W, H = f.H;
     const std::vector<F4> ping = f.ping;
 #pragma omp parallel for schedule(dynamic, 4)
-    for (int y = 0; y < H; ++y)
+    for (int y = f.by0(); y < f.by1(); ++y)
         for (int x = 0; x < W; ++x) {
             const size_t i = (size_t)y * W + x;
             const float z = f.depth[i], hist = f.histLen[i];
@@ -451,7 +451,7 @@ void pass_history_fix(const Scene &s, Frame &f) {
 void pass_history_clamp(Frame &f) {
     const int W = f.W, H = f.H;
 #pragma omp parallel for schedule(dynamic, 4)
-    for (int y = 0; y < H; ++y)
+    for (int y = f.by0(); y < f.by1(); ++y)
         for (int x = 0; x < W; ++x) {
             const size_t i = (size_t)y * W + x;
             if (f.depth[i] > kRange) continue;
@@ -528,7 +528,7 @@ void pass_atrous_smem(const Scene &s, Frame &f, const DenoiseParams &p) {
         }
     const float k3[2] = {0.44198f, 0.27901f};
 #pragma omp parallel for schedule(dynamic, 4)
-    for (int y = 0; y < H; ++y)
+    for (int y = f.by0(); y < f.by1(); ++y)
         for (int x = 0; x < W; ++x) {
             const size_t i = (size_t)y * W + x;
             const float z = f.depth[i];
@@ -616,7 +616,7 @@ void pass_atrous(const Scene &s, Frame &f, const std::vector<F4> &in, std::vecto
     const int W = f.W, H = f.H;
     const float k3[2] = {0.44198f, 0.27901f};
 #pragma omp parallel for schedule(dynamic, 4)
-    for (int y = 0; y < H; ++y)
+    for (int y = f.by0(); y < f.by1(); ++y)
         for (int x = 0; x < W; ++x) {
             const size_t i = (size_t)y * W + x;
             const float z = f.depth[i];
@@ -679,8 +679,17 @@ void pass_atrous(const Scene &s, Frame &f, const std::vector<F4> &in, std::vecto
 
 // ---------------------------------------------------------------- D8
 void pass_copy_nonsky(Frame &f, const std::vector<F4> &in) {
-    for (size_t i = 0; i < (size_t)f.W * f.H; ++i)
+    for (size_t i = (size_t)f.by0() * f.W; i < (size_t)f.by1() * f.W; ++i)
         if (!(f.depth[i] > kRange)) f.output[i] = F4(in[i].xyz() * f.albedo[i].xyz(), 0.0f);
+}
+// frame 0 (Denoiser.cu:121-142): history := noisy input, zero history length (band rows)
+void pass_frame0(Frame &f) {
+    for (size_t i = (size_t)f.by0() * f.W; i < (size_t)f.by1() * f.W; ++i) {
+        f.prevIllum[i] = f.illum[i];
+        f.prevFast[i] = f.illum[i];
+        f.histLen[i] = 0.0f;
+        f.prevHistLen[i] = 0.0f;
+    }
 }
 void pass_history_copies(Frame &f) {
     f.prevNormalRough = f.normalRough;
@@ -693,12 +702,7 @@ void denoise_frame(const Scene &s, Frame &f, const DenoiseParams &p, int frameNu
     const int used = it > 0 ? it - 1 : 0;
     if (p.enableFireflyFilter) pass_firefly(s, f, used & 1, p.phiLuminance);
     pass_copy_sky(f);
-    if (frameNum == 0) {
-        f.prevIllum = f.illum;
-        f.prevFast = f.illum;
-        std::fill(f.histLen.begin(), f.histLen.end(), 0.0f);
-        std::fill(f.prevHistLen.begin(), f.prevHistLen.end(), 0.0f);
-    }
+    if (frameNum == 0) pass_frame0(f);
     int fin = 0;
     if (p.enableTemporalAccumulation && frameNum > 0) {
         pass_temporal(s, f, p);

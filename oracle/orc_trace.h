@@ -35,6 +35,10 @@ struct DenoiseParams {  // DenoisingParams (GlobalSettings.h:82-141) with yaml v
 // All per-pixel surfaces of BufferManager.cpp:150-206 that the hot path touches.
 struct Frame {
     int W = 0, H = 0;
+    // band of rows the denoiser passes compute (multi-GPU schedule; y1 == 0: whole frame)
+    int y0 = 0, y1 = 0;
+    int by0() const { return y0; }
+    int by1() const { return y1 > 0 ? y1 : H; }
     std::vector<F4> illum, normalRough, geoNormalThin, albedo, matParam, motion;
     std::vector<float> depth, material;
     std::vector<F4> prevNormalRough, prevGeoNormalThin, prevAlbedo, prevMatParam;
@@ -75,5 +79,6 @@ void pass_atrous(const Scene &s, Frame &f, const std::vector<F4> &in, std::vecto
                  unsigned frameIndex, unsigned step);
 void pass_copy_nonsky(Frame &f, const std::vector<F4> &in);
 void pass_history_copies(Frame &f);
+void pass_frame0(Frame &f);
 
 }  // namespace orc

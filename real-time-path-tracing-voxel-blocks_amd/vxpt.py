@@ -22,7 +22,7 @@ DATA_DIR = os.path.join(REPO, "data")
 BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERIAL=5, MAT_PARAM=6, MOTION=7,
            PREV_NORMAL_ROUGH=8, PREV_GEO_NORMAL_THIN=9, PREV_ALBEDO=10, PREV_MAT_PARAM=11, PREV_DEPTH=12,
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
-           PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34)
+           PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
@@ -105,6 +105,9 @@ def load_library(path=LIB_PATH):
         "vxpt_stream": (P, [P]),
         "vxpt_probe_rays": (I, [P, I, P, P, P, I]),
         "vxpt_probe_rng": (I, [P, I, P, P]),
+        "vxpt_set_band": (I, [P, I, I]),
+        "vxpt_row_bytes": (I, [P, I]),
+        "vxpt_copy_rows": (I, [P, I, I, I, P, I]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -197,6 +200,25 @@ class Renderer:
         self._chk(self.lib.vxpt_trace(self.ctx, iteration_index, TRACE_PRIMARY_ONLY if primary_only else 0),
                   "vxpt_trace")
 
+    def trace_flags(self, iteration_index, flags):
+        """vxpt_trace with raw flags (VXPT_TRACE_ACCUMULATE | ACCUM_FIRST | spp << 8)."""
+        self._chk(self.lib.vxpt_trace(self.ctx, iteration_index, flags), "vxpt_trace")
+
+    # --- band partition (multi-GPU, bands.py) ---
+    def set_band(self, y0, y1):
+        self._chk(self.lib.vxpt_set_band(self.ctx, y0, y1), "vxpt_set_band")
+
+    def row_bytes(self, name):
+        n = self.lib.vxpt_row_bytes(self.ctx, BUF[name] if isinstance(name, str) else int(name))
+        if n <= 0:
+            raise VxptError("buffer %s has no row layout" % name)
+        return n
+
+    def copy_rows(self, name, y, rows, dev_ptr, to_buffer):
+        which = BUF[name] if isinstance(name, str) else int(name)
+        self._chk(self.lib.vxpt_copy_rows(self.ctx, which, y, rows, ctypes.c_void_p(dev_ptr), int(to_buffer)),
+                  "vxpt_copy_rows")
+
     def denoise(self, frame_num, iteration_index, params=None):
         p = params or DenoiseParams.defaults()
         self._chk(self.lib.vxpt_denoise(self.ctx, ctypes.byref(p), frame_num, iteration_index), "vxpt_denoise")
@@ -222,6 +244,8 @@ class Renderer:
         n = self.W * self.H
         if which == BUF["RESERVOIRS"]:
             return np.zeros(2 * n, RESERVOIR_DTYPE)
+        if which in (BUF["RES_EVEN"], BUF["RES_ODD"]):
+            return np.zeros((self.H, self.W), RESERVOIR_DTYPE)
         if which == BUF["SKY"]:
             return np.zeros((512, 1024, 4), np.float32)
         if which == BUF["SUN"]:

@@ -1,0 +1,140 @@
+"""Multi-GPU band partition (bands.py): the banded render with
+its halo exchanges equals the single-band render bit for bit.
+
+CPU: the schedule runs over oracle backends, in one process (LocalExchange)
+and across two gloo ranks (DistExchange, the transport the GPU path drives
+with RCCL).  GPU: two vxpt contexts on one device, spp = 4.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import bands
+import oracle
+from band_backends import OracleBand
+from golden.make_golden import C1_CAMERA
+
+W, H = 48, 160           # tall frame: two bands of 80 rows >= TRACE_HALO
+DN = ([30, 6, 2, 0.5, 0.15, 0.003, 0.01, 0.05, 500000], [1, 1, 1, 1, 1, 1])
+P = dict(ta=True, hf=True, hc=True, spatial=True, firefly=True, iters=1)
+FRAMES = 3
+
+
+def _oracle():
+    o = oracle.Oracle(W, H)
+    o.terrain((2, 1, 2))
+    o.set_camera(*C1_CAMERA[:2], fov=C1_CAMERA[2])
+    o.set_camera(*C1_CAMERA[:2], fov=C1_CAMERA[2], which=1)
+    o.set_sky()
+    o.set_denoise_params(*DN)
+    return o
+
+
+def _reference_outputs():
+    o = _oracle()
+    outs = []
+    for f in range(FRAMES):
+        o.trace(f)
+        o.post_trace()
+        o.denoise(f, f + 1)
+        outs.append(o.read(21))
+    return outs
+
+
+def test_band_rows_and_plan():
+    rows = [bands.band_rows(2160, 8, r) for r in range(8)]
+    assert rows[0] == (0, 272) and rows[-1] == (1904, 2160)
+    assert all(y0 % 8 == 0 for y0, _ in rows)
+    assert sum(y1 - y0 for y0, y1 in rows) == 2160
+    for r in range(8):
+        for peer, ((sy, sn), (ry, rn)) in bands.halo_plan(rows, r, 72).items():
+            back = bands.halo_plan(rows, peer, 72)[r]
+            assert (sy, sn) == back[1] and (ry, rn) == back[0]   # what r sends is what peer receives
+
+
+def test_frame_ops_cover_every_pass():
+    ops = list(bands.frame_ops(1, 4, P))
+    passes = [o[1] for o in ops if o[0] == "pass"]
+    assert passes == [11, 0, 2, 3, 4, 5, 6, 7, 10, 14]
+    assert sum(1 for o in ops if o[0] == "trace") == 4
+    assert [o[2] for o in ops if o[0] == "trace"] == [2 | 4 | 1024, 2 | 1024, 2 | 1024, 2 | 1024]
+    first = list(bands.frame_ops(0, 1, P))
+    assert [o[1] for o in first if o[0] == "pass"] == [11, 0, 12, 5, 6, 7, 10, 14]
+
+
+def test_oracle_bands_in_process():
+    ref = _reference_outputs()
+    bands_ = [bands.band_rows(H, 2, r) for r in range(2)]
+    backs = [OracleBand(_oracle(), *b) for b in bands_]
+    ex = bands.LocalExchange(backs, bands_)
+    for f in range(FRAMES):
+        bands.run_frame(backs, ex, f, 1, P)
+        out = np.concatenate([b.o.read(21)[y0:y1] for b, (y0, y1) in zip(backs, bands_)])
+        np.testing.assert_array_equal(out.view(np.uint32), ref[f].view(np.uint32))
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bands_ = [bands.band_rows(H, world, r) for r in range(world)]
+        back = OracleBand(_oracle(), *bands_[rank])
+        ex = bands.DistExchange(back, bands_, rank)
+        outs = []
+        for f in range(FRAMES):
+            bands.run_frame([back], ex, f, 1, P)
+            y0, y1 = bands_[rank]
+            outs.append(back.o.read(21)[y0:y1].copy())
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_oracle_bands_gloo_two_ranks():
+    import multiprocessing as mp
+    import socket
+    ref = _reference_outputs()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for f in range(FRAMES):
+        out = np.concatenate([res[0][f], res[1][f]])
+        np.testing.assert_array_equal(out.view(np.uint32), ref[f].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_bands_match_single_context():
+    import vxpt
+    w, h, spp = 64, 160, 4
+    cam = C1_CAMERA
+
+    def make(rows=None):
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    single = make()
+    bands_ = [bands.band_rows(h, 2, r) for r in range(2)]
+    backs = [bands.GpuBand(make(), y0, y1, p) for y0, y1 in bands_]
+    ex = bands.LocalExchange(backs, bands_)
+    for f in range(3):
+        single.render_frame(f, spp, p)
+        bands.run_frame(backs, ex, f, spp, bands.params_dict(p))
+        ref = single.read("OUTPUT")
+        out = np.concatenate([b.r.read("OUTPUT")[y0:y1] for b, (y0, y1) in zip(backs, bands_)])
+        np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
