@@ -959,7 +959,8 @@ int vxpt_set_band(vxpt_ctx *c, int row_begin, int row_end) {
 int vxpt_row_bytes(vxpt_ctx *c, int which) {
     void *p, *mirror;
     size_t n;
-    if (!c || !buffer_ptr(c, which, p, n, false, &mirror) || which >= 32 || which == VXPT_BUF_RESERVOIRS)
+    if (!c || !buffer_ptr(c, which, p, n, false, &mirror) || (which >= 32 && which <= 34) ||
+        which == VXPT_BUF_RESERVOIRS)
         return VXPT_ERR_ARG;
     return (int)(n / (size_t)c->H);
 }
@@ -997,7 +998,9 @@ int vxpt_upload(vxpt_ctx *c, int which, const void *host, size_t bytes) {
     HIPCHK(c, hipSetDevice(c->dev));
     void *p, *mirror;
     size_t n;
-    if (!buffer_ptr(c, which, p, n, true, &mirror) || which >= 32) return fail(c, VXPT_ERR_ARG, "unknown buffer");
+    // sky, sun and voxels are derived state: set them through their own entry points
+    if (!buffer_ptr(c, which, p, n, true, &mirror) || (which >= 32 && which <= 34))
+        return fail(c, VXPT_ERR_ARG, "unknown or read-only buffer");
     if (bytes < n) return fail(c, VXPT_ERR_ARG, "host buffer too small");
     HIPCHK(c, hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
     if (mirror) HIPCHK(c, hipMemcpyAsync(mirror, host, n, hipMemcpyHostToDevice, c->stream));
