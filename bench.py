@@ -19,6 +19,7 @@ ranks exchange halo rows with RCCL between passes.  Total work is fixed
 (strong scaling); value = whole-frame paths / max-over-ranks time.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -174,6 +175,14 @@ def main():
     else:
         alg_bytes, dur_ms, kern = B_ALG_PER_PX * band_px, avg_dn, "denoiser chain"
     achieved = alg_bytes / (dur_ms * 1e-3) / 1e9
+    # measured HBM bytes of the chain per frame: committed rocprofv3 PMC passes
+    # (tools/gpu_pmc.sh -> profiles/*_pmc_denoise.json); PMC cannot run inside this timed process
+    traffic, traffic_src = None, None
+    pmc = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_denoise.json")))
+    if pmc and not a.primary_only and a.width == 1920 and a.height == 1080:
+        with open(pmc[-1]) as f:
+            traffic = json.load(f)["traffic_bytes_per_frame"] * band_px / (a.width * a.height)
+        traffic_src = os.path.relpath(pmc[-1], REPO)
     depth = r.read("DEPTH")
     hit_frac = float((depth < 1e26).mean())  # scene sanity: fraction of primary rays that hit voxels
     cpu = None
@@ -192,7 +201,8 @@ def main():
                        "bounces": "3 total / 1 diffuse",
                        "parallelism": ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "avg_duration_ms": round(dur_ms, 4)},
             "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4), "primary_hit_frac": round(hit_frac, 4),
             # single GPU: the frame's spp passes; bands: one 1-spp pass over this rank's band

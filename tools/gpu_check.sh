@@ -10,5 +10,5 @@ rc=$?; echo "pytest rc=$rc"
 timeout -k 10 300 python bench.py "$@" > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed rc=$?"; exit 1; }
 echo bench ok
 cd /tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 4 --warmup 4 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 4 --warmup 4 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
 echo "prof rc=$?"
