@@ -64,41 +64,79 @@ VX_D V2 restir_disk(float r0, float r1) {
 }
 
 // ----------------------------------------------------------------- traversal
+#ifdef VX_STATS
+// traversal statistics (experiment builds only), per kind 8 counters:
+// rays, waves, sum of per-wave max outer iterations, outer iterations by level
+// (64^3 skip, 16^3 skip, 4^3 skip, brick walk), in-brick cell steps
+__device__ unsigned long long g_stats[8 * 8];
+VX_D int wsum(int v) { for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o); return v; }
+VX_D void stat_wave(int kind, bool active, const int *it) {
+    const unsigned long long m = __ballot(active);
+    int tot = 0;
+    for (int k = 0; k < 4; ++k) tot += active ? it[k] : 0;
+    int mx = tot;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    int v[5];
+    for (int k = 0; k < 5; ++k) v[k] = wsum(active ? it[k] : 0);
+    if ((threadIdx.x & 63) == 0 && m) {
+        unsigned long long *g = g_stats + kind * 8;
+        atomicAdd(&g[0], (unsigned long long)__popcll(m));
+        atomicAdd(&g[1], 1ull);
+        atomicAdd(&g[2], (unsigned long long)mx);
+        for (int k = 0; k < 5; ++k) atomicAdd(&g[3 + k], (unsigned long long)v[k]);
+    }
+}
+#define VX_IT , iters
+#else
+#define VX_IT
+#endif
 // mode 2: camera rays (RayGen.cu:102-126; initialises the path state);
 // mode 0: continuing path rays; mode 1: BRDF-candidate queue.
 __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     int px, py;
-    if (!slot_pixel(a, s, px, py)) return;
+    bool active = slot_pixel(a, s, px, py);
     const WaveBufs &w = a.wb;
     V3 o, d;
     float tmax = kRayMax;
-    if (mode == 2) {
-        Rng rng{&a.bn, px, py, a.iterationIndex, 0};
-        const float j0 = rng.next(), j1 = rng.next();
-        const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
-        o = a.cam.pos;
-        d = a.cam.uv_to_dir(uv);
-        w.pPos[s] = f4(o, kRayMax);
-        w.pDir[s] = f4(d, 0.0f);
-        w.pThr[s] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-        w.pRad[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        w.pMeta[s] = make_int4(F_ALIVE, rng.idx, 0, 0);
-    } else if (mode == 0) {
-        if (!(w.pMeta[s].x & F_ALIVE)) return;
-        o = xyz(w.pPos[s]);
-        d = xyz(w.pDir[s]);
-    } else {
-        if (!(w.pMeta[s].x & F_NEE)) return;
-        const float4 ro = w.cRayO[s];
-        if (!(ro.w >= 0.0f)) return;
-        o = xyz(ro);
-        d = xyz(w.cRayD[s]);
-        tmax = ro.w;
+    if (active) {
+        if (mode == 2) {
+            Rng rng{&a.bn, px, py, a.iterationIndex, 0};
+            const float j0 = rng.next(), j1 = rng.next();
+            const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
+            o = a.cam.pos;
+            d = a.cam.uv_to_dir(uv);
+            w.pPos[s] = f4(o, kRayMax);
+            w.pDir[s] = f4(d, 0.0f);
+            w.pThr[s] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+            w.pRad[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            w.pMeta[s] = make_int4(F_ALIVE, rng.idx, 0, 0);
+        } else if (mode == 0) {
+            active = (w.pMeta[s].x & F_ALIVE) != 0;
+            if (active) {
+                o = xyz(w.pPos[s]);
+                d = xyz(w.pDir[s]);
+            }
+        } else {
+            active = (w.pMeta[s].x & F_NEE) != 0;
+            if (active) {
+                const float4 ro = w.cRayO[s];
+                active = ro.w >= 0.0f;
+                o = xyz(ro);
+                d = xyz(w.cRayD[s]);
+                tmax = ro.w;
+            }
+        }
     }
-    const Hit h = dda_closest(a.world, o, d, tmax);
-    w.cHit[s] = pack_hit(h);
-    w.cT[s] = h.t;
+    int iters[5] = {0, 0, 0, 0, 0};
+    if (active) {
+        const Hit h = dda_closest(a.world, o, d, tmax VX_IT);
+        w.cHit[s] = pack_hit(h);
+        w.cT[s] = h.t;
+    }
+#ifdef VX_STATS
+    stat_wave(mode, active, iters);
+#endif
 }
 
 // Visibility rays, 4 per slot; perSlot = 1 traces only ray 0 of each slot.
@@ -107,13 +145,138 @@ __global__ __launch_bounds__(256) void k_occluded(TraceArgs a, int perSlot) {
     const int s = perSlot == 4 ? (r >> 2) : r;
     const int q = perSlot == 4 ? r : s * 4;
     int px, py;
-    if (!slot_pixel(a, s, px, py)) return;
+    bool active = slot_pixel(a, s, px, py);
     const WaveBufs &w = a.wb;
-    if (!(w.pMeta[s].x & F_NEE)) return;
+    if (active) active = (w.pMeta[s].x & F_NEE) != 0;
+    float4 rd = make_float4(0.f, 0.f, 0.f, -1.0f);
+    if (active) rd = w.oRayD[q];
+    active = active && rd.w >= 0.0f;
+    int iters[5] = {0, 0, 0, 0, 0};
+    if (active) {
+        const float4 ro = w.oRayO[q];
+        w.oHit[q] = dda_occluded(a.world, xyz(ro), xyz(rd), ro.w, rd.w VX_IT) ? 1 : 0;
+    }
+#ifdef VX_STATS
+    stat_wave(perSlot == 4 ? 3 : 4, active, iters);
+#endif
+}
+
+// Persistent traversal with per-lane ray refill.  Secondary and visibility
+// rays are incoherent: a one-ray-per-lane wave runs as long as its longest ray
+// (measured: 26-31 % of lanes busy, tools/trace_stats.py).  Here a wave pulls
+// chunks of ray ids from a queue head and hands a new ray to every lane whose
+// walk has ended, whenever at least kRefill lanes are idle; the walk itself is
+// the resumable dda_begin / dda_iter pair, so every ray's result is the one
+// dda_closest / dda_occluded returns.
+// kind: 0 continuing path rays, 1 BRDF-candidate rays (closest hit),
+//       2 RIS visibility rays (ray 4s), 3 all four visibility rays of a slot.
+constexpr int kChunk = 256, kRefill = 24;
+
+template <int KIND>
+VX_D bool fetch_ray(const TraceArgs &a, int id, V3 &o, V3 &d, float &tmin, float &tmax) {
+    const int s = KIND == 3 ? (id >> 2) : id;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return false;
+    const WaveBufs &w = a.wb;
+    const int flags = w.pMeta[s].x;
+    if (KIND == 0) {
+        if (!(flags & F_ALIVE)) return false;
+        o = xyz(w.pPos[s]);
+        d = xyz(w.pDir[s]);
+        tmin = 0.0f;
+        tmax = kRayMax;
+        return true;
+    }
+    if (!(flags & F_NEE)) return false;
+    if (KIND == 1) {
+        const float4 ro = w.cRayO[s];
+        if (!(ro.w >= 0.0f)) return false;
+        o = xyz(ro);
+        d = xyz(w.cRayD[s]);
+        tmin = 0.0f;
+        tmax = ro.w;
+        return true;
+    }
+    const int q = KIND == 3 ? id : 4 * id;
     const float4 rd = w.oRayD[q];
-    if (!(rd.w >= 0.0f)) return;
+    if (!(rd.w >= 0.0f)) return false;
     const float4 ro = w.oRayO[q];
-    w.oHit[q] = dda_occluded(a.world, xyz(ro), xyz(rd), ro.w, rd.w) ? 1 : 0;
+    o = xyz(ro);
+    d = xyz(rd);
+    tmin = ro.w;
+    tmax = rd.w;
+    return true;
+}
+
+template <int KIND>
+VX_D void store_ray(const TraceArgs &a, int id, int rc, const Hit &h) {
+    const WaveBufs &w = a.wb;
+    if (KIND <= 1) {
+        const Hit r = rc == DdaEvent ? h : Hit{0, 0, 0, 0, -1, 0, kRayMax};
+        w.cHit[id] = pack_hit(r);
+        w.cT[id] = r.t;
+    } else {
+        w.oHit[KIND == 3 ? id : 4 * id] = rc == DdaEvent ? 1 : 0;
+    }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_traverse(TraceArgs a, int nRays) {
+    constexpr bool OCC = KIND >= 2;
+    unsigned *head = a.wb.qHead + KIND;
+    int cBase = 0, cEnd = 0;  // wave-uniform: the unassigned part of the wave's chunk
+    bool drained = false;     // wave-uniform: the queue is empty
+    bool has = false;
+    int id = 0;
+    Dda st;
+    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+    const unsigned lane = threadIdx.x & 63;
+    while (true) {
+        unsigned long long idle = __ballot(!has);
+        if (!drained && __popcll(idle) >= (idle == ~0ull ? 1 : kRefill)) {
+            // hand out ray ids to the idle lanes until they are all busy or the queue is empty
+            while (idle && !drained) {
+                if (cBase >= cEnd) {
+                    int v = 0;
+                    if (lane == 0) v = (int)atomicAdd(head, (unsigned)kChunk);
+                    v = __shfl(v, 0);
+                    if (v >= nRays) { drained = true; break; }
+                    cBase = v;
+                    cEnd = min(v + kChunk, nRays);
+                }
+                const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+                const int avail = cEnd - cBase;
+                const bool mine = !has && rank < avail;
+                const int taken = min(__popcll(idle), avail);
+                if (mine) {
+                    id = cBase + rank;
+                    V3 o, d;
+                    float tmin, tmax;
+                    if (fetch_ray<KIND>(a, id, o, d, tmin, tmax)) {
+                        h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
+                        const int rc = dda_begin<OCC>(a.world, o, d, tmin, tmax, st, h);
+                        if (rc == DdaRun) has = true;
+                        else store_ray<KIND>(a, id, rc, h);
+                    }
+                }
+                cBase += taken;
+                idle = __ballot(!has);
+                // lanes whose ray ended at once stay idle for the next round
+                if (__popcll(idle) < kRefill) break;
+            }
+        }
+        if (!__ballot(has)) {
+            if (drained) break;
+            continue;
+        }
+        if (has) {
+            const int rc = dda_iter<OCC>(a.world, st, h);
+            if (rc != DdaRun) {
+                store_ray<KIND>(a, id, rc, h);
+                has = false;
+            }
+        }
+    }
 }
 
 // ----------------------------------------------------------------- shading
@@ -636,6 +799,17 @@ __global__ __launch_bounds__(256) void k_probe_rng(BlueNoiseDev bn, int n, const
 
 }  // namespace
 
+#ifdef VX_STATS
+extern "C" int vxpt_debug_stats(unsigned long long *out64, int reset) {
+    hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_stats), sizeof(g_stats), 0, hipMemcpyDeviceToHost);
+    if (reset) {
+        static const unsigned long long z[64] = {};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return 0;
+}
+#endif
+
 hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st) {
     hipLaunchKernelGGL(k_probe_rng, dim3((n + 255) / 256), dim3(256), 0, st, bn, n, q, out);
     return hipGetLastError();
@@ -653,15 +827,35 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k_primary_gbuffer, g, b, 0, st, a);
         return hipGetLastError();
     }
+    if (!a.persistent) {
+        for (int seg = 0; seg < a.segments; ++seg) {
+            if (seg > 0) hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
+            hipLaunchKernelGGL(k_shade, g, b, 0, st, a, seg);
+            hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 1);
+            hipLaunchKernelGGL(k_nee, g, b, 0, st, a);
+            hipLaunchKernelGGL(k_occluded, g, b, 0, st, a, 1);
+            hipLaunchKernelGGL(k_restir, g, b, 0, st, a, seg);
+            if (seg == 0) {
+                hipLaunchKernelGGL(k_occluded, g4, b, 0, st, a, 4);
+                hipLaunchKernelGGL(k_finish, g, b, 0, st, a);
+            }
+        }
+        return hipGetLastError();
+    }
+    // persistent traversal (experiment, VXPT_PERSISTENT=1): enough 4-wave workgroups to fill every SIMD
+    const dim3 gp(a.numCU * 8);
+    hipMemsetAsync(a.wb.qHead, 0, 16 * sizeof(unsigned) * 3, st);
     for (int seg = 0; seg < a.segments; ++seg) {
-        if (seg > 0) hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
+        TraceArgs as = a;
+        as.wb.qHead = a.wb.qHead + 16 * (seg < 3 ? seg : 2);
+        if (seg > 0) hipLaunchKernelGGL(k_traverse<0>, gp, b, 0, st, as, a.nSlots);
         hipLaunchKernelGGL(k_shade, g, b, 0, st, a, seg);
-        hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 1);
+        hipLaunchKernelGGL(k_traverse<1>, gp, b, 0, st, as, a.nSlots);
         hipLaunchKernelGGL(k_nee, g, b, 0, st, a);
-        hipLaunchKernelGGL(k_occluded, g, b, 0, st, a, 1);
+        hipLaunchKernelGGL(k_traverse<2>, gp, b, 0, st, as, a.nSlots);
         hipLaunchKernelGGL(k_restir, g, b, 0, st, a, seg);
         if (seg == 0) {
-            hipLaunchKernelGGL(k_occluded, g4, b, 0, st, a, 4);
+            hipLaunchKernelGGL(k_traverse<3>, gp, b, 0, st, as, 4 * a.nSlots);
             hipLaunchKernelGGL(k_finish, g, b, 0, st, a);
         }
     }

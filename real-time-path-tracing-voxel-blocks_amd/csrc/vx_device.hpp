@@ -48,31 +48,13 @@ VX_D int pick3(float tx, float ty, float tz) {
 }
 VX_D bool before(float t1, int a1, float t2, int a2) { return t1 < t2 || (t1 == t2 && a1 > a2); }
 
-VX_D int macro_of(const WorldDev &w, int x, int y, int z) { return (x >> 4) + w.mx * ((z >> 4) + w.mz * (y >> 4)); }
-VX_D int brick_bit(int x, int y, int z) { return ((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3)); }
-// Cached occupancy words of the walk's current macro cell and brick.
-struct Look { int m; uint64_t mw; int nb; uint64_t cm; };
-// Block id of cell (x,y,z) for the DDA (0 = empty or not a cube) and the
-// largest empty box around it: lvl 0 = empty 64^3 block, 1 = empty 16^3 macro,
-// 2 = empty 4^3 brick, 3 = occupied brick.  The id byte is read only for cube
-// cells; all other tests are bit tests on cached words.
-VX_D int classify(const WorldDev &w, Look &L, int x, int y, int z, int &lvl) {
-    if (w.topValid) {
-        const int tb = (x >> 6) + w.tx * ((z >> 6) + w.tz * (y >> 6));
-        if (!((w.top >> tb) & 1ull)) { lvl = 0; return 0; }
-    }
-    const int m = macro_of(w, x, y, z);
-    if (m != L.m) { L.m = m; L.mw = w.macro[m]; }
-    if (L.mw == 0) { lvl = 1; return 0; }
-    const int lb = brick_bit(x, y, z);
-    if (!((L.mw >> lb) & 1ull)) { lvl = 2; return 0; }
-    lvl = 3;
-    const int nb = m * 64 + lb;
-    if (nb != L.nb) { L.nb = nb; L.cm = w.cellMask[nb]; }
-    const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
-    if (!((L.cm >> lc) & 1ull)) return 0;
-    return w.bricks[(size_t)nb * 64 + lc];
+// brick index shared by bdist / cellMask / bricks (macro-major: a 16^3 macro
+// cell's 64 bricks are contiguous) and the cell inside the brick
+VX_D int brick_index(const WorldDev &w, int x, int y, int z) {
+    const int m = (x >> 4) + w.mx * ((z >> 4) + w.mz * (y >> 4));
+    return m * 64 + (((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3)));
 }
+VX_D int cell_of(int x, int y, int z) { return (x & 3) + 4 * ((z & 3) + 4 * (y & 3)); }
 
 // Advance one axis to the cell it occupies when the walk leaves the box through
 // the crossing (Te, ea): exactly the planes the cell-by-cell walk would cross first.
@@ -92,11 +74,15 @@ VX_D void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int 
     cb = est;
     tb = tn;
 }
-// Jump from the current cell to the last cell of an empty box [lo, lo+size) the
-// ray visits; the box exit crossing is then the walk's next step.
-VX_D void skip_box(const WorldDev &w, const Ray3 &r, Cell &c, int size) {
-    const int lx = c.x & ~(size - 1), ly = c.y & ~(size - 1), lz = c.z & ~(size - 1);
-    const int hx = min(lx + size - 1, w.wx - 1), hy = min(ly + size - 1, w.wy - 1), hz = min(lz + size - 1, w.wz - 1);
+// Jump from the current cell to the last cell, inside the empty cube of S
+// bricks that starts at the current brick and extends in the ray's octant
+// (clamped to the world), that the ray visits; the cube's exit crossing is
+// then the walk's next step.
+VX_D void skip_cube(const WorldDev &w, const Ray3 &r, Cell &c, int S) {
+    const int e = 4 * (S - 1);
+    const int lx = r.sx > 0 ? (c.x & ~3) : max((c.x & ~3) - e, 0), hx = r.sx > 0 ? min((c.x | 3) + e, w.wx - 1) : (c.x | 3);
+    const int ly = r.sy > 0 ? (c.y & ~3) : max((c.y & ~3) - e, 0), hy = r.sy > 0 ? min((c.y | 3) + e, w.wy - 1) : (c.y | 3);
+    const int lz = r.sz > 0 ? (c.z & ~3) : max((c.z & ~3) - e, 0), hz = r.sz > 0 ? min((c.z | 3) + e, w.wz - 1) : (c.z | 3);
     const float Tx = r.mx ? ((float)(r.sx > 0 ? hx + 1 : lx) - r.ox) * r.ix : INFINITY;
     const float Ty = r.my ? ((float)(r.sy > 0 ? hy + 1 : ly) - r.oy) * r.iy : INFINITY;
     const float Tz = r.mz ? ((float)(r.sz > 0 ? hz + 1 : lz) - r.oz) * r.iz : INFINITY;
@@ -173,20 +159,80 @@ VX_D int entry_face_of(int ax, V3 d) {
     return ax == 0 ? (d.x > 0.0f ? 2 : 3) : (ax == 1 ? (d.y > 0.0f ? 1 : 0) : (d.z > 0.0f ? 5 : 4));
 }
 
-// Walk the crossings that stay inside the current occupied 4^3 brick (the
-// cell bitmask is in L.cm), touching memory only for cube cells' ids.  Inside
-// a brick no crossing is a chunk plane or leaves the world, so with ids 0/cube:
-// radiance rays hit iff b != 0 && b != prevId, visibility rays iff b != prevId.
-// Returns 0 when the next crossing leaves the brick (state = last cell inside),
-// 1 on a hit / occlusion (h filled for radiance rays), 2 when t exceeds tmax.
+// Resumable walk state (dda_begin + dda_iter).  Block ids are read lazily:
+// the face rule needs an id only when a crossing joins two cube cells (or for
+// the hit record), so `prevId` is 0 (empty cell), the cube's id, or -1 (a
+// cube whose id has not been read; its byte is bricks[prevLoc]).
+struct Dda {
+    Ray3 r;
+    Cell c;
+    const uint8_t *od;  // the ray octant's empty-cube table
+    int nb;        // brick of the current cell
+    int dist;      // its empty-cube edge in bricks (0 = occupied: walk its cells)
+    uint64_t cm;   // its cube-cell mask (dist == 0)
+    int prevId, prevLoc, steps;
+    float tmin, tmax;
+};
+enum { DdaRun = 0, DdaEvent = 1, DdaNone = 2 };
+
+// brick data of the walk's current cell (cached per brick); returns the cube bit
+VX_D bool locate(const WorldDev &w, Dda &s) {
+    const int nb = brick_index(w, s.c.x, s.c.y, s.c.z);
+    if (nb != s.nb) {
+        s.nb = nb;
+        s.dist = s.od[nb];
+        s.cm = s.dist ? 0ull : w.cellMask[nb];
+    }
+    return (s.cm >> cell_of(s.c.x, s.c.y, s.c.z)) & 1ull;
+}
+VX_D int prev_id(const WorldDev &w, const Dda &s) { return s.prevId > 0 ? s.prevId : (int)w.bricks[s.prevLoc]; }
+
+// The face rule at one crossing into a cell with cube bit `solid` (byte index
+// `loc`).  Radiance rays (OCC = false): entering cube b from cell a hits iff
+// a is empty, b != a, or the plane is a chunk boundary.  Visibility rays
+// (OCC = true, t >= tmin): any crossing that enters or leaves a cube face
+// (no culling).  Returns true on an event; otherwise updates prevId/prevLoc.
 template <bool OCC>
-VX_D int brick_walk(const WorldDev &w, const Ray3 &r, Cell &c, const Look &L, int &prevId, float tmin, float tmax,
-                    Hit &h) {
-    int lc = (c.x & 3) + 4 * ((c.z & 3) + 4 * (c.y & 3));
-    const uint64_t cm = L.cm;
-    const uint8_t *cells = w.bricks + (size_t)L.nb * 64;
+VX_D bool cross(const WorldDev &w, Dda &s, bool solid, int loc, bool chunkPlane, float t, int face, Hit &h) {
+    if (OCC) {
+        if (t >= s.tmin) {
+            if (solid != (s.prevId != 0)) return true;
+            if (solid) {
+                if (chunkPlane) return true;
+                const int bid = w.bricks[loc];
+                if (bid != prev_id(w, s)) return true;
+                s.prevId = bid;
+            }
+            return false;
+        }
+        s.prevId = solid ? -1 : 0;
+        s.prevLoc = loc;
+        return false;
+    }
+    if (!solid) { s.prevId = 0; return false; }
+    const int bid = w.bricks[loc];
+    if (s.prevId == 0 || chunkPlane || bid != prev_id(w, s)) {
+        h = {1, s.c.x, s.c.y, s.c.z, face, bid, t};
+        return true;
+    }
+    s.prevId = bid;
+    return false;
+}
+
+// Walk the crossings that stay inside the current occupied 4^3 brick (cube
+// bits in s.cm).  Inside a brick no crossing is a chunk plane or leaves the
+// world.  Returns 0 when the next crossing leaves the brick (state = last cell
+// inside), 1 on an event (h filled for radiance rays), 2 when t exceeds tmax.
+template <bool OCC>
+VX_D int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
+    const Ray3 &r = s.r;
+    Cell &c = s.c;
+    int lc = cell_of(c.x, c.y, c.z);
+    const uint64_t cm = s.cm;
+    const int base = s.nb * 64;
     for (int k = 0; k < 10; ++k) {  // at most 9 crossings stay inside a 4^3 brick
         const int a = pick3(c.tx, c.ty, c.tz);
+        if (cnt) ++*cnt;
         // per-axis choices as bit blends, not selects between struct fields (a
         // select of two loads becomes a load through a selected pointer, which
         // pins the walk state in scratch)
@@ -196,7 +242,7 @@ VX_D int brick_walk(const WorldDev &w, const Ray3 &r, Cell &c, const Look &L, in
         if (sa > 0 ? la == 3 : la == 0) return 0;
         const float t = __int_as_float((__float_as_int(c.tx) & mx) | (__float_as_int(c.ty) & my) |
                                        (__float_as_int(c.tz) & mz));
-        if (!(t <= tmax)) return 2;
+        if (!(t <= s.tmax)) return 2;
         c.x += sa & mx;
         c.y += sa & my;
         c.z += sa & mz;
@@ -210,30 +256,14 @@ VX_D int brick_walk(const WorldDev &w, const Ray3 &r, Cell &c, const Look &L, in
         c.ty = my ? nt : c.ty;
         c.tz = mz ? nt : c.tz;
         lc += sa * ((1 & mx) | (16 & my) | (4 & mz));
-        const int b = ((cm >> lc) & 1ull) ? (int)cells[lc] : 0;
-        if (OCC) {
-            if (t >= tmin && b != prevId) return 1;
-        } else if (b != 0 && b != prevId) {
+        const bool solid = (cm >> lc) & 1ull;
+        if (solid || s.prevId != 0) {
             const int face = (mx & (sa > 0 ? 2 : 3)) | (my & (sa > 0 ? 1 : 0)) | (mz & (sa > 0 ? 5 : 4));
-            h = {1, c.x, c.y, c.z, face, b, t};
-            return 1;
+            if (cross<OCC>(w, s, solid, base + lc, false, t, face, h)) return 1;
         }
-        prevId = b;
     }
     return 0;
 }
-
-// Resumable walk state: dda_begin + dda_iter (one outer iteration: the
-// crossings inside an occupied brick or one empty-box jump, then one crossing
-// out of it).  The traversal kernels interleave many rays per lane with it.
-struct Dda {
-    Ray3 r;
-    Cell c;
-    Look L;
-    int lvl, prevId, steps;
-    float tmin, tmax;
-};
-enum { DdaRun = 0, DdaEvent = 1, DdaNone = 2 };
 
 // Radiance rays (OCC = false): closest front-facing cube face, t <= tmax.
 // Contract A4': entering cube cell b from a hits iff b != a, or the crossed
@@ -249,12 +279,15 @@ VX_D int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s
     s.tmax = tmax;
     s.steps = 0;
     if (!walk_begin(w, o, d, s.r, s.c, outside, ax, tEnter)) return DdaNone;
-    s.L = Look{-1, 0ull, -1, 0ull};
-    s.prevId = classify(w, s.L, s.c.x, s.c.y, s.c.z, s.lvl);
+    s.od = w.bdist + (size_t)w.nBricks * ((s.r.sx > 0 ? 1 : 0) | (s.r.sy > 0 ? 2 : 0) | (s.r.sz > 0 ? 4 : 0));
+    s.nb = -1;
+    const bool solid = locate(w, s);
+    s.prevId = solid ? -1 : 0;
+    s.prevLoc = s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z);
     if (outside) {
         if (tEnter > tmax) return DdaNone;
-        if (is_cube(s.prevId) && tEnter >= (OCC ? tmin : 0.0f)) {
-            if (!OCC) h = {1, s.c.x, s.c.y, s.c.z, entry_face_of(ax, d), s.prevId, tEnter};
+        if (solid && tEnter >= (OCC ? tmin : 0.0f)) {
+            if (!OCC) h = {1, s.c.x, s.c.y, s.c.z, entry_face_of(ax, d), (int)w.bricks[s.prevLoc], tEnter};
             return DdaEvent;
         }
     }
@@ -262,14 +295,15 @@ VX_D int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s
 }
 
 template <bool OCC>
-VX_D int dda_iter(const WorldDev &w, Dda &s, Hit &h) {
+VX_D int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;
-    if (s.lvl == 3) {
-        const int rc = brick_walk<OCC>(w, s.r, s.c, s.L, s.prevId, s.tmin, s.tmax, h);
+    if (cnt) ++cnt[s.dist == 0 ? 3 : (s.dist == 1 ? 2 : 1)];
+    if (s.dist == 0) {
+        const int rc = brick_walk<OCC>(w, s, h, cnt ? cnt + 4 : nullptr);
         if (rc == 1) return DdaEvent;
         if (rc == 2) return DdaNone;
     } else {
-        skip_box(w, s.r, s.c, s.lvl == 0 ? 64 : (s.lvl == 1 ? 16 : 4));
+        skip_cube(w, s.r, s.c, s.dist);
     }
     // the next crossing leaves the brick (or the skipped box)
     float t;
@@ -278,38 +312,32 @@ VX_D int dda_iter(const WorldDev &w, Dda &s, Hit &h) {
     if (!(t <= s.tmax)) return DdaNone;
     const bool chunkPlane = (planeCoord & 31) == 0;
     const bool out = !in_world(w, s.c);
-    if (!OCC && out) return DdaNone;
-    int b = 0;
-    if (!out) b = classify(w, s.L, s.c.x, s.c.y, s.c.z, s.lvl);
-    if (OCC) {
-        if (t >= s.tmin) {
-            const bool frontB = is_cube(b) && (b != s.prevId || chunkPlane);
-            const bool backA = is_cube(s.prevId) && (s.prevId != b || chunkPlane || out);
-            if (frontB || backA) return DdaEvent;
-        }
-        if (out) return DdaNone;
-    } else if (is_cube(b) && (b != s.prevId || chunkPlane)) {
-        h = {1, s.c.x, s.c.y, s.c.z, face, b, t};
-        return DdaEvent;
+    if (out) {
+        // leaving the world: only a visibility ray leaving a cube cell sees a face
+        return (OCC && t >= s.tmin && s.prevId != 0) ? DdaEvent : DdaNone;
     }
-    s.prevId = b;
+    const bool solid = locate(w, s);
+    if (solid || s.prevId != 0) {
+        if (cross<OCC>(w, s, solid, s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z), chunkPlane, t, face, h))
+            return DdaEvent;
+    }
     return DdaRun;
 }
 
-VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax) {
+VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax, int *iters = nullptr) {
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
     Dda s;
     int rc = dda_begin<false>(w, o, d, 0.0f, tmax, s, h);
-    while (rc == DdaRun) rc = dda_iter<false>(w, s, h);
+    while (rc == DdaRun) rc = dda_iter<false>(w, s, h, iters);
     if (rc != DdaEvent) h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
     return h;
 }
 
-VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax) {
+VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int *iters = nullptr) {
     Hit h;
     Dda s;
     int rc = dda_begin<true>(w, o, d, tmin, tmax, s, h);
-    while (rc == DdaRun) rc = dda_iter<true>(w, s, h);
+    while (rc == DdaRun) rc = dda_iter<true>(w, s, h, iters);
     return rc == DdaEvent;
 }
 

@@ -46,6 +46,10 @@ struct WorldDev {
     const uint8_t *bricks;
     const uint64_t *macro;
     const uint64_t *cellMask;
+    const uint8_t *bdist;     // 8 octant tables of nBricks bytes (brick index as cellMask): edge in bricks
+                              // of the largest empty brick cube cornered at the brick and extending into
+                              // the octant (0 = occupied, capped at 255); octant = (dx>0) | (dy>0)<<1 | (dz>0)<<2
+    int nBricks;
     uint64_t top;
     int topValid;
     int cx, cy, cz;       // chunks
@@ -101,6 +105,8 @@ struct WaveBufs {
     // visibility queue: 4 rays per slot (0: RIS/final visibility, 1-3: bias-correction taps)
     float4 *oRayO, *oRayD;  // o xyz + tmin, d xyz + tmax (< 0: inactive)
     uint8_t *oHit;
+    // work-queue heads of the persistent traversal launches, zeroed once per pass
+    unsigned *qHead;
 };
 
 struct TraceArgs {
@@ -124,6 +130,7 @@ struct TraceArgs {
     WaveBufs wb;
     int tilesX, nSlots;         // 8x8 tiles across the frame width; slots in the band
     int numCU;                  // compute units of the device (traversal grid sizing)
+    int persistent;             // persistent refill traversal kernels (experiment)
 };
 
 // kernel launchers (defined in the .hip translation units)

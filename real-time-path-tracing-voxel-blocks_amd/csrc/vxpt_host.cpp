@@ -142,6 +142,8 @@ struct vxpt_ctx {
     DBuf<uint8_t> voxels;
     DBuf<uint8_t> bricks;
     DBuf<uint64_t> macro, cellMask;
+    DBuf<uint8_t> bdist;
+    int nBricks = 0;
     uint64_t top = 0;
     int topValid = 0;
     MatDev mats[13] = {};
@@ -308,6 +310,8 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.bricks = c->bricks.p;
     w.macro = c->macro.p;
     w.cellMask = c->cellMask.p;
+    w.bdist = c->bdist.p;
+    w.nBricks = c->nBricks;
     w.top = c->top;
     w.topValid = c->topValid;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
@@ -429,6 +433,58 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
             }
     c->topValid = (tx * ty * tz <= 64) ? 1 : 0;
     c->top = top;
+    // Per-octant empty-box sizes: for every 4^3 brick and each of the 8 ray
+    // octants, S = the edge (in bricks) of the largest brick-aligned cube with
+    // that brick at its corner, extending in the octant's directions, that holds
+    // no cube cell (0 = the brick is occupied; out-of-world counts as empty;
+    // capped at 255).  A ray in that octant can leave the whole cube in one jump.
+    // 3-D "largest empty square" recurrence: S = 1 + min(S of the 7 forward neighbours).
+    {
+        const int BX = wx / 4, BY = wy / 4, BZ = wz / 4;
+        const size_t nB = (size_t)BX * BY * BZ;
+        std::vector<uint8_t> occ(nB), S(nB), od(8 * nB);
+        auto lin = [&](int x, int y, int z) { return (size_t)x + (size_t)BX * (z + (size_t)BZ * y); };
+        for (int y = 0; y < BY; ++y)
+            for (int z = 0; z < BZ; ++z)
+                for (int x = 0; x < BX; ++x) {
+                    const size_t m = (size_t)(x >> 2) + (size_t)mx * ((z >> 2) + (size_t)mz * (y >> 2));
+                    const int lb = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
+                    occ[lin(x, y, z)] = cellMask[m * 64 + lb] ? 1 : 0;
+                }
+        for (int oct = 0; oct < 8; ++oct) {
+            const int sx = (oct & 1) ? 1 : -1, sy = (oct & 2) ? 1 : -1, sz = (oct & 4) ? 1 : -1;
+            auto get = [&](int x, int y, int z) -> int {
+                if (x < 0 || y < 0 || z < 0 || x >= BX || y >= BY || z >= BZ) return 255;
+                return S[lin(x, y, z)];
+            };
+            for (int iy = 0; iy < BY; ++iy)
+                for (int iz = 0; iz < BZ; ++iz)
+                    for (int ix = 0; ix < BX; ++ix) {
+                        // visit bricks against the octant's direction so forward neighbours are done
+                        const int x = sx > 0 ? BX - 1 - ix : ix, y = sy > 0 ? BY - 1 - iy : iy,
+                                  z = sz > 0 ? BZ - 1 - iz : iz;
+                        int v = 0;
+                        if (!occ[lin(x, y, z)]) {
+                            int mn = 255;
+                            for (int k = 1; k < 8; ++k)
+                                mn = std::min(mn, get(x + ((k & 1) ? sx : 0), y + ((k & 2) ? sy : 0),
+                                                      z + ((k & 4) ? sz : 0)));
+                            v = std::min(255, 1 + mn);
+                        }
+                        S[lin(x, y, z)] = (uint8_t)v;
+                    }
+            for (int y = 0; y < BY; ++y)
+                for (int z = 0; z < BZ; ++z)
+                    for (int x = 0; x < BX; ++x) {
+                        const size_t m = (size_t)(x >> 2) + (size_t)mx * ((z >> 2) + (size_t)mz * (y >> 2));
+                        const int lb = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
+                        od[(size_t)oct * nB + m * 64 + lb] = S[lin(x, y, z)];
+                    }
+        }
+        c->nBricks = (int)nB;
+        if (int r = upload_vec(c, c->bdist, od.data(), od.size())) return r;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     if (int r = upload_vec(c, c->bricks, bricks.data(), bricks.size())) return r;
     if (int r = upload_vec(c, c->macro, macro.data(), macro.size())) return r;
     if (int r = upload_vec(c, c->cellMask, cellMask.data(), cellMask.size())) return r;
@@ -474,6 +530,7 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.tilesX = (c->W + 7) / 8;
     a.nSlots = a.tilesX * ((a.y1 - a.y0 + 7) / 8) * 64;
     a.numCU = c->numCU;
+    a.persistent = getenv("VXPT_PERSISTENT") ? atoi(getenv("VXPT_PERSISTENT")) : 0;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_trace(a, c->stream));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -592,7 +649,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
             dalloc(c, w.sGeo, ns) || dalloc(c, w.sAlb, ns) || dalloc(c, w.sWo, ns) || dalloc(c, w.rSun, ns) ||
             dalloc(c, w.rSky, ns) || dalloc(c, w.rRis, ns) || dalloc(c, w.rRR, ns) || dalloc(c, w.nIdx, ns) ||
             dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
-            dalloc(c, w.oRayO, 4 * ns) || dalloc(c, w.oRayD, 4 * ns) || dalloc(c, w.oHit, 4 * ns))
+            dalloc(c, w.oRayO, 4 * ns) || dalloc(c, w.oRayD, 4 * ns) || dalloc(c, w.oHit, 4 * ns) ||
+            dalloc(c, w.qHead, 64))
             return VXPT_ERR_HIP;
     }
     // tables

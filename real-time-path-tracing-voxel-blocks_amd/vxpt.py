@@ -15,7 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_HERE, "libvxpt.so")
+LIB_PATH = os.environ.get("VXPT_LIB") or os.path.join(_HERE, "libvxpt.so")
 DATA_DIR = os.path.join(REPO, "data")
 
 # logical buffers (include/vxpt.h enum vxpt_buffer)
