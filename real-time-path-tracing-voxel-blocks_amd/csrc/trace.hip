@@ -139,140 +139,128 @@ __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
 #endif
 }
 
-// Visibility rays, 4 per slot; perSlot = 1 traces only ray 0 of each slot.
-__global__ __launch_bounds__(256) void k_occluded(TraceArgs a, int perSlot) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    const int s = perSlot == 4 ? (r >> 2) : r;
-    const int q = perSlot == 4 ? r : s * 4;
-    int px, py;
-    bool active = slot_pixel(a, s, px, py);
+// ----------------------------------------------------------------- ray queues
+// Secondary and visibility rays are produced compacted: each producing
+// workgroup appends its rays to a queue (one atomic per workgroup) as
+// {o xyz + tmin, d xyz + tmax, result id}, so the traversal kernels see only
+// live rays.  Result ids: closest-hit rays write cHit/cT[id] (id = slot),
+// visibility rays oHit[id] (id = 4*slot + k).
+struct QRays {  // up to 4 rays of one slot sharing a direction
+    unsigned mask;
+    int id0;
+    V3 d;
+    float tmax;
+    V3 o0, o1, o2, o3;
+    float t0, t1, t2, t3;
+};
+
+// Appends every lane's rays (bits of r.mask) to queue q.  Every thread of the
+// 256-thread workgroup must call it.
+VX_D void block_enqueue(const TraceArgs &a, int q, const QRays &r) {
+    __shared__ unsigned sTot[4], sBase[4];
     const WaveBufs &w = a.wb;
-    if (active) active = (w.pMeta[s].x & F_NEE) != 0;
-    float4 rd = make_float4(0.f, 0.f, 0.f, -1.0f);
-    if (active) rd = w.oRayD[q];
-    active = active && rd.w >= 0.0f;
-    int iters[5] = {0, 0, 0, 0, 0};
-    if (active) {
-        const float4 ro = w.oRayO[q];
-        w.oHit[q] = dda_occluded(a.world, xyz(ro), xyz(rd), ro.w, rd.w VX_IT) ? 1 : 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int n = __popc(r.mask);
+    int incl = n;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
     }
-#ifdef VX_STATS
-    stat_wave(perSlot == 4 ? 3 : 4, active, iters);
-#endif
+    if (lane == 63) sTot[wv] = (unsigned)incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t0 = sTot[0], t1 = sTot[1], t2 = sTot[2], t3 = sTot[3];
+        const unsigned base = (t0 + t1 + t2 + t3) ? atomicAdd(&w.qCount[q], t0 + t1 + t2 + t3) : 0u;
+        sBase[0] = base;
+        sBase[1] = base + t0;
+        sBase[2] = base + t0 + t1;
+        sBase[3] = base + t0 + t1 + t2;
+    }
+    __syncthreads();
+    int k = (int)sBase[wv] + incl - n;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (!(r.mask & (1u << i))) continue;
+        const V3 o = i == 0 ? r.o0 : (i == 1 ? r.o1 : (i == 2 ? r.o2 : r.o3));
+        const float tmin = i == 0 ? r.t0 : (i == 1 ? r.t1 : (i == 2 ? r.t2 : r.t3));
+        w.qO[k] = f4(o, tmin);
+        w.qD[k] = f4(r.d, r.tmax);
+        w.qId[k] = r.id0 + i;
+        ++k;
+    }
 }
 
-// Persistent traversal with per-lane ray refill.  Secondary and visibility
-// rays are incoherent: a one-ray-per-lane wave runs as long as its longest ray
-// (measured: 26-31 % of lanes busy, tools/trace_stats.py).  Here a wave pulls
-// chunks of ray ids from a queue head and hands a new ray to every lane whose
-// walk has ended, whenever at least kRefill lanes are idle; the walk itself is
-// the resumable dda_begin / dda_iter pair, so every ray's result is the one
-// dda_closest / dda_occluded returns.
-// kind: 0 continuing path rays, 1 BRDF-candidate rays (closest hit),
-//       2 RIS visibility rays (ray 4s), 3 all four visibility rays of a slot.
-constexpr int kChunk = 256, kRefill = 24;
-
-template <int KIND>
-VX_D bool fetch_ray(const TraceArgs &a, int id, V3 &o, V3 &d, float &tmin, float &tmax) {
-    const int s = KIND == 3 ? (id >> 2) : id;
-    int px, py;
-    if (!slot_pixel(a, s, px, py)) return false;
-    const WaveBufs &w = a.wb;
-    const int flags = w.pMeta[s].x;
-    if (KIND == 0) {
-        if (!(flags & F_ALIVE)) return false;
-        o = xyz(w.pPos[s]);
-        d = xyz(w.pDir[s]);
-        tmin = 0.0f;
-        tmax = kRayMax;
-        return true;
-    }
-    if (!(flags & F_NEE)) return false;
-    if (KIND == 1) {
-        const float4 ro = w.cRayO[s];
-        if (!(ro.w >= 0.0f)) return false;
-        o = xyz(ro);
-        d = xyz(w.cRayD[s]);
-        tmin = 0.0f;
-        tmax = ro.w;
-        return true;
-    }
-    const int q = KIND == 3 ? id : 4 * id;
-    const float4 rd = w.oRayD[q];
-    if (!(rd.w >= 0.0f)) return false;
-    const float4 ro = w.oRayO[q];
-    o = xyz(ro);
-    d = xyz(rd);
-    tmin = ro.w;
-    tmax = rd.w;
-    return true;
-}
-
-template <int KIND>
-VX_D void store_ray(const TraceArgs &a, int id, int rc, const Hit &h) {
-    const WaveBufs &w = a.wb;
-    if (KIND <= 1) {
+template <bool OCC>
+VX_D void store_result(const WaveBufs &w, int id, int rc, const Hit &h) {
+    if (!OCC) {
         const Hit r = rc == DdaEvent ? h : Hit{0, 0, 0, 0, -1, 0, kRayMax};
         w.cHit[id] = pack_hit(r);
         w.cT[id] = r.t;
     } else {
-        w.oHit[KIND == 3 ? id : 4 * id] = rc == DdaEvent ? 1 : 0;
+        w.oHit[id] = rc == DdaEvent ? 1 : 0;
     }
 }
 
-template <int KIND>
-__global__ __launch_bounds__(256) void k_traverse(TraceArgs a, int nRays) {
-    constexpr bool OCC = KIND >= 2;
-    unsigned *head = a.wb.qHead + KIND;
-    int cBase = 0, cEnd = 0;  // wave-uniform: the unassigned part of the wave's chunk
-    bool drained = false;     // wave-uniform: the queue is empty
-    bool has = false;
-    int id = 0;
+// one ray per lane over queue q (grid sized for the queue's capacity)
+template <bool OCC>
+__global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q) {
+    const WaveBufs &w = a.wb;
+    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= w.qCount[q]) return;
+    const float4 ro = w.qO[i], rd = w.qD[i];
+    const int id = w.qId[i];
+    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+    Dda st;
+#ifdef VX_STATS
+    int iters[5] = {0, 0, 0, 0, 0};
+    int rc = dda_begin<OCC>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
+    while (rc == DdaRun) rc = dda_iter<OCC>(a.world, st, h, iters);
+    stat_wave((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), true, iters);
+#else
+    int rc = dda_begin<OCC>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
+    while (rc == DdaRun) rc = dda_iter<OCC>(a.world, st, h);
+#endif
+    store_result<OCC>(w, id, rc, h);
+}
+
+// Persistent variant (VXPT_PERSISTENT=1): every lane walks its own sequence of
+// queue entries (i, i + stride, ...), the next one prefetched into registers,
+// and starts it when its walk ends -- gated so the divergent start runs only
+// when at least kRefill lanes (or all waiting lanes) are ready for one.
+constexpr int kRefill = 16;
+template <bool OCC>
+__global__ __launch_bounds__(256) void k_queue_persistent(TraceArgs a, int q) {
+    const WaveBufs &w = a.wb;
+    const int n = (int)w.qCount[q];
+    const int stride = gridDim.x * 256;
+    int next = blockIdx.x * 256 + threadIdx.x;
+    bool pend = next < n, has = false;
+    float4 po = make_float4(0.f, 0.f, 0.f, 0.f), pd = po;
+    int pid = 0, id = 0;
+    if (pend) { po = w.qO[next]; pd = w.qD[next]; pid = w.qId[next]; }
     Dda st;
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
-    const unsigned lane = threadIdx.x & 63;
     while (true) {
-        unsigned long long idle = __ballot(!has);
-        if (!drained && __popcll(idle) >= (idle == ~0ull ? 1 : kRefill)) {
-            // hand out ray ids to the idle lanes until they are all busy or the queue is empty
-            while (idle && !drained) {
-                if (cBase >= cEnd) {
-                    int v = 0;
-                    if (lane == 0) v = (int)atomicAdd(head, (unsigned)kChunk);
-                    v = __shfl(v, 0);
-                    if (v >= nRays) { drained = true; break; }
-                    cBase = v;
-                    cEnd = min(v + kChunk, nRays);
-                }
-                const int rank = __popcll(idle & ((1ull << lane) - 1ull));
-                const int avail = cEnd - cBase;
-                const bool mine = !has && rank < avail;
-                const int taken = min(__popcll(idle), avail);
-                if (mine) {
-                    id = cBase + rank;
-                    V3 o, d;
-                    float tmin, tmax;
-                    if (fetch_ray<KIND>(a, id, o, d, tmin, tmax)) {
-                        h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
-                        const int rc = dda_begin<OCC>(a.world, o, d, tmin, tmax, st, h);
-                        if (rc == DdaRun) has = true;
-                        else store_ray<KIND>(a, id, rc, h);
-                    }
-                }
-                cBase += taken;
-                idle = __ballot(!has);
-                // lanes whose ray ended at once stay idle for the next round
-                if (__popcll(idle) < kRefill) break;
+        const unsigned long long want = __ballot(!has && pend), busy = __ballot(has);
+        if (!want && !busy) break;
+        if (want && (__popcll(want) >= kRefill || __popcll(busy) <= __popcll(want))) {
+            if (!has && pend) {
+                id = pid;
+                const V3 o = xyz(po), d = xyz(pd);
+                const float tmin = po.w, tmax = pd.w;
+                next += stride;
+                pend = next < n;
+                if (pend) { po = w.qO[next]; pd = w.qD[next]; pid = w.qId[next]; }
+                h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
+                const int rc = dda_begin<OCC>(a.world, o, d, tmin, tmax, st, h);
+                if (rc == DdaRun) has = true;
+                else store_result<OCC>(w, id, rc, h);
             }
-        }
-        if (!__ballot(has)) {
-            if (drained) break;
-            continue;
         }
         if (has) {
             const int rc = dda_iter<OCC>(a.world, st, h);
             if (rc != DdaRun) {
-                store_ray<KIND>(a, id, rc, h);
+                store_result<OCC>(w, id, rc, h);
                 has = false;
             }
         }
@@ -360,8 +348,7 @@ VX_D V3 shade_light(const SurfS &sf, bool skipAlbedo, const LSample &ls, const R
 }
 
 // closesthit / miss for the segment's ray; candidate generation for NEE
-__global__ __launch_bounds__(256) void k_shade(TraceArgs a, int seg) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
+VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
@@ -484,6 +471,14 @@ __global__ __launch_bounds__(256) void k_shade(TraceArgs a, int seg) {
                       sf.roughness, sd, bop, bp);
         w.cRayO[s] = f4(frontPos, bp > 0.0f ? kFltMax : -1.0f);
         w.cRayD[s] = f4(sd, 0.0f);
+        if (bp > 0.0f) {
+            qr.mask = 1u;
+            qr.id0 = s;
+            qr.o0 = frontPos;
+            qr.t0 = 0.0f;
+            qr.d = sd;
+            qr.tmax = kFltMax;
+        }
     }
     w.sPos[s] = f4(frontPos, h.t);
     w.sNrm[s] = f4(sf.normal, sf.roughness);
@@ -499,9 +494,15 @@ __global__ __launch_bounds__(256) void k_shade(TraceArgs a, int seg) {
     w.pMeta[s] = meta;
 }
 
+__global__ __launch_bounds__(256) void k_shade(TraceArgs a, int seg) {
+    QRays qr;
+    qr.mask = 0u;
+    shade_slot(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
+    block_enqueue(a, 4 * seg + 1, qr);
+}
+
 // BRDF candidate from its traced ray, RIS over {local, sun, sky, BRDF}, visibility ray
-__global__ __launch_bounds__(256) void k_nee(TraceArgs a) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
+VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
@@ -575,18 +576,30 @@ __global__ __launch_bounds__(256) void k_nee(TraceArgs a) {
     ris.M = 1;
     const LSample ls = selBrdf ? brdfLs : (selSky ? skyLs : (selSun ? sunLs : invalid_ls()));
     const bool trace = ls.type != LtInvalid && ris.lightData != 0;
-    w.oRayO[4 * s] = f4(sf.pos, 0.0f);
-    w.oRayD[4 * s] = f4(ls.position, trace ? kRayMax : -1.0f);
+    if (trace) {
+        qr.mask = 1u;
+        qr.id0 = 4 * s;
+        qr.o0 = sf.pos;
+        qr.t0 = 0.0f;
+        qr.d = ls.position;
+        qr.tmax = kRayMax;
+    }
     w.rRis[s] = ris;
     store_ls(w, s, ls);
     meta.y = rng.idx;
     w.pMeta[s] = meta;
 }
 
+__global__ __launch_bounds__(256) void k_nee(TraceArgs a, int seg) {
+    QRays qr;
+    qr.mask = 0u;
+    nee_slot(a, blockIdx.x * 256 + threadIdx.x, qr);
+    block_enqueue(a, 4 * seg + 2, qr);
+}
+
 // visibility of the RIS sample; seg 0: ReSTIR temporal reuse (Restir.h:11-415,
 // closesthit.cu:626-851) up to its visibility rays; seg > 0: final shading.
-__global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
+VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
@@ -660,8 +673,11 @@ __global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
     }
     // bias-correction rays: the selected light seen from each accepted tap's surface
     float psv0 = 0, psv1 = 0, psv2 = 0;
+    qr.id0 = 4 * s;
+    qr.d = ls.position;
+    qr.tmax = kRayMax;
+#pragma unroll
     for (int i = 0; i < 3; ++i) {
-        float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = make_float4(0.f, 0.f, 0.f, -1.0f);
         if (rr.lightData != 0 && (cached & (1u << i))) {
             const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
             const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
@@ -672,21 +688,21 @@ __global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;
             if (psv > 0 && !(i == 0 && i == selLoop)) {
-                ro = f4(ts.pos, 0.01f + 0.01f * ts.depth);
-                rd = f4(ls.position, kRayMax);
+                qr.mask |= 2u << i;
+                const float tmin = 0.01f + 0.01f * ts.depth;
+                if (i == 0) { qr.o1 = ts.pos; qr.t1 = tmin; }
+                else if (i == 1) { qr.o2 = ts.pos; qr.t2 = tmin; }
+                else { qr.o3 = ts.pos; qr.t3 = tmin; }
             }
         }
-        w.oRayO[4 * s + 1 + i] = ro;
-        w.oRayD[4 * s + 1 + i] = rd;
         w.oHit[4 * s + 1 + i] = 0;
     }
     // final visibility: with no tap selected the sample is the RIS one and the
     // ray equals the RIS visibility ray, whose result is already in oHit[4s]
     if (ls.type != LtInvalid && selLoop >= 0) {
-        w.oRayO[4 * s] = f4(sf.pos, 0.0f);
-        w.oRayD[4 * s] = f4(ls.position, kRayMax);
-    } else {
-        w.oRayD[4 * s] = make_float4(0.f, 0.f, 0.f, -1.0f);
+        qr.mask |= 1u;
+        qr.o0 = sf.pos;
+        qr.t0 = 0.0f;
     }
     w.rRR[s] = rr;
     store_ls(w, s, ls);
@@ -695,6 +711,13 @@ __global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
     w.tapM[s] = make_float4(tapM0, tapM1, tapM2, 0.0f);
     meta.y = rng.idx;
     w.pMeta[s] = meta;
+}
+
+__global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
+    QRays qr;
+    qr.mask = 0u;
+    restir_slot(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
+    block_enqueue(a, 4 * seg + 3, qr);
 }
 
 // seg 0: bias-corrected ReSTIR weight, final visibility, shading, reservoir store
@@ -827,35 +850,29 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k_primary_gbuffer, g, b, 0, st, a);
         return hipGetLastError();
     }
-    if (!a.persistent) {
-        for (int seg = 0; seg < a.segments; ++seg) {
-            if (seg > 0) hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
-            hipLaunchKernelGGL(k_shade, g, b, 0, st, a, seg);
-            hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 1);
-            hipLaunchKernelGGL(k_nee, g, b, 0, st, a);
-            hipLaunchKernelGGL(k_occluded, g, b, 0, st, a, 1);
-            hipLaunchKernelGGL(k_restir, g, b, 0, st, a, seg);
-            if (seg == 0) {
-                hipLaunchKernelGGL(k_occluded, g4, b, 0, st, a, 4);
-                hipLaunchKernelGGL(k_finish, g, b, 0, st, a);
-            }
-        }
-        return hipGetLastError();
-    }
-    // persistent traversal (experiment, VXPT_PERSISTENT=1): enough 4-wave workgroups to fill every SIMD
+    // secondary / visibility rays go through the compacted queues; their
+    // counters (4 per segment) are zeroed once per pass
+    hipMemsetAsync(a.wb.qCount, 0, 64 * sizeof(unsigned), st);
     const dim3 gp(a.numCU * 8);
-    hipMemsetAsync(a.wb.qHead, 0, 16 * sizeof(unsigned) * 3, st);
+    auto trav = [&](bool occ, int q, int cap) {
+        if (a.persistent) {
+            if (occ) hipLaunchKernelGGL(k_queue_persistent<true>, gp, b, 0, st, a, q);
+            else hipLaunchKernelGGL(k_queue_persistent<false>, gp, b, 0, st, a, q);
+        } else {
+            const dim3 gq((cap + 255) / 256);
+            if (occ) hipLaunchKernelGGL(k_queue<true>, gq, b, 0, st, a, q);
+            else hipLaunchKernelGGL(k_queue<false>, gq, b, 0, st, a, q);
+        }
+    };
     for (int seg = 0; seg < a.segments; ++seg) {
-        TraceArgs as = a;
-        as.wb.qHead = a.wb.qHead + 16 * (seg < 3 ? seg : 2);
-        if (seg > 0) hipLaunchKernelGGL(k_traverse<0>, gp, b, 0, st, as, a.nSlots);
+        if (seg > 0) hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
         hipLaunchKernelGGL(k_shade, g, b, 0, st, a, seg);
-        hipLaunchKernelGGL(k_traverse<1>, gp, b, 0, st, as, a.nSlots);
-        hipLaunchKernelGGL(k_nee, g, b, 0, st, a);
-        hipLaunchKernelGGL(k_traverse<2>, gp, b, 0, st, as, a.nSlots);
+        trav(false, 4 * seg + 1, a.nSlots);
+        hipLaunchKernelGGL(k_nee, g, b, 0, st, a, seg);
+        trav(true, 4 * seg + 2, a.nSlots);
         hipLaunchKernelGGL(k_restir, g, b, 0, st, a, seg);
         if (seg == 0) {
-            hipLaunchKernelGGL(k_traverse<3>, gp, b, 0, st, as, 4 * a.nSlots);
+            trav(true, 4 * seg + 3, 4 * a.nSlots);
             hipLaunchKernelGGL(k_finish, g, b, 0, st, a);
         }
     }

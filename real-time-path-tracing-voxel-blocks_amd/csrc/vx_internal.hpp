@@ -102,11 +102,13 @@ struct WaveBufs {
     float4 *ls1;    // radiance xyz, light type
     float4 *tapPsv; // target pdf of the selection at the three temporal taps, first-visibility flag
     float4 *tapM;   // the taps' clamped M
-    // visibility queue: 4 rays per slot (0: RIS/final visibility, 1-3: bias-correction taps)
-    float4 *oRayO, *oRayD;  // o xyz + tmin, d xyz + tmax (< 0: inactive)
+    // visibility results: 4 rays per slot (0: RIS/final visibility, 1-3: bias-correction taps)
     uint8_t *oHit;
-    // work-queue heads of the persistent traversal launches, zeroed once per pass
-    unsigned *qHead;
+    // compacted ray queue (trace.hip block_enqueue): o xyz + tmin, d xyz + tmax,
+    // result id; one storage reused by the pass's queues, counters 4 per segment
+    float4 *qO, *qD;
+    int *qId;
+    unsigned *qCount;
 };
 
 struct TraceArgs {

@@ -614,6 +614,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (!cfg || !out) return VXPT_ERR_ARG;
     *out = nullptr;
     if (cfg->width <= 0 || cfg->height <= 0 || cfg->width % 8 || cfg->height % 8) return VXPT_ERR_ARG;
+    // the trace pass keeps 4 ray-queue counters per path segment, 64 in all
+    if (cfg->total_bounce_limit > 16 || cfg->diffuse_bounce_limit > 16) return VXPT_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return VXPT_ERR_NODEV;
     auto *c = new vxpt_ctx();
@@ -649,8 +651,9 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
             dalloc(c, w.sGeo, ns) || dalloc(c, w.sAlb, ns) || dalloc(c, w.sWo, ns) || dalloc(c, w.rSun, ns) ||
             dalloc(c, w.rSky, ns) || dalloc(c, w.rRis, ns) || dalloc(c, w.rRR, ns) || dalloc(c, w.nIdx, ns) ||
             dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
-            dalloc(c, w.oRayO, 4 * ns) || dalloc(c, w.oRayD, 4 * ns) || dalloc(c, w.oHit, 4 * ns) ||
-            dalloc(c, w.qHead, 64))
+            dalloc(c, w.oHit, 4 * ns) ||
+            dalloc(c, w.qO, 4 * ns) || dalloc(c, w.qD, 4 * ns) ||
+            dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, 64))
             return VXPT_ERR_HIP;
     }
     // tables
