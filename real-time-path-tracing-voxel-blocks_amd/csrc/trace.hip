@@ -68,7 +68,7 @@ VX_D V2 restir_disk(float r0, float r1) {
 // traversal statistics (experiment builds only), per kind 8 counters:
 // rays, waves, sum of per-wave max outer iterations, outer iterations by level
 // (64^3 skip, 16^3 skip, 4^3 skip, brick walk), in-brick cell steps
-__device__ unsigned long long g_stats[8 * 8];
+__device__ unsigned long long g_stats[8 * 8];  // kinds 0-4 as tools/trace_stats.py, 5 = stragglers
 VX_D int wsum(int v) { for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o); return v; }
 VX_D void stat_wave(int kind, bool active, const int *it) {
     const unsigned long long m = __ballot(active);
@@ -201,67 +201,121 @@ VX_D void store_result(const WaveBufs &w, int id, int rc, const Hit &h) {
     }
 }
 
-// one ray per lane over queue q (grid sized for the queue's capacity)
-template <bool OCC>
-__global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q) {
-    const WaveBufs &w = a.wb;
-    const unsigned i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= w.qCount[q]) return;
-    const float4 ro = w.qO[i], rd = w.qD[i];
-    const int id = w.qId[i];
-    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
-    Dda st;
-#ifdef VX_STATS
-    int iters[5] = {0, 0, 0, 0, 0};
-    int rc = dda_begin<OCC>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
-    while (rc == DdaRun) rc = dda_iter<OCC>(a.world, st, h, iters);
-    stat_wave((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), true, iters);
-#else
-    int rc = dda_begin<OCC>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
-    while (rc == DdaRun) rc = dda_iter<OCC>(a.world, st, h);
-#endif
-    store_result<OCC>(w, id, rc, h);
+// Traversal of queue q, one ray per lane (grid sized for the queue's
+// capacity; workgroups past the queue's end leave at once).  A wave lasts as
+// long as its longest walk and incoherent rays have a long tail of walk
+// lengths, so this phase stops every walk after `cap` outer iterations and
+// moves the unfinished ones -- their walk state -- to a straggler queue that
+// k_resume finishes densely packed.  The straggler queue has 8 shards
+// (workgroup b appends to shard b % 8, one atomic per workgroup on that
+// shard's counter word) so no single word serialises the appends.
+constexpr int kShards = 8;
+VX_D unsigned *straggler_count(const WaveBufs &w, int level, int q, int k) {
+    return w.qCount + 64 + (((level - 1) * 16 + q) * kShards + k) * 16;
 }
 
-// Persistent variant (VXPT_PERSISTENT=1): every lane walks its own sequence of
-// queue entries (i, i + stride, ...), the next one prefetched into registers,
-// and starts it when its walk ends -- gated so the divergent start runs only
-// when at least kRefill lanes (or all waiting lanes) are ready for one.
-constexpr int kRefill = 16;
 template <bool OCC>
-__global__ __launch_bounds__(256) void k_queue_persistent(TraceArgs a, int q) {
+__global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int shardCap) {
+    __shared__ unsigned sTot[4], sBase[4];
     const WaveBufs &w = a.wb;
-    const int n = (int)w.qCount[q];
-    const int stride = gridDim.x * 256;
-    int next = blockIdx.x * 256 + threadIdx.x;
-    bool pend = next < n, has = false;
-    float4 po = make_float4(0.f, 0.f, 0.f, 0.f), pd = po;
-    int pid = 0, id = 0;
-    if (pend) { po = w.qO[next]; pd = w.qD[next]; pid = w.qId[next]; }
-    Dda st;
+    const unsigned n = w.qCount[q];
+    if (blockIdx.x * 256 >= n) return;  // whole workgroup past the end
+    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    const bool live = i < n;
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
-    while (true) {
-        const unsigned long long want = __ballot(!has && pend), busy = __ballot(has);
-        if (!want && !busy) break;
-        if (want && (__popcll(want) >= kRefill || __popcll(busy) <= __popcll(want))) {
-            if (!has && pend) {
-                id = pid;
-                const V3 o = xyz(po), d = xyz(pd);
-                const float tmin = po.w, tmax = pd.w;
-                next += stride;
-                pend = next < n;
-                if (pend) { po = w.qO[next]; pd = w.qD[next]; pid = w.qId[next]; }
-                h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
-                const int rc = dda_begin<OCC>(a.world, o, d, tmin, tmax, st, h);
-                if (rc == DdaRun) has = true;
-                else store_result<OCC>(w, id, rc, h);
-            }
+    Dda st;
+    int rc = DdaNone, id = 0;
+#ifdef VX_STATS
+    int iters[5] = {0, 0, 0, 0, 0};
+    int *itp = iters;
+#else
+    int *itp = nullptr;
+#endif
+    if (live) {
+        const float4 ro = w.qO[i], rd = w.qD[i];
+        id = w.qId[i];
+        rc = dda_begin<OCC>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
+        for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC>(a.world, st, h, itp);
+    }
+#ifdef VX_STATS
+    stat_wave((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), live, iters);
+#endif
+    if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h);
+    // unfinished walks -> straggler queue
+    const bool defer = live && rc == DdaRun;
+    const unsigned long long m = __ballot(defer);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, shard = blockIdx.x % kShards;
+    if (lane == 0) sTot[wv] = (unsigned)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t0 = sTot[0], t1 = sTot[1], t2 = sTot[2], t3 = sTot[3], tot = t0 + t1 + t2 + t3;
+        const unsigned base = tot ? atomicAdd(straggler_count(w, 1, q, shard), tot) : 0u;
+        sBase[0] = base;
+        sBase[1] = base + t0;
+        sBase[2] = base + t0 + t1;
+        sBase[3] = base + t0 + t1 + t2;
+    }
+    __syncthreads();
+    if (defer) {
+        const unsigned k = (unsigned)(shard * shardCap) + sBase[wv] + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+        const DdaSaved sv = dda_save(st, (int)i);
+        w.sCell[0][k] = sv.cell;
+        w.sT[0][k] = sv.t;
+        w.sFace[0][k] = sv.face;
+    }
+}
+
+// Resumes the level-`level` stragglers of queue q (level 1: from k_queue,
+// level 2: from the level-1 resume).  Each wave serves one shard (wave index
+// % 8), 64 consecutive entries per round, striding over the shard (the fixed
+// grid normally covers every straggler in one round).  With cap > 0 the walks
+// stop after cap more iterations and the unfinished ones move on to the next
+// level, same shard, one atomic per wave.
+template <bool OCC>
+__global__ __launch_bounds__(256) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
+    const WaveBufs &w = a.wb;
+    const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
+    const int shard = wv % kShards, step = gridDim.x * 256 / kShards;
+    const int n = (int)*straggler_count(w, level, q, shard);
+    const int in = (level - 1) & 1, out = level & 1;
+    for (int j = (wv / kShards) * 64 + lane; j - lane < n; j += step) {
+        const bool live = j < n;
+        Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+        Dda st;
+        int rc = DdaNone, id = 0, e = 0;
+#ifdef VX_STATS
+        int iters[5] = {0, 0, 0, 0, 0};
+        int *itp = iters;
+#else
+        int *itp = nullptr;
+#endif
+        if (live) {
+            const int k = shard * shardCap + j;
+            const DdaSaved sv{w.sCell[in][k], w.sT[in][k], w.sFace[in][k]};
+            e = sv.cell.w;
+            const float4 ro = w.qO[e], rd = w.qD[e];
+            id = w.qId[e];
+            dda_resume(a.world, xyz(ro), xyz(rd), ro.w, rd.w, sv, st);
+            rc = DdaRun;
+            for (int it = 0; rc == DdaRun && (cap <= 0 || it < cap); ++it) rc = dda_iter<OCC>(a.world, st, h, itp);
         }
-        if (has) {
-            const int rc = dda_iter<OCC>(a.world, st, h);
-            if (rc != DdaRun) {
-                store_result<OCC>(w, id, rc, h);
-                has = false;
+#ifdef VX_STATS
+        stat_wave(5, live, iters);
+#endif
+        if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h);
+        const bool defer = live && rc == DdaRun;
+        const unsigned long long m = __ballot(defer);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(straggler_count(w, level + 1, q, shard), (unsigned)__popcll(m));
+            base = __shfl(base, leader);
+            if (defer) {
+                const int k = shard * shardCap + (int)base + __popcll(m & ((1ull << lane) - 1ull));
+                const DdaSaved sv = dda_save(st, e);
+                w.sCell[out][k] = sv.cell;
+                w.sT[out][k] = sv.t;
+                w.sFace[out][k] = sv.face;
             }
         }
     }
@@ -852,16 +906,19 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
     }
     // secondary / visibility rays go through the compacted queues; their
     // counters (4 per segment) are zeroed once per pass
-    hipMemsetAsync(a.wb.qCount, 0, 64 * sizeof(unsigned), st);
-    const dim3 gp(a.numCU * 8);
+    hipMemsetAsync(a.wb.qCount, 0, (64 + 3 * 16 * kShards * 16) * sizeof(unsigned), st);
+    const dim3 gr(a.numCU * 16);
     auto trav = [&](bool occ, int q, int cap) {
-        if (a.persistent) {
-            if (occ) hipLaunchKernelGGL(k_queue_persistent<true>, gp, b, 0, st, a, q);
-            else hipLaunchKernelGGL(k_queue_persistent<false>, gp, b, 0, st, a, q);
+        const dim3 gq((cap + 255) / 256);
+        const int shardCap = (int)((gq.x + kShards - 1) / kShards) * 256;
+        if (occ) {
+            hipLaunchKernelGGL(k_queue<true>, gq, b, 0, st, a, q, a.iterCap, shardCap);
+            hipLaunchKernelGGL(k_resume<true>, gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
+            if (a.iterCap2 > 0) hipLaunchKernelGGL(k_resume<true>, gr, b, 0, st, a, q, 2, shardCap, 0);
         } else {
-            const dim3 gq((cap + 255) / 256);
-            if (occ) hipLaunchKernelGGL(k_queue<true>, gq, b, 0, st, a, q);
-            else hipLaunchKernelGGL(k_queue<false>, gq, b, 0, st, a, q);
+            hipLaunchKernelGGL(k_queue<false>, gq, b, 0, st, a, q, a.iterCap, shardCap);
+            hipLaunchKernelGGL(k_resume<false>, gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
+            if (a.iterCap2 > 0) hipLaunchKernelGGL(k_resume<false>, gr, b, 0, st, a, q, 2, shardCap, 0);
         }
     };
     for (int seg = 0; seg < a.segments; ++seg) {

@@ -109,12 +109,15 @@ VX_D bool slab(float o, float d, float W, int a, float &t0, float &t1, int &ax) 
 // Start a walk; returns false if the ray never meets the world box.  For an
 // origin outside the box, `outside` is set and the entry crossing (axis `ax`,
 // t `tEnter`) is already taken.
-VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outside, int &ax, float &tEnter) {
+VX_D void ray_setup(V3 o, V3 d, Ray3 &r) {
     r.ox = o.x; r.oy = o.y; r.oz = o.z;
     r.dx = d.x; r.dy = d.y; r.dz = d.z;
     r.mx = d.x != 0.0f; r.my = d.y != 0.0f; r.mz = d.z != 0.0f;
     r.sx = d.x > 0.0f ? 1 : -1; r.sy = d.y > 0.0f ? 1 : -1; r.sz = d.z > 0.0f ? 1 : -1;
     r.ix = r.mx ? 1.0f / d.x : 0.0f; r.iy = r.my ? 1.0f / d.y : 0.0f; r.iz = r.mz ? 1.0f / d.z : 0.0f;
+}
+VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outside, int &ax, float &tEnter) {
+    ray_setup(o, d, r);
     c.x = (int)floorf(o.x); c.y = (int)floorf(o.y); c.z = (int)floorf(o.z);
     outside = !(c.x >= 0 && c.x < w.wx && c.y >= 0 && c.y < w.wy && c.z >= 0 && c.z < w.wz);
     if (outside) {
@@ -292,6 +295,28 @@ VX_D int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s
         }
     }
     return DdaRun;
+}
+
+// Walk state as saved between launches (straggler continuation): the cell
+// and its plane crossings, the face-rule state and the step count; the rest
+// is rebuilt from the ray exactly as dda_begin builds it.
+struct DdaSaved { int4 cell; float4 t; int2 face; };
+VX_D DdaSaved dda_save(const Dda &s, int entry) {
+    return DdaSaved{make_int4(s.c.x, s.c.y, s.c.z, entry), make_float4(s.c.tx, s.c.ty, s.c.tz, 0.0f),
+                    make_int2(s.prevLoc, (s.prevId + 1) | (s.steps << 16))};
+}
+VX_D void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, const DdaSaved &v, Dda &s) {
+    ray_setup(o, d, s.r);
+    s.c.x = v.cell.x; s.c.y = v.cell.y; s.c.z = v.cell.z;
+    s.c.tx = v.t.x; s.c.ty = v.t.y; s.c.tz = v.t.z;
+    s.tmin = tmin;
+    s.tmax = tmax;
+    s.od = w.bdist + (size_t)w.nBricks * ((s.r.sx > 0 ? 1 : 0) | (s.r.sy > 0 ? 2 : 0) | (s.r.sz > 0 ? 4 : 0));
+    s.nb = -1;
+    locate(w, s);
+    s.prevLoc = v.face.x;
+    s.prevId = (v.face.y & 0xFFFF) - 1;
+    s.steps = v.face.y >> 16;
 }
 
 template <bool OCC>

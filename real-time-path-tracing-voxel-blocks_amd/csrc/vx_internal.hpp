@@ -108,7 +108,11 @@ struct WaveBufs {
     // result id; one storage reused by the pass's queues, counters 4 per segment
     float4 *qO, *qD;
     int *qId;
-    unsigned *qCount;
+    unsigned *qCount;  // 64 queue counters, then per straggler level (1-3) 16 queues x 8 shard counters 16 words apart
+    // straggler queues (ping-pong by level): walk state of rays stopped at an iteration cap (DdaSaved)
+    int4 *sCell[2];
+    float4 *sT[2];
+    int2 *sFace[2];
 };
 
 struct TraceArgs {
@@ -132,7 +136,7 @@ struct TraceArgs {
     WaveBufs wb;
     int tilesX, nSlots;         // 8x8 tiles across the frame width; slots in the band
     int numCU;                  // compute units of the device (traversal grid sizing)
-    int persistent;             // persistent refill traversal kernels (experiment)
+    int iterCap, iterCap2;      // outer DDA iterations before a ray moves to the level-1 / level-2 straggler queue
 };
 
 // kernel launchers (defined in the .hip translation units)

@@ -530,7 +530,8 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.tilesX = (c->W + 7) / 8;
     a.nSlots = a.tilesX * ((a.y1 - a.y0 + 7) / 8) * 64;
     a.numCU = c->numCU;
-    a.persistent = getenv("VXPT_PERSISTENT") ? atoi(getenv("VXPT_PERSISTENT")) : 0;
+    a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
+    a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_trace(a, c->stream));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -653,7 +654,10 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
             dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
             dalloc(c, w.oHit, 4 * ns) ||
             dalloc(c, w.qO, 4 * ns) || dalloc(c, w.qD, 4 * ns) ||
-            dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, 64))
+            dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, 64 + 3 * 16 * 8 * 16) ||
+            dalloc(c, w.sCell[0], 4 * ns + 2048) || dalloc(c, w.sT[0], 4 * ns + 2048) ||
+            dalloc(c, w.sFace[0], 4 * ns + 2048) || dalloc(c, w.sCell[1], 4 * ns + 2048) ||
+            dalloc(c, w.sT[1], 4 * ns + 2048) || dalloc(c, w.sFace[1], 4 * ns + 2048))
             return VXPT_ERR_HIP;
     }
     // tables

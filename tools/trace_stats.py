@@ -17,7 +17,8 @@ import numpy as np  # noqa: E402
 import vxpt  # noqa: E402
 from bench import C1_DIR, scene_args  # noqa: E402
 
-KINDS = {0: "path rays", 1: "BRDF candidate", 2: "camera", 3: "visibility x4 (ReSTIR)", 4: "visibility (RIS)"}
+KINDS = {0: "path rays", 1: "BRDF candidate", 2: "camera", 3: "visibility x4 (ReSTIR)", 4: "visibility (RIS)",
+         5: "stragglers (all queues)"}
 
 
 class A:
