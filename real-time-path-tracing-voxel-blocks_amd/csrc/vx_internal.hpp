@@ -172,7 +172,10 @@ struct DenoiseArgs {
     // once per frame by k_world_pos: the stencil passes read it instead of
     // re-deriving a camera ray per tap
     float4 *wpos;
-    // firefly scratch
+    // history-fix lists (k_temporal -> k_history_fix), per 16x16 tile of the band's
+    // grid: up to 256 pixel indices at tile*256, count in hfCount[tile]
+    uint32_t *hfList, *hfCount;
+    // firefly scratch; ffCount[0..3] are zeroed by k_world_pos
     uint32_t *ffCount;
     uint32_t *ffIndex;
     float4 *ffColor;

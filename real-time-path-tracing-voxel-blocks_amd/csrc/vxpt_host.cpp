@@ -173,7 +173,7 @@ struct vxpt_ctx {
     float4 *dnPrevNormalRough = nullptr;
     float *dnPrevDepth = nullptr, *dnPrevMaterial = nullptr;
     float4 *wpos = nullptr;
-    uint32_t *ffCount = nullptr, *ffIndex = nullptr;
+    uint32_t *ffCount = nullptr, *ffIndex = nullptr, *hfList = nullptr, *hfCount = nullptr;
     float4 *ffColor = nullptr;
     Reservoir *ffRes = nullptr;
     bool denoiseInputIsAccum = false;
@@ -353,6 +353,7 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.output = c->output;
     a.histLen = c->histLen; a.prevHistLen = c->prevHistLen;
     a.ffCount = c->ffCount; a.ffIndex = c->ffIndex; a.ffColor = c->ffColor; a.ffRes = c->ffRes;
+    a.hfList = c->hfList; a.hfCount = c->hfCount;
     a.wpos = c->wpos;
 }
 
@@ -641,7 +642,9 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         dalloc(c, c->ping, n) || dalloc(c, c->pong, n) || dalloc(c, c->prevIllum, n) || dalloc(c, c->prevFast, n) ||
         dalloc(c, c->output, n) || dalloc(c, c->histLen, n) || dalloc(c, c->prevHistLen, n) ||
         dalloc(c, c->dnPrevNormalRough, n) || dalloc(c, c->dnPrevDepth, n) || dalloc(c, c->dnPrevMaterial, n) ||
-        dalloc(c, c->ffCount, 4) || dalloc(c, c->wpos, n) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n))
+        dalloc(c, c->ffCount, 4) || dalloc(c, c->wpos, n) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n) ||
+        dalloc(c, c->hfList, (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16) * 256) ||
+        dalloc(c, c->hfCount, (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16)))
         return VXPT_ERR_HIP;
     {   // wavefront trace state: one slot per pixel (8x8 tiles), 4 visibility rays per slot
         const size_t ns = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64;

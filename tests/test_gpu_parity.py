@@ -207,6 +207,43 @@ def test_denoiser_on_identical_inputs():
     r.close()
 
 
+def test_denoiser_history_fix_after_camera_move():
+    """8 frames on injected inputs, the camera moving at frame 6: converged
+    history everywhere except the disoccluded pixels, so the history fix runs
+    on sparse per-tile lists (one wave per pixel) as well as dense ones."""
+    r, o = _setup(64, 48)
+    o.set_sky()
+    r.trace(0)
+    p = _dn_params()
+    pos, d, fov = C1_CAMERA[0], C1_CAMERA[1], C1_CAMERA[2]
+    pos2 = (pos[0] + 0.35, pos[1] + 0.05, pos[2] - 0.25)
+    sparse_seen = False
+    for f in range(8):
+        if f == 6:
+            r.set_camera(pos2, d, fov=fov, prev=(pos, d, fov))
+            o.set_camera(pos2, d, fov=fov)
+            o.set_camera(pos, d, fov=fov, which=1)
+        if f == 7:
+            r.set_camera(pos2, d, fov=fov, prev=(pos2, d, fov))
+            o.set_camera(pos2, d, fov=fov, which=1)
+        o.trace(f)
+        o.post_trace()
+        _inject_frame(r, o)
+        r.denoise(f, f + 1, p)
+        o.denoise(f, f + 1)
+        for name in ("OUTPUT", "PREV_ILLUM", "PREV_FAST"):
+            g, c = r.read(name), o.read(vxpt.BUF[name])
+            rel = _rel(g, c)
+            assert rel.max() < RTOL_DN, (f, name, rel.max(), np.unravel_index(rel.argmax(), rel.shape))
+        h = r.read("HIST_LEN")
+        np.testing.assert_allclose(h, o.read(19), rtol=1e-6)
+        low = (h <= 4) & (r.read("DEPTH") < 5e5)
+        if f >= 5 and 0 < low.sum() < 0.3 * low.size:
+            sparse_seen = True
+    assert sparse_seen
+    r.close()
+
+
 def test_render_frame_spp4_properties(pair):
     r, _ = pair
     r.render_frame(0, 1, _dn_params())

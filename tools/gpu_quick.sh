@@ -9,5 +9,5 @@ rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/tq_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python bench.py --steps 10 --warmup 4 --no-cpu-baseline "$@" > gpurun_out/bq_$TAG.log 2>&1 || { echo "bench failed"; tail gpurun_out/bq_$TAG.log; exit 1; }
 tail -1 gpurun_out/bq_$TAG.log
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv rocpd -d gpurun_out/pq_$TAG -o run -- python bench.py --steps 3 --warmup 2 --no-cpu-baseline "$@" > gpurun_out/pq_$TAG.log 2>&1 || { echo "prof failed"; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv rocpd -d gpurun_out/pq_$TAG -o run -- python bench.py --steps 3 --warmup 8 --no-cpu-baseline "$@" > gpurun_out/pq_$TAG.log 2>&1 || { echo "prof failed"; exit 1; }
 python tools/profsum.py gpurun_out/pq_$TAG/run_results.db 24
