@@ -39,6 +39,8 @@ VX_D V3 xyz4(float4 v) { return V3(v.x, v.y, v.z); }
 // world position of the (edge-clamped) pixel's hit, from the per-frame plane
 VX_D V3 wp(const DenoiseArgs &a, int x, int y) { return xyz4(a.wpos[(size_t)cl(y, a.H) * a.W + cl(x, a.W)]); }
 __global__ __launch_bounds__(256) void k_world_pos(DenoiseArgs a) {
+    // the first pass of every denoise: zero the firefly list counter
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) a.ffCount[threadIdx.x] = 0u;
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.y1) return;
     const size_t i = (size_t)y * a.W + x;
@@ -285,13 +287,13 @@ VX_D V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
     return out;
 }
 
-__global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
+// Returns whether the history fix must filter the pixel (HistoryFix.h:20-22:
+// non-sky and history <= 4; pixels past the denoising range keep last frame's length).
+VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
     const int W = a.W, H = a.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= a.y1) return;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
-    if (z > a.p.denoisingRange) return;
+    if (z > a.p.denoisingRange) return z <= kRange && a.histLen[i] <= 4.0f;
     const CamDev &cam = a.cam, &pc = a.prevCam;
     const V3 cN = f4(a.normalRough[i]).xyz();
     V3 avgN = cN;
@@ -399,16 +401,30 @@ __global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
     a.ping[i] = tf(acc);
     a.pong[i] = make_float4(accR.x, accR.y, accR.z, 0.0f);
     a.histLen[i] = hist;
+    return hist <= 4.0f;
+}
+
+// The pixels the history fix must filter (rare once history has built up)
+// are listed per 16x16 tile: hfList[tile*256 + k] = pixel index, hfCount[tile]
+// = k's; no atomics, and the history-fix launch only works on listed pixels.
+__global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
+    __shared__ unsigned sTot[4];
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+    const bool fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y);
+    const unsigned long long m = __ballot(fix);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) sTot[wv] = (unsigned)__popcll(m);
+    __syncthreads();
+    const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    unsigned off = 0;
+    for (int k = 0; k < wv; ++k) off += sTot[k];
+    if (fix) a.hfList[tile * 256 + off + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)((size_t)y * a.W + x);
+    if (threadIdx.x == 0) a.hfCount[tile] = sTot[0] + sTot[1] + sTot[2] + sTot[3];
 }
 
 // ---------------------------------------------------------------- HF
-__global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
-    const int W = a.W, H = a.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= a.y1) return;
-    const size_t i = (size_t)y * W + x;
+VX_D void history_fix_px(const DenoiseArgs &a, int W, int H, int x, int y, size_t i) {
     const float z = a.depth[i], hist = a.histLen[i];
-    if (z > kRange || hist > 4.0f) return;
     const float cMat = ld_ushort(a.material, W, H, x, y);
     const V3 cN = f4(a.normalRough[i]).xyz();
     const V3 cWP = wp(a, x, y);
@@ -435,6 +451,68 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
             }
         }
     a.pong[i] = tf(sum / wsum);
+}
+
+// One pixel per wave: lane t < 25 takes tap t of the 5x5 pattern (t = 12 is
+// the centre, weight 1), so all 24 sparse taps are fetched at once instead of
+// one dependent round trip after another; the sums are combined across lanes
+// (the V4 operators keep the reference's w-from-z behaviour).
+VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, size_t i, int lane) {
+    const float z = a.depth[i], hist = a.histLen[i];
+    const float cMat = ld_ushort(a.material, W, H, x, y);
+    const V3 cN = f4(a.normalRough[i]).xyz();
+    const V3 cWP = wp(a, x, y);
+    const float dthr = 0.003f * z;
+    const float r = exp2f(4.0f - hist) + 1.0f;
+    V4 sum;
+    float wsum = 0.0f;
+    if (lane < 25) {
+        const int j = lane / 5 - 2, k = lane % 5 - 2;
+        if (j == 0 && k == 0) {
+            sum = f4(a.ping[i]);
+            wsum = 1.0f;
+        } else {
+            const int sx = x + (int)(k * r), sy = y + (int)(j * r);
+            const bool inside = sx >= 0 && sy >= 0 && sx < W && sy < H;
+            const float sMat = ld_ushort(a.material, W, H, sx, sy);
+            const V3 sN = ld4(a.normalRough, W, H, sx, sy).xyz();
+            const V3 sWP = wp(a, sx, sy);
+            float w = plane_w(cWP, cN, sWP, dthr);
+            w *= powf(fmaxf(0.01f, dot(cN, sN)), 8.0f);
+            w = inside ? w : 0;
+            w *= (float)(sMat == cMat);
+            if (w > 1e-4f) {
+                sum = ld4(a.ping, W, H, sx, sy) * w;
+                wsum = w;
+            }
+        }
+    }
+    for (int o = 16; o > 0; o >>= 1) {  // lanes 0..31 hold every tap
+        sum.x += __shfl_xor(sum.x, o);
+        sum.y += __shfl_xor(sum.y, o);
+        sum.z += __shfl_xor(sum.z, o);
+        sum.w += __shfl_xor(sum.w, o);
+        wsum += __shfl_xor(wsum, o);
+    }
+    if (lane == 0) a.pong[i] = tf(sum / wsum);
+}
+
+// One workgroup per 16x16 tile, over the tile's list from k_temporal: a
+// sparse list (<= 4 pixels, the steady state) gets one wave per pixel,
+// a dense one (history just reset) one lane per pixel.
+__global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
+    const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned n = a.hfCount[tile];
+    const unsigned wv = threadIdx.x >> 6;
+    if (n <= 4) {
+        if (wv >= n) return;
+        const size_t i = a.hfList[tile * 256 + wv];
+        history_fix_wave(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i, threadIdx.x & 63);
+        return;
+    }
+    if (threadIdx.x >= n) return;
+    const size_t i = a.hfList[tile * 256 + threadIdx.x];
+    history_fix_px(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i);
 }
 
 // ---------------------------------------------------------------- HC
@@ -710,7 +788,6 @@ hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st) {
 hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st) {
     const int used = 0;
     (void)used;
-    hipMemsetAsync(a.ffCount, 0, 16, st);
     // parity is baked into a.reservoir by the host
     hipLaunchKernelGGL(k_firefly, dim3((a.W + 7) / 8, (a.y1 - a.y0 + 7) / 8), dim3(64), 0, st, a, 0);
     hipLaunchKernelGGL(k_firefly_apply, dim3(64), dim3(256), 0, st, a);
