@@ -44,8 +44,11 @@ __global__ __launch_bounds__(256) void k_world_pos(DenoiseArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.y1) return;
     const size_t i = (size_t)y * a.W + x;
-    const V3 p = world_pos(a.cam, x, y, a.depth[i]);
-    a.wpos[i] = make_float4(p.x, p.y, p.z, 0.0f);
+    const float z = a.depth[i];
+    const V3 p = world_pos(a.cam, x, y, z);
+    // w: the pixel's 16-bit material read (Load2DUshort1 quirk, ld_ushort) for
+    // the a-trous / history-fix material tests, -1 for sky (no tap weight)
+    a.wpos[i] = make_float4(p.x, p.y, p.z, z > kRange ? -1.0f : ld_ushort(a.material, a.W, a.H, x, y));
 }
 VX_D float smooth_step10(float x) {  // SmoothStep(1, 0, x)
     const float t = saturate((x - 1.0f) / (0.0f - 1.0f));
@@ -702,9 +705,10 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
         if (final) a.output[i] = a.illum[i];  // BufferCopySky
         return;
     }
-    const float cMat = ld_ushort(a.material, W, H, x, y);
+    const V4 cP = f4(a.wpos[i]);
+    const float cMat = cP.w;
     const V3 cN = f4(a.normalRough[i]).xyz();
-    const V3 cWP = wp(a, x, y);
+    const V3 cWP = cP.xyz();
     const float hist = a.histLen[i];
     float lobe = a.p.lobeAngleFraction / sqrtf((float)step);
     lobe = lerpf(0.99f, lobe, saturate(hist / 5.0f));
@@ -736,13 +740,15 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
             const int px = x + ofx + xx * (int)step, py = y + ofy + yy * (int)step;
             const bool inside = px >= 0 && py >= 0 && px < W && py < H;
             const float kernel = k3[abs(xx)] * k3[abs(yy)];
-            const float sMat = ld_ushort(a.material, W, H, px, py);
+            // packed tap: world position + 16-bit material (-1 = sky: weight 0 like the
+            // reference's depth test); out-of-frame taps get weight 0 below
+            const V4 sP = ld4(a.wpos, W, H, px, py);
             const V3 sN = ld4(a.normalRough, W, H, px, py).xyz();
-            const float sz = ld1(a.depth, W, H, px, py);
-            const V3 sWP = wp(a, px, py);  // out-of-frame taps get weight 0 below
+            const float sMat = sP.w;
+            const V3 sWP = sP.xyz();
             float geo = plane_w(cWP, cN, sWP, dthr);
             geo *= kernel;
-            geo *= float(inside && sz < 500000.0f);
+            geo *= float(inside);
             const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
             float w = geo * nw;
             w *= (float)(sMat == cMat);
