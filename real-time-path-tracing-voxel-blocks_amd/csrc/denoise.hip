@@ -51,7 +51,9 @@ __global__ __launch_bounds__(256) void k_world_pos(DenoiseArgs a) {
     a.wpos[i] = make_float4(p.x, p.y, p.z, z > kRange ? -1.0f : ld_ushort(a.material, a.W, a.H, x, y));
 }
 VX_D float smooth_step10(float x) {  // SmoothStep(1, 0, x)
-    const float t = saturate((x - 1.0f) / (0.0f - 1.0f));
+    // (x - 1) / (0 - 1): dividing by -1 is exact and round-to-nearest is sign
+    // symmetric, so this equals 1 - x bit for bit -- without a division per tap
+    const float t = saturate(1.0f - x);
     return t * t * (3.0f - 2.0f * t);
 }
 VX_D float acos_approx(float x) { return sqrtf(2.0f) * sqrtf(saturate(1.0f - x)); }
