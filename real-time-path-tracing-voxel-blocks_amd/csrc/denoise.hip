@@ -77,13 +77,15 @@ VX_D uint32_t explode(uint32_t x) {
 }
 
 // ---------------------------------------------------------------- firefly
-// 64-thread workgroups = two 8x4 tiles (one per 32-lane half of the wave).
-__global__ __launch_bounds__(64) void k_firefly(DenoiseArgs a, int parity) {
+// 256-thread workgroups over 8x32 pixels; each wave covers two 8x4 tiles
+// (one per 32-lane half of the wave).
+__global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int parity) {
     const int W = a.W, H = a.H;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int l32 = lane & 31;
     const int x = blockIdx.x * 8 + (l32 & 7);
-    const int y = a.y0 + blockIdx.y * 8 + (lane >> 5) * 4 + (l32 >> 3);  // band starts on an 8-row boundary
+    // band starts on an 8-row boundary, so the 8x4 tiles stay aligned
+    const int y = a.y0 + blockIdx.y * 32 + wv * 8 + (lane >> 5) * 4 + (l32 >> 3);
     const bool inb = x < W && y < a.y1;
     const size_t i = (size_t)y * W + x;
     const float cd = inb ? a.depth[i] : 0.0f;
@@ -551,7 +553,7 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
             m1 += s;
             m2 += s * s;
             const V3 nz(sR[0][k], sR[1][k], sR[2][k]);
-            const float nl = luminance(nz);
+            const float nl = luminance_fast(nz);
             nm1 += nz;
             nm2 += nl * nl;
         }
@@ -624,9 +626,11 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
     if (z > 500000.0f) return;
-    const V3 cN = f4(a.normalRough[i]).xyz();
-    const V3 cWP = wp(a, x, y);
-    const float cMat = a.material[i];
+    // the centre's normal, position and material come from the staged tile
+    const int kc = (ty + 2) * 20 + tx + 2;
+    const V3 cN(sNx[kc], sNy[kc], sNz[kc]);
+    const V3 cWP(sPx[kc], sPy[kc], sPz[kc]);
+    const float cMat = sM[kc];
     const float hist = a.histLen[i];
     const float k3[2] = {0.44198f, 0.27901f};
     if (hist >= 3.0f) {
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
                 vs += f4(sI[(ty + 2 + dy) * 20 + tx + 2 + dx]) * kern[abs(dx) * 2 + abs(dy)];
         const float vm1 = luminance(vs.xyz());
         const float var = fmaxf(0.0f, vs.w - vm1 * vm1);
-        const float cLum = luminance(f4(a.prevIllum[i]).xyz());
+        const float cLum = luminance_fast(f4(sI[kc]).xyz());
         const float phiInv = 1.0f / fmaxf(1.0e-4f, a.p.phiL * sqrtf(var));
         const float nwp = normal_weight_param(1.0f, a.p.lobeAngleFraction);
         float sumW = 0.0f;
@@ -654,9 +658,9 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
                 const V3 sWP(sPx[k], sPy[k], sPz[k]);
                 const float sMat = sM[k];
                 float geo = plane_w(cWP, cN, sWP, dthr) * kernel;
-                const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
+                const float nw = nonexp_w(acos_approx(dot_fast(cN, sN)), nwp);
                 const V4 si = f4(sI[k]);
-                const float lw = fabsf(cLum - luminance(si.xyz())) * phiInv;
+                const float lw = fabsf(cLum - luminance_fast(si.xyz())) * phiInv;
                 float w = geo * nw * expf(-lw);
                 w = isC ? kernel : w;
                 w *= (float)(sMat == cMat);
@@ -675,14 +679,14 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
             for (int cy = -2; cy <= 2; ++cy) {
                 const int k = (ty + 2 + cy) * 20 + tx + 2 + cx;
                 const V3 sN(sNx[k], sNy[k], sNz[k]);
-                const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
+                const float nw = nonexp_w(acos_approx(dot_fast(cN, sN)), nwp);
                 const V4 smp = f4(sI[k]);
                 const V3 sill = smp.xyz();
                 float w = nw * 1.0f;
                 w *= (float)(sM[k] == cMat);
                 sw += w;
                 si += sill * w;
-                s1 += luminance(sill) * w;
+                s1 += luminance_fast(sill) * w;
                 s2 += smp.w * w;
             }
         const float boost = fmaxf(1.0f, 4.0f / (hist + 1.0f));
@@ -715,7 +719,7 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
     float lobe = a.p.lobeAngleFraction / sqrtf((float)step);
     lobe = lerpf(0.99f, lobe, saturate(hist / 5.0f));
     const V4 c = f4(in[i]);
-    const float cLum = luminance(c.xyz());
+    const float cLum = luminance_fast(c.xyz());
     const float phiInv = 1.0f / fmaxf(1.0e-4f, a.p.phiL * sqrtf(c.w));
     const float nwp = normal_weight_param(1.0f, lobe);
     float sumW = 0.44198f * 0.44198f;
@@ -751,12 +755,12 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
             float geo = plane_w(cWP, cN, sWP, dthr);
             geo *= kernel;
             geo *= float(inside);
-            const float nw = nonexp_w(acos_approx(dot(cN, sN)), nwp);
+            const float nw = nonexp_w(acos_approx(dot_fast(cN, sN)), nwp);
             float w = geo * nw;
             w *= (float)(sMat == cMat);
             if (w > 1e-4f) {
                 const V4 sv = ld4(in, W, H, px, py);
-                float lw = fabsf(cLum - luminance(sv.xyz())) * phiInv;
+                float lw = fabsf(cLum - luminance_fast(sv.xyz())) * phiInv;
                 lw = fminf(INFINITY, lw);
                 w *= expf(-lw);
                 sumW += w;
@@ -797,7 +801,7 @@ hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st) {
     const int used = 0;
     (void)used;
     // parity is baked into a.reservoir by the host
-    hipLaunchKernelGGL(k_firefly, dim3((a.W + 7) / 8, (a.y1 - a.y0 + 7) / 8), dim3(64), 0, st, a, 0);
+    hipLaunchKernelGGL(k_firefly, dim3((a.W + 7) / 8, (a.y1 - a.y0 + 31) / 32), dim3(256), 0, st, a, 0);
     hipLaunchKernelGGL(k_firefly_apply, dim3(64), dim3(256), 0, st, a);
     return hipGetLastError();
 }
