@@ -164,14 +164,18 @@ struct vxpt_ctx {
     DBuf<uint8_t> bnSobol, bnScramble, bnRank;
 
     // frame buffers
-    GSlot gb[2];
+    // G-buffer ring of 3 slots: every trace pass writes a slot that is neither
+    // the previous pass's (its ReSTIR history) nor the denoiser's history slot
+    // (the previous frame's final G-buffer, Denoiser.cu:394-407), so the frame
+    // end hands the last slot to the denoiser by index instead of copying planes.
+    GSlot gb[3];
     int last = 0;              // slot of the most recent trace output
+    int tracePrev = 0;         // slot the most recent trace read as its previous pass
+    int hist = 2;              // denoiser history slot (zero at frame 0)
     float4 *illum = nullptr, *accum = nullptr, *motion = nullptr;
     Reservoir *res = nullptr;  // 2*W*H
     float4 *ping = nullptr, *pong = nullptr, *prevIllum = nullptr, *prevFast = nullptr, *output = nullptr;
     float *histLen = nullptr, *prevHistLen = nullptr;
-    float4 *dnPrevNormalRough = nullptr;
-    float *dnPrevDepth = nullptr, *dnPrevMaterial = nullptr;
     float4 *wpos = nullptr;
     uint32_t *ffCount = nullptr, *ffIndex = nullptr, *hfList = nullptr, *hfCount = nullptr;
     float4 *ffColor = nullptr;
@@ -346,8 +350,8 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.motion = c->motion;
     a.depth = g.depth;
     a.material = g.material;
-    a.prevNormalRough = c->dnPrevNormalRough;
-    a.prevDepth = c->dnPrevDepth;
+    a.prevNormalRough = c->gb[c->hist].normalRough;
+    a.prevDepth = c->gb[c->hist].depth;
     a.reservoir = c->res + (size_t)parity * c->W * c->H;
     a.ping = c->ping; a.pong = c->pong; a.prevIllum = c->prevIllum; a.prevFast = c->prevFast;
     a.output = c->output;
@@ -365,10 +369,12 @@ const vxpt_denoise_params &default_denoise() {
 // pointer + byte size of a logical buffer
 bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, void **mirror) {
     const size_t n = (size_t)c->W * c->H;
-    // current = the slot the last trace wrote; previous = the other ring slot,
-    // which the next trace reads as its history (ReSTIR prev surface) and then overwrites
+    // current = the slot the last trace wrote; PREV_GEO_NORMAL_THIN / ALBEDO /
+    // MAT_PARAM = the slot it read as the previous pass (ReSTIR history);
+    // PREV_NORMAL_ROUGH / DEPTH / MATERIAL = the denoiser's history slot
     const GSlot &g = c->gb[c->last];
-    const GSlot &gp = c->gb[1 - c->last];
+    const GSlot &gp = c->gb[c->tracePrev];
+    const GSlot &gh = c->gb[c->hist];
     *mirror = nullptr;
     switch (which) {
         case VXPT_BUF_ILLUM: p = c->denoiseInputIsAccum ? c->accum : c->illum; bytes = n * 16; return true;
@@ -382,11 +388,9 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_MAT_PARAM: p = g.matParam; bytes = n * 16; return true;
         case VXPT_BUF_PREV_MAT_PARAM: p = gp.matParam; bytes = n * 16; return true;
         case VXPT_BUF_MOTION: p = c->motion; bytes = n * 16; return true;
-        case VXPT_BUF_PREV_NORMAL_ROUGH:
-            p = c->dnPrevNormalRough; bytes = n * 16; if (forWrite) *mirror = gp.normalRough; return true;
-        case VXPT_BUF_PREV_DEPTH: p = c->dnPrevDepth; bytes = n * 4; if (forWrite) *mirror = gp.depth; return true;
-        case VXPT_BUF_PREV_MATERIAL:
-            p = c->dnPrevMaterial; bytes = n * 4; if (forWrite) *mirror = gp.material; return true;
+        case VXPT_BUF_PREV_NORMAL_ROUGH: p = gh.normalRough; bytes = n * 16; return true;
+        case VXPT_BUF_PREV_DEPTH: p = gh.depth; bytes = n * 4; return true;
+        case VXPT_BUF_PREV_MATERIAL: p = gh.material; bytes = n * 4; return true;
         case VXPT_BUF_RESERVOIRS: p = c->res; bytes = 2 * n * sizeof(Reservoir); return true;
         case VXPT_BUF_RES_EVEN: p = c->res; bytes = n * sizeof(Reservoir); return true;
         case VXPT_BUF_RES_ODD: p = c->res + n; bytes = n * sizeof(Reservoir); return true;
@@ -503,7 +507,8 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     for (int i = 0; i < 13; ++i) a.mats[i] = c->mats[i];
     a.cam = c->cam;
     a.prevCam = c->prevCam;
-    const int next = 1 - c->last;
+    int next = 0;
+    while (next == c->last || next == c->hist) ++next;
     const GSlot &cur = c->gb[next], &prev = c->gb[c->last];
     a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material};
     a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material};
@@ -536,19 +541,17 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_trace(a, c->stream));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    c->tracePrev = c->last;
     c->last = next;
     return 0;
 }
 
-// history copies NormalRough/Depth/Material -> Prev (Denoiser.cu:394-407); whole
-// planes, so the rows a band received from its neighbours are carried along
+// history hand-over NormalRough/Depth/Material -> Prev (Denoiser.cu:394-407):
+// the slot the frame's last trace wrote becomes the denoiser's history slot
+// (whole planes, so the rows a band received from its neighbours come along)
 hipError_t history_copies(vxpt_ctx *c) {
-    const size_t n = (size_t)c->W * c->H;
-    const GSlot &g = c->gb[c->last];
-    hipError_t e = hipMemcpyAsync(c->dnPrevNormalRough, g.normalRough, n * 16, hipMemcpyDeviceToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(c->dnPrevDepth, g.depth, n * 4, hipMemcpyDeviceToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(c->dnPrevMaterial, g.material, n * 4, hipMemcpyDeviceToDevice, c->stream);
-    return e;
+    c->hist = c->last;
+    return hipSuccess;
 }
 
 // world positions for the band and kWposHalo rows either side (the widest
@@ -641,7 +644,6 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (dalloc(c, c->illum, n) || dalloc(c, c->accum, n) || dalloc(c, c->motion, n) || dalloc(c, c->res, 2 * n) ||
         dalloc(c, c->ping, n) || dalloc(c, c->pong, n) || dalloc(c, c->prevIllum, n) || dalloc(c, c->prevFast, n) ||
         dalloc(c, c->output, n) || dalloc(c, c->histLen, n) || dalloc(c, c->prevHistLen, n) ||
-        dalloc(c, c->dnPrevNormalRough, n) || dalloc(c, c->dnPrevDepth, n) || dalloc(c, c->dnPrevMaterial, n) ||
         dalloc(c, c->ffCount, 4) || dalloc(c, c->wpos, n) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n) ||
         dalloc(c, c->hfList, (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16) * 256) ||
         dalloc(c, c->hfCount, (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16)))

@@ -180,7 +180,7 @@ def test_frames_end_to_end():
 
 
 def _inject_frame(r, o):
-    # previous-frame planes first: their upload also fills the other G-buffer slot
+    # previous-frame planes (the denoiser's history slot), then the current ones
     for name in ("PREV_NORMAL_ROUGH", "PREV_DEPTH", "PREV_MATERIAL", "PREV_ILLUM", "PREV_FAST", "PREV_HIST_LEN",
                  "HIST_LEN", "ILLUM", "DEPTH", "NORMAL_ROUGH", "MATERIAL", "ALBEDO", "GEO_NORMAL_THIN",
                  "MAT_PARAM", "MOTION", "RESERVOIRS"):
@@ -194,6 +194,7 @@ def test_denoiser_on_identical_inputs():
     r.trace(0)  # establishes the G-buffer ring slots; every plane is overwritten below
     p = _dn_params()
     for f in range(3):
+        r.trace(f)  # moves the G-buffer ring like a frame's trace; its planes are overwritten below
         o.trace(f)
         o.post_trace()
         _inject_frame(r, o)
@@ -226,6 +227,7 @@ def test_denoiser_history_fix_after_camera_move():
         if f == 7:
             r.set_camera(pos2, d, fov=fov, prev=(pos2, d, fov))
             o.set_camera(pos2, d, fov=fov, which=1)
+        r.trace(f)
         o.trace(f)
         o.post_trace()
         _inject_frame(r, o)
