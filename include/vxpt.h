@@ -156,8 +156,23 @@ int vxpt_row_bytes(vxpt_ctx *ctx, int which);
 /* copy `rows` rows starting at row y between a buffer and device memory `dev`
  * (to_buffer = 1: dev -> buffer), enqueued on the context stream */
 int vxpt_copy_rows(vxpt_ctx *ctx, int which, int y, int rows, void *dev, int to_buffer);
-/* kept for ABI compatibility: no-op (the host drives the exchange with vxpt_copy_rows) */
+/* kept for ABI compatibility: no-op (the halo exchanges belong to the band schedule below) */
 int vxpt_exchange_halo(vxpt_ctx *ctx, uint32_t buffer_mask, int rows);
+
+/* Multi-GPU band partition driven by the library (replaces the single-GPU
+ * OfflineBackend::renderFrame, OfflineBackend.cpp:46-89, with one band per GPU).  One process
+ * per GPU: rank 0 calls vxpt_band_comm_id (an RCCL unique id, 128 bytes), the host broadcasts
+ * it, every rank calls vxpt_band_comm_init.  The context then owns rows band_rows(H, nranks,
+ * rank) and vxpt_render_frame renders that band, enqueueing every halo exchange (grouped
+ * ncclSend/ncclRecv with the neighbours rank +/- 1, rows moved in place) on the context
+ * stream.  Bands must be >= 72 rows tall. */
+int vxpt_band_comm_id(void *id, size_t bytes);
+int vxpt_band_comm_init(vxpt_ctx *ctx, const void *id, size_t bytes, int nranks, int rank);
+/* The same schedule over n contexts of one process (tests, one-GPU boxes): context k owns band
+ * k of n; halo rows move by device copies between the contexts. */
+int vxpt_band_link(vxpt_ctx **ctxs, int n);
+int vxpt_render_frame_linked(vxpt_ctx **ctxs, int n, const vxpt_denoise_params *p, int32_t frame_num,
+                             int32_t spp);
 
 /* copy any logical buffer to/from host memory (parity hooks, PNG output) */
 int vxpt_readback(vxpt_ctx *ctx, int which, void *host, size_t bytes);

@@ -6,6 +6,7 @@
 // AliasTable.cu:66-153), generates the Perlin terrain (VoxelSceneGen.cu:341-388)
 // and sequences the kernels of one frame (OfflineBackend.cpp:46-89).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -188,6 +189,13 @@ struct vxpt_ctx {
     vxpt_denoise_params yamlDenoise{};
     float skyParams[4] = {0.25f, 45.0f, 0.0f, 1.0f};
     vxpt_material yamlMats[13] = {};
+
+    // band partition (multi-GPU): this context's rank among nranks bands and the
+    // transport its halo rows move by -- an RCCL communicator (one process per
+    // GPU) or the other contexts of this process (vxpt_band_link)
+    int nranks = 1, rank = 0;
+    ncclComm_t comm = nullptr;
+    std::vector<vxpt_ctx *> linked;
 };
 
 namespace {
@@ -608,6 +616,208 @@ int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) 
     return 0;
 }
 
+// one denoiser pass on the context's band, enqueued on its stream (vxpt_denoise_pass ids)
+int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int arg2) {
+    DenoiseArgs a{};
+    fill_denoise(c, p, a, pass == 0 ? (arg & 1) : 0);
+    switch (pass) {
+        case 0: HIPCHK(c, launch_firefly(a, c->stream)); break;
+        case 2: HIPCHK(c, launch_temporal(a, c->stream)); break;
+        case 3: HIPCHK(c, launch_history_fix(a, c->stream)); break;
+        case 4: HIPCHK(c, launch_history_clamp(a, c->stream)); break;
+        case 5: HIPCHK(c, launch_atrous_smem(a, c->stream)); break;
+        case 6: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
+        case 7: HIPCHK(c, launch_atrous(a, a.pong, a.ping, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
+        case 10: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, true, c->stream)); break;
+        case 11: HIPCHK(c, world_pos_band(a, c->stream)); break;
+        case 12: HIPCHK(c, launch_frame0_init(a, c->stream)); break;
+        case 13: {
+            const float4 *src = arg == 1 ? a.ping : (arg == 2 ? a.pong : (arg == 3 ? a.prevIllum : a.illum));
+            HIPCHK(c, launch_copy_output(a, src, c->stream));
+        } break;
+        case 14: HIPCHK(c, history_copies(c)); break;
+        default: return fail(c, VXPT_ERR_ARG, "unknown pass");
+    }
+    return VXPT_OK;
+}
+
+// ---------------------------------------------------------------- band partition
+// The multi-GPU schedule of one frame (bands.py restates it for
+// the CPU tests): every rank traces and denoises its 8-row-aligned band into
+// full-frame buffers, and every pass that reads a neighbourhood is preceded by
+// an exchange of exactly the rows it reads outside the band, with the band
+// neighbours r +/- 1.  Rows are contiguous in every plane, so a halo is one
+// ncclSend / ncclRecv per plane and neighbour, grouped, enqueued on the
+// context stream behind the kernels that produced the rows -- no packing, no
+// host synchronisation.
+constexpr int kTraceHalo = 72;  // ReSTIR temporal taps: 64-pixel disk + reprojection (Restir.h:348-381)
+const int kGbufBufs[] = {VXPT_BUF_DEPTH, VXPT_BUF_NORMAL_ROUGH, VXPT_BUF_GEO_NORMAL_THIN,
+                         VXPT_BUF_ALBEDO, VXPT_BUF_MATERIAL, VXPT_BUF_MAT_PARAM};
+const int kHistoryBufs[] = {VXPT_BUF_PREV_ILLUM, VXPT_BUF_PREV_FAST, VXPT_BUF_PREV_HIST_LEN};
+
+void band_rows(int H, int world, int rank, int &y0, int &y1) {
+    const int per = (H + 8 * world - 1) / (8 * world) * 8;
+    y0 = std::min(H, rank * per);
+    y1 = std::min(H, y0 + per);
+}
+
+struct Halo { int peer, sy, sn, ry, rn; };
+// rows rank sends to / receives from each band neighbour (both sides of a border move
+// min(rows, the two band heights) rows)
+std::vector<Halo> halo_plan(int H, int world, int rank, int rows) {
+    std::vector<Halo> plan;
+    int y0, y1;
+    band_rows(H, world, rank, y0, y1);
+    if (rank > 0) {
+        int p0, p1;
+        band_rows(H, world, rank - 1, p0, p1);
+        const int n = std::min(rows, std::min(y1 - y0, p1 - p0));
+        plan.push_back({rank - 1, y0, n, y0 - n, n});
+    }
+    if (rank < world - 1) {
+        int p0, p1;
+        band_rows(H, world, rank + 1, p0, p1);
+        const int n = std::min(rows, std::min(y1 - y0, p1 - p0));
+        plan.push_back({rank + 1, y1 - n, n, y1, n});
+    }
+    return plan;
+}
+
+char *buffer_rows(vxpt_ctx *c, int which, int y, size_t &rowBytes) {
+    void *p, *mirror;
+    size_t n;
+    buffer_ptr(c, which, p, n, false, &mirror);
+    rowBytes = n / (size_t)c->H;
+    return static_cast<char *>(p) + (size_t)y * rowBytes;
+}
+
+// Halo exchange of `bufs` over `rows` rows for every context of the frame
+// (one with RCCL, all of this process's bands when linked).
+int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows) {
+    if (cs.size() == 1 && cs[0]->comm) {
+        vxpt_ctx *c = cs[0];
+        if (ncclGroupStart() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupStart");
+        for (int b : bufs)
+            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, rows)) {
+                size_t rb;
+                char *send = buffer_rows(c, b, h.sy, rb);
+                char *recv = buffer_rows(c, b, h.ry, rb);
+                ncclSend(send, (size_t)h.sn * rb, ncclUint8, h.peer, c->comm, c->stream);
+                ncclRecv(recv, (size_t)h.rn * rb, ncclUint8, h.peer, c->comm, c->stream);
+            }
+        if (ncclGroupEnd() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupEnd (halo exchange)");
+        return VXPT_OK;
+    }
+    // linked contexts of one process: device copies from each neighbour's own rows
+    // (never written by an exchange), after every band finished the producing pass
+    for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (vxpt_ctx *c : cs)
+        for (int b : bufs)
+            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, rows)) {
+                size_t rb;
+                char *dst = buffer_rows(c, b, h.ry, rb);
+                const char *src = buffer_rows(cs[h.peer], b, h.ry, rb);
+                HIPCHK(c, hipMemcpyAsync(dst, src, (size_t)h.rn * rb, hipMemcpyDeviceToDevice, c->stream));
+            }
+    for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+int atrous_rows(int step) { return step + (step > 4 ? step / 4 : 0); }  // Atrous.h:79-84 jitter above step 4
+
+#define BANDCHK(expr)              \
+    do {                           \
+        if (int r_ = (expr)) return r_; \
+    } while (0)
+#define FOR_BANDS(expr)                 \
+    do {                                \
+        for (vxpt_ctx *c : cs) BANDCHK(expr); \
+    } while (0)
+
+// One banded OfflineBackend::renderFrame over cs (vxpt_render_frame's order).
+int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int frame, int spp) {
+    const int it0 = frame * spp;
+    for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+    for (int s = 0; s < spp; ++s) {
+        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp));
+        std::vector<int> bufs(std::begin(kGbufBufs), std::end(kGbufBufs));
+        bufs.push_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN);
+        BANDCHK(exchange(cs, bufs, kTraceHalo));
+    }
+    for (vxpt_ctx *c : cs) {
+        c->denoiseInputIsAccum = spp > 1;
+        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    }
+    BANDCHK(exchange(cs, {VXPT_BUF_ILLUM}, 2));
+    const int it = it0 + spp, used = it > 0 ? it - 1 : 0;
+    FOR_BANDS(run_pass(c, p, 11, 0, 0));
+    if (p->enable_firefly_filter) {
+        FOR_BANDS(run_pass(c, p, 0, used & 1, 0));
+        BANDCHK(exchange(cs, {(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN}, kTraceHalo));
+        BANDCHK(exchange(cs, {VXPT_BUF_ILLUM}, 2));
+    }
+    const std::vector<int> hist(std::begin(kHistoryBufs), std::end(kHistoryBufs));
+    if (frame == 0) {
+        FOR_BANDS(run_pass(c, p, 12, 0, 0));
+        BANDCHK(exchange(cs, hist, 2));
+    }
+    int fin = 0;
+    if (p->enable_temporal_accumulation && frame > 0) {
+        FOR_BANDS(run_pass(c, p, 2, 0, 0));
+        BANDCHK(exchange(cs, {VXPT_BUF_PING}, 34));  // HistoryFix taps: 2 x (2^3 + 1) rows
+        BANDCHK(exchange(cs, {VXPT_BUF_PONG}, 2));
+        fin = 1;
+        if (p->enable_history_fix) {
+            FOR_BANDS(run_pass(c, p, 3, 0, 0));
+            BANDCHK(exchange(cs, {VXPT_BUF_PONG}, 2));
+            fin = 2;
+        }
+        if (p->enable_history_clamping) {
+            FOR_BANDS(run_pass(c, p, 4, 0, 0));
+            BANDCHK(exchange(cs, hist, 2));
+            fin = 3;
+        }
+    }
+    bool outDone = false;
+    if (p->enable_spatial_filtering) {
+        FOR_BANDS(run_pass(c, p, 5, 0, 0));
+        BANDCHK(exchange(cs, {VXPT_BUF_PING}, atrous_rows(2)));
+        fin = 1;
+        if (p->atrous_iteration_num > 0) {
+            int idx = 1, step = 2;
+            while (idx < 2 * p->atrous_iteration_num) {
+                FOR_BANDS(run_pass(c, p, 6, step, it));
+                step = 1 << ++idx;
+                BANDCHK(exchange(cs, {VXPT_BUF_PONG}, atrous_rows(step)));
+                FOR_BANDS(run_pass(c, p, 7, step, it));
+                step = 1 << ++idx;
+                BANDCHK(exchange(cs, {VXPT_BUF_PING}, atrous_rows(step)));
+            }
+            FOR_BANDS(run_pass(c, p, 10, step, it));
+            fin = 2;
+            outDone = true;
+        }
+    }
+    if (!outDone) FOR_BANDS(run_pass(c, p, 13, fin, 0));
+    FOR_BANDS(run_pass(c, p, 14, 0, 0));
+    for (vxpt_ctx *c : cs) {
+        HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+    }
+    for (vxpt_ctx *c : cs) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        float t = 0, d = 0, f = 0;
+        hipEventElapsedTime(&t, c->ev[6], c->ev[1]);
+        hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+        hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
+        c->timing.trace_ms = t;   // the band's trace passes and their halo exchanges
+        c->timing.denoise_ms = d; // the band's denoiser passes and their halo exchanges
+        c->timing.frame_ms = f;
+    }
+    return VXPT_OK;
+}
+
 }  // namespace
 
 // =====================================================================  C ABI
@@ -695,6 +905,7 @@ void vxpt_destroy(vxpt_ctx *c) {
     for (auto &e : c->ev)
         if (e) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
     delete c;
 }
 
@@ -965,26 +1176,7 @@ int vxpt_denoise_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int a
     if (!c) return VXPT_ERR_ARG;
     if (!p) p = &default_denoise();
     HIPCHK(c, hipSetDevice(c->dev));
-    DenoiseArgs a{};
-    fill_denoise(c, p, a, pass == 0 ? (arg & 1) : 0);
-    switch (pass) {
-        case 0: HIPCHK(c, launch_firefly(a, c->stream)); break;
-        case 2: HIPCHK(c, launch_temporal(a, c->stream)); break;
-        case 3: HIPCHK(c, launch_history_fix(a, c->stream)); break;
-        case 4: HIPCHK(c, launch_history_clamp(a, c->stream)); break;
-        case 5: HIPCHK(c, launch_atrous_smem(a, c->stream)); break;
-        case 6: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
-        case 7: HIPCHK(c, launch_atrous(a, a.pong, a.ping, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
-        case 10: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, true, c->stream)); break;
-        case 11: HIPCHK(c, world_pos_band(a, c->stream)); break;
-        case 12: HIPCHK(c, launch_frame0_init(a, c->stream)); break;
-        case 13: {
-            const float4 *src = arg == 1 ? a.ping : (arg == 2 ? a.pong : (arg == 3 ? a.prevIllum : a.illum));
-            HIPCHK(c, launch_copy_output(a, src, c->stream));
-        } break;
-        case 14: HIPCHK(c, history_copies(c)); break;
-        default: return fail(c, VXPT_ERR_ARG, "unknown pass");
-    }
+    if (int r = run_pass(c, p, pass, arg, arg2)) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return VXPT_OK;
 }
@@ -992,6 +1184,10 @@ int vxpt_denoise_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int a
 int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNum, int32_t spp) {
     if (!c || spp < 1) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
+    if (c->comm) {
+        std::vector<vxpt_ctx *> cs{c};
+        return band_frame(cs, p ? p : &default_denoise(), frameNum, spp);
+    }
     const int it0 = frameNum * spp;
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
@@ -1050,6 +1246,57 @@ int vxpt_copy_rows(vxpt_ctx *c, int which, int y, int rows, void *dev, int to_bu
 }
 
 int vxpt_exchange_halo(vxpt_ctx *c, uint32_t, int) { return c ? VXPT_OK : VXPT_ERR_ARG; }
+
+int vxpt_band_comm_id(void *id, size_t bytes) {
+    if (!id || bytes < sizeof(ncclUniqueId)) return VXPT_ERR_ARG;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return VXPT_ERR_HIP;
+    std::memcpy(id, &u, sizeof(u));
+    return VXPT_OK;
+}
+
+int vxpt_band_comm_init(vxpt_ctx *c, const void *id, size_t bytes, int nranks, int rank) {
+    if (!c || !id || bytes < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    int y0, y1;
+    band_rows(c->H, nranks, rank, y0, y1);
+    if (nranks > 1 && (y1 - y0 < kTraceHalo))
+        return fail(c, VXPT_ERR_ARG, "bands must be at least 72 rows tall (ReSTIR halo)");
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    if (c->comm) ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclCommInitRank");
+    c->nranks = nranks;
+    c->rank = rank;
+    return vxpt_set_band(c, y0, y1);
+}
+
+int vxpt_band_link(vxpt_ctx **cs, int n) {
+    if (!cs || n < 1) return VXPT_ERR_ARG;
+    for (int k = 0; k < n; ++k) {
+        vxpt_ctx *c = cs[k];
+        if (!c || c->W != cs[0]->W || c->H != cs[0]->H) return VXPT_ERR_ARG;
+        int y0, y1;
+        band_rows(c->H, n, k, y0, y1);
+        if (n > 1 && (y1 - y0 < kTraceHalo)) return fail(c, VXPT_ERR_ARG, "bands must be at least 72 rows tall");
+        c->nranks = n;
+        c->rank = k;
+        c->linked.assign(cs, cs + n);
+        if (int r = vxpt_set_band(c, y0, y1)) return r;
+    }
+    return VXPT_OK;
+}
+
+int vxpt_render_frame_linked(vxpt_ctx **cs, int n, const vxpt_denoise_params *p, int32_t frameNum, int32_t spp) {
+    if (!cs || n < 1 || spp < 1) return VXPT_ERR_ARG;
+    std::vector<vxpt_ctx *> v(cs, cs + n);
+    for (int k = 0; k < n; ++k)
+        if (!cs[k] || cs[k]->rank != k || cs[k]->nranks != n) return VXPT_ERR_STATE;
+    HIPCHK(cs[0], hipSetDevice(cs[0]->dev));
+    return band_frame(v, p ? p : &default_denoise(), frameNum, spp);
+}
+
 
 int vxpt_readback(vxpt_ctx *c, int which, void *host, size_t bytes) {
     if (!c || !host) return VXPT_ERR_ARG;

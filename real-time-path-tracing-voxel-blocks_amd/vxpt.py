@@ -108,6 +108,11 @@ def load_library(path=LIB_PATH):
         "vxpt_set_band": (I, [P, I, I]),
         "vxpt_row_bytes": (I, [P, I]),
         "vxpt_copy_rows": (I, [P, I, I, I, P, I]),
+        "vxpt_band_comm_id": (I, [P, ctypes.c_size_t]),
+        "vxpt_band_comm_init": (I, [P, P, ctypes.c_size_t, I, I]),
+        "vxpt_band_link": (I, [ctypes.POINTER(P), I]),
+        "vxpt_render_frame_linked": (I, [ctypes.POINTER(P), I, ctypes.POINTER(DenoiseParams), ctypes.c_int32,
+                                         ctypes.c_int32]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -219,6 +224,12 @@ class Renderer:
         self._chk(self.lib.vxpt_copy_rows(self.ctx, which, y, rows, ctypes.c_void_p(dev_ptr), int(to_buffer)),
                   "vxpt_copy_rows")
 
+    def band_comm_init(self, comm_id, nranks, rank):
+        """Attach an RCCL communicator (vxpt_band_comm_init): this context renders band `rank`
+        of `nranks` and vxpt_render_frame exchanges the halos itself."""
+        buf = ctypes.create_string_buffer(bytes(comm_id), len(comm_id))
+        self._chk(self.lib.vxpt_band_comm_init(self.ctx, buf, len(comm_id), nranks, rank), "vxpt_band_comm_init")
+
     def denoise(self, frame_num, iteration_index, params=None):
         p = params or DenoiseParams.defaults()
         self._chk(self.lib.vxpt_denoise(self.ctx, ctypes.byref(p), frame_num, iteration_index), "vxpt_denoise")
@@ -303,3 +314,29 @@ def render_offline(width, height, frames, spp=1, chunks=(2, 1, 2), height_scale=
     for f in range(frames):
         r.render_frame(f, spp)
     return r
+
+
+def band_comm_id():
+    """RCCL unique id for vxpt_band_comm_init (rank 0 makes it, the host broadcasts it)."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(128)
+    if lib.vxpt_band_comm_id(buf, 128) != 0:
+        raise VxptError("vxpt_band_comm_id failed")
+    return buf.raw
+
+
+class LinkedBands:
+    """n contexts of this process rendering the bands of one frame (vxpt_band_link):
+    the library's multi-GPU schedule with device copies as the transport."""
+
+    def __init__(self, renderers):
+        self.rs = list(renderers)
+        self.lib = load_library()
+        self._arr = (ctypes.c_void_p * len(self.rs))(*[r.ctx for r in self.rs])
+        if self.lib.vxpt_band_link(self._arr, len(self.rs)) != 0:
+            raise VxptError("vxpt_band_link: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
+
+    def render_frame(self, frame_num, spp=1, params=None):
+        p = params or DenoiseParams.defaults()
+        if self.lib.vxpt_render_frame_linked(self._arr, len(self.rs), ctypes.byref(p), frame_num, spp) != 0:
+            raise VxptError("vxpt_render_frame_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())

@@ -138,3 +138,33 @@ def test_gpu_bands_match_single_context():
         ref = single.read("OUTPUT")
         out = np.concatenate([b.r.read("OUTPUT")[y0:y1] for b, (y0, y1) in zip(backs, bands_)])
         np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_library_band_schedule_matches_single_context():
+    """The library's own band schedule (vxpt_band_link / vxpt_render_frame_linked: the one
+    vxpt_band_comm_init runs over RCCL, with device copies between the contexts as the
+    transport) equals the single-context render bit for bit."""
+    import vxpt
+    w, h, spp = 64, 160, 4
+    cam = C1_CAMERA
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    single = make()
+    rs = [make(), make()]
+    linked = vxpt.LinkedBands(rs)
+    rows = [bands.band_rows(h, 2, k) for k in range(2)]
+    for f in range(3):
+        single.render_frame(f, spp, p)
+        linked.render_frame(f, spp, p)
+        ref = single.read("OUTPUT")
+        out = np.concatenate([r.read("OUTPUT")[y0:y1] for r, (y0, y1) in zip(rs, rows)])
+        np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
