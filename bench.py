@@ -7,16 +7,18 @@ world (8x8x8 chunks, C1 terrain scaled x4: heights 128, freq 1/256, world-y
 heights), camera = C1 camera with position x4.  One step = one
 OfflineBackend::renderFrame = 4 trace passes + 1 denoise.
 
-value = whole-job Mpaths/s = n_gpus * W*H*spp * K / max-over-ranks wall time of K steps.
+value = whole-job Mpaths/s = W*H*spp * K / max-over-ranks wall time of K steps.
 roofline = the denoiser chain (HBM-bound): algorithmic bytes 568 B/px * W*H per
 frame / its HIP-event duration on the context's stream.
 cpu_baseline = the oracle (C++ restatement, OpenMP) tracing a bounded band of
 rows of the same frame on this host's cores (rank 0, N=1 only).
 
 Multi-GPU (N>1, launched by torch.distributed.run): the frame is split into N
-horizontal bands (bands.py); each rank traces and denoises its band and the
-ranks exchange halo rows with RCCL between passes.  Total work is fixed
-(strong scaling); value = whole-frame paths / max-over-ranks time.
+horizontal bands; each rank's library context renders its band and enqueues
+the halo exchanges itself (RCCL over xGMI: grouped send/recv with the band
+neighbours on the context stream, vxpt_band_comm_init).  Total work is fixed
+(strong scaling); value = whole-frame paths / max-over-ranks time; roofline =
+the rank's band (its denoiser time includes the exchanges).
 """
 import argparse
 import glob
@@ -109,17 +111,16 @@ def main():
     params = vxpt.DenoiseParams.defaults()
     band = None
     if world > 1:
-        rows = [bands.band_rows(a.height, world, k) for k in range(world)]
-        band = bands.GpuBand(r, rows[rank][0], rows[rank][1], params)
-        exchange = bands.DistExchange(band, rows, rank, device=torch.device("cuda", local))
-        pdict = bands.params_dict(params)
+        # the library renders this rank's band and enqueues the halo exchanges itself
+        # (RCCL over xGMI on the context stream); the host only hands out the unique id
+        obj = [vxpt.band_comm_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        r.band_comm_init(obj[0], world, rank)
+        band = bands.band_rows(a.height, world, rank)
 
     def step(frame):
         if a.primary_only:
             r.trace(frame, primary_only=True)
-            r.sync()
-        elif band is not None:
-            bands.run_frame([band], exchange, frame, a.spp, pdict)
             r.sync()
         else:
             r.render_frame(frame, a.spp, params)
@@ -141,10 +142,9 @@ def main():
     for _ in range(a.steps):
         step(frame)
         frame += 1
-        if band is None:
-            t = r.timings()
-            trace_ms.append(t["trace_ms"])
-            denoise_ms.append(t["denoise_ms"])
+        t = r.timings()
+        trace_ms.append(t["trace_ms"])
+        denoise_ms.append(t["denoise_ms"])
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -154,14 +154,7 @@ def main():
 
     band_px = a.width * a.height
     if band is not None:
-        # the denoiser chain on this rank's band, HIP events (untimed extra frame, no exchanges)
-        r.trace_flags(frame * a.spp, 0)
-        r.denoise(frame, frame * a.spp + 1, params)
-        t = r.timings()
-        trace_ms.append(t["trace_ms"])
-        denoise_ms.append(t["denoise_ms"])
-        y0, y1 = bands.band_rows(a.height, world, rank)
-        band_px = a.width * (y1 - y0)
+        band_px = a.width * (band[1] - band[0])
     spp = 1 if a.primary_only else a.spp
     paths = a.width * a.height * spp
     # single GPU / bands: the whole frame's paths per step
@@ -205,8 +198,8 @@ def main():
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "avg_duration_ms": round(dur_ms, 4)},
             "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4), "primary_hit_frac": round(hit_frac, 4),
-            # single GPU: the frame's spp passes; bands: one 1-spp pass over this rank's band
-            "trace_mpaths_s": round((paths if band is None else band_px) / (avg_trace * 1e-3) / 1e6, 3),
+            # the trace passes over this rank's rows (bands: with their halo exchanges)
+            "trace_mpaths_s": round(band_px * spp / (avg_trace * 1e-3) / 1e6, 3),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
