@@ -897,7 +897,7 @@ hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, f
     return hipGetLastError();
 }
 
-hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
+hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir) {
     const dim3 g((a.nSlots + 255) / 256), g4((4 * a.nSlots + 255) / 256), b(256);
     hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 2);
     if (a.primaryOnly) {
@@ -927,6 +927,9 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st) {
         trav(false, 4 * seg + 1, a.nSlots);
         hipLaunchKernelGGL(k_nee, g, b, 0, st, a, seg);
         trav(true, 4 * seg + 2, a.nSlots);
+        // the first reader of the previous pass's G-buffer and reservoirs (temporal taps):
+        // a band's halo rows of them may still be in flight on the exchange stream
+        if (seg == 0 && waitBeforeRestir) hipStreamWaitEvent(st, waitBeforeRestir, 0);
         hipLaunchKernelGGL(k_restir, g, b, 0, st, a, seg);
         if (seg == 0) {
             trav(true, 4 * seg + 3, 4 * a.nSlots);

@@ -144,7 +144,8 @@ hipError_t launch_sky(const float *cfg90, const float *rad10, const float *solar
                       float brightness, float4 *sky, float4 *sun, float *skyPdf, float *sunPdf, int skyW, int skyH,
                       int sunW, int sunH, hipStream_t st);
 hipError_t launch_sky_lower(float4 *sky, float *skyPdf, int skyW, int skyH, float sumUpper, hipStream_t st);
-hipError_t launch_trace(const TraceArgs &a, hipStream_t st);
+// waitBeforeRestir: event the pass's temporal-reuse kernel waits for (band halo exchange), or null
+hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir = nullptr);
 hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st);
 
 struct DenoiseParamsDev {

@@ -196,6 +196,11 @@ struct vxpt_ctx {
     int nranks = 1, rank = 0;
     ncclComm_t comm = nullptr;
     std::vector<vxpt_ctx *> linked;
+    // the trace-halo exchange runs on its own stream, overlapped with the next
+    // pass up to its temporal-reuse kernel (haloDone: recorded after the exchange)
+    hipStream_t commStream = nullptr;
+    hipEvent_t haloReady = nullptr, haloDone = nullptr;
+    bool haloPending = false;
 };
 
 namespace {
@@ -547,7 +552,8 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
     a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(c, launch_trace(a, c->stream));
+    HIPCHK(c, launch_trace(a, c->stream, c->haloPending ? c->haloDone : nullptr));
+    c->haloPending = false;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     c->tracePrev = c->last;
     c->last = next;
@@ -693,19 +699,34 @@ char *buffer_rows(vxpt_ctx *c, int which, int y, size_t &rowBytes) {
 
 // Halo exchange of `bufs` over `rows` rows for every context of the frame
 // (one with RCCL, all of this process's bands when linked).
-int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows) {
+// With overlap (RCCL only) the exchange runs on the context's exchange stream
+// after the rows' producer and the next trace pass's temporal-reuse kernel waits
+// for it (do_trace); the trace passes touch neither the sent rows nor the
+// received ones before that kernel (they write the other G-buffer slot and
+// reservoir parity).
+int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows, bool overlap = false) {
     if (cs.size() == 1 && cs[0]->comm) {
         vxpt_ctx *c = cs[0];
+        hipStream_t st = c->stream;
+        if (overlap) {
+            HIPCHK(c, hipEventRecord(c->haloReady, c->stream));
+            HIPCHK(c, hipStreamWaitEvent(c->commStream, c->haloReady, 0));
+            st = c->commStream;
+        }
         if (ncclGroupStart() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupStart");
         for (int b : bufs)
             for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, rows)) {
                 size_t rb;
                 char *send = buffer_rows(c, b, h.sy, rb);
                 char *recv = buffer_rows(c, b, h.ry, rb);
-                ncclSend(send, (size_t)h.sn * rb, ncclUint8, h.peer, c->comm, c->stream);
-                ncclRecv(recv, (size_t)h.rn * rb, ncclUint8, h.peer, c->comm, c->stream);
+                ncclSend(send, (size_t)h.sn * rb, ncclUint8, h.peer, c->comm, st);
+                ncclRecv(recv, (size_t)h.rn * rb, ncclUint8, h.peer, c->comm, st);
             }
         if (ncclGroupEnd() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupEnd (halo exchange)");
+        if (overlap) {
+            HIPCHK(c, hipEventRecord(c->haloDone, c->commStream));
+            c->haloPending = true;
+        }
         return VXPT_OK;
     }
     // linked contexts of one process: device copies from each neighbour's own rows
@@ -742,7 +763,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp));
         std::vector<int> bufs(std::begin(kGbufBufs), std::end(kGbufBufs));
         bufs.push_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN);
-        BANDCHK(exchange(cs, bufs, kTraceHalo));
+        // all but the last pass: overlapped with the next pass up to its temporal reuse
+        BANDCHK(exchange(cs, bufs, kTraceHalo, s + 1 < spp));
     }
     for (vxpt_ctx *c : cs) {
         c->denoiseInputIsAccum = spp > 1;
@@ -906,6 +928,9 @@ void vxpt_destroy(vxpt_ctx *c) {
         if (e) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->commStream) hipStreamDestroy(c->commStream);
+    if (c->haloReady) hipEventDestroy(c->haloReady);
+    if (c->haloDone) hipEventDestroy(c->haloDone);
     delete c;
 }
 
@@ -1267,6 +1292,9 @@ int vxpt_band_comm_init(vxpt_ctx *c, const void *id, size_t bytes, int nranks, i
     if (c->comm) ncclCommDestroy(c->comm);
     c->comm = nullptr;
     if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclCommInitRank");
+    if (!c->commStream) HIPCHK(c, hipStreamCreateWithFlags(&c->commStream, hipStreamNonBlocking));
+    if (!c->haloReady) HIPCHK(c, hipEventCreateWithFlags(&c->haloReady, hipEventDisableTiming));
+    if (!c->haloDone) HIPCHK(c, hipEventCreateWithFlags(&c->haloDone, hipEventDisableTiming));
     c->nranks = nranks;
     c->rank = rank;
     return vxpt_set_band(c, y0, y1);
