@@ -47,7 +47,8 @@ enum vxpt_buffer {
     VXPT_BUF_VOXELS = 34,    /* chunk-major u8 block ids                        */
     VXPT_BUF_RES_EVEN = 35,  /* reservoirs of even iterationIndex (W*H*20 B)   */
     VXPT_BUF_RES_ODD = 36,   /* reservoirs of odd iterationIndex               */
-    VXPT_BUF_WPOS = 37       /* per-pixel hit world position (denoiser)        */
+    VXPT_BUF_WPOS = 37,      /* per-pixel hit world position (denoiser)        */
+    VXPT_BUF_FRAME = 38      /* post-processed frame, Float4(sRGB, 0) (OfflineBackend m_frameBuffer) */
 };
 
 typedef struct vxpt_config {
@@ -81,6 +82,31 @@ typedef struct vxpt_denoise_params { /* DenoisingParams, GlobalSettings.h:82-141
     int32_t enable_temporal_accumulation, enable_history_fix, enable_history_clamping;
     int32_t enable_spatial_filtering, enable_firefly_filter, atrous_iteration_num;
 } vxpt_denoise_params;
+
+typedef struct vxpt_post_params { /* ToneMappingParams + PostProcessingPipelineParams (GlobalSettings.h:10-186),
+                                      yaml section `postprocess` */
+    float manual_exposure;
+    int32_t tone_mapping_curve;      /* 0 Narkowicz ACES, 1 Uncharted 2, 2 Reinhard */
+    float white_point, contrast, saturation, lift, gain;
+    int32_t enable_bloom;
+    float bloom_threshold, bloom_intensity, bloom_radius;
+    int32_t enable_auto_exposure;
+    float exposure_speed, exposure_min, exposure_max, exposure_compensation;
+    float histogram_min_percent, histogram_max_percent, target_luminance;
+    int32_t enable_vignette;
+    float vignette_strength, vignette_radius, vignette_smoothness;
+    int32_t enable_lens_flare;
+    float lens_flare_intensity, lens_flare_ghost_spacing;
+    int32_t lens_flare_ghost_count;
+    float lens_flare_halo_radius, lens_flare_sun_size, lens_flare_distortion;
+    int32_t draw_crosshair;          /* DrawCrosshair (PostProcessor.cu:14-46), on in the reference */
+} vxpt_post_params;
+
+typedef struct vxpt_image_diff_result { /* ImageDiffResult (renderer/util/ImageDiff.h:7-26) */
+    int32_t total_pixels, different_pixels;
+    float pixel_difference_ratio, rmse, ssim;
+    int32_t is_identical, is_very_close, is_close;
+} vxpt_image_diff_result;
 
 typedef struct vxpt_timing {  /* HIP-event times of the last frame, ms (replaces PerformanceTracker) */
     float trace_ms;
@@ -145,6 +171,25 @@ int vxpt_denoise_pass(vxpt_ctx *ctx, const vxpt_denoise_params *p, int pass, int
 /* OfflineBackend::renderFrame: spp trace passes (radiance averaged) + denoise.  frame_num as
  * OfflineBackend::m_frameNum; iteration indices frame_num*spp .. +spp-1. */
 int vxpt_render_frame(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame_num, int32_t spp);
+
+/* PostProcessor::run (PostProcessor.cu:74-122): histogram auto-exposure, bloom, lens flare,
+ * vignette, filmic tone mapping, crosshair; the denoiser output -> VXPT_BUF_FRAME.  p = NULL
+ * takes the yaml values (vxpt_load_settings); dt_ms = Timer::getDeltaTime (milliseconds) for the
+ * exposure adaptation (OfflineBackend.cpp:79; any dt >= 1 ms adapts fully in one frame). */
+int vxpt_get_post_params(vxpt_ctx *ctx, vxpt_post_params *out);
+/* the lens flare's sun (ProjectSunToScreen, PostProcessingPipeline.cu:187-206): on-screen flag,
+ * pixel x, y, uv, and the accumulated sun luminance (parity hook) */
+int vxpt_get_sun_projection(vxpt_ctx *ctx, float out6[6]);
+int vxpt_postprocess(vxpt_ctx *ctx, const vxpt_post_params *p, float dt_ms);
+/* OfflineBackend::writeFrameBufferToPNG (OfflineBackend.cpp:191-221): rgba = W*H float4 (the
+ * frame), clamped to [0,1], x255 truncated, rows flipped, written as 8-bit RGB PNG */
+int vxpt_write_png_rgba32f(const char *path, int w, int h, const float *rgba);
+/* 8-bit PNG reader (query with pixels = NULL, then read w*h*channels bytes) */
+int vxpt_read_png(const char *path, int *w, int *h, int *channels, uint8_t *pixels, size_t cap);
+/* ImageDiff::compare / generateDiffImage (renderer/util/ImageDiff.cpp:94-185): the canonical-image
+ * gate of mainOffline --test-canonical (mainOffline.cpp:450-497) */
+int vxpt_image_diff(const char *png_a, const char *png_b, vxpt_image_diff_result *out);
+int vxpt_image_diff_png(const char *png_a, const char *png_b, const char *diff_png);
 
 /* multi-GPU band partition: the context traces and denoises only rows
  * [row_begin, row_end) (8-aligned; 0,0 = whole frame) of full-frame buffers.  Rows

@@ -58,6 +58,7 @@ def lib():
             "orc_set_camera": (None, [P, P, P, F, I]),
             "orc_get_camera": (None, [P, I, P]),
             "orc_camera_kat": (None, [I, I, F, F, P, I, P, P]),
+            "orc_postprocess": (None, [I, I, P, P, P, P, F, I, I, I, F, F, F, P]),
             "orc_copy_camera_to_prev": (None, [P]),
             "orc_trace": (None, [P, I, I, I, I]),
             "orc_post_trace": (None, [P]),
@@ -205,3 +206,20 @@ class Oracle:
         t = np.zeros(n, np.float32)
         self.L.orc_dda(self.h, n, _p(rays), _p(out), _p(t), mode)
         return out, t
+
+
+def postprocess(frame_in, depth, params, state, dt_ms, sun=None, sun_luminance=1.0):
+    """PostProcessor::run restated (orc_post.cpp) on a W x H x 4 float32 denoiser output.
+    params: a ctypes struct laid out as vxpt_post_params; state: float32[2] (average
+    luminance, exposure), updated in place; sun: (px, py, u, v) when the sun projects
+    on screen.  Returns the W x H x 4 frame."""
+    L = lib()
+    h, w = frame_in.shape[:2]
+    src = np.ascontiguousarray(frame_in, dtype=np.float32)
+    dep = np.ascontiguousarray(depth, dtype=np.float32)
+    out = np.zeros((h, w, 4), np.float32)
+    on, px, py, u, v = (0, 0, 0, 0.0, 0.0) if sun is None else (1,) + tuple(sun)
+    L.orc_postprocess(w, h, src.ctypes.data, dep.ctypes.data, ctypes.addressof(params), state.ctypes.data,
+                      float(dt_ms), int(on), int(px), int(py), float(u), float(v), float(sun_luminance),
+                      out.ctypes.data)
+    return out

@@ -183,6 +183,40 @@ struct DenoiseArgs {
     Reservoir *ffRes;
 };
 
+// post-processing (postprocess.hip; ToneMappingParams + PostProcessingPipelineParams, GlobalSettings.h:10-186)
+struct PostParamsDev {
+    float manualExposure;
+    int curve;                      // 0 Narkowicz ACES, 1 Uncharted 2, 2 Reinhard
+    float whitePoint, contrast, saturation, lift, gain;
+    int enableBloom;
+    float bloomThreshold, bloomIntensity, bloomRadius;
+    int enableAutoExposure;
+    float exposureSpeed, exposureMin, exposureMax, exposureCompensation;
+    float histogramMinPercent, histogramMaxPercent, targetLuminance;
+    int enableVignette;
+    float vignetteStrength, vignetteRadius, vignetteSmoothness;
+    int enableLensFlare;
+    float lensFlareIntensity, lensFlareGhostSpacing;
+    int lensFlareGhostCount;
+    float lensFlareHaloRadius, lensFlareSunSize, lensFlareDistortion;
+    int crosshair;
+};
+
+struct PostArgs {
+    int W, H;
+    PostParamsDev p;
+    const float4 *input;            // the denoiser output (IlluminationOutputBuffer)
+    float4 *work, *bloomA, *bloomB; // working plane, bloom extract / temp planes
+    float4 *frame;                  // result: Float4(sRGB colour, 0) (CopyToInteropBuffer)
+    const float *depth;             // lens-flare sun visibility
+    float *hist;                    // 256 luminance bins
+    float *state;                   // [0] current average luminance, [1] exposure of this frame
+    float dtMs;                     // frame time for the exposure adaptation (Timer::getDeltaTime, ms)
+    int sunOnScreen, sunPx, sunPy;  // ProjectSunToScreen (PostProcessingPipeline.cu:187-206)
+    float sunU, sunV, sunLuminance;
+};
+hipError_t launch_postprocess(const PostArgs &a, hipStream_t st);
+
 hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st);

@@ -186,6 +186,13 @@ struct vxpt_ctx {
     int numCU = 256;
     std::vector<void *> allocs;
 
+    // post-processing (PostProcessor / PostProcessingPipeline): working, bloom and frame
+    // planes, luminance histogram, device exposure state
+    vxpt_post_params yamlPost{};
+    float4 *postWork = nullptr, *bloomA = nullptr, *bloomB = nullptr, *frame = nullptr;
+    float *postHist = nullptr, *postState = nullptr;
+    float sunLuminance = 1.0f;     // SkyModel::getAccumulatedSunLuminance: the sun map's total pdf
+
     vxpt_denoise_params yamlDenoise{};
     float skyParams[4] = {0.25f, 45.0f, 0.0f, 1.0f};
     vxpt_material yamlMats[13] = {};
@@ -374,6 +381,23 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.wpos = c->wpos;
 }
 
+// GlobalSettings.h:10-186 defaults (the reference yaml overrides most of them: vxpt_load_settings)
+vxpt_post_params default_post() {
+    vxpt_post_params p{};
+    p.manual_exposure = 10.0f; p.tone_mapping_curve = 0; p.white_point = 10.0f;
+    p.contrast = 1.0f; p.saturation = 1.0f; p.lift = 0.0f; p.gain = 1.0f;
+    p.enable_bloom = 1; p.bloom_threshold = 1.0f; p.bloom_intensity = 0.15f; p.bloom_radius = 2.0f;
+    p.enable_auto_exposure = 1; p.exposure_speed = 1.0f; p.exposure_min = -8.0f; p.exposure_max = 8.0f;
+    p.exposure_compensation = 0.0f; p.histogram_min_percent = 40.0f; p.histogram_max_percent = 80.0f;
+    p.target_luminance = 0.18f;
+    p.enable_vignette = 0; p.vignette_strength = 0.5f; p.vignette_radius = 0.8f; p.vignette_smoothness = 0.5f;
+    p.enable_lens_flare = 0; p.lens_flare_intensity = 0.00001f; p.lens_flare_ghost_spacing = 0.15f;
+    p.lens_flare_ghost_count = 4; p.lens_flare_halo_radius = 0.1f; p.lens_flare_sun_size = 0.006f;
+    p.lens_flare_distortion = 0.015f;
+    p.draw_crosshair = 1;
+    return p;
+}
+
 const vxpt_denoise_params &default_denoise() {
     static vxpt_denoise_params d{30.f, 6.f, 2.f, 0.5f, 0.15f, 0.003f, 0.01f, 0.05f, 500000.f, 1, 1, 1, 1, 1, 1};
     return d;
@@ -408,6 +432,7 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_RES_EVEN: p = c->res; bytes = n * sizeof(Reservoir); return true;
         case VXPT_BUF_RES_ODD: p = c->res + n; bytes = n * sizeof(Reservoir); return true;
         case VXPT_BUF_WPOS: p = c->wpos; bytes = n * 16; return true;
+        case VXPT_BUF_FRAME: p = c->frame; bytes = n * 16; return c->frame != nullptr;
         case VXPT_BUF_PING: p = c->ping; bytes = n * 16; return true;
         case VXPT_BUF_PONG: p = c->pong; bytes = n * 16; return true;
         case VXPT_BUF_PREV_ILLUM: p = c->prevIllum; bytes = n * 16; return true;
@@ -862,6 +887,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (cfg->total_bounce_limit > 0) c->totalBounce = cfg->total_bounce_limit;
     if (cfg->diffuse_bounce_limit > 0) c->diffuseBounce = cfg->diffuse_bounce_limit;
     c->dataDir = cfg->data_dir ? cfg->data_dir : "data";
+    c->yamlPost = default_post();
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -940,6 +966,7 @@ int vxpt_load_settings(vxpt_ctx *c) {
     std::ifstream f(c->dataDir + "/settings/global_settings.yaml");
     if (!f) return fail(c, VXPT_ERR_IO, "missing settings/global_settings.yaml");
     vxpt_denoise_params d = default_denoise();
+    vxpt_post_params pp = default_post();
     std::string line, section;
     while (std::getline(f, line)) {
         const size_t hash = line.find('#');
@@ -967,6 +994,39 @@ int vxpt_load_settings(vxpt_ctx *c) {
             else if (key == "disocclusionThreshold") d.disocclusion_threshold = v;
             else if (key == "disocclusionThresholdAlternate") d.disocclusion_threshold_alternate = v;
             else if (key == "denoisingRange") d.denoising_range = v;
+        } else if (section == "postprocess") {  // GlobalSettings.cpp:277-355
+            const float v = (float)std::atof(val.c_str());
+            const int b = as_bool(val) ? 1 : 0;
+            if (key == "manualExposure") pp.manual_exposure = v;
+            else if (key == "toneMappingCurve") pp.tone_mapping_curve = (int)v;
+            else if (key == "whitePoint") pp.white_point = v;
+            else if (key == "contrast") pp.contrast = v;
+            else if (key == "saturation") pp.saturation = v;
+            else if (key == "gain") pp.gain = v;
+            else if (key == "lift") pp.lift = v;
+            else if (key == "enableBloom") pp.enable_bloom = b;
+            else if (key == "bloomThreshold") pp.bloom_threshold = v;
+            else if (key == "bloomIntensity") pp.bloom_intensity = v;
+            else if (key == "bloomRadius") pp.bloom_radius = v;
+            else if (key == "enableAutoExposure") pp.enable_auto_exposure = b;
+            else if (key == "exposureSpeed") pp.exposure_speed = v;
+            else if (key == "exposureMin") pp.exposure_min = v;
+            else if (key == "exposureMax") pp.exposure_max = v;
+            else if (key == "exposureCompensation") pp.exposure_compensation = v;
+            else if (key == "histogramMinPercent") pp.histogram_min_percent = v;
+            else if (key == "histogramMaxPercent") pp.histogram_max_percent = v;
+            else if (key == "targetLuminance") pp.target_luminance = v;
+            else if (key == "enableVignette") pp.enable_vignette = b;
+            else if (key == "vignetteStrength") pp.vignette_strength = v;
+            else if (key == "vignetteRadius") pp.vignette_radius = v;
+            else if (key == "vignetteSmoothness") pp.vignette_smoothness = v;
+            else if (key == "enableLensFlare") pp.enable_lens_flare = b;
+            else if (key == "lensFlareIntensity") pp.lens_flare_intensity = v;
+            else if (key == "lensFlareGhostSpacing") pp.lens_flare_ghost_spacing = v;
+            else if (key == "lensFlareGhostCount") pp.lens_flare_ghost_count = (int)v;
+            else if (key == "lensFlareHaloRadius") pp.lens_flare_halo_radius = v;
+            else if (key == "lensFlareSunSize") pp.lens_flare_sun_size = v;
+            else if (key == "lensFlareDistortion") pp.lens_flare_distortion = v;
         } else if (section == "sky") {
             const float v = (float)std::atof(val.c_str());
             if (key == "timeOfDay") c->skyParams[0] = v;
@@ -976,6 +1036,7 @@ int vxpt_load_settings(vxpt_ctx *c) {
         }
     }
     c->yamlDenoise = d;
+    c->yamlPost = pp;
     // materials.yaml (order == material index, MaterialManager.cpp:84-97) + blocks.yaml
     std::ifstream fm(c->dataDir + "/assets/materials.yaml");
     if (!fm) return fail(c, VXPT_ERR_IO, "missing assets/materials.yaml");
@@ -1138,6 +1199,7 @@ int vxpt_set_sky(vxpt_ctx *c, float tod, float axisAngle, float axisRotate, floa
     float s1, s2;
     c->hSkyAlias = build_alias(pdf, s1);
     const std::vector<AliasBin> sunA = build_alias(spdf, s2);
+    c->sunLuminance = s2;
     if (upload_vec(c, c->skyAlias, c->hSkyAlias.data(), c->hSkyAlias.size()) ||
         upload_vec(c, c->sunAlias, sunA.data(), sunA.size()))
         return VXPT_ERR_HIP;
@@ -1271,6 +1333,74 @@ int vxpt_copy_rows(vxpt_ctx *c, int which, int y, int rows, void *dev, int to_bu
 }
 
 int vxpt_exchange_halo(vxpt_ctx *c, uint32_t, int) { return c ? VXPT_OK : VXPT_ERR_ARG; }
+
+// ProjectSunToScreen (PostProcessingPipeline.cu:187-206) on the host, like the reference;
+// sunLuminance = SkyModel::getAccumulatedSunLuminance, 1 when not positive (:569-571)
+static void sun_projection(vxpt_ctx *c, int &on, int &px, int &py, float &u, float &v, float &lum) {
+    const V3 uvw = m3_apply(c->cam.worldToUv, normalize(c->sunDir));
+    on = 0; px = py = 0; u = v = 0.0f;
+    if (uvw.z > 0.0f) {
+        const float uu = uvw.x / uvw.z, vv = uvw.y / uvw.z;
+        if (!(uu < 0.0f || uu > 1.0f || vv < 0.0f || vv > 1.0f)) {
+            on = 1;
+            u = uu; v = vv;
+            px = std::min(std::max((int)(uu * c->W), 0), c->W - 1);
+            py = std::min(std::max((int)(vv * c->H), 0), c->H - 1);
+        }
+    }
+    lum = c->sunLuminance > 0.0f ? c->sunLuminance : 1.0f;
+}
+
+int vxpt_get_sun_projection(vxpt_ctx *c, float out6[6]) {
+    if (!c || !out6) return VXPT_ERR_ARG;
+    int on, px, py;
+    float u, v, lum;
+    sun_projection(c, on, px, py, u, v, lum);
+    out6[0] = (float)on; out6[1] = (float)px; out6[2] = (float)py; out6[3] = u; out6[4] = v; out6[5] = lum;
+    return VXPT_OK;
+}
+
+int vxpt_get_post_params(vxpt_ctx *c, vxpt_post_params *out) {
+    if (!c || !out) return VXPT_ERR_ARG;
+    *out = c->yamlPost;
+    return VXPT_OK;
+}
+
+int vxpt_postprocess(vxpt_ctx *c, const vxpt_post_params *pp, float dtMs) {
+    if (!c) return VXPT_ERR_ARG;
+    if (!pp) pp = &c->yamlPost;
+    HIPCHK(c, hipSetDevice(c->dev));
+    const size_t n = (size_t)c->W * c->H;
+    if (!c->frame) {
+        if (dalloc(c, c->postWork, n) || dalloc(c, c->bloomA, n) || dalloc(c, c->bloomB, n) ||
+            dalloc(c, c->frame, n) || dalloc(c, c->postHist, 256) || dalloc(c, c->postState, 4))
+            return VXPT_ERR_HIP;
+        const float init[4] = {0.18f, 1.0f, 0.0f, 0.0f};  // m_currentAvgLuminance (PostProcessingPipeline.cu:433)
+        HIPCHK(c, hipMemcpyAsync(c->postState, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    PostArgs a{};
+    a.W = c->W; a.H = c->H;
+    a.p = {pp->manual_exposure, pp->tone_mapping_curve, pp->white_point, pp->contrast, pp->saturation, pp->lift,
+           pp->gain, pp->enable_bloom, pp->bloom_threshold, pp->bloom_intensity, pp->bloom_radius,
+           pp->enable_auto_exposure, pp->exposure_speed, pp->exposure_min, pp->exposure_max,
+           pp->exposure_compensation, pp->histogram_min_percent, pp->histogram_max_percent, pp->target_luminance,
+           pp->enable_vignette, pp->vignette_strength, pp->vignette_radius, pp->vignette_smoothness,
+           pp->enable_lens_flare, pp->lens_flare_intensity, pp->lens_flare_ghost_spacing,
+           pp->lens_flare_ghost_count, pp->lens_flare_halo_radius, pp->lens_flare_sun_size,
+           pp->lens_flare_distortion, pp->draw_crosshair};
+    a.input = c->output;
+    a.work = c->postWork; a.bloomA = c->bloomA; a.bloomB = c->bloomB; a.frame = c->frame;
+    a.depth = c->gb[c->last].depth;
+    a.hist = c->postHist;
+    a.state = c->postState;
+    a.dtMs = dtMs;
+    sun_projection(c, a.sunOnScreen, a.sunPx, a.sunPy, a.sunU, a.sunV, a.sunLuminance);
+    HIPCHK(c, launch_postprocess(a, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
 
 int vxpt_band_comm_id(void *id, size_t bytes) {
     if (!id || bytes < sizeof(ncclUniqueId)) return VXPT_ERR_ARG;

@@ -22,7 +22,7 @@ DATA_DIR = os.path.join(REPO, "data")
 BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERIAL=5, MAT_PARAM=6, MOTION=7,
            PREV_NORMAL_ROUGH=8, PREV_GEO_NORMAL_THIN=9, PREV_ALBEDO=10, PREV_MAT_PARAM=11, PREV_DEPTH=12,
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
-           PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37)
+           PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
@@ -61,6 +61,30 @@ class DenoiseParams(ctypes.Structure):
     def defaults(cls):
         """global_settings.yaml denoising section (atrousIterationNum: 1)."""
         return cls(30.0, 6.0, 2.0, 0.5, 0.15, 0.003, 0.01, 0.05, 500000.0, 1, 1, 1, 1, 1, 1)
+
+
+class PostParams(ctypes.Structure):
+    """vxpt_post_params (ToneMappingParams + PostProcessingPipelineParams, GlobalSettings.h:10-186)."""
+    _fields_ = [("manual_exposure", ctypes.c_float), ("tone_mapping_curve", ctypes.c_int32)] + \
+        [(n, ctypes.c_float) for n in ("white_point", "contrast", "saturation", "lift", "gain")] + \
+        [("enable_bloom", ctypes.c_int32)] + \
+        [(n, ctypes.c_float) for n in ("bloom_threshold", "bloom_intensity", "bloom_radius")] + \
+        [("enable_auto_exposure", ctypes.c_int32)] + \
+        [(n, ctypes.c_float) for n in ("exposure_speed", "exposure_min", "exposure_max", "exposure_compensation",
+                                       "histogram_min_percent", "histogram_max_percent", "target_luminance")] + \
+        [("enable_vignette", ctypes.c_int32)] + \
+        [(n, ctypes.c_float) for n in ("vignette_strength", "vignette_radius", "vignette_smoothness")] + \
+        [("enable_lens_flare", ctypes.c_int32)] + \
+        [(n, ctypes.c_float) for n in ("lens_flare_intensity", "lens_flare_ghost_spacing")] + \
+        [("lens_flare_ghost_count", ctypes.c_int32)] + \
+        [(n, ctypes.c_float) for n in ("lens_flare_halo_radius", "lens_flare_sun_size", "lens_flare_distortion")] + \
+        [("draw_crosshair", ctypes.c_int32)]
+
+
+class ImageDiffResult(ctypes.Structure):
+    _fields_ = [("total_pixels", ctypes.c_int32), ("different_pixels", ctypes.c_int32),
+                ("pixel_difference_ratio", ctypes.c_float), ("rmse", ctypes.c_float), ("ssim", ctypes.c_float),
+                ("is_identical", ctypes.c_int32), ("is_very_close", ctypes.c_int32), ("is_close", ctypes.c_int32)]
 
 
 class Timing(ctypes.Structure):
@@ -108,6 +132,14 @@ def load_library(path=LIB_PATH):
         "vxpt_set_band": (I, [P, I, I]),
         "vxpt_row_bytes": (I, [P, I]),
         "vxpt_copy_rows": (I, [P, I, I, I, P, I]),
+        "vxpt_get_post_params": (I, [P, ctypes.POINTER(PostParams)]),
+        "vxpt_postprocess": (I, [P, ctypes.POINTER(PostParams), F]),
+        "vxpt_get_sun_projection": (I, [P, P]),
+        "vxpt_write_png_rgba32f": (I, [ctypes.c_char_p, I, I, P]),
+        "vxpt_read_png": (I, [ctypes.c_char_p, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I), P,
+                              ctypes.c_size_t]),
+        "vxpt_image_diff": (I, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ImageDiffResult)]),
+        "vxpt_image_diff_png": (I, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]),
         "vxpt_band_comm_id": (I, [P, ctypes.c_size_t]),
         "vxpt_band_comm_init": (I, [P, P, ctypes.c_size_t, I, I]),
         "vxpt_band_link": (I, [ctypes.POINTER(P), I]),
@@ -223,6 +255,26 @@ class Renderer:
         which = BUF[name] if isinstance(name, str) else int(name)
         self._chk(self.lib.vxpt_copy_rows(self.ctx, which, y, rows, ctypes.c_void_p(dev_ptr), int(to_buffer)),
                   "vxpt_copy_rows")
+
+    # --- post-processing + frame output (PostProcessor::run, OfflineBackend::writeFrameBufferToPNG) ---
+    def post_params(self):
+        p = PostParams()
+        self._chk(self.lib.vxpt_get_post_params(self.ctx, ctypes.byref(p)), "vxpt_get_post_params")
+        return p
+
+    def postprocess(self, params=None, dt_ms=16.6667):
+        self._chk(self.lib.vxpt_postprocess(self.ctx, ctypes.byref(params) if params is not None else None,
+                                            float(dt_ms)), "vxpt_postprocess")
+
+    def sun_projection(self):
+        """(on_screen, px, py, u, v, accumulated sun luminance) of the lens flare."""
+        o = np.zeros(6, np.float32)
+        self._chk(self.lib.vxpt_get_sun_projection(self.ctx, o.ctypes.data), "vxpt_get_sun_projection")
+        return bool(o[0]), int(o[1]), int(o[2]), float(o[3]), float(o[4]), float(o[5])
+
+    def write_png(self, path):
+        """The post-processed frame as the reference's offline PNG."""
+        write_png(path, self.read("FRAME"))
 
     def band_comm_init(self, comm_id, nranks, rank):
         """Attach an RCCL communicator (vxpt_band_comm_init): this context renders band `rank`
@@ -340,3 +392,33 @@ class LinkedBands:
         p = params or DenoiseParams.defaults()
         if self.lib.vxpt_render_frame_linked(self._arr, len(self.rs), ctypes.byref(p), frame_num, spp) != 0:
             raise VxptError("vxpt_render_frame_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
+
+
+def write_png(path, frame):
+    """OfflineBackend::writeFrameBufferToPNG: H x W x 4 float32 -> 8-bit RGB PNG (clamped, x255, Y flip)."""
+    lib = load_library()
+    f = np.ascontiguousarray(frame, dtype=np.float32)
+    if lib.vxpt_write_png_rgba32f(os.fsencode(path), f.shape[1], f.shape[0], f.ctypes.data) != 0:
+        raise VxptError("vxpt_write_png_rgba32f(%s) failed" % path)
+
+
+def read_png(path):
+    lib = load_library()
+    w, h, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    if lib.vxpt_read_png(os.fsencode(path), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c), None, 0) != 0:
+        raise VxptError("cannot read %s" % path)
+    px = np.zeros((h.value, w.value, c.value), np.uint8)
+    if lib.vxpt_read_png(os.fsencode(path), None, None, None, px.ctypes.data, px.size) != 0:
+        raise VxptError("cannot read %s" % path)
+    return px
+
+
+def image_diff(a, b, diff_png=None):
+    """ImageDiff::compare (+ generateDiffImage when diff_png is given)."""
+    lib = load_library()
+    r = ImageDiffResult()
+    if lib.vxpt_image_diff(os.fsencode(a), os.fsencode(b), ctypes.byref(r)) != 0:
+        raise VxptError("image diff failed: %s vs %s" % (a, b))
+    if diff_png and lib.vxpt_image_diff_png(os.fsencode(a), os.fsencode(b), os.fsencode(diff_png)) != 0:
+        raise VxptError("diff image failed")
+    return {f: getattr(r, f) for f, _ in r._fields_}

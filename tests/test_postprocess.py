@@ -1,0 +1,132 @@
+"""Offline output path: post-processing (PostProcessor::run), the PNG frame
+writer (OfflineBackend::writeFrameBufferToPNG) and the canonical-image gate
+(ImageDiff).
+
+CPU: PNG round trip and the writer's conversion, ImageDiff metrics against a
+numpy restatement, the oracle post-process on a synthetic frame (exposure,
+bloom, tone curve sanity).  GPU: the HIP post-process chain against the oracle
+on a rendered frame, with the sun on screen (lens flare) and off.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import vxpt
+from golden.make_golden import C1_CAMERA
+
+
+def _frame(h=48, w=64, seed=3):
+    rng = np.random.default_rng(seed)
+    f = rng.uniform(-0.2, 1.4, (h, w, 4)).astype(np.float32)
+    return f
+
+
+def test_png_writer_matches_reference_conversion(tmp_path):
+    f = _frame()
+    path = str(tmp_path / "f.png")
+    vxpt.write_png(path, f)
+    px = vxpt.read_png(path)
+    exp = (np.clip(f[..., :3], 0.0, 1.0) * np.float32(255.0)).astype(np.uint8)[::-1]  # Y flip
+    assert px.shape == exp.shape
+    np.testing.assert_array_equal(px, exp)
+
+
+def _ssim_ref(a, b):
+    def gray(im):
+        return (np.float32(0.299) * im[..., 0] + np.float32(0.587) * im[..., 1] +
+                np.float32(0.114) * im[..., 2]).astype(np.float64)
+
+    def gauss(g):
+        k = np.array([[1, 2, 1], [2, 4, 2], [1, 2, 1]], np.float64) / 16
+        p = np.pad(g, 1, mode="edge")
+        return sum(k[i, j] * p[i:i + g.shape[0], j:j + g.shape[1]] for i in range(3) for j in range(3))
+    ga, gb = gauss(gray(a.astype(np.float32))), gauss(gray(b.astype(np.float32)))
+    c1, c2 = (0.01 * 255) ** 2, (0.03 * 255) ** 2
+    ma, mb = ga.mean(), gb.mean()
+    va, vb = ga.var(ddof=1), gb.var(ddof=1)
+    cov = ((ga - ma) * (gb - mb)).sum() / (ga.size - 1)
+    return (2 * ma * mb + c1) * (2 * cov + c2) / ((ma * ma + mb * mb + c1) * (va + vb + c2))
+
+
+def test_image_diff_metrics(tmp_path):
+    a = _frame(seed=1)
+    b = a.copy()
+    b[10:20, 5:30, :3] += 0.05
+    pa, pb, pd = (str(tmp_path / n) for n in ("a.png", "b.png", "d.png"))
+    vxpt.write_png(pa, a)
+    vxpt.write_png(pb, b)
+    same = vxpt.image_diff(pa, pa)
+    assert same["is_identical"] and same["rmse"] == 0.0 and abs(same["ssim"] - 1.0) < 1e-6
+    r = vxpt.image_diff(pa, pb, pd)
+    ia, ib = vxpt.read_png(pa).astype(np.int32), vxpt.read_png(pb).astype(np.int32)
+    diff_px = (np.abs(ia - ib) / 255.0 > 0.01).any(axis=2).sum()
+    assert r["different_pixels"] == diff_px and r["total_pixels"] == ia.shape[0] * ia.shape[1]
+    assert abs(r["rmse"] - np.sqrt(((ia - ib) ** 2).mean())) < 1e-4
+    assert abs(r["ssim"] - _ssim_ref(ia, ib)) < 1e-4
+    d = vxpt.read_png(pd)
+    np.testing.assert_array_equal(d, np.minimum(255, np.abs(ia - ib) * 3).astype(np.uint8))
+
+
+def _post_params(**kw):
+    p = vxpt.PostParams(0.8, 0, 10.0, 1.0, 1.0, 0.0, 1.0, 1, 1.0, 0.15, 2.0, 1, 1.0, -8.0, 8.0, 0.0, 50.0, 95.0, 0.25,
+                        1, 0.42, 0.8, 0.56, 1, 0.00001, 0.15, 4, 0.1, 0.006, 0.015, 1)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def test_oracle_postprocess_sanity():
+    f = _frame() * 3
+    depth = np.full(f.shape[:2], 10.0, np.float32)
+    st = np.array([0.18, 1.0], np.float32)
+    out = oracle.postprocess(f, depth, _post_params(), st, 16.6667)
+    assert np.isfinite(out).all() and out[..., :3].min() >= 0.0 and out[..., :3].max() <= 1.0
+    assert (out[..., 3] == 0).all()
+    h, w = f.shape[:2]
+    assert (out[h // 2, w // 2 - 10:w // 2 + 11, :3] == 1.0).all()  # crosshair
+    # exposure adapts fully in one frame for any dt >= 1 ms (Timer::getDeltaTime is in ms)
+    assert 0.0 < st[0] < 10.0 and st[1] == pytest.approx(0.25 / st[0], rel=1e-6)
+    # manual exposure, no effects: the pure tone curve of the reference (ACES + sRGB)
+    p = _post_params(enable_auto_exposure=0, enable_bloom=0, enable_vignette=0, enable_lens_flare=0,
+                     draw_crosshair=0, manual_exposure=1.0)
+    o2 = oracle.postprocess(f, depth, p, st.copy(), 16.6667)
+    x = f[..., :3].astype(np.float64)
+    aces = np.clip(x * (2.51 * x + 0.03) / (x * (2.43 * x + 0.59) + 0.14), 0, 1)
+    srgb = np.where(aces <= 0.0031308, 12.92 * aces, 1.055 * aces ** (1 / 2.4) - 0.055)
+    np.testing.assert_allclose(o2[..., :3], srgb, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("look_at_sun", [False, True])
+def test_gpu_postprocess_matches_oracle(look_at_sun, tmp_path):
+    w, h = 128, 96
+    r = vxpt.Renderer(w, h)
+    r.load_settings()
+    r.generate_terrain((2, 1, 2))
+    r.set_sky()
+    d = C1_CAMERA[1]
+    if look_at_sun:
+        d = tuple(float(v) for v in r.sky_alias()[3])  # the sun at the screen centre: lens flare
+    cam = (C1_CAMERA[0], d, C1_CAMERA[2])
+    r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+    p = r.post_params()
+    st = np.array([0.18, 1.0], np.float32)
+    for f in range(2):
+        r.render_frame(f, 1, vxpt.DenoiseParams.defaults())
+        r.postprocess(p, 16.6667)
+        g = r.read("FRAME")
+        on, px, py, u, v, lum = r.sun_projection()
+        assert on == look_at_sun
+        c = oracle.postprocess(r.read("OUTPUT"), r.read("DEPTH"), p, st, 16.6667,
+                               sun=(px, py, u, v) if on else None, sun_luminance=lum)
+        err = np.abs(g - c)
+        assert err.max() < 2e-4, (f, float(err.max()), np.unravel_index(err.argmax(), err.shape))
+    if look_at_sun:
+        assert r.read("DEPTH")[py, px] > 1e26  # the flare branch really ran
+    path = str(tmp_path / "frame.png")
+    r.write_png(path)
+    px = vxpt.read_png(path)
+    assert px.shape == (h, w, 3)
+    r.close()
