@@ -171,6 +171,9 @@ int vxpt_denoise_pass(vxpt_ctx *ctx, const vxpt_denoise_params *p, int pass, int
 /* OfflineBackend::renderFrame: spp trace passes (radiance averaged) + denoise.  frame_num as
  * OfflineBackend::m_frameNum; iteration indices frame_num*spp .. +spp-1. */
 int vxpt_render_frame(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame_num, int32_t spp);
+/* the denoiser parameters of global_settings.yaml's `denoising` section (GlobalSettings.h:82-141),
+ * the ones every call above uses when p = NULL */
+int vxpt_get_denoise_params(vxpt_ctx *ctx, vxpt_denoise_params *out);
 
 /* PostProcessor::run (PostProcessor.cu:74-122): histogram auto-exposure, bloom, lens flare,
  * vignette, filmic tone mapping, crosshair; the denoiser output -> VXPT_BUF_FRAME.  p = NULL

@@ -2,12 +2,17 @@
 // histogram auto-exposure, bloom, lens flare, vignette (PostProcessingPipeline.cu:11-601),
 // filmic tone mapping (FilmicToneMapping.h:11-117), crosshair, copy to the frame buffer.
 //
-// The reference works in place on IlluminationOutputBuffer; here the denoiser
-// output stays intact (parity hook) and the chain runs on a working plane,
-// ending in the frame plane (Float4(colour, 0), CopyToInteropBuffer).  The
-// auto-exposure state (current average luminance) lives on the device, so the
-// reference's host round trip (cudaMemcpy of the average, PostProcessingPipeline.cu:495-514)
-// becomes a one-thread kernel and the frame needs no host synchronisation.
+// The reference runs one kernel per effect in place on IlluminationOutputBuffer (8 full-frame
+// passes, a float atomic per pixel for the histogram, a host round trip for the exposure).  Here
+// the chain is three passes and the denoiser output stays intact (parity hook):
+//   1. k_lum_bloom  -- 64x16 tile in LDS: the luminance histogram (LDS bins, one global atomic per
+//                      non-empty bin and tile), the bloom extract and the horizontal blur -> bloomB
+//   2. k_exposure   -- one wave: the reference's histogram scans and exposure adaptation on the
+//                      device (state[0] = current average luminance, state[1] = exposure)
+//   3. k_compose    -- vertical blur + composite, lens flare, vignette, tone curve, crosshair ->
+//                      Float4(sRGB, 0)
+// Each stage keeps the reference's per-pixel arithmetic and order; the exchanges through the
+// working plane were exact float4 round trips, so fusing them changes no value.
 #include "vx_internal.hpp"
 
 namespace vx {
@@ -24,41 +29,139 @@ VX_D void st3(float4 *b, int W, int x, int y, V3 c, float w) { b[(size_t)y * W +
 VX_D V3 clamp3(V3 v, float lo, float hi) { return V3(clampf(v.x, lo, hi), clampf(v.y, lo, hi), clampf(v.z, lo, hi)); }
 VX_D float lum_ref(V3 c) { return dot(c, V3(0.2126f, 0.7152f, 0.0722f)); }  // compensated Float3 dot
 
-// ComputeLuminanceHistogramKernel (PostProcessingPipeline.cu:319-350): counts are exact (< 2^24)
-__global__ __launch_bounds__(256) void k_histogram(PostArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
-    const float l = lum_ref(ld3(a.work, a.W, x, y));
-    if (l < 0.001f) return;
+// ComputeLuminanceHistogramKernel (PostProcessingPipeline.cu:319-350) bin of one pixel
+VX_D int hist_bin(float l) {
     const float logLum = log10f(l);
     const float t = clampf((logLum - kMinLogLum) / (kMaxLogLum - kMinLogLum), 0.0f, 1.0f);
-    const int bin = min((int)(t * kBins), kBins - 1);
-    atomicAdd(&a.hist[bin], 1.0f);
+    return min((int)(t * kBins), kBins - 1);
 }
 
-// ComputeAverageLuminanceKernel (:353-428) + the host's adaptation and exposure
-// (:499-514), one thread; state[0] = current average luminance, state[1] = exposure
-__global__ void k_exposure(PostArgs a) {
-    const float *h = a.hist;
+// BloomExtractBrightPixelsKernel (:12-80), neighbour filter on: c = the pixel, l its luminance,
+// n[4] the luminances of the (x-1, x+1, y-1, y+1) neighbours, -inf where outside the image
+VX_D V3 bloom_extract(V3 c, float l, const float n[4], float thr) {
+    if (!(l > thr)) return V3(0.0f);
+    float maxN = 0.0f;
+    for (int i = 0; i < 4; i++) maxN = fmaxf(maxN, n[i]);  // fmaxf(m, -inf) = m: a skipped neighbour
+    if (maxN < thr * 0.4f) return V3(0.0f);
+    return clamp3((c - V3(thr)) * 0.7f, 0.0f, 100.0f);
+}
+
+// BloomBlurKernel (:83-125) half width
+__host__ __device__ inline int blur_half(const PostParamsDev &p) { return ((int)(p.bloomRadius * 2.0f) + 1) / 2; }
+
+constexpr int TX = 64, TY = 16, kHalo = 8;
+constexpr int LW = TX + 2 * kHalo + 2;  // luminance row: blur apron + the extract's x neighbours
+constexpr int CW = TX + 2 * kHalo;      // colour / extract row
+
+// Pass 1.  Every input pixel of the tile and its apron is read once; the histogram counts
+// only the tile's own pixels.  Counts are integers (< 2^24 per frame), so the u32 totals equal
+// the reference's float atomics exactly.
+__global__ __launch_bounds__(256) void k_lum_bloom(PostArgs a, int doHist, int doBloom) {
+    __shared__ float sL[TY + 2][LW];
+    __shared__ float sC[TY][CW][3];
+    __shared__ unsigned sH[kBins];
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int W = a.W, H = a.H;
+    sH[tid] = 0u;
+    __syncthreads();
+    for (int i = tid; i < (TY + 2) * LW; i += 256) {
+        const int ly = i / LW, lx = i - ly * LW;
+        const int gy = y0 - 1 + ly, gx = x0 - kHalo - 1 + lx;
+        float l = -INFINITY;
+        if (gx >= 0 && gx < W && gy >= 0 && gy < H) {
+            const V3 c = ld3(a.input, W, gx, gy);
+            l = lum_ref(c);
+            if (ly >= 1 && ly <= TY && lx >= 1 && lx <= CW) {
+                sC[ly - 1][lx - 1][0] = c.x;
+                sC[ly - 1][lx - 1][1] = c.y;
+                sC[ly - 1][lx - 1][2] = c.z;
+                if (doHist && lx > kHalo && lx <= kHalo + TX && !(l < 0.001f)) atomicAdd(&sH[hist_bin(l)], 1u);
+            }
+        }
+        sL[ly][lx] = l;
+    }
+    __syncthreads();
+    if (doHist) {
+        const unsigned h = sH[tid];
+        if (h) atomicAdd(&a.hist[tid], h);
+    }
+    if (!doBloom) return;
+    const float thr = a.p.bloomThreshold;
+    // extract in place at every in-image position (each position reads only its own colour)
+    for (int i = tid; i < TY * CW; i += 256) {
+        const int ey = i / CW, ex = i - ey * CW;
+        const int gx = x0 - kHalo + ex, gy = y0 + ey;
+        if (gx < 0 || gx >= W || gy >= H) continue;
+        const int lx = ex + 1, ly = ey + 1;
+        const float n[4] = {sL[ly][lx - 1], sL[ly][lx + 1], sL[ly - 1][lx], sL[ly + 1][lx]};
+        const V3 e = bloom_extract(V3(sC[ey][ex][0], sC[ey][ex][1], sC[ey][ex][2]), sL[ly][lx], n, thr);
+        sC[ey][ex][0] = e.x;
+        sC[ey][ex][1] = e.y;
+        sC[ey][ex][2] = e.z;
+    }
+    __syncthreads();
+    const int half = blur_half(a.p);  // <= kHalo, checked by the launcher
+    for (int i = tid; i < TY * TX; i += 256) {
+        const int ey = i / TX, ex = i - ey * TX;
+        const int x = x0 + ex, y = y0 + ey;
+        if (x >= W || y >= H) continue;
+        V3 r(0.0f);
+        float tw = 0.0f;
+        for (int k = -half; k <= half; k++) {  // edge-clamped taps; a clamped tap stays in the apron
+            const int sx = clampi(x + k, 0, W - 1) - x0 + kHalo;
+            r += V3(sC[ey][sx][0], sC[ey][sx][1], sC[ey][sx][2]) * 1.0f;
+            tw += 1.0f;
+        }
+        if (tw > 0.0f) r /= tw;
+        st3(a.bloomB, W, x, y, r, 1.0f);
+    }
+}
+
+// Pass 2: ComputeAverageLuminanceKernel (:353-428) + the host's adaptation and exposure
+// (:499-514), one wave.  The bin counts are integers below 2^24, so the total and the running
+// sums of the reference's two serial scans are exact in any order: the wave computes them with
+// a prefix scan and finds the first bin reaching each percentile with a ballot.  Only the
+// weighted log-luminance sum rounds, and lane 0 accumulates it serially in the reference's order.
+__global__ __launch_bounds__(64) void k_exposure(PostArgs a) {
+    __shared__ float h[kBins];
+    const int lane = threadIdx.x;
+    float c4[4], run = 0.0f;
+    for (int k = 0; k < 4; k++) {  // lane owns bins 4*lane .. 4*lane+3
+        c4[k] = (float)a.hist[4 * lane + k];
+        a.hist[4 * lane + k] = 0u;
+        h[4 * lane + k] = c4[k];
+        run += c4[k];
+    }
+    float incl = run;  // inclusive prefix over lanes
+    for (int off = 1; off < 64; off <<= 1) {
+        const float v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const float total = __shfl(incl, 63, 64);
     const PostParamsDev &p = a.p;
-    float total = 0.0f;
-    for (int i = 0; i < kBins; i++) total += h[i];
     float avgLum = 0.18f;
     if (total != 0.0f) {
         const float minCount = total * p.histogramMinPercent / 100.0f;
         const float maxCount = total * p.histogramMaxPercent / 100.0f;
-        float acc = 0.0f;
-        int minBin = 0, maxBin = kBins - 1;
-        for (int i = 0; i < kBins; i++) {
-            acc += h[i];
-            if (acc >= minCount) { minBin = i; break; }
+        // the first bin whose running sum reaches the count (the serial scan's break)
+        int firstMin = kBins, firstMax = kBins;
+        float acc = incl - run;
+        for (int k = 0; k < 4; k++) {
+            acc += c4[k];
+            if (acc >= minCount && firstMin == kBins) firstMin = 4 * lane + k;
+            if (acc >= maxCount && firstMax == kBins) firstMax = 4 * lane + k;
         }
-        acc = 0.0f;
-        for (int i = 0; i < kBins; i++) {
-            acc += h[i];
-            if (acc >= maxCount) { maxBin = i; break; }
+        for (int off = 32; off >= 1; off >>= 1) {
+            firstMin = min(firstMin, __shfl_xor(firstMin, off, 64));
+            firstMax = min(firstMax, __shfl_xor(firstMax, off, 64));
         }
+        const int minBin = firstMin < kBins ? firstMin : 0;
+        const int maxBin = firstMax < kBins ? firstMax : kBins - 1;
+        __syncthreads();
+        if (lane != 0) return;
         float ws = 0.0f, wt = 0.0f;
+#pragma unroll 8
         for (int i = minBin; i <= maxBin; i++) {
             const float binCenter = kMinLogLum + (i + 0.5f) * (kMaxLogLum - kMinLogLum) / kBins;
             ws += h[i] * binCenter;
@@ -66,6 +169,7 @@ __global__ void k_exposure(PostArgs a) {
         }
         if (wt > 0.0f) avgLum = powf(10.0f, ws / wt);
     }
+    if (lane != 0) return;
     const float adapt = p.exposureSpeed * a.dtMs;
     const float cur = a.state[0];
     const float next = cur + clampf(adapt, 0.0f, 1.0f) * (avgLum - cur);
@@ -76,58 +180,36 @@ __global__ void k_exposure(PostArgs a) {
     a.state[1] = e;
 }
 
-// BloomExtractBrightPixelsKernel (:12-80), neighbour filter on
+// Bloom for radii wider than the LDS apron: extract -> bloomA, horizontal blur -> bloomB
 __global__ __launch_bounds__(256) void k_bloom_extract(PostArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.H) return;
-    const float thr = a.p.bloomThreshold;
-    V3 c = ld3(a.work, a.W, x, y);
-    if (lum_ref(c) > thr) {
-        float maxN = 0.0f;
-        const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
-        for (int i = 0; i < 4; i++)
-            if (nx[i] >= 0 && nx[i] < a.W && ny[i] >= 0 && ny[i] < a.H)
-                maxN = fmaxf(maxN, lum_ref(ld3(a.work, a.W, nx[i], ny[i])));
-        if (maxN < thr * 0.4f) c = V3(0.0f);
-        else c = clamp3((c - V3(thr)) * 0.7f, 0.0f, 100.0f);
-    } else {
-        c = V3(0.0f);
-    }
-    st3(a.bloomA, a.W, x, y, c, 1.0f);
+    const V3 c = ld3(a.input, a.W, x, y);
+    float n[4];
+    const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
+    for (int i = 0; i < 4; i++)
+        n[i] = (nx[i] >= 0 && nx[i] < a.W && ny[i] >= 0 && ny[i] < a.H) ? lum_ref(ld3(a.input, a.W, nx[i], ny[i]))
+                                                                        : -INFINITY;
+    st3(a.bloomA, a.W, x, y, bloom_extract(c, lum_ref(c), n, a.p.bloomThreshold), 1.0f);
 }
 
-// BloomBlurKernel (:83-125): box blur along one axis, edge-clamped
-__global__ __launch_bounds__(256) void k_bloom_blur(PostArgs a, const float4 *in, float4 *out, int dx, int dy) {
+__global__ __launch_bounds__(256) void k_bloom_blur_h(PostArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.H) return;
-    const int half = ((int)(a.p.bloomRadius * 2.0f) + 1) / 2;
+    const int half = blur_half(a.p);
     V3 r(0.0f);
     float tw = 0.0f;
     for (int i = -half; i <= half; i++) {
-        const int sx = clampi(x + dx * i, 0, a.W - 1), sy = clampi(y + dy * i, 0, a.H - 1);
-        r += ld3(in, a.W, sx, sy) * 1.0f;
+        r += ld3(a.bloomA, a.W, clampi(x + i, 0, a.W - 1), y) * 1.0f;
         tw += 1.0f;
     }
     if (tw > 0.0f) r /= tw;
-    st3(out, a.W, x, y, r, 1.0f);
+    st3(a.bloomB, a.W, x, y, r, 1.0f);
 }
 
-// BloomCompositeKernel (:128-148)
-__global__ __launch_bounds__(256) void k_bloom_composite(PostArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
-    const V3 c = ld3(a.work, a.W, x, y) + ld3(a.bloomA, a.W, x, y) * a.p.bloomIntensity;
-    st3(a.work, a.W, x, y, c, 1.0f);
-}
-
-// LensFlareKernel (:223-316); the sun-visibility test of the host (IsSunVisible,
-// :208-221: depth at the sun pixel >= RayMaxLowerBound) is read here on the device
-__global__ __launch_bounds__(256) void k_lens_flare(PostArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
-    if (!(a.depth[(size_t)a.sunPy * a.W + a.sunPx] >= 1.0e26f)) return;
+// LensFlareKernel (:223-316) for one pixel: the flare added to the pixel
+VX_D V3 lens_flare(const PostArgs &a, int x, int y) {
     const PostParamsDev &p = a.p;
-    const V3 orig = ld3(a.work, a.W, x, y);
     V3 flare(0.0f);
     const V2 uv((float)x / a.W, (float)y / a.H);
     const V2 center(0.5f, 0.5f);
@@ -173,24 +255,18 @@ __global__ __launch_bounds__(256) void k_lens_flare(PostArgs a) {
             flare += V3(strength, 0.0f, -strength) * fall;
         }
     }
-    st3(a.work, a.W, x, y, orig + flare, 1.0f);
+    return flare;
 }
 
-// VignetteKernel (:151-185)
-__global__ __launch_bounds__(256) void k_vignette(PostArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
-    const PostParamsDev &p = a.p;
-    V3 c = ld3(a.work, a.W, x, y);
-    const float nx = (float)(2 * x - a.W) / (float)a.W, ny = (float)(2 * y - a.H) / (float)a.H;
+// VignetteKernel (:151-185) factor
+VX_D float vignette(const PostParamsDev &p, int W, int H, int x, int y) {
+    const float nx = (float)(2 * x - W) / (float)W, ny = (float)(2 * y - H) / (float)H;
     const float d = sqrtf(nx * nx + ny * ny);
     const float t = clampf((d - p.vignetteRadius) / p.vignetteSmoothness, 0.0f, 1.0f);
     const float sm = t * t * (3.0f - 2.0f * t);
     float v = 1.0f - sm;
     v = 1.0f - p.vignetteStrength * (1.0f - v);
-    v = clampf(v, 0.0f, 1.0f);
-    c *= v;
-    st3(a.work, a.W, x, y, c, 1.0f);
+    return clampf(v, 0.0f, 1.0f);
 }
 
 VX_D V3 aces(V3 x) {  // FilmicToneMapping.h:12-20
@@ -203,13 +279,28 @@ VX_D V3 uncharted2(V3 x) {  // :23-32
 }
 VX_D float srgb(float c) { return (c <= 0.0031308f) ? 12.92f * c : 1.055f * powf(c, 1.0f / 2.4f) - 0.055f; }
 
-// FilmicToneMapping (:58-117) + DrawCrosshair (PostProcessor.cu:14-46) +
-// CopyToInteropBuffer (:48-63)
-__global__ __launch_bounds__(256) void k_tonemap(PostArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+// Pass 3: vertical blur + BloomCompositeKernel (:128-148), LensFlareKernel (its sun-visibility
+// test, IsSunVisible :208-221 -- depth at the sun pixel >= RayMaxLowerBound -- read on the device),
+// VignetteKernel, FilmicToneMapping (:58-117), DrawCrosshair (PostProcessor.cu:14-46),
+// CopyToInteropBuffer (:48-63).  64-wide rows: the vertical taps are coalesced row reads.
+__global__ __launch_bounds__(256) void k_compose(PostArgs a, int flare) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= a.W || y >= a.H) return;
     const PostParamsDev &p = a.p;
-    V3 c = ld3(a.work, a.W, x, y);
+    V3 c = ld3(a.input, a.W, x, y);
+    if (p.enableBloom) {
+        const int half = blur_half(p);
+        V3 r(0.0f);
+        float tw = 0.0f;
+        for (int i = -half; i <= half; i++) {
+            r += ld3(a.bloomB, a.W, x, clampi(y + i, 0, a.H - 1)) * 1.0f;
+            tw += 1.0f;
+        }
+        if (tw > 0.0f) r /= tw;
+        c = c + r * p.bloomIntensity;
+    }
+    if (flare && a.depth[(size_t)a.sunPy * a.W + a.sunPx] >= 1.0e26f) c = c + lens_flare(a, x, y);
+    if (p.enableVignette) c *= vignette(p, a.W, a.H, x, y);
     c *= p.enableAutoExposure ? a.state[1] : p.manualExposure;
     V3 t;
     if (p.curve == 1) {
@@ -223,7 +314,8 @@ __global__ __launch_bounds__(256) void k_tonemap(PostArgs a) {
         t = aces(c);
     }
     t = clamp3(t, 0.0f, 1.0f);
-    t = V3(powf(t.x, p.contrast), powf(t.y, p.contrast), powf(t.z, p.contrast));
+    if (p.contrast != 1.0f)  // pow(x, 1) = x exactly
+        t = V3(powf(t.x, p.contrast), powf(t.y, p.contrast), powf(t.z, p.contrast));
     const float l = lum_ref(t);
     t = V3(l) + p.saturation * (t - V3(l));
     t = clamp3(t * p.gain + V3(p.lift), 0.0f, 1.0f);
@@ -235,27 +327,24 @@ __global__ __launch_bounds__(256) void k_tonemap(PostArgs a) {
     a.frame[(size_t)y * a.W + x] = make_float4(t.x, t.y, t.z, 0.0f);
 }
 
-inline dim3 grid(const PostArgs &a) { return dim3((a.W + 15) / 16, (a.H + 15) / 16); }
-
 }  // namespace
 
+// HBM traffic per pixel with bloom on: pass 1 reads 16 B (+ apron) and writes 16 B of bloomB,
+// pass 3 reads 16 B input + 16 B bloomB (+ taps from cache) and writes 16 B: 80 B per pixel.
 hipError_t launch_postprocess(const PostArgs &a, hipStream_t st) {
-    const dim3 g = grid(a), b(256);
-    hipMemcpyAsync(a.work, a.input, (size_t)a.W * a.H * sizeof(float4), hipMemcpyDeviceToDevice, st);
-    if (a.p.enableAutoExposure) {
-        hipMemsetAsync(a.hist, 0, kBins * sizeof(float), st);
-        hipLaunchKernelGGL(k_histogram, g, b, 0, st, a);
-        hipLaunchKernelGGL(k_exposure, dim3(1), dim3(1), 0, st, a);
+    const bool lds = blur_half(a.p) <= kHalo;
+    const int hist = a.p.enableAutoExposure ? 1 : 0, bloomLds = a.p.enableBloom && lds ? 1 : 0;
+    if (hist || bloomLds)
+        hipLaunchKernelGGL(k_lum_bloom, dim3((a.W + TX - 1) / TX, (a.H + TY - 1) / TY), dim3(256), 0, st, a, hist,
+                           bloomLds);
+    if (a.p.enableBloom && !lds) {
+        const dim3 g((a.W + 15) / 16, (a.H + 15) / 16);
+        hipLaunchKernelGGL(k_bloom_extract, g, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_bloom_blur_h, g, dim3(256), 0, st, a);
     }
-    if (a.p.enableBloom) {
-        hipLaunchKernelGGL(k_bloom_extract, g, b, 0, st, a);
-        hipLaunchKernelGGL(k_bloom_blur, g, b, 0, st, a, a.bloomA, a.bloomB, 1, 0);
-        hipLaunchKernelGGL(k_bloom_blur, g, b, 0, st, a, a.bloomB, a.bloomA, 0, 1);
-        hipLaunchKernelGGL(k_bloom_composite, g, b, 0, st, a);
-    }
-    if (a.p.enableLensFlare && a.sunOnScreen) hipLaunchKernelGGL(k_lens_flare, g, b, 0, st, a);
-    if (a.p.enableVignette) hipLaunchKernelGGL(k_vignette, g, b, 0, st, a);
-    hipLaunchKernelGGL(k_tonemap, g, b, 0, st, a);
+    if (hist) hipLaunchKernelGGL(k_exposure, dim3(1), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_compose, dim3((a.W + 63) / 64, (a.H + 3) / 4), dim3(256), 0, st, a,
+                       a.p.enableLensFlare && a.sunOnScreen ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -206,10 +206,10 @@ struct PostArgs {
     int W, H;
     PostParamsDev p;
     const float4 *input;            // the denoiser output (IlluminationOutputBuffer)
-    float4 *work, *bloomA, *bloomB; // working plane, bloom extract / temp planes
+    float4 *bloomA, *bloomB;        // bloom extract (wide-radius path) / horizontally blurred bloom
     float4 *frame;                  // result: Float4(sRGB colour, 0) (CopyToInteropBuffer)
     const float *depth;             // lens-flare sun visibility
-    float *hist;                    // 256 luminance bins
+    unsigned *hist;                 // 256 luminance bins (integer counts, cleared by k_exposure)
     float *state;                   // [0] current average luminance, [1] exposure of this frame
     float dtMs;                     // frame time for the exposure adaptation (Timer::getDeltaTime, ms)
     int sunOnScreen, sunPx, sunPy;  // ProjectSunToScreen (PostProcessingPipeline.cu:187-206)

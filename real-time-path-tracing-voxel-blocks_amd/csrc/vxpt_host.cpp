@@ -189,8 +189,9 @@ struct vxpt_ctx {
     // post-processing (PostProcessor / PostProcessingPipeline): working, bloom and frame
     // planes, luminance histogram, device exposure state
     vxpt_post_params yamlPost{};
-    float4 *postWork = nullptr, *bloomA = nullptr, *bloomB = nullptr, *frame = nullptr;
-    float *postHist = nullptr, *postState = nullptr;
+    float4 *bloomA = nullptr, *bloomB = nullptr, *frame = nullptr;
+    unsigned *postHist = nullptr;
+    float *postState = nullptr;
     float sunLuminance = 1.0f;     // SkyModel::getAccumulatedSunLuminance: the sun map's total pdf
 
     vxpt_denoise_params yamlDenoise{};
@@ -604,7 +605,7 @@ hipError_t world_pos_band(const DenoiseArgs &a, hipStream_t st) {
 }
 
 int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) {
-    if (!p) p = &default_denoise();
+    if (!p) p = &c->yamlDenoise;
     const int used = it > 0 ? it - 1 : 0;
     DenoiseArgs a{};
     fill_denoise(c, p, a, used & 1);
@@ -888,6 +889,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (cfg->diffuse_bounce_limit > 0) c->diffuseBounce = cfg->diffuse_bounce_limit;
     c->dataDir = cfg->data_dir ? cfg->data_dir : "data";
     c->yamlPost = default_post();
+    c->yamlDenoise = default_denoise();
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1261,7 +1263,7 @@ int vxpt_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNum, in
 
 int vxpt_denoise_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int arg2) {
     if (!c) return VXPT_ERR_ARG;
-    if (!p) p = &default_denoise();
+    if (!p) p = &c->yamlDenoise;
     HIPCHK(c, hipSetDevice(c->dev));
     if (int r = run_pass(c, p, pass, arg, arg2)) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1273,7 +1275,7 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
     HIPCHK(c, hipSetDevice(c->dev));
     if (c->comm) {
         std::vector<vxpt_ctx *> cs{c};
-        return band_frame(cs, p ? p : &default_denoise(), frameNum, spp);
+        return band_frame(cs, p ? p : &cs[0]->yamlDenoise, frameNum, spp);
     }
     const int it0 = frameNum * spp;
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
@@ -1360,6 +1362,12 @@ int vxpt_get_sun_projection(vxpt_ctx *c, float out6[6]) {
     return VXPT_OK;
 }
 
+int vxpt_get_denoise_params(vxpt_ctx *c, vxpt_denoise_params *out) {
+    if (!c || !out) return VXPT_ERR_ARG;
+    *out = c->yamlDenoise;
+    return VXPT_OK;
+}
+
 int vxpt_get_post_params(vxpt_ctx *c, vxpt_post_params *out) {
     if (!c || !out) return VXPT_ERR_ARG;
     *out = c->yamlPost;
@@ -1372,11 +1380,12 @@ int vxpt_postprocess(vxpt_ctx *c, const vxpt_post_params *pp, float dtMs) {
     HIPCHK(c, hipSetDevice(c->dev));
     const size_t n = (size_t)c->W * c->H;
     if (!c->frame) {
-        if (dalloc(c, c->postWork, n) || dalloc(c, c->bloomA, n) || dalloc(c, c->bloomB, n) ||
+        if (dalloc(c, c->bloomA, n) || dalloc(c, c->bloomB, n) ||
             dalloc(c, c->frame, n) || dalloc(c, c->postHist, 256) || dalloc(c, c->postState, 4))
             return VXPT_ERR_HIP;
         const float init[4] = {0.18f, 1.0f, 0.0f, 0.0f};  // m_currentAvgLuminance (PostProcessingPipeline.cu:433)
         HIPCHK(c, hipMemcpyAsync(c->postState, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->postHist, 0, 256 * sizeof(unsigned), c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     PostArgs a{};
@@ -1390,14 +1399,13 @@ int vxpt_postprocess(vxpt_ctx *c, const vxpt_post_params *pp, float dtMs) {
            pp->lens_flare_ghost_count, pp->lens_flare_halo_radius, pp->lens_flare_sun_size,
            pp->lens_flare_distortion, pp->draw_crosshair};
     a.input = c->output;
-    a.work = c->postWork; a.bloomA = c->bloomA; a.bloomB = c->bloomB; a.frame = c->frame;
+    a.bloomA = c->bloomA; a.bloomB = c->bloomB; a.frame = c->frame;
     a.depth = c->gb[c->last].depth;
     a.hist = c->postHist;
     a.state = c->postState;
     a.dtMs = dtMs;
     sun_projection(c, a.sunOnScreen, a.sunPx, a.sunPy, a.sunU, a.sunV, a.sunLuminance);
     HIPCHK(c, launch_postprocess(a, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     return VXPT_OK;
 }
 
@@ -1452,7 +1460,7 @@ int vxpt_render_frame_linked(vxpt_ctx **cs, int n, const vxpt_denoise_params *p,
     for (int k = 0; k < n; ++k)
         if (!cs[k] || cs[k]->rank != k || cs[k]->nranks != n) return VXPT_ERR_STATE;
     HIPCHK(cs[0], hipSetDevice(cs[0]->dev));
-    return band_frame(v, p ? p : &default_denoise(), frameNum, spp);
+    return band_frame(v, p ? p : &v[0]->yamlDenoise, frameNum, spp);
 }
 
 

@@ -1,0 +1,329 @@
+// vxpt_offline -- the offline renderer executable over the vxpt C ABI.
+//
+// Mirrors the reference's mainOffline.cpp (flags :57-133, set-up :140-251, frame loop :273-408,
+// canonical gate :423-498) and OfflineBackend::renderFrame / writeAllBatchedFrames
+// (OfflineBackend.cpp:46-184).  Host code only: every GPU operation goes through include/vxpt.h.
+//
+// Same flags and outputs as the reference: saved frames are the 1-indexed {1, 4, 16, 64} written
+// as <prefix>_%04d.png with the 0-indexed frame number, the canonical gate compares frame
+// totalFrames-1 and writes <prefix>_diff.png.  Additions: --spp (samples per pixel per frame,
+// the reference traces 1), --chunks X Y Z (world size, default the reference's 2 1 2), --device,
+// --data (the data directory), --perf-report (the reference writes ../../data/perf/...).
+// The scripted voxel-edit sequences (--test-sequence, --test-remove20, --test-remove-circle) need
+// the voxel edit path, which is not built yet: they are rejected with a message.
+#include "../../include/vxpt.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <future>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+#include <iomanip>
+
+namespace {
+
+struct Options {
+    int width = 3840, height = 2160;
+    std::string outputPrefix = "offline_render";
+    std::string sceneFile = "data/scene/scene_export.yaml";
+    bool testCanonical = false, updateCanonical = false;
+    std::string canonicalImagePath = "../../data/canonical/canonical_render.png";
+    std::string runComment = "default run";
+    int totalFrames = 64;
+    std::vector<int> savedFrames = {1, 4, 16, 64};
+    int spp = 1;
+    int chunks[3] = {2, 1, 2};
+    int device = 0;
+    std::string dataDir = "data";
+    std::string perfReport;
+};
+
+void usage(const char *argv0) {
+    std::cout << "Offline Voxel Path Tracer (MI355X)\n"
+              << "Usage: " << argv0 << " [options]\n"
+              << "Options:\n"
+              << "  --width <int>          Output width (default: 3840)\n"
+              << "  --height <int>         Output height (default: 2160)\n"
+              << "  --output <string>      Output filename prefix (default: offline_render)\n"
+              << "  --scene <file>         Scene configuration YAML file (camera)\n"
+              << "  --test-canonical       Compare output with canonical image\n"
+              << "  --update-canonical     Update the canonical reference image\n"
+              << "  --canonical-image <p>  Path to canonical image (default: ../../data/canonical/canonical_render.png)\n"
+              << "  --comment <text>       Comment for performance report (default: default run)\n"
+              << "  --frames <int>         Number of frames to render (default: 64, use 1 for single frame)\n"
+              << "  --spp <int>            Samples per pixel per frame (default: 1)\n"
+              << "  --chunks <x> <y> <z>   World size in 32^3 chunks (default: 2 1 2)\n"
+              << "  --device <int>         HIP device (default: 0)\n"
+              << "  --data <dir>           Data directory: settings/, assets/, tables/ (default: data)\n"
+              << "  --perf-report <file>   Performance report path (default: <output>_performance_report.txt)\n"
+              << "  --help, -h             Show this help message\n";
+}
+
+// returns 1 = run, 0 = exit 0 (help), -1 = exit 2 (bad args)
+int parse(int argc, char **argv, Options &o) {
+    for (int i = 1; i < argc; i++) {
+        const std::string a = argv[i];
+        auto next = [&](const char *what) -> const char * {
+            if (i + 1 >= argc) {
+                std::cerr << "missing value for " << what << "\n";
+                return nullptr;
+            }
+            return argv[++i];
+        };
+        const char *v = nullptr;
+        if (a == "--width") { if (!(v = next("--width"))) return -1; o.width = std::atoi(v); }
+        else if (a == "--height") { if (!(v = next("--height"))) return -1; o.height = std::atoi(v); }
+        else if (a == "--output") { if (!(v = next("--output"))) return -1; o.outputPrefix = v; }
+        else if (a == "--scene") { if (!(v = next("--scene"))) return -1; o.sceneFile = v; }
+        else if (a == "--test-canonical" || a == "--test") o.testCanonical = true;
+        else if (a == "--update-canonical") o.updateCanonical = true;
+        else if (a == "--canonical-image") { if (!(v = next("--canonical-image"))) return -1; o.canonicalImagePath = v; }
+        else if (a == "--comment") { if (!(v = next("--comment"))) return -1; o.runComment = v; }
+        else if (a == "--frames") {
+            if (!(v = next("--frames"))) return -1;
+            o.totalFrames = std::atoi(v);
+            if (o.totalFrames == 1) o.savedFrames = {1};  // mainOffline.cpp:108-111
+        }
+        else if (a == "--spp") { if (!(v = next("--spp"))) return -1; o.spp = std::atoi(v); }
+        else if (a == "--chunks") {
+            for (int k = 0; k < 3; k++) {
+                if (!(v = next("--chunks"))) return -1;
+                o.chunks[k] = std::atoi(v);
+            }
+        }
+        else if (a == "--device") { if (!(v = next("--device"))) return -1; o.device = std::atoi(v); }
+        else if (a == "--data") { if (!(v = next("--data"))) return -1; o.dataDir = v; }
+        else if (a == "--perf-report") { if (!(v = next("--perf-report"))) return -1; o.perfReport = v; }
+        else if (a == "--test-sequence" || a == "--test-remove20" || a == "--test-remove-circle") {
+            std::cerr << a << ": scripted voxel edits are not supported by this build\n";
+            return -1;
+        }
+        else if (a == "--help" || a == "-h") { usage(argv[0]); return 0; }
+        else { std::cerr << "unknown option " << a << "\n"; return -1; }
+    }
+    if (o.width <= 0 || o.height <= 0 || o.width % 8 || o.height % 8) {
+        std::cerr << "width and height must be positive multiples of 8\n";
+        return -1;
+    }
+    if (o.totalFrames <= 0 || o.spp <= 0 || o.chunks[0] <= 0 || o.chunks[1] <= 0 || o.chunks[2] <= 0) {
+        std::cerr << "frames, spp and chunks must be positive\n";
+        return -1;
+    }
+    if (o.perfReport.empty()) o.perfReport = o.outputPrefix + "_performance_report.txt";
+    return 1;
+}
+
+std::string frame_path(const std::string &prefix, int frame0) {
+    std::ostringstream s;
+    s << prefix << "_" << std::setfill('0') << std::setw(4) << frame0 << ".png";
+    return s.str();
+}
+
+struct BatchedFrame {
+    std::vector<float> rgba;
+    std::string path;
+};
+
+struct FrameRecord {  // PerformanceTracker's per-frame row, from the library's HIP-event timings
+    int frame;
+    std::string comment;
+    vxpt_timing t;
+    double postMs, wallMs;
+    float dtMs;
+};
+
+void print_diff(const vxpt_image_diff_result &r) {  // ImageDiffResult::print (ImageDiff.cpp)
+    std::cout << "=== Image Comparison Results ===\n"
+              << "Total pixels: " << r.total_pixels << "\n"
+              << "Different pixels: " << r.different_pixels << " (" << std::fixed << std::setprecision(2)
+              << r.pixel_difference_ratio * 100.0f << "%)\n"
+              << std::setprecision(4) << "RMSE: " << r.rmse << "\n"
+              << "SSIM: " << r.ssim << "\n"
+              << "Assessment: "
+              << (r.is_identical ? "IDENTICAL" : r.is_very_close ? "VERY CLOSE" : r.is_close ? "CLOSE" : "DIFFERENT")
+              << "\n";
+    std::cout.unsetf(std::ios::floatfield);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    Options o;
+    const int pr = parse(argc, argv, o);
+    if (pr <= 0) return pr == 0 ? 0 : 2;
+
+    std::cout << "=== Offline Voxel Path Tracer ===\n"
+              << "Resolution: " << o.width << "x" << o.height << "\n"
+              << "Frames to render: " << o.totalFrames << " at " << o.spp << " spp\n"
+              << "Output prefix: " << o.outputPrefix << std::endl;
+
+    vxpt_config cfg{};
+    cfg.width = o.width;
+    cfg.height = o.height;
+    cfg.device = o.device;
+    cfg.total_bounce_limit = 3;    // RayGen.cu:146
+    cfg.diffuse_bounce_limit = 1;  // RayGen.cu:147
+    cfg.data_dir = o.dataDir.c_str();
+    vxpt_ctx *ctx = nullptr;
+    if (vxpt_create(&cfg, &ctx) != VXPT_OK) {
+        std::cerr << "Error: vxpt_create failed: " << vxpt_last_error(ctx) << std::endl;
+        vxpt_destroy(ctx);
+        return 1;
+    }
+    auto last = std::chrono::steady_clock::now();  // OfflineBackend::init starts m_timer (OfflineBackend.cpp:43)
+    auto fail = [&](const char *what) {
+        std::cerr << "Error: " << what << ": " << vxpt_last_error(ctx) << std::endl;
+        vxpt_destroy(ctx);
+        return 1;
+    };
+
+    // mainOffline.cpp:140-198: settings, assets, the voxel world
+    if (vxpt_load_settings(ctx) != VXPT_OK) return fail("loading settings");
+    if (vxpt_generate_terrain(ctx, o.chunks[0], o.chunks[1], o.chunks[2], 32.0f, 32.0f * o.chunks[0], 0) != VXPT_OK)
+        return fail("generating terrain");
+
+    // :200-251: camera from the scene file (defaults when it is absent), history camera = camera
+    vxpt_camera cam{};
+    const bool haveScene = !o.sceneFile.empty() && std::filesystem::exists(o.sceneFile);
+    if (!haveScene && !o.sceneFile.empty())
+        std::cout << "Scene file not found: " << o.sceneFile << ", using defaults" << std::endl;
+    if (vxpt_load_scene_camera(ctx, haveScene ? o.sceneFile.c_str() : nullptr, &cam) != VXPT_OK)
+        return fail("loading the scene camera");
+    if (vxpt_set_camera(ctx, &cam, &cam) != VXPT_OK) return fail("setting the camera");
+    if (vxpt_set_sky(ctx, 0.25f, 45.0f, 0.0f, 1.0f) != VXPT_OK) return fail("building the sky");
+    std::cout << "Camera setup - Position: (" << cam.pos[0] << ", " << cam.pos[1] << ", " << cam.pos[2] << ")\n"
+              << "Camera setup - Direction: (" << cam.dir[0] << ", " << cam.dir[1] << ", " << cam.dir[2] << ")\n"
+              << "Camera setup - FOV: " << cam.fov_deg << " degrees\n"
+              << "Camera movement: DISABLED (static camera)\nStarting rendering..." << std::endl;
+
+    vxpt_denoise_params dp{};
+    vxpt_post_params pp{};
+    if (vxpt_get_post_params(ctx, &pp) != VXPT_OK) return fail("reading post-process settings");
+    if (vxpt_get_denoise_params(ctx, &dp) != VXPT_OK) return fail("reading denoise settings");
+
+    std::vector<BatchedFrame> batch;
+    std::vector<FrameRecord> perf;
+    const size_t frameBytes = (size_t)o.width * o.height * 4 * sizeof(float);
+
+    for (int frame = 0; frame < o.totalFrames; frame++) {  // mainOffline.cpp:273-408
+        const int frameNumber = frame + 1;
+        const auto t0 = std::chrono::steady_clock::now();
+        const float dtMs = std::chrono::duration<float, std::milli>(t0 - last).count();  // Timer::getDeltaTime
+        last = t0;
+        const bool shouldSave =
+            std::find(o.savedFrames.begin(), o.savedFrames.end(), frameNumber) != o.savedFrames.end();
+
+        if (vxpt_render_frame(ctx, &dp, frame, o.spp) != VXPT_OK) return fail("rendering");
+        const auto tp = std::chrono::steady_clock::now();
+        if (vxpt_postprocess(ctx, &pp, dtMs) != VXPT_OK) return fail("post-processing");
+        if (shouldSave) {  // storeFrameInBatch (OfflineBackend.cpp:117-131)
+            BatchedFrame b;
+            b.rgba.resize((size_t)o.width * o.height * 4);
+            if (vxpt_readback(ctx, VXPT_BUF_FRAME, b.rgba.data(), frameBytes) != VXPT_OK)
+                return fail("reading the frame");
+            b.path = frame_path(o.outputPrefix, frame);
+            batch.push_back(std::move(b));
+        }
+        if (vxpt_sync(ctx) != VXPT_OK) return fail("synchronising");
+        const auto t1 = std::chrono::steady_clock::now();
+        FrameRecord rec{frameNumber,
+                        (shouldSave ? "Saved frame " : "Convergence frame ") + std::to_string(frameNumber) + "/" +
+                            std::to_string(o.totalFrames),
+                        {}, std::chrono::duration<double, std::milli>(t1 - tp).count(),
+                        std::chrono::duration<double, std::milli>(t1 - t0).count(), dtMs};
+        vxpt_timings(ctx, &rec.t);
+        perf.push_back(rec);
+        if (shouldSave || frameNumber % 16 == 0)
+            std::cout << "Frame " << frameNumber << "/" << o.totalFrames << " completed"
+                      << (shouldSave ? " (SAVED)" : "") << std::endl;
+    }
+
+    // writeAllBatchedFrames (OfflineBackend.cpp:133-184): PNG encoding in parallel on host threads
+    std::cout << "\n=== Rendering Complete - Writing all frames to disk ===" << std::endl;
+    std::vector<std::future<int>> writers;
+    for (const auto &b : batch)
+        writers.push_back(std::async(std::launch::async, [&o, &b] {
+            return vxpt_write_png_rgba32f(b.path.c_str(), o.width, o.height, b.rgba.data());
+        }));
+    int writeErrors = 0;
+    for (auto &w : writers) writeErrors += w.get() != VXPT_OK;
+    if (writeErrors) {
+        std::cerr << "Error: " << writeErrors << " frame(s) failed to write" << std::endl;
+        vxpt_destroy(ctx);
+        return 1;
+    }
+    std::cout << "Output files saved with prefix: " << o.outputPrefix << std::endl;
+
+    {  // PerformanceTracker::saveReport
+        std::ofstream rep(o.perfReport);
+        rep << "# " << o.runComment << "\n# " << o.width << "x" << o.height << ", " << o.spp << " spp\n"
+            << "frame,trace_ms,denoise_ms,sky_ms,frame_ms,post_ms,wall_ms,dt_ms,comment\n";
+        double sumTrace = 0, sumDen = 0, sumWall = 0;
+        for (const auto &r : perf) {
+            rep << r.frame << "," << r.t.trace_ms << "," << r.t.denoise_ms << "," << r.t.sky_ms << ","
+                << r.t.frame_ms << "," << r.postMs << "," << r.wallMs << "," << std::setprecision(9) << r.dtMs
+                << std::setprecision(6) << "," << r.comment << "\n";
+            sumTrace += r.t.trace_ms;
+            sumDen += r.t.denoise_ms;
+            sumWall += r.wallMs;
+        }
+        const double n = (double)perf.size();
+        std::cout << "\n=== Performance Report ===\n"
+                  << "avg path tracing " << sumTrace / n << " ms, denoiser " << sumDen / n << " ms, wall "
+                  << sumWall / n << " ms per frame\nPerformance data saved to: " << o.perfReport << std::endl;
+    }
+
+    int rc = 0;
+    if (o.testCanonical || o.updateCanonical) {  // mainOffline.cpp:423-498
+        const std::string testImagePath = frame_path(o.outputPrefix, o.totalFrames - 1);
+        if (o.updateCanonical) {
+            std::cout << "\n=== Updating Canonical Image ===" << std::endl;
+            std::error_code ec;
+            if (std::filesystem::copy_file(testImagePath, o.canonicalImagePath,
+                                           std::filesystem::copy_options::overwrite_existing, ec))
+                std::cout << "Canonical image updated: " << o.canonicalImagePath << std::endl;
+            else
+                std::cerr << "Failed to update canonical image: " << ec.message() << std::endl;
+        }
+        if (o.testCanonical) {
+            std::cout << "\n=== Canonical Image Testing ===" << std::endl;
+            if (!std::filesystem::exists(o.canonicalImagePath)) {
+                std::cout << "Warning: Canonical image not found at " << o.canonicalImagePath << "\n"
+                          << "Use --update-canonical to create it from current render" << std::endl;
+            } else if (!std::filesystem::exists(testImagePath)) {
+                std::cerr << "Error: Test image not found at " << testImagePath << std::endl;
+            } else {
+                std::cout << "Comparing: " << testImagePath << " vs " << o.canonicalImagePath << std::endl;
+                vxpt_image_diff_result r{};
+                if (vxpt_image_diff(testImagePath.c_str(), o.canonicalImagePath.c_str(), &r) != VXPT_OK) {
+                    std::cerr << "Error: image comparison failed" << std::endl;
+                    rc = 1;
+                } else {
+                    print_diff(r);
+                    const std::string diffPath = o.outputPrefix + "_diff.png";
+                    if (vxpt_image_diff_png(testImagePath.c_str(), o.canonicalImagePath.c_str(),
+                                            diffPath.c_str()) == VXPT_OK)
+                        std::cout << "Difference visualization saved to: " << diffPath << std::endl;
+                    else
+                        std::cerr << "Failed to generate difference image" << std::endl;
+                    if (!r.is_identical && !r.is_very_close) {
+                        std::cout << "\nWarning: Significant differences detected from canonical image!\n"
+                                  << "This may indicate a regression or intentional change." << std::endl;
+                        if (!r.is_close) std::cout << "Consider investigating the differences." << std::endl;
+                    } else {
+                        std::cout << "\nImage matches canonical reference within acceptable tolerance." << std::endl;
+                    }
+                }
+            }
+        }
+    }
+    vxpt_destroy(ctx);
+    return rc;
+}

@@ -135,6 +135,7 @@ def load_library(path=LIB_PATH):
         "vxpt_get_post_params": (I, [P, ctypes.POINTER(PostParams)]),
         "vxpt_postprocess": (I, [P, ctypes.POINTER(PostParams), F]),
         "vxpt_get_sun_projection": (I, [P, P]),
+        "vxpt_get_denoise_params": (I, [P, ctypes.POINTER(DenoiseParams)]),
         "vxpt_write_png_rgba32f": (I, [ctypes.c_char_p, I, I, P]),
         "vxpt_read_png": (I, [ctypes.c_char_p, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I), P,
                               ctypes.c_size_t]),
@@ -257,6 +258,12 @@ class Renderer:
                   "vxpt_copy_rows")
 
     # --- post-processing + frame output (PostProcessor::run, OfflineBackend::writeFrameBufferToPNG) ---
+    def denoise_params(self):
+        """The settings file's denoiser parameters (what NULL params mean to the library)."""
+        p = DenoiseParams()
+        self._chk(self.lib.vxpt_get_denoise_params(self.ctx, ctypes.byref(p)), "vxpt_get_denoise_params")
+        return p
+
     def post_params(self):
         p = PostParams()
         self._chk(self.lib.vxpt_get_post_params(self.ctx, ctypes.byref(p)), "vxpt_get_post_params")

@@ -98,9 +98,20 @@ def test_oracle_postprocess_sanity():
     np.testing.assert_allclose(o2[..., :3], srgb, atol=2e-6)
 
 
+VARIANTS = {
+    "defaults": {},
+    # the wide-radius bloom path (radius beyond the LDS apron) and the Uncharted 2 curve
+    "wide_bloom_uncharted2": dict(bloom_radius=10.0, tone_mapping_curve=1, bloom_threshold=0.05),
+    # manual exposure, no bloom, Reinhard, vignette off
+    "manual_reinhard": dict(enable_auto_exposure=0, enable_bloom=0, tone_mapping_curve=2, enable_vignette=0,
+                            manual_exposure=2.0),
+}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("look_at_sun", [False, True])
-def test_gpu_postprocess_matches_oracle(look_at_sun, tmp_path):
+@pytest.mark.parametrize("look_at_sun,variant", [(False, "defaults"), (True, "defaults"),
+                                                 (False, "wide_bloom_uncharted2"), (True, "manual_reinhard")])
+def test_gpu_postprocess_matches_oracle(look_at_sun, variant, tmp_path):
     w, h = 128, 96
     r = vxpt.Renderer(w, h)
     r.load_settings()
@@ -112,6 +123,8 @@ def test_gpu_postprocess_matches_oracle(look_at_sun, tmp_path):
     cam = (C1_CAMERA[0], d, C1_CAMERA[2])
     r.set_camera(*cam[:2], fov=cam[2], prev=cam)
     p = r.post_params()
+    for k, v in VARIANTS[variant].items():
+        setattr(p, k, v)
     st = np.array([0.18, 1.0], np.float32)
     for f in range(2):
         r.render_frame(f, 1, vxpt.DenoiseParams.defaults())
