@@ -48,7 +48,12 @@ enum vxpt_buffer {
     VXPT_BUF_RES_EVEN = 35,  /* reservoirs of even iterationIndex (W*H*20 B)   */
     VXPT_BUF_RES_ODD = 36,   /* reservoirs of odd iterationIndex               */
     VXPT_BUF_WPOS = 37,      /* per-pixel hit world position (denoiser)        */
-    VXPT_BUF_FRAME = 38      /* post-processed frame, Float4(sRGB, 0) (OfflineBackend m_frameBuffer) */
+    VXPT_BUF_FRAME = 38,     /* post-processed frame, Float4(sRGB, 0) (OfflineBackend m_frameBuffer) */
+    /* traversal structures (read-only parity hooks for the incremental edit path) */
+    VXPT_BUF_OCTANT_TABLES = 39, /* 8 x nBricks u8: empty-cube edge per brick and ray octant  */
+    VXPT_BUF_CELL_MASKS = 40,    /* nBricks u64: cube-cell bits of each 4^3 brick             */
+    VXPT_BUF_BRICK_IDS = 41,     /* nBricks x 64 u8: ids in brick-major order                 */
+    VXPT_BUF_MACRO_MASKS = 42    /* nBricks/64 u64: occupied-brick bits of each 16^3 cell      */
 };
 
 typedef struct vxpt_config {
@@ -148,6 +153,26 @@ int vxpt_set_sky(vxpt_ctx *ctx, float time_of_day, float sun_axis_angle_deg, flo
 int vxpt_set_camera(vxpt_ctx *ctx, const vxpt_camera *cur, const vxpt_camera *prev);
 /* Camera matrices as the kernels see them: pos3 dir3 uvToWorld9 worldToUv9 res2 invRes2 tanHalfFov2 yaw pitch */
 int vxpt_get_camera(vxpt_ctx *ctx, int which, float out32[32]);
+/* Camera::update from yaw/pitch (Camera.h:44-100) after historyCamera = camera (mainOffline.cpp:278-307,
+ * the circular-removal test's orientation changes); out32[30..31] of vxpt_get_camera are yaw, pitch */
+int vxpt_set_camera_angles(vxpt_ctx *ctx, const float pos[3], float yaw, float pitch, float fov_deg);
+
+/* ---- voxel edits (VoxelEngine::update click path, VoxelEngine.cu:855-975, 1040-1346) ---- */
+/* performRayTraversal (:1040-1166) of the current camera ray on the world.  out: hit, hit x, y, z,
+ * hit id, has space to place, place x, y, z, cells walked */
+int vxpt_pick_block(vxpt_ctx *ctx, int32_t out[10]);
+/* setVoxelAtGlobal + the geometry update (:265-276; VoxelSceneGen.cu:643-786): one cell's id, with
+ * the traversal structures updated incrementally; the next trace pass's ReSTIR temporal visibility
+ * sees no previous scene (OptixRenderer.cpp:916-919) */
+int vxpt_set_block(vxpt_ctx *ctx, int x, int y, int z, int block_id);
+/* the click (:906-975): block_id 0 deletes the picked block, another id is placed in front of it;
+ * out (may be NULL) = the pick */
+int vxpt_click_block(vxpt_ctx *ctx, int block_id, int32_t out[10]);
+/* WorldSceneManager::SaveScene / LoadScene (WorldSceneManager.cpp:240-458): chunk files named by
+ * the FNV-1a 64 hash of their bytes + a scene yaml with the camera, chunk_config and chunk records;
+ * load fills cam_out (may be NULL) and rebuilds the world */
+int vxpt_save_world(vxpt_ctx *ctx, const char *scene_yaml, const char *chunk_dir);
+int vxpt_load_world(vxpt_ctx *ctx, const char *scene_yaml, const char *chunk_dir, vxpt_camera *cam_out);
 
 /* OptixRenderer::render (OptixRenderer.cpp:411-485): one 1-spp trace pass with the given
  * iterationIndex.  flags: VXPT_TRACE_PRIMARY_ONLY = C2 bring-up mode (DDA + sky + G-buffer). */

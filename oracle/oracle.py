@@ -50,6 +50,7 @@ def lib():
             "orc_set_bounces": (None, [P, I, I]),
             "orc_terrain": (I, [P, I, I, I, F, F, I, I]),
             "orc_set_voxels": (I, [P, P, I, I, I]),
+            "orc_set_prev_scene_empty": (None, [P, I]),
             "orc_get_voxels": (I, [P, P]),
             "orc_set_material": (None, [P, I, F, F, F, F, I, F, I]),
             "orc_set_sky": (I, [P, F, F, F, F]),
@@ -159,6 +160,10 @@ class Oracle:
 
     def trace(self, it, y0=0, y1=None, primary_only=False):
         self.L.orc_trace(self.h, it, y0, self.H if y1 is None else y1, int(primary_only))
+
+    def set_prev_scene_empty(self, on):
+        """The next trace's ReSTIR temporal visibility sees no previous scene (after a voxel edit)."""
+        self.L.orc_set_prev_scene_empty(self.h, int(on))
 
     def post_trace(self):
         self.L.orc_post_trace(self.h)

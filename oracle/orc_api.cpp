@@ -157,6 +157,7 @@ void orc_trace(void *p, int it, int y0, int y1, int primaryOnly) {
     trace_frame(c->s, c->f, it, y0, y1, primaryOnly != 0);
 }
 void orc_post_trace(void *p) { post_trace_copies(static_cast<Ctx *>(p)->f); }
+void orc_set_prev_scene_empty(void *p, int on) { static_cast<Ctx *>(p)->s.prevSceneEmpty = on != 0; }
 // rows [y0, y1) the denoiser passes compute (multi-GPU band schedule; 0,0 = whole frame)
 void orc_set_band(void *p, int y0, int y1) {
     Frame &f = static_cast<Ctx *>(p)->f;

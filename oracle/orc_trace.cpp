@@ -655,7 +655,7 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
                 LightSample sel;
                 light_from_reservoir(s, sel, rr);
                 float ps = target_pdf(sel, ts);
-                if (ps > 0 && !(i == 0 && i == selLoop)) {
+                if (ps > 0 && !(i == 0 && i == selLoop) && !s.prevSceneEmpty) {
                     const float extra = 0.01f + 0.01f * ts.depth;
                     F3 sd = lightSample.position;
                     if (dda_occluded(s.world, ts.pos, sd, extra, kRayMax)) ps = 0.0f;

@@ -56,6 +56,9 @@ struct Scene {
     Material mats[13];   // index = block id (1..12); 0 unused
     Camera cam, prevCam;
     int totalBounceLimit = 3, diffuseBounceLimit = 1;  // RayGen.cu:146-147
+    // the pass after a geometry change: prevTopObject = 0 (OptixRenderer.cpp:916-919, 464), so the
+    // ReSTIR temporal visibility rays (closesthit.cu:736-755) traverse no scene and see the light
+    bool prevSceneEmpty = false;
 };
 
 // One 1-spp trace pass (OptixRenderer::render, OptixRenderer.cpp:411-485),

@@ -741,7 +741,8 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             light_from_res(k, sel, rr);
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;
-            if (psv > 0 && !(i == 0 && i == selLoop)) {
+            // prevSceneEmpty: OptiX's null prevTopObject -- the ray misses, the sample is visible
+            if (psv > 0 && !(i == 0 && i == selLoop) && !a.prevSceneEmpty) {
                 qr.mask |= 2u << i;
                 const float tmin = 0.01f + 0.01f * ts.depth;
                 if (i == 0) { qr.o1 = ts.pos; qr.t1 = tmin; }

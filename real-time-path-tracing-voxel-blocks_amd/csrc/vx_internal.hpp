@@ -137,6 +137,7 @@ struct TraceArgs {
     int tilesX, nSlots;         // 8x8 tiles across the frame width; slots in the band
     int numCU;                  // compute units of the device (traversal grid sizing)
     int iterCap, iterCap2;      // outer DDA iterations before a ray moves to the level-1 / level-2 straggler queue
+    int prevSceneEmpty;         // the pass after a voxel edit: temporal visibility rays see no previous scene
 };
 
 // kernel launchers (defined in the .hip translation units)

@@ -13,6 +13,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <filesystem>
+#include <cfloat>
 #include <fstream>
 #include <map>
 #include <queue>
@@ -147,6 +149,12 @@ struct vxpt_ctx {
     int nBricks = 0;
     uint64_t top = 0;
     int topValid = 0;
+    // host mirrors of the world: picking, incremental edits, chunk files (the device copies are
+    // updated from them in place)
+    std::vector<uint8_t> hIds, hBricks, hOd;
+    std::vector<uint64_t> hMacro, hCell;
+    std::vector<int> topCount;  // cube cells per 64^3 block
+    int prevSceneEmpty = 0;     // the next trace pass's temporal visibility sees no previous scene
     MatDev mats[13] = {};
     CamDev cam{}, prevCam{};
     float camYaw = 0, camPitch = 0;
@@ -257,14 +265,12 @@ V3 yaw_pitch_to_dir(float yaw, float pitch) {
     const float sy = std::sin(yaw), cyw = std::cos(yaw), sp = std::sin(pitch), cp = std::cos(pitch);
     return normalize(V3(sy * cp, sp, cyw * cp));
 }
-CamDev make_camera(int W, int H, const vxpt_camera &in, float *yawOut, float *pitchOut) {
+CamDev make_camera_angles(int W, int H, const float pos[3], float yaw, float pitch, float fovDeg) {
     CamDev c{};
     c.res = V2((float)W, (float)H);
     c.invRes = V2(1.0f / c.res.x, 1.0f / c.res.y);
-    c.pos = V3(in.pos[0], in.pos[1], in.pos[2]);
-    const V3 d = normalized_c(normalize(V3(in.dir[0], in.dir[1], in.dir[2])));
-    const float yaw = std::atan2(d.x, d.z), pitch = std::asin(d.y);
-    const float fovX = in.fov_deg * kPiOver180;
+    c.pos = V3(pos[0], pos[1], pos[2]);
+    const float fovX = fovDeg * kPiOver180;
     const float fovY = fovX * (c.res.y / c.res.x);
     c.tanHalfFov = V2(std::tan(fovX * 0.5f), std::tan(fovY * 0.5f));
     c.dir = yaw_pitch_to_dir(yaw, pitch);
@@ -285,9 +291,15 @@ CamDev make_camera(int W, int H, const vxpt_camera &in, float *yawOut, float *pi
     viewToNdc.m11 = 1.0f / c.tanHalfFov.y;
     viewToNdc.m22 = 1.0f;
     c.worldToUv = m3_mul(m3_mul(ndcToUv, viewToNdc), worldToView);
+    return c;
+}
+// the scene's direction -> yaw/pitch (DirToYawPitch) -> Camera::update
+CamDev make_camera(int W, int H, const vxpt_camera &in, float *yawOut, float *pitchOut) {
+    const V3 d = normalized_c(normalize(V3(in.dir[0], in.dir[1], in.dir[2])));
+    const float yaw = std::atan2(d.x, d.z), pitch = std::asin(d.y);
     if (yawOut) *yawOut = yaw;
     if (pitchOut) *pitchOut = pitch;
-    return c;
+    return make_camera_angles(W, H, in.pos, yaw, pitch, in.fov_deg);
 }
 
 std::vector<AliasBin> build_alias(const std::vector<float> &w, float &sumOut) {
@@ -444,95 +456,145 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_SKY: p = c->sky.p; bytes = 1024 * 512 * 16; return c->sky.p != nullptr;
         case VXPT_BUF_SUN: p = c->sun.p; bytes = 32 * 32 * 16; return c->sun.p != nullptr;
         case VXPT_BUF_VOXELS: p = c->voxels.p; bytes = (size_t)c->cx * c->cy * c->cz * 32768; return c->voxels.p != nullptr;
+        case VXPT_BUF_OCTANT_TABLES: p = c->bdist.p; bytes = (size_t)8 * c->nBricks; return !forWrite && c->bdist.p;
+        case VXPT_BUF_CELL_MASKS: p = c->cellMask.p; bytes = (size_t)c->nBricks * 8; return !forWrite && c->cellMask.p;
+        case VXPT_BUF_BRICK_IDS: p = c->bricks.p; bytes = (size_t)c->nBricks * 64; return !forWrite && c->bricks.p;
+        case VXPT_BUF_MACRO_MASKS: p = c->macro.p; bytes = (size_t)c->nBricks / 64 * 8; return !forWrite && c->macro.p;
         default: return false;
     }
 }
 
-// DDA acceleration layout (WorldDev): macro occupancy words + brick-major ids
+// brick coordinates (4^3 cells) -> cellMask / octant-table index (16^3 macro cell m, brick lb)
+inline size_t brick_lin(const vxpt_ctx *c, int bx, int by, int bz) {
+    const size_t m = (size_t)(bx >> 2) + (size_t)(c->cx * 2) * ((bz >> 2) + (size_t)(c->cz * 2) * (by >> 2));
+    return m * 64 + (size_t)((bx & 3) + 4 * ((bz & 3) + 4 * (by & 3)));
+}
+inline bool is_cube(int id) { return id >= 1 && id <= 12; }
+
+// Per-octant empty-box sizes: for every 4^3 brick and each of the 8 ray octants,
+// S = the edge (in bricks) of the largest brick-aligned cube with that brick at its
+// corner, extending in the octant's directions, that holds no cube cell (0 = the
+// brick is occupied; out-of-world counts as empty; capped at 255).  A ray in that
+// octant can leave the whole cube in one jump.  3-D "largest empty square"
+// recurrence S = 1 + min(S of the 7 forward neighbours), evaluated over the brick box
+// [x0,x1] x [y0,y1] x [z0,z1] against the octant's direction; bricks outside the box
+// keep their values (an edit recomputes only the bricks behind it).
+void octant_fill(vxpt_ctx *c, int oct, int x0, int x1, int y0, int y1, int z0, int z1) {
+    const int BX = c->cx * 8, BY = c->cy * 8, BZ = c->cz * 8;
+    const size_t nB = (size_t)BX * BY * BZ;
+    uint8_t *S = c->hOd.data() + (size_t)oct * nB;
+    const int sx = (oct & 1) ? 1 : -1, sy = (oct & 2) ? 1 : -1, sz = (oct & 4) ? 1 : -1;
+    auto get = [&](int x, int y, int z) -> int {
+        if (x < 0 || y < 0 || z < 0 || x >= BX || y >= BY || z >= BZ) return 255;
+        return S[brick_lin(c, x, y, z)];
+    };
+    for (int iy = 0; iy <= y1 - y0; ++iy)
+        for (int iz = 0; iz <= z1 - z0; ++iz)
+            for (int ix = 0; ix <= x1 - x0; ++ix) {
+                const int x = sx > 0 ? x1 - ix : x0 + ix, y = sy > 0 ? y1 - iy : y0 + iy, z = sz > 0 ? z1 - iz : z0 + iz;
+                const size_t b = brick_lin(c, x, y, z);
+                int v = 0;
+                if (!c->hCell[b]) {
+                    int mn = 255;
+                    for (int k = 1; k < 8; ++k)
+                        mn = std::min(mn, get(x + ((k & 1) ? sx : 0), y + ((k & 2) ? sy : 0), z + ((k & 4) ? sz : 0)));
+                    v = std::min(255, 1 + mn);
+                }
+                S[b] = (uint8_t)v;
+            }
+}
+
+inline int top_block(const vxpt_ctx *c, int x, int y, int z) {
+    const int tx = (c->cx * 32 + 63) / 64, tz = (c->cz * 32 + 63) / 64;
+    return (x >> 6) + tx * ((z >> 6) + tz * (y >> 6));
+}
+void refresh_top(vxpt_ctx *c) {
+    c->top = 0;
+    for (size_t t = 0; t < c->topCount.size() && t < 64; ++t)
+        if (c->topCount[t]) c->top |= 1ull << t;
+}
+
+// DDA acceleration layout (WorldDev) from chunk-major ids, built in the host mirrors and uploaded
 int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     const int wx = c->cx * 32, wy = c->cy * 32, wz = c->cz * 32;
     const int mx = wx / 16, my = wy / 16, mz = wz / 16;
-    std::vector<uint64_t> macro((size_t)mx * my * mz, 0ull);
-    std::vector<uint8_t> bricks((size_t)wx * wy * wz, 0);
-    std::vector<uint64_t> cellMask((size_t)mx * my * mz * 64, 0ull);
+    c->hMacro.assign((size_t)mx * my * mz, 0ull);
+    c->hBricks.assign((size_t)wx * wy * wz, 0);
+    c->hCell.assign((size_t)mx * my * mz * 64, 0ull);
     const int tx = (wx + 63) / 64, ty = (wy + 63) / 64, tz = (wz + 63) / 64;
-    uint64_t top = 0;
+    c->topCount.assign((size_t)tx * ty * tz, 0);
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
                 const int ch = (x >> 5) + c->cx * ((z >> 5) + c->cz * (y >> 5));
                 const uint8_t id = ids[(size_t)ch * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
                 if (!id) continue;
-                const size_t m = (size_t)(x >> 4) + (size_t)mx * ((z >> 4) + (size_t)mz * (y >> 4));
-                const int lb = ((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3));
+                const size_t b = brick_lin(c, x >> 2, y >> 2, z >> 2);
                 const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
-                bricks[(m * 64 + lb) * 64 + lc] = id;
+                c->hBricks[b * 64 + lc] = id;
                 // only cube ids (1..12) make a brick visible to the DDA; other ids are empty for it
-                if (id >= 1 && id <= 12) {
-                    macro[m] |= 1ull << lb;
-                    cellMask[m * 64 + lb] |= 1ull << lc;
-                    const int tb = (x >> 6) + tx * ((z >> 6) + tz * (y >> 6));
-                    if (tb < 64) top |= 1ull << tb;
+                if (is_cube(id)) {
+                    c->hMacro[b / 64] |= 1ull << (b % 64);
+                    c->hCell[b] |= 1ull << lc;
+                    c->topCount[top_block(c, x, y, z)]++;
                 }
             }
     c->topValid = (tx * ty * tz <= 64) ? 1 : 0;
-    c->top = top;
-    // Per-octant empty-box sizes: for every 4^3 brick and each of the 8 ray
-    // octants, S = the edge (in bricks) of the largest brick-aligned cube with
-    // that brick at its corner, extending in the octant's directions, that holds
-    // no cube cell (0 = the brick is occupied; out-of-world counts as empty;
-    // capped at 255).  A ray in that octant can leave the whole cube in one jump.
-    // 3-D "largest empty square" recurrence: S = 1 + min(S of the 7 forward neighbours).
-    {
-        const int BX = wx / 4, BY = wy / 4, BZ = wz / 4;
-        const size_t nB = (size_t)BX * BY * BZ;
-        std::vector<uint8_t> occ(nB), S(nB), od(8 * nB);
-        auto lin = [&](int x, int y, int z) { return (size_t)x + (size_t)BX * (z + (size_t)BZ * y); };
-        for (int y = 0; y < BY; ++y)
-            for (int z = 0; z < BZ; ++z)
-                for (int x = 0; x < BX; ++x) {
-                    const size_t m = (size_t)(x >> 2) + (size_t)mx * ((z >> 2) + (size_t)mz * (y >> 2));
-                    const int lb = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
-                    occ[lin(x, y, z)] = cellMask[m * 64 + lb] ? 1 : 0;
-                }
-        for (int oct = 0; oct < 8; ++oct) {
-            const int sx = (oct & 1) ? 1 : -1, sy = (oct & 2) ? 1 : -1, sz = (oct & 4) ? 1 : -1;
-            auto get = [&](int x, int y, int z) -> int {
-                if (x < 0 || y < 0 || z < 0 || x >= BX || y >= BY || z >= BZ) return 255;
-                return S[lin(x, y, z)];
-            };
-            for (int iy = 0; iy < BY; ++iy)
-                for (int iz = 0; iz < BZ; ++iz)
-                    for (int ix = 0; ix < BX; ++ix) {
-                        // visit bricks against the octant's direction so forward neighbours are done
-                        const int x = sx > 0 ? BX - 1 - ix : ix, y = sy > 0 ? BY - 1 - iy : iy,
-                                  z = sz > 0 ? BZ - 1 - iz : iz;
-                        int v = 0;
-                        if (!occ[lin(x, y, z)]) {
-                            int mn = 255;
-                            for (int k = 1; k < 8; ++k)
-                                mn = std::min(mn, get(x + ((k & 1) ? sx : 0), y + ((k & 2) ? sy : 0),
-                                                      z + ((k & 4) ? sz : 0)));
-                            v = std::min(255, 1 + mn);
-                        }
-                        S[lin(x, y, z)] = (uint8_t)v;
-                    }
-            for (int y = 0; y < BY; ++y)
-                for (int z = 0; z < BZ; ++z)
-                    for (int x = 0; x < BX; ++x) {
-                        const size_t m = (size_t)(x >> 2) + (size_t)mx * ((z >> 2) + (size_t)mz * (y >> 2));
-                        const int lb = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
-                        od[(size_t)oct * nB + m * 64 + lb] = S[lin(x, y, z)];
-                    }
+    refresh_top(c);
+    const int BX = wx / 4, BY = wy / 4, BZ = wz / 4;
+    const size_t nB = (size_t)BX * BY * BZ;
+    c->hOd.assign(8 * nB, 0);
+    for (int oct = 0; oct < 8; ++oct) octant_fill(c, oct, 0, BX - 1, 0, BY - 1, 0, BZ - 1);
+    c->nBricks = (int)nB;
+    if (int r = upload_vec(c, c->bdist, c->hOd.data(), c->hOd.size())) return r;
+    if (int r = upload_vec(c, c->bricks, c->hBricks.data(), c->hBricks.size())) return r;
+    if (int r = upload_vec(c, c->macro, c->hMacro.data(), c->hMacro.size())) return r;
+    if (int r = upload_vec(c, c->cellMask, c->hCell.data(), c->hCell.size())) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// One voxel edit (VoxelEngine::setVoxelAtGlobal, VoxelEngine.cu:265-276, and the uninstanced
+// face-mesh update updateSingleVoxelGlobal, VoxelSceneGen.cu:643-786, whose DDA equivalent is
+// this): the id in both layouts, the brick's cube mask, and -- when the brick turns occupied or
+// empty -- its macro bit, the 64^3 block bit and the octant tables of the bricks behind it.
+int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
+    const int wx = c->cx * 32, wy = c->cy * 32, wz = c->cz * 32;
+    if (x < 0 || y < 0 || z < 0 || x >= wx || y >= wy || z >= wz || id < 0 || id > 255)
+        return fail(c, VXPT_ERR_ARG, "block position or id out of range");
+    const size_t ci = (size_t)((x >> 5) + c->cx * ((z >> 5) + c->cz * (y >> 5))) * 32768 + (x & 31) +
+                      32 * ((z & 31) + 32 * (y & 31));
+    const int old = c->hIds[ci];
+    if (old == id) return 0;
+    hipStream_t st = c->stream;
+    c->hIds[ci] = (uint8_t)id;
+    HIPCHK(c, hipMemcpyAsync(c->voxels.p + ci, &c->hIds[ci], 1, hipMemcpyHostToDevice, st));
+    const size_t b = brick_lin(c, x >> 2, y >> 2, z >> 2);
+    const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
+    c->hBricks[b * 64 + lc] = (uint8_t)id;
+    HIPCHK(c, hipMemcpyAsync(c->bricks.p + b * 64 + lc, &c->hBricks[b * 64 + lc], 1, hipMemcpyHostToDevice, st));
+    if (is_cube(old) != is_cube(id)) {
+        const uint64_t before = c->hCell[b];
+        c->hCell[b] = is_cube(id) ? (before | (1ull << lc)) : (before & ~(1ull << lc));
+        HIPCHK(c, hipMemcpyAsync(c->cellMask.p + b, &c->hCell[b], 8, hipMemcpyHostToDevice, st));
+        c->topCount[top_block(c, x, y, z)] += is_cube(id) ? 1 : -1;
+        refresh_top(c);
+        if ((before != 0) != (c->hCell[b] != 0)) {
+            const size_t m = b / 64;
+            c->hMacro[m] = c->hCell[b] ? (c->hMacro[m] | (1ull << (b % 64))) : (c->hMacro[m] & ~(1ull << (b % 64)));
+            HIPCHK(c, hipMemcpyAsync(c->macro.p + m, &c->hMacro[m], 8, hipMemcpyHostToDevice, st));
+            const int bx = x >> 2, by = y >> 2, bz = z >> 2, BX = c->cx * 8, BY = c->cy * 8, BZ = c->cz * 8;
+            for (int oct = 0; oct < 8; ++oct)
+                octant_fill(c, oct, (oct & 1) ? 0 : bx, (oct & 1) ? bx : BX - 1, (oct & 2) ? 0 : by,
+                            (oct & 2) ? by : BY - 1, (oct & 4) ? 0 : bz, (oct & 4) ? bz : BZ - 1);
+            HIPCHK(c, hipMemcpyAsync(c->bdist.p, c->hOd.data(), c->hOd.size(), hipMemcpyHostToDevice, st));
         }
-        c->nBricks = (int)nB;
-        if (int r = upload_vec(c, c->bdist, od.data(), od.size())) return r;
-        HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    if (int r = upload_vec(c, c->bricks, bricks.data(), bricks.size())) return r;
-    if (int r = upload_vec(c, c->macro, macro.data(), macro.size())) return r;
-    if (int r = upload_vec(c, c->cellMask, cellMask.data(), cellMask.size())) return r;
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors die on return
+    // the mirrors are the copies' sources: let them land before the host edits them again
+    HIPCHK(c, hipStreamSynchronize(st));
+    // OptixRenderer::update (:916-919): after a geometry change the previous frame's scene is
+    // gone, so the next pass's ReSTIR temporal visibility rays (closesthit.cu:736-755) miss
+    c->prevSceneEmpty = 1;
     return 0;
 }
 
@@ -577,6 +639,8 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.numCU = c->numCU;
     a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
     a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
+    a.prevSceneEmpty = c->prevSceneEmpty;
+    c->prevSceneEmpty = 0;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_trace(a, c->stream, c->haloPending ? c->haloDone : nullptr));
     c->haloPending = false;
@@ -1144,8 +1208,9 @@ int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int cz
     HIPCHK(c, hipSetDevice(c->dev));
     c->cx = cxn; c->cy = cyn; c->cz = czn;
     const size_t n = (size_t)cxn * cyn * czn * 32768;
-    if (int r = upload_vec(c, c->voxels, ids, n)) return r;
-    if (int r = build_occupancy(c, ids)) return r;
+    c->hIds.assign(ids, ids + n);
+    if (int r = upload_vec(c, c->voxels, c->hIds.data(), n)) return r;
+    if (int r = build_occupancy(c, c->hIds.data())) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return VXPT_OK;
 }
@@ -1218,6 +1283,174 @@ int vxpt_set_camera(vxpt_ctx *c, const vxpt_camera *cur, const vxpt_camera *prev
     c->cam = make_camera(c->W, c->H, *cur, &c->camYaw, &c->camPitch);
     c->prevCam = make_camera(c->W, c->H, prev ? *prev : *cur, nullptr, nullptr);
     return VXPT_OK;
+}
+
+int vxpt_set_camera_angles(vxpt_ctx *c, const float pos[3], float yaw, float pitch, float fovDeg) {
+    if (!c || !pos) return VXPT_ERR_ARG;
+    c->prevCam = c->cam;  // historyCamera = camera (mainOffline.cpp:278-279)
+    c->cam = make_camera_angles(c->W, c->H, pos, yaw, pitch, fovDeg);
+    c->camYaw = yaw;
+    c->camPitch = pitch;
+    return VXPT_OK;
+}
+
+// VoxelEngine::performRayTraversal (VoxelEngine.cu:1040-1166): a unit-step walk of the camera
+// ray over the host grid; the last empty cell before the first non-empty one is where a block
+// would be placed.  out: hit, hit x, y, z, hit id, has space, place x, y, z, cells walked
+int vxpt_pick_block(vxpt_ctx *c, int32_t out[10]) {
+    if (!c || !out) return VXPT_ERR_ARG;
+    if (c->hIds.empty()) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
+    for (int i = 0; i < 10; ++i) out[i] = 0;
+    const int W = c->cx * 32, H = c->cy * 32, D = c->cz * 32;
+    const V3 o = c->cam.pos;
+    V3 d = c->cam.dir;
+    const float len = std::sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+    if (len <= 1e-8f) return VXPT_OK;
+    d = V3(d.x / len, d.y / len, d.z / len);
+    int x = (int)std::floor(o.x), y = (int)std::floor(o.y), z = (int)std::floor(o.z);
+    const int stx = d.x > 0.0f ? 1 : -1, sty = d.y > 0.0f ? 1 : -1, stz = d.z > 0.0f ? 1 : -1;
+    auto delta = [](float v) { return std::fabs(v) < 1e-8f ? FLT_MAX : 1.0f / std::fabs(v); };
+    auto first = [](float v, int cell, int step, float orig) {
+        const float bound = step > 0 ? (float)(cell + 1) : (float)cell;
+        return std::fabs(v) < 1e-8f ? FLT_MAX : (bound - orig) / v;
+    };
+    const float tdx = delta(d.x), tdy = delta(d.y), tdz = delta(d.z);
+    float tmx = first(d.x, x, stx, o.x), tmy = first(d.y, y, sty, o.y), tmz = first(d.z, z, stz, o.z);
+    int n = 0;
+    while (n++ < 1000) {
+        if (x < 0 || x >= W || y < 0 || y >= H || z < 0 || z >= D) break;
+        const int id = c->hIds[(size_t)((x >> 5) + c->cx * ((z >> 5) + c->cz * (y >> 5))) * 32768 + (x & 31) +
+                                32 * ((z & 31) + 32 * (y & 31))];
+        if (id == 0) {
+            out[5] = 1; out[6] = x; out[7] = y; out[8] = z;
+        } else {
+            out[0] = 1; out[1] = x; out[2] = y; out[3] = z; out[4] = id;
+            break;
+        }
+        if (tmx < tmy) {
+            if (tmx < tmz) { x += stx; tmx += tdx; }
+            else { z += stz; tmz += tdz; }
+        } else {
+            if (tmy < tmz) { y += sty; tmy += tdy; }
+            else { z += stz; tmz += tdz; }
+        }
+    }
+    out[9] = n;
+    return VXPT_OK;
+}
+
+int vxpt_set_block(vxpt_ctx *c, int x, int y, int z, int block_id) {
+    if (!c) return VXPT_ERR_ARG;
+    if (c->hIds.empty()) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
+    HIPCHK(c, hipSetDevice(c->dev));
+    return set_block(c, x, y, z, block_id);
+}
+
+// VoxelEngine::update's click (VoxelEngine.cu:906-975): block 0 deletes the picked block,
+// another id is placed in the last empty cell before it.  out = the pick (vxpt_pick_block)
+int vxpt_click_block(vxpt_ctx *c, int block_id, int32_t out[10]) {
+    int32_t pk[10];
+    if (int r = vxpt_pick_block(c, pk)) return r;
+    if (out) std::memcpy(out, pk, sizeof(pk));
+    if (block_id == 0) {
+        if (pk[0]) return vxpt_set_block(c, pk[1], pk[2], pk[3], 0);
+    } else if (pk[5] && pk[0]) {
+        return vxpt_set_block(c, pk[6], pk[7], pk[8], block_id);
+    }
+    return VXPT_OK;
+}
+
+// WorldSceneManager chunk files (WorldSceneManager.cpp:240-307): each 32^3 chunk's bytes in
+// <chunk_dir>/<FNV-1a 64 of the bytes, 16 hex digits>.bin; the scene yaml (SceneConfig.cpp:116-151)
+// lists them under `chunks:` with the camera and `chunk_config`.
+static std::string fnv1a_hex(const uint8_t *p, size_t n) {
+    unsigned long long h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= (unsigned long long)p[i];
+        h *= 1099511628211ull;
+    }
+    char buf[17];
+    std::snprintf(buf, sizeof buf, "%016llx", h);
+    return buf;
+}
+
+int vxpt_save_world(vxpt_ctx *c, const char *scene_yaml, const char *chunk_dir) {
+    if (!c || !scene_yaml || !chunk_dir) return VXPT_ERR_ARG;
+    if (c->hIds.empty()) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
+    std::error_code ec;
+    std::filesystem::create_directories(chunk_dir, ec);
+    const int nch = c->cx * c->cy * c->cz;
+    std::vector<std::string> hashes(nch);
+    for (int i = 0; i < nch; ++i) {
+        const uint8_t *d = c->hIds.data() + (size_t)i * 32768;
+        hashes[i] = fnv1a_hex(d, 32768);
+        std::ofstream f(std::filesystem::path(chunk_dir) / (hashes[i] + ".bin"), std::ios::binary | std::ios::trunc);
+        f.write((const char *)d, 32768);
+        if (!f.good()) return fail(c, VXPT_ERR_IO, "cannot write chunk " + std::to_string(i));
+    }
+    std::ofstream y(scene_yaml, std::ios::trunc);
+    if (!y) return fail(c, VXPT_ERR_IO, std::string("cannot write ") + scene_yaml);
+    auto f3 = [](V3 v) {
+        std::ostringstream o;
+        o << "[" << v.x << ", " << v.y << ", " << v.z << "]";
+        return o.str();
+    };
+    y << "# Scene Configuration File\n# Generated automatically\n\n"
+      << "camera:\n  position: " << f3(c->cam.pos) << "\n  direction: " << f3(c->cam.dir)
+      << "\n  up: " << f3(V3(0.0f, 1.0f, 0.0f)) << "\n  fov: " << 90.0f << "\n\n"
+      << "character:\n  position: " << f3(V3(16.0f, 10.0f, 16.0f)) << "\n  rotation: " << f3(V3(0.0f))
+      << "\n  scale: " << f3(V3(1.0f)) << "\n"
+      << "\nchunk_config:\n  chunksX: " << c->cx << "\n  chunksY: " << c->cy << "\n  chunksZ: " << c->cz << "\n"
+      << "\nchunks:\n";
+    for (int i = 0; i < nch; ++i) y << "  " << i << ": " << hashes[i] << "\n";
+    return y.good() ? VXPT_OK : fail(c, VXPT_ERR_IO, "scene yaml write failed");
+}
+
+// WorldSceneManager::LoadScene (:365-458): the camera and every listed chunk file; a world of
+// another chunk configuration keeps the runtime one (records past it are errors), and without a
+// world yet the scene's configuration is used.  The world is then rebuilt (VoxelEngine::reload).
+int vxpt_load_world(vxpt_ctx *c, const char *scene_yaml, const char *chunk_dir, vxpt_camera *cam_out) {
+    if (!c || !scene_yaml || !chunk_dir) return VXPT_ERR_ARG;
+    std::ifstream f(scene_yaml);
+    if (!f) return fail(c, VXPT_ERR_IO, std::string("cannot open ") + scene_yaml);
+    std::string line, section;
+    int cfg[3] = {0, 0, 0};
+    std::vector<std::pair<int, std::string>> recs;
+    while (std::getline(f, line)) {
+        line = trim(line);
+        if (line.empty() || line[0] == '#') continue;
+        if (line.back() == ':') { section = line.substr(0, line.size() - 1); continue; }
+        const size_t col = line.find(':');
+        if (col == std::string::npos) continue;
+        const std::string key = trim(line.substr(0, col)), val = trim(line.substr(col + 1));
+        if (section == "chunk_config") {
+            if (key == "chunksX") cfg[0] = std::atoi(val.c_str());
+            else if (key == "chunksY") cfg[1] = std::atoi(val.c_str());
+            else if (key == "chunksZ") cfg[2] = std::atoi(val.c_str());
+        } else if (section == "chunks" && !key.empty() && std::isdigit((unsigned char)key[0])) {
+            recs.emplace_back(std::atoi(key.c_str()), val);
+        }
+    }
+    if (cam_out && vxpt_load_scene_camera(c, scene_yaml, cam_out) != VXPT_OK) return VXPT_ERR_IO;
+    if (c->hIds.empty()) {
+        if (cfg[0] <= 0 || cfg[1] <= 0 || cfg[2] <= 0) return fail(c, VXPT_ERR_STATE, "no world and no chunk_config");
+        c->cx = cfg[0]; c->cy = cfg[1]; c->cz = cfg[2];
+        c->hIds.assign((size_t)c->cx * c->cy * c->cz * 32768, 0);
+    }
+    const int nch = c->cx * c->cy * c->cz;
+    std::vector<uint8_t> ids = c->hIds;
+    bool ok = true;
+    for (const auto &r : recs) {
+        if (r.first < 0 || r.first >= nch) { ok = false; continue; }
+        const auto path = std::filesystem::path(chunk_dir) / (r.second + ".bin");
+        std::error_code ec;
+        if (std::filesystem::file_size(path, ec) != 32768 || ec) { ok = false; continue; }
+        std::ifstream in(path, std::ios::binary);
+        in.read((char *)ids.data() + (size_t)r.first * 32768, 32768);
+        if (in.gcount() != 32768) ok = false;
+    }
+    if (int r = vxpt_upload_voxels(c, ids.data(), c->cx, c->cy, c->cz)) return r;
+    return ok ? VXPT_OK : fail(c, VXPT_ERR_IO, "some chunk records could not be loaded");
 }
 
 int vxpt_get_camera(vxpt_ctx *c, int which, float *o) {

@@ -9,12 +9,16 @@
 // totalFrames-1 and writes <prefix>_diff.png.  Additions: --spp (samples per pixel per frame,
 // the reference traces 1), --chunks X Y Z (world size, default the reference's 2 1 2), --device,
 // --data (the data directory), --perf-report (the reference writes ../../data/perf/...).
-// The scripted voxel-edit sequences (--test-sequence, --test-remove20, --test-remove-circle) need
-// the voxel edit path, which is not built yet: they are rejected with a message.
+// The scripted voxel-edit sequences (--test-sequence, --test-remove20, --test-remove-circle) follow
+// the reference's timing: a click set after frame N is picked at frame N+1 against the world as
+// edited so far (VoxelEngine::update, VoxelEngine.cu:906-975) and the geometry changes at frame
+// N+2 (OptixRenderer::update rebuilds the chunk's acceleration structure a frame later,
+// OptixRenderer.cpp:846-925), the frame whose ReSTIR temporal visibility sees no previous scene.
 #include "../../include/vxpt.h"
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,6 +47,7 @@ struct Options {
     int device = 0;
     std::string dataDir = "data";
     std::string perfReport;
+    bool testSequence = false, removal20 = false, removalCircle = false;
 };
 
 void usage(const char *argv0) {
@@ -57,6 +62,9 @@ void usage(const char *argv0) {
               << "  --update-canonical     Update the canonical reference image\n"
               << "  --canonical-image <p>  Path to canonical image (default: ../../data/canonical/canonical_render.png)\n"
               << "  --comment <text>       Comment for performance report (default: default run)\n"
+              << "  --test-sequence        Enable scripted block placement test sequence\n"
+              << "  --test-remove20        Enable scripted removal test (20 deletions)\n"
+              << "  --test-remove-circle   Enable circular removal test (8 directions, 5 deletions each)\n"
               << "  --frames <int>         Number of frames to render (default: 64, use 1 for single frame)\n"
               << "  --spp <int>            Samples per pixel per frame (default: 1)\n"
               << "  --chunks <x> <y> <z>   World size in 32^3 chunks (default: 2 1 2)\n"
@@ -101,10 +109,9 @@ int parse(int argc, char **argv, Options &o) {
         else if (a == "--device") { if (!(v = next("--device"))) return -1; o.device = std::atoi(v); }
         else if (a == "--data") { if (!(v = next("--data"))) return -1; o.dataDir = v; }
         else if (a == "--perf-report") { if (!(v = next("--perf-report"))) return -1; o.perfReport = v; }
-        else if (a == "--test-sequence" || a == "--test-remove20" || a == "--test-remove-circle") {
-            std::cerr << a << ": scripted voxel edits are not supported by this build\n";
-            return -1;
-        }
+        else if (a == "--test-sequence") o.testSequence = true;
+        else if (a == "--test-remove20") o.removal20 = true;
+        else if (a == "--test-remove-circle") o.removalCircle = true;
         else if (a == "--help" || a == "-h") { usage(argv[0]); return 0; }
         else { std::cerr << "unknown option " << a << "\n"; return -1; }
     }
@@ -208,6 +215,23 @@ int main(int argc, char **argv) {
     if (vxpt_get_post_params(ctx, &pp) != VXPT_OK) return fail("reading post-process settings");
     if (vxpt_get_denoise_params(ctx, &dp) != VXPT_OK) return fail("reading denoise settings");
 
+    // scripted clicks (mainOffline.cpp:43-50, 166-188, 281-395; VoxelEngine.cu:206-217, 906-945)
+    constexpr int kRemovals20 = 20, kDirections = 8, kPerDirection = 5, kCircleRemovals = kDirections * kPerDirection;
+    constexpr float kPi = 3.14159265358979323846f, kPiOver180 = kPi / 180.0f, kTwoPi = 2.0f * kPi;
+    constexpr float kYawAmp = 12.0f * kPiOver180, kPitchAmp = 6.0f * kPiOver180;
+    std::vector<int> clickSequence;  // empty: the default {16, 0, 16} cycle
+    if (o.removalCircle) clickSequence.assign(kCircleRemovals, 0);
+    else if (o.removal20) clickSequence.assign(kRemovals20, 0);
+    size_t clickIndex = 0, defaultIndex = 0;
+    bool clickPending = false, editPending = false;
+    int edit[4] = {0, 0, 0, 0};
+    int removals = 0, circleDone = 0, lastDirection = -1;
+    bool circleRestored = false;
+    float camInfo[32];
+    if (vxpt_get_camera(ctx, 0, camInfo) != VXPT_OK) return fail("reading the camera");
+    const float baseYaw = camInfo[30], basePitch = camInfo[31];
+    float yaw = baseYaw, pitch = basePitch;
+
     std::vector<BatchedFrame> batch;
     std::vector<FrameRecord> perf;
     const size_t frameBytes = (size_t)o.width * o.height * 4 * sizeof(float);
@@ -219,6 +243,59 @@ int main(int argc, char **argv) {
         last = t0;
         const bool shouldSave =
             std::find(o.savedFrames.begin(), o.savedFrames.end(), frameNumber) != o.savedFrames.end();
+
+        // the edit picked last frame reaches the geometry now
+        if (editPending) {
+            if (vxpt_set_block(ctx, edit[0], edit[1], edit[2], edit[3]) != VXPT_OK) return fail("editing a block");
+            editPending = false;
+        }
+        if (o.removalCircle) {  // mainOffline.cpp:281-305
+            if (circleDone < kCircleRemovals) {
+                const int dirIndex = circleDone / kPerDirection;
+                if (dirIndex != lastDirection) {
+                    const float angle = (float)dirIndex * (kTwoPi / (float)kDirections);
+                    const float yawOff = (float)(kYawAmp * std::cos(angle)), pitchOff = (float)(kPitchAmp * std::sin(angle));
+                    yaw = baseYaw + yawOff;
+                    pitch = basePitch + pitchOff;
+                    std::cout << "CIRCULAR TEST: Switching to view direction #" << dirIndex + 1 << " (yaw offset "
+                              << yawOff << ", pitch offset " << pitchOff << ")" << std::endl;
+                    lastDirection = dirIndex;
+                }
+            } else if (!circleRestored) {
+                yaw = baseYaw;
+                pitch = basePitch;
+                circleRestored = true;
+                std::cout << "CIRCULAR TEST: Restored base camera orientation after scripted removals." << std::endl;
+            }
+            // historyCamera = camera; camera.update() (:278-279, 307)
+            if (vxpt_set_camera_angles(ctx, cam.pos, yaw, pitch, cam.fov_deg) != VXPT_OK) return fail("camera");
+            std::cout << "CAMERA: frame " << frameNumber << " yaw " << std::hexfloat << yaw << " pitch " << pitch
+                      << std::defaultfloat << std::endl;
+        }
+        if (clickPending) {  // VoxelEngine::update's click, against the world as edited so far
+            clickPending = false;
+            int blockId;
+            if (!clickSequence.empty()) {
+                const size_t idx = std::min(clickIndex, clickSequence.size() - 1);
+                blockId = clickSequence[idx];
+                clickIndex = idx + 1 < clickSequence.size() ? idx + 1 : idx;
+            } else {
+                static const int defaultSequence[3] = {16, 0, 16};
+                blockId = defaultSequence[defaultIndex++ % 3];
+            }
+            int32_t pk[10];
+            if (vxpt_pick_block(ctx, pk) != VXPT_OK) return fail("picking");
+            if (blockId == 0 && pk[0]) {
+                edit[0] = pk[1]; edit[1] = pk[2]; edit[2] = pk[3]; edit[3] = 0;
+                editPending = true;
+            } else if (blockId != 0 && pk[5] && pk[0]) {
+                edit[0] = pk[6]; edit[1] = pk[7]; edit[2] = pk[8]; edit[3] = blockId;
+                editPending = true;
+            }
+            if (editPending)
+                std::cout << "EDIT: frame " << frameNumber << " block " << edit[3] << " at (" << edit[0] << ","
+                          << edit[1] << "," << edit[2] << ")" << std::endl;
+        }
 
         if (vxpt_render_frame(ctx, &dp, frame, o.spp) != VXPT_OK) return fail("rendering");
         const auto tp = std::chrono::steady_clock::now();
@@ -240,6 +317,22 @@ int main(int argc, char **argv) {
                         std::chrono::duration<double, std::milli>(t1 - t0).count(), dtMs};
         vxpt_timings(ctx, &rec.t);
         perf.push_back(rec);
+        // the clicks the reference scripts after a frame (mainOffline.cpp:346-395)
+        if (o.removalCircle) {
+            if (circleDone < kCircleRemovals) {
+                ++circleDone;
+                std::cout << "CIRCULAR TEST: Frame " << frameNumber << " deleting block #" << circleDone << std::endl;
+                clickPending = true;
+            }
+        } else if (o.removal20) {
+            if (removals < kRemovals20) {
+                ++removals;
+                std::cout << "REMOVAL TEST: Frame " << frameNumber << " deleting block #" << removals << std::endl;
+                clickPending = true;
+            }
+        } else if (o.testSequence) {
+            if (frameNumber == 2 || frameNumber == 5 || frameNumber == 8) clickPending = true;
+        }
         if (shouldSave || frameNumber % 16 == 0)
             std::cout << "Frame " << frameNumber << "/" << o.totalFrames << " completed"
                       << (shouldSave ? " (SAVED)" : "") << std::endl;

@@ -22,7 +22,8 @@ DATA_DIR = os.path.join(REPO, "data")
 BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERIAL=5, MAT_PARAM=6, MOTION=7,
            PREV_NORMAL_ROUGH=8, PREV_GEO_NORMAL_THIN=9, PREV_ALBEDO=10, PREV_MAT_PARAM=11, PREV_DEPTH=12,
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
-           PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38)
+           PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38,
+           OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
@@ -116,6 +117,12 @@ def load_library(path=LIB_PATH):
         "vxpt_set_sky": (I, [P, F, F, F, F]),
         "vxpt_set_camera": (I, [P, ctypes.POINTER(Camera), ctypes.POINTER(Camera)]),
         "vxpt_get_camera": (I, [P, I, P]),
+        "vxpt_set_camera_angles": (I, [P, P, F, F, F]),
+        "vxpt_pick_block": (I, [P, P]),
+        "vxpt_set_block": (I, [P, I, I, I, I]),
+        "vxpt_click_block": (I, [P, I, P]),
+        "vxpt_save_world": (I, [P, ctypes.c_char_p, ctypes.c_char_p]),
+        "vxpt_load_world": (I, [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Camera)]),
         "vxpt_trace": (I, [P, ctypes.c_int32, U32]),
         "vxpt_denoise": (I, [P, ctypes.POINTER(DenoiseParams), ctypes.c_int32, ctypes.c_int32]),
         "vxpt_denoise_pass": (I, [P, ctypes.POINTER(DenoiseParams), I, I, I]),
@@ -233,6 +240,48 @@ class Renderer:
         self._chk(self.lib.vxpt_get_camera(self.ctx, which, _ptr(out)), "vxpt_get_camera")
         return out
 
+    def set_camera_angles(self, pos, yaw, pitch, fov=90.0):
+        """historyCamera = camera, then Camera::update from yaw/pitch (radians)."""
+        p = np.ascontiguousarray(pos, np.float32)
+        self._chk(self.lib.vxpt_set_camera_angles(self.ctx, _ptr(p), float(yaw), float(pitch), float(fov)),
+                  "vxpt_set_camera_angles")
+
+    # --- voxel edits (VoxelEngine click path) and world files (WorldSceneManager) ---
+    @staticmethod
+    def _pick_dict(o):
+        return dict(hit=bool(o[0]), hit_pos=tuple(int(v) for v in o[1:4]), hit_id=int(o[4]), space=bool(o[5]),
+                    place_pos=tuple(int(v) for v in o[6:9]), cells=int(o[9]))
+
+    def pick_block(self):
+        o = np.zeros(10, np.int32)
+        self._chk(self.lib.vxpt_pick_block(self.ctx, _ptr(o)), "vxpt_pick_block")
+        return self._pick_dict(o)
+
+    def set_block(self, x, y, z, block_id):
+        self._chk(self.lib.vxpt_set_block(self.ctx, int(x), int(y), int(z), int(block_id)), "vxpt_set_block")
+
+    def click_block(self, block_id):
+        o = np.zeros(10, np.int32)
+        self._chk(self.lib.vxpt_click_block(self.ctx, int(block_id), _ptr(o)), "vxpt_click_block")
+        return self._pick_dict(o)
+
+    def save_world(self, scene_yaml, chunk_dir):
+        self._chk(self.lib.vxpt_save_world(self.ctx, str(scene_yaml).encode(), str(chunk_dir).encode()),
+                  "vxpt_save_world")
+
+    def load_world(self, scene_yaml, chunk_dir):
+        cam = Camera()
+        self._chk(self.lib.vxpt_load_world(self.ctx, str(scene_yaml).encode(), str(chunk_dir).encode(),
+                                           ctypes.byref(cam)), "vxpt_load_world")
+        if not hasattr(self, "chunks"):  # a fresh context takes the scene's chunk_config
+            cfg = {}
+            for line in open(scene_yaml):
+                k, _, v = line.strip().partition(":")
+                if k in ("chunksX", "chunksY", "chunksZ"):
+                    cfg[k] = int(v)
+            self.chunks = (cfg["chunksX"], cfg["chunksY"], cfg["chunksZ"])
+        return cam
+
     # --- frame (OfflineBackend::renderFrame) ---
     def trace(self, iteration_index, primary_only=False):
         self._chk(self.lib.vxpt_trace(self.ctx, iteration_index, TRACE_PRIMARY_ONLY if primary_only else 0),
@@ -323,6 +372,11 @@ class Renderer:
         if which == BUF["VOXELS"]:
             cx, cy, cz = self.chunks
             return np.zeros(cx * cy * cz * 32768, np.uint8)
+        if which in (BUF["OCTANT_TABLES"], BUF["CELL_MASKS"], BUF["BRICK_IDS"], BUF["MACRO_MASKS"]):
+            nb = int(np.prod(self.chunks)) * 512
+            return {BUF["OCTANT_TABLES"]: np.zeros(8 * nb, np.uint8), BUF["CELL_MASKS"]: np.zeros(nb, np.uint64),
+                    BUF["BRICK_IDS"]: np.zeros(nb * 64, np.uint8),
+                    BUF["MACRO_MASKS"]: np.zeros(nb // 64, np.uint64)}[which]
         if which in FLOAT1_BUFS:
             return np.zeros((self.H, self.W), np.float32)
         return np.zeros((self.H, self.W, 4), np.float32)

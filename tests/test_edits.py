@@ -1,0 +1,295 @@
+"""Voxel edits and world files: VoxelEngine's click path
+(performRayTraversal pick, add/delete, VoxelEngine.cu:855-975, 1040-1346), the
+traversal structures kept up to date incrementally, the frame after an edit
+(prevTopObject = 0, OptixRenderer.cpp:916-919), WorldSceneManager's chunk
+files (WorldSceneManager.cpp:240-458), and the offline executable's scripted
+edit sequences (mainOffline.cpp:43-50, 166-188, 281-395).
+
+Checks: after random edits, every traversal structure equals a full rebuild
+of the edited grid (bit-exact) and the DDA equals the oracle on it; the pick
+equals a float32 restatement of the reference's walk; frames rendered across
+an edit match the oracle given the same grid and flag; saved chunk files are
+named by the FNV-1a 64 hash of their bytes and load back bit-exact.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import vxpt
+from golden.make_golden import C1_CAMERA
+from test_oracle import _random_rays
+from test_gpu_parity import _compare_radiance, _inject_sky, _setup, _dn_params
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(REPO, "real-time-path-tracing-voxel-blocks_amd", "vxpt_offline")
+CH = (2, 1, 2)
+
+
+def _idx(x, y, z, chunks=CH):
+    cx, cy, cz = chunks
+    return ((x >> 5) + cx * ((z >> 5) + cz * (y >> 5))) * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))
+
+
+def pick_ref(ids, chunks, pos, d):
+    """VoxelEngine::performRayTraversal (VoxelEngine.cu:1040-1166) in float32."""
+    f = np.float32
+    W, H, D = chunks[0] * 32, chunks[1] * 32, chunks[2] * 32
+    o = [f(v) for v in pos]
+    d = [f(v) for v in d]
+    ln = np.sqrt(f(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]))
+    d = [f(v / ln) for v in d]
+    c = [int(np.floor(v)) for v in o]
+    step = [1 if v > 0 else -1 for v in d]
+    big = np.finfo(np.float32).max
+    tdel = [big if abs(v) < f(1e-8) else f(f(1.0) / abs(v)) for v in d]
+    tmax = []
+    for k in range(3):
+        bound = f(c[k] + 1) if step[k] > 0 else f(c[k])
+        tmax.append(big if abs(d[k]) < f(1e-8) else f(f(bound - o[k]) / d[k]))
+    res = dict(hit=False, hit_pos=(0, 0, 0), hit_id=0, space=False, place_pos=(0, 0, 0))
+    n = 0
+    while n < 1000:
+        n += 1
+        x, y, z = c
+        if not (0 <= x < W and 0 <= y < H and 0 <= z < D):
+            break
+        v = int(ids[_idx(x, y, z, chunks)])
+        if v == 0:
+            res["space"], res["place_pos"] = True, (x, y, z)
+        else:
+            res.update(hit=True, hit_pos=(x, y, z), hit_id=v)
+            break
+        if tmax[0] < tmax[1]:
+            k = 0 if tmax[0] < tmax[2] else 2
+        else:
+            k = 1 if tmax[1] < tmax[2] else 2
+        c[k] += step[k]
+        tmax[k] = f(tmax[k] + tdel[k])
+    return res
+
+
+def _random_edits(r, ids, n, seed):
+    rng = np.random.default_rng(seed)
+    for _ in range(n):
+        x, y, z = int(rng.integers(0, 64)), int(rng.integers(0, 32)), int(rng.integers(0, 64))
+        b = int(rng.choice([0, 0, 0, 1, 3, 7, 12, 16]))
+        r.set_block(x, y, z, b)
+        ids[_idx(x, y, z)] = b
+    # a whole brick emptied and a lone cube in empty air: occupancy transitions both ways
+    for x in range(8, 12):
+        for y in range(0, 4):
+            for z in range(20, 24):
+                r.set_block(x, y, z, 0)
+                ids[_idx(x, y, z)] = 0
+    r.set_block(40, 30, 9, 5)
+    ids[_idx(40, 30, 9)] = 5
+
+
+STRUCTS = ("VOXELS", "OCTANT_TABLES", "CELL_MASKS", "BRICK_IDS", "MACRO_MASKS")
+
+
+@pytest.mark.gpu
+def test_incremental_edits_match_full_rebuild_and_oracle_dda():
+    r = vxpt.Renderer(64, 64)
+    r.load_settings()
+    r.generate_terrain(CH)
+    ids = r.read("VOXELS").copy()
+    _random_edits(r, ids, 400, 5)
+    r2 = vxpt.Renderer(64, 64)
+    r2.upload_voxels(ids, CH)
+    for name in STRUCTS:
+        np.testing.assert_array_equal(r.read(name), r2.read(name), err_msg=name)
+    o = oracle.Oracle(64, 64)
+    o.set_voxels(ids, CH)
+    for outside in (False, True):
+        rays = _random_rays(20000, 31 + outside, outside=outside)
+        g, tg = r.probe_rays(rays, 0)
+        c, tc = o.rays(rays, 0)
+        np.testing.assert_array_equal(g, c)
+        np.testing.assert_array_equal(tg.view(np.uint32), tc.view(np.uint32))
+    r.close()
+    r2.close()
+
+
+@pytest.mark.gpu
+def test_pick_and_click_follow_the_reference_walk():
+    r = vxpt.Renderer(64, 64)
+    r.load_settings()
+    r.generate_terrain(CH)
+    r.set_camera(C1_CAMERA[0], C1_CAMERA[1], fov=C1_CAMERA[2], prev=C1_CAMERA)
+    info = r.camera_info(0)
+    yaw0, pitch0 = float(info[30]), float(info[31])
+    hits = 0
+    for dy, dp in [(0, 0), (0.2, -0.3), (-0.4, -0.1), (1.0, -0.6), (2.5, 0.2), (0, -1.2)]:
+        r.set_camera_angles(C1_CAMERA[0], yaw0 + dy, pitch0 + dp, C1_CAMERA[2])
+        info = r.camera_info(0)
+        exp = pick_ref(r.read("VOXELS"), CH, info[0:3], info[3:6])
+        got = r.pick_block()
+        for k in ("hit", "hit_pos", "hit_id", "space", "place_pos"):
+            assert got[k] == exp[k], (dy, dp, k, got, exp)
+        hits += got["hit"]
+        if got["hit"]:
+            before = r.read("VOXELS")
+            got2 = r.click_block(0)  # delete the picked block
+            after = r.read("VOXELS")
+            assert got2["hit_pos"] == got["hit_pos"] and after[_idx(*got["hit_pos"])] == 0
+            assert (before != after).sum() == 1
+            nxt = r.pick_block()
+            if nxt["hit"] and nxt["space"]:
+                r.click_block(9)  # place a block in front of the next one
+                assert r.read("VOXELS")[_idx(*nxt["place_pos"])] == 9
+    assert hits >= 4
+    r.close()
+
+
+@pytest.mark.gpu
+def test_frames_across_an_edit_match_oracle():
+    """Frames before and after deleting the block under the crosshair: the edit's frame
+    traces ReSTIR temporal visibility against no previous scene on both sides."""
+    r, o = _setup()
+    _inject_sky(r, o)
+    p = _dn_params()
+    for f in range(5):
+        if f == 2:
+            pk = r.click_block(0)
+            assert pk["hit"]
+            o.set_voxels(r.read("VOXELS"), CH)
+            o.set_prev_scene_empty(True)
+        r.trace(f)
+        r.denoise(f, f + 1, p)
+        o.trace(f)
+        o.set_prev_scene_empty(False)
+        o.post_trace()
+        o.denoise(f, f + 1)
+        _compare_radiance(r.read("ILLUM"), o.read(0), "frame%d illum" % f)
+        _compare_radiance(r.read("OUTPUT"), o.read(21), "frame%d output" % f)
+    r.close()
+
+
+def _fnv1a64(b):
+    h = 1469598103934665603
+    for v in b:
+        h ^= int(v)
+        h = (h * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return "%016x" % h
+
+
+@pytest.mark.gpu
+def test_world_files_round_trip(tmp_path):
+    r = vxpt.Renderer(64, 64)
+    r.load_settings()
+    r.generate_terrain(CH)
+    ids = r.read("VOXELS").copy()
+    _random_edits(r, ids, 50, 9)
+    r.set_camera(C1_CAMERA[0], C1_CAMERA[1], fov=C1_CAMERA[2])
+    scene, chunks = tmp_path / "scene.yaml", tmp_path / "chunks"
+    r.save_world(scene, chunks)
+    text = scene.read_text()
+    assert "chunk_config:" in text and "chunksX: 2" in text
+    for i in range(4):
+        data = ids[i * 32768:(i + 1) * 32768]
+        h = _fnv1a64(data.tobytes())
+        assert ("  %d: %s" % (i, h)) in text
+        assert (chunks / (h + ".bin")).read_bytes() == data.tobytes()
+    r2 = vxpt.Renderer(64, 64)
+    r2.load_settings()
+    cam = r2.load_world(scene, chunks)
+    for name in STRUCTS:
+        np.testing.assert_array_equal(r2.read(name), r.read(name), err_msg=name)
+    np.testing.assert_allclose(list(cam.pos), C1_CAMERA[0], atol=1e-3)
+    r.close()
+    r2.close()
+
+
+def _run_cli(*args):
+    return subprocess.run([EXE, *args], cwd=REPO, capture_output=True, text=True, timeout=120)
+
+
+def test_cli_accepts_the_edit_sequence_flags():
+    r = _run_cli("--help")
+    for flag in ("--test-sequence", "--test-remove20", "--test-remove-circle"):
+        assert flag in r.stdout
+
+
+def _mirror(mode, w, h, frames, dts, angles):
+    """mainOffline.cpp's frame loop with scripted clicks, through the Python mirror
+    (the circular test's camera angles are the CLI's own, printed exactly)."""
+    r = vxpt.Renderer(w, h)
+    r.load_settings()
+    r.generate_terrain(CH)
+    cam = r.scene_camera(os.path.join(REPO, "data", "scene", "scene_export.yaml"))
+    c = (list(cam.pos), list(cam.dir), cam.fov_deg)
+    r.set_camera(*c[:2], fov=c[2], prev=c)
+    r.set_sky()
+    dp, pp = r.denoise_params(), r.post_params()
+    seq = [0] * (40 if mode == "circle" else 20) if mode in ("circle", "remove20") else []
+    seq_i, def_i, click, pending, done, last_dir, restored = 0, 0, False, None, 0, -1, False
+    for frame in range(frames):
+        fn = frame + 1
+        if pending:
+            r.set_block(*pending)
+            pending = None
+        if mode == "circle":
+            if done < 40 and done // 5 != last_dir:
+                last_dir = done // 5
+            elif done >= 40 and not restored:
+                restored = True
+            yaw, pitch = angles[fn]
+            r.set_camera_angles(c[0], yaw, pitch, c[2])
+        if click:
+            click = False
+            if seq:
+                k = min(seq_i, len(seq) - 1)
+                b = seq[k]
+                seq_i = k + 1 if k + 1 < len(seq) else k
+            else:
+                b = (16, 0, 16)[def_i % 3]
+                def_i += 1
+            pk = r.pick_block()
+            if b == 0 and pk["hit"]:
+                pending = (*pk["hit_pos"], 0)
+            elif b != 0 and pk["space"] and pk["hit"]:
+                pending = (*pk["place_pos"], b)
+        r.render_frame(frame, 1, dp)
+        r.postprocess(pp, dts[frame])
+        if mode == "circle" and done < 40:
+            done += 1
+            click = True
+        elif mode == "remove20" and done < 20:
+            done += 1
+            click = True
+        elif mode == "sequence" and fn in (2, 5, 8):
+            click = True
+    out = r.read("FRAME")
+    vox = r.read("VOXELS")
+    r.close()
+    return out, vox
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,flag,frames", [("remove20", "--test-remove20", 24),
+                                              ("circle", "--test-remove-circle", 44),
+                                              ("sequence", "--test-sequence", 10)])
+def test_cli_edit_sequences_match_mirror(mode, flag, frames, tmp_path):
+    w, h = 64, 64
+    prefix = str(tmp_path / "e")
+    res = _run_cli("--width", str(w), "--height", str(h), "--frames", str(frames), "--output", prefix, flag)
+    assert res.returncode == 0, (res.stdout[-2000:], res.stderr[-2000:])
+    assert res.stdout.count("EDIT: frame") >= (3 if mode == "sequence" else 10)
+    rows = [ln.split(",") for ln in open(prefix + "_performance_report.txt") if ln[0].isdigit()]
+    dts = [float(x[7]) for x in rows]
+    angles = {}
+    for ln in res.stdout.splitlines():
+        if ln.startswith("CAMERA: frame "):
+            t = ln.split()
+            angles[int(t[2])] = (float.fromhex(t[4]), float.fromhex(t[6]))
+    assert mode != "circle" or len(angles) == frames
+    # the last saved frame (1-indexed 1/4/16/64) through the Python mirror, bit for bit
+    last_saved = max(k for k in (1, 4, 16, 64) if k <= frames)
+    out, vox = _mirror(mode, w, h, last_saved, dts, angles)
+    mine = str(tmp_path / "m.png")
+    vxpt.write_png(mine, out)
+    np.testing.assert_array_equal(vxpt.read_png(mine), vxpt.read_png("%s_%04d.png" % (prefix, last_saved - 1)))

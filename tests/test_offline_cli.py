@@ -33,7 +33,7 @@ def test_cli_built_and_help():
         assert flag in r.stdout
 
 
-@pytest.mark.parametrize("args", [("--width", "100"), ("--frames", "0"), ("--bogus",), ("--test-remove20",),
+@pytest.mark.parametrize("args", [("--width", "100"), ("--frames", "0"), ("--bogus",), ("--chunks", "2", "1"),
                                   ("--output",)])
 def test_cli_rejects_bad_arguments(args):
     r = run(*args)
