@@ -53,7 +53,8 @@ enum vxpt_buffer {
     VXPT_BUF_OCTANT_TABLES = 39, /* 8 x nBricks u8: empty-cube edge per brick and ray octant  */
     VXPT_BUF_CELL_MASKS = 40,    /* nBricks u64: cube-cell bits of each 4^3 brick             */
     VXPT_BUF_BRICK_IDS = 41,     /* nBricks x 64 u8: ids in brick-major order                 */
-    VXPT_BUF_MACRO_MASKS = 42    /* nBricks/64 u64: occupied-brick bits of each 16^3 cell      */
+    VXPT_BUF_MACRO_MASKS = 42,   /* nBricks/64 u64: occupied-brick bits of each 16^3 cell      */
+    VXPT_BUF_TEXELS = 43         /* every loaded texture's RGBA8 mip chain (vxpt_texture_table) */
 };
 
 typedef struct vxpt_config {
@@ -156,6 +157,16 @@ int vxpt_get_camera(vxpt_ctx *ctx, int which, float out32[32]);
 /* Camera::update from yaw/pitch (Camera.h:44-100) after historyCamera = camera (mainOffline.cpp:278-307,
  * the circular-removal test's orientation changes); out32[30..31] of vxpt_get_camera are yaw, pitch */
 int vxpt_set_camera_angles(vxpt_ctx *ctx, const float pos[3], float yaw, float pitch, float fov_deg);
+
+/* ---- textures (TextureManager.cu:133-330; shading closesthit.cu:167-254) ---- */
+/* load every texture the cube materials name (paths from assets/materials.yaml, relative to root;
+ * NULL = data_dir) as RGBA8 mip chains and turn textured shading on; missing or non-square files
+ * are skipped (their materials stay untextured).  *loaded = textures loaded */
+int vxpt_load_textures(vxpt_ctx *ctx, const char *root, int *loaded);
+/* textured shading on/off once loaded (the untextured parity scenes use off) */
+int vxpt_enable_textures(vxpt_ctx *ctx, int on);
+/* texture table: per texture size, maxLod, maxLod + 1 level offsets in texels (parity hook) */
+int vxpt_texture_table(vxpt_ctx *ctx, int32_t *out, int cap, int *n_textures, int64_t *n_texels);
 
 /* ---- voxel edits (VoxelEngine::update click path, VoxelEngine.cu:855-975, 1040-1346) ---- */
 /* performRayTraversal (:1040-1166) of the current camera ray on the world.  out: hit, hit x, y, z,

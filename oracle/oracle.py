@@ -51,6 +51,8 @@ def lib():
             "orc_terrain": (I, [P, I, I, I, F, F, I, I]),
             "orc_set_voxels": (I, [P, P, I, I, I]),
             "orc_set_prev_scene_empty": (None, [P, I]),
+            "orc_set_textures": (None, [P, P, ctypes.c_size_t, P, I]),
+            "orc_set_material_textures": (None, [P, I, I, I, I, I, F, I]),
             "orc_get_voxels": (I, [P, P]),
             "orc_set_material": (None, [P, I, F, F, F, F, I, F, I]),
             "orc_set_sky": (I, [P, F, F, F, F]),
@@ -160,6 +162,24 @@ class Oracle:
 
     def trace(self, it, y0=0, y1=None, primary_only=False):
         self.L.orc_trace(self.h, it, y0, self.H if y1 is None else y1, int(primary_only))
+
+    def set_textures(self, chains):
+        """chains: list of mip-level lists (level l = (S>>l, S>>l, 4) uint8 RGBA)."""
+        info, parts, off = [], [], 0
+        for levels in chains:
+            info += [levels[0].shape[0], len(levels) - 1]
+            for lv in levels:
+                info.append(off)
+                parts.append(np.ascontiguousarray(lv, np.uint8).reshape(-1))
+                off += lv.shape[0] * lv.shape[1]
+        self._texels = np.concatenate(parts) if parts else np.zeros(4, np.uint8)
+        self._texinfo = np.array(info, np.int32)
+        self.L.orc_set_textures(self.h, _p(self._texels), off, _p(self._texinfo), len(chains))
+
+    def set_material_textures(self, block_id, albedo=-1, normal=-1, rough=-1, metal=-1, uv_scale=1.0,
+                              world_grid=True):
+        self.L.orc_set_material_textures(self.h, block_id, albedo, normal, rough, metal, float(uv_scale),
+                                         int(world_grid))
 
     def set_prev_scene_empty(self, on):
         """The next trace's ReSTIR temporal visibility sees no previous scene (after a voxel edit)."""

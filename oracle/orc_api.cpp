@@ -158,6 +158,26 @@ void orc_trace(void *p, int it, int y0, int y1, int primaryOnly) {
 }
 void orc_post_trace(void *p) { post_trace_copies(static_cast<Ctx *>(p)->f); }
 void orc_set_prev_scene_empty(void *p, int on) { static_cast<Ctx *>(p)->s.prevSceneEmpty = on != 0; }
+// textures: nTex mip chains; info per texture = size, maxLod, then maxLod + 1 level offsets (texels)
+void orc_set_textures(void *p, const uint8_t *texels, size_t nTexels, const int *info, int nTex) {
+    Scene &s = static_cast<Ctx *>(p)->s;
+    s.texels.assign(texels, texels + 4 * nTexels);
+    s.textures.clear();
+    for (int i = 0; i < nTex; ++i) {
+        Texture t;
+        t.size = *info++;
+        t.maxLod = *info++;
+        for (int l = 0; l <= t.maxLod; ++l) t.off.push_back((unsigned)*info++);
+        s.textures.push_back(t);
+    }
+}
+void orc_set_material_textures(void *p, int blockId, int albedo, int normal, int rough, int metal, float uvScale,
+                               int worldGrid) {
+    Material &m = static_cast<Ctx *>(p)->s.mats[blockId];
+    m.tex[0] = albedo; m.tex[1] = normal; m.tex[2] = rough; m.tex[3] = metal;
+    m.uvScale = uvScale;
+    m.worldGridUV = worldGrid != 0;
+}
 // rows [y0, y1) the denoiser passes compute (multi-GPU band schedule; 0,0 = whole frame)
 void orc_set_band(void *p, int y0, int y1) {
     Frame &f = static_cast<Ctx *>(p)->f;

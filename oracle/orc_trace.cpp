@@ -362,6 +362,7 @@ bool prev_surface(Px &c, Surf &sf, int x, int y) {  // GetPrevSurface (Restir.h:
 struct Ray {
     F3 pos, wo, wi, radiance, bsdfOverPdf;
     float distance = kRayMax, pdf = 0;
+    float travelled = 0;  // sum of hit distances: ray cone width = spread * travelled (closesthit.cu:195)
     unsigned depth = 0;
     bool hitFirstDiffuse = false, terminate = false, curDiffuse = false, lastDiffuse = false;
 };
@@ -423,6 +424,50 @@ void on_miss(Px &c, Ray &rd) {  // miss.cu:9-82
     rd.terminate = true;
 }
 
+// tex2DLod on an RGBA8 mip chain (TextureManager.cu:228-246: wrap, linear, linear mip, unorm,
+// lod clamped to [0, maxLod]) with float filter weights
+struct TexSample { float r, g, b, a; };
+TexSample texel(const Scene &s, const Texture &t, int l, int x, int y) {
+    const int S = t.size >> l;
+    const uint8_t *p = s.texels.data() + 4 * ((size_t)t.off[l] + (size_t)(y * S + x));
+    return {p[0] / 255.0f, p[1] / 255.0f, p[2] / 255.0f, p[3] / 255.0f};
+}
+int wrap_i(int i, int S) {
+    const int m = i % S;
+    return m < 0 ? m + S : m;
+}
+TexSample tex_bilinear(const Scene &s, const Texture &t, int l, float u, float v) {
+    const int S = t.size >> l;
+    const float x = u * (float)S - 0.5f, y = v * (float)S - 0.5f;
+    const float fx = std::floor(x), fy = std::floor(y);
+    const float ax = x - fx, ay = y - fy;
+    const int x0 = wrap_i((int)fx, S), x1 = wrap_i((int)fx + 1, S), y0 = wrap_i((int)fy, S), y1 = wrap_i((int)fy + 1, S);
+    const TexSample a = texel(s, t, l, x0, y0), b = texel(s, t, l, x1, y0), c = texel(s, t, l, x0, y1),
+                    d = texel(s, t, l, x1, y1);
+    const float w00 = (1.0f - ax) * (1.0f - ay), w10 = ax * (1.0f - ay), w01 = (1.0f - ax) * ay, w11 = ax * ay;
+    return {a.r * w00 + b.r * w10 + c.r * w01 + d.r * w11, a.g * w00 + b.g * w10 + c.g * w01 + d.g * w11,
+            a.b * w00 + b.b * w10 + c.b * w01 + d.b * w11, a.a * w00 + b.a * w10 + c.a * w01 + d.a * w11};
+}
+TexSample tex_lod(const Scene &s, int id, float u, float v, float lod) {
+    const Texture &t = s.textures[id];
+    lod = std::fmin(std::fmax(lod, 0.0f), (float)t.maxLod);
+    const int l0 = (int)std::floor(lod);
+    const float fl = lod - (float)l0;
+    const TexSample c0 = tex_bilinear(s, t, l0, u, v);
+    if (!(fl > 0.0f)) return c0;
+    const TexSample c1 = tex_bilinear(s, t, std::min(l0 + 1, t.maxLod), u, v);
+    return {c0.r * (1.0f - fl) + c1.r * fl, c0.g * (1.0f - fl) + c1.g * fl, c0.b * (1.0f - fl) + c1.b * fl,
+            c0.a * (1.0f - fl) + c1.a * fl};
+}
+// Camera::getRayConeWidth (Camera.h:133-149)
+float ray_cone_spread(const Camera &cam, int px, int py) {
+    const F2 pc = (F2((float)px, (float)py) + 0.5f) - cam.res / 2.0f;
+    const F2 po(std::copysign(0.5f, pc.x), std::copysign(0.5f, pc.y));
+    const F2 uvN = (pc - po) * cam.invRes * 2.0f, uvF = (pc + po) * cam.invRes * 2.0f;
+    const F2 pN = uvN * cam.tanHalfFov, pF = uvF * cam.tanHalfFov;
+    return std::atan(std::sqrt(pF.x * pF.x + pF.y * pF.y)) - std::atan(std::sqrt(pN.x * pN.x + pN.y * pN.y));
+}
+
 void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
     const Scene &s = c.s;
     Frame &f = c.f;
@@ -445,13 +490,47 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
     State st;
     st.geoNormal = geoNormal;
     st.wo = rd.wo;
-    st.albedo = max3f(m.albedo, F3(0.001f));
-    st.roughness = m.roughness;
+    st.metallic = m.metallic;
+    if (!s.textures.empty()) {  // closesthit.cu:167-254
+        rd.travelled += h.t;
+        const float cone = ray_cone_spread(s.cam, c.px, c.py) * rd.travelled;
+        F2 tc(0.0f, 0.0f);
+        const F3 p = frontPos;
+        if (m.worldGridUV) {
+            if (std::fabs(geoNormal.x) > 0.9f) tc = F2(std::fmod(p.z, m.uvScale), std::fmod(p.y, m.uvScale));
+            else if (std::fabs(geoNormal.y) > 0.9f) tc = F2(std::fmod(p.x, m.uvScale), std::fmod(p.z, m.uvScale));
+            else if (std::fabs(geoNormal.z) > 0.9f) tc = F2(std::fmod(p.x, m.uvScale), std::fmod(p.y, m.uvScale));
+        }
+        tc = tc / m.uvScale;
+        const float mip0 = std::sqrt(1024.0f * 1024.0f + 1024.0f * 1024.0f);
+        const float lod = std::log2(cone / mymax(dot(geoNormal, rd.wo), 0.2f) / m.uvScale * 2.0f * mip0) - 3.0f;
+        st.albedo = m.albedo;
+        if (m.tex[0] >= 0) {
+            const TexSample t = tex_lod(s, m.tex[0], tc.x, tc.y, lod);
+            st.albedo = st.albedo * F3(t.r, t.g, t.b);
+        }
+        st.albedo = max3f(st.albedo, F3(0.001f));
+        st.roughness = m.roughness;
+        if (m.tex[2] >= 0) st.roughness = tex_lod(s, m.tex[2], tc.x, tc.y, lod).r;
+        if (m.tex[3] >= 0) st.metallic = tex_lod(s, m.tex[3], tc.x, tc.y, lod).r > 0.5f;
+        if (m.tex[1] >= 0) {
+            const TexSample t = tex_lod(s, m.tex[1], tc.x, tc.y, lod);
+            F3 n = normalize(F3(t.r, t.g, t.b) - 0.5f);
+            n.x = -n.x;
+            n.y = -n.y;
+            align_vector(geoNormal, n);
+            st.normal = n;
+        } else {
+            st.normal = st.geoNormal;
+        }
+    } else {
+        st.albedo = max3f(m.albedo, F3(0.001f));
+        st.roughness = m.roughness;
+        st.normal = st.geoNormal;
+    }
     if (rd.hitFirstDiffuse) st.roughness = mymin(st.roughness * 2.0f + 0.1f, 1.0f);
     bool isDiffuse = st.roughness > kRoughThresh;
-    st.metallic = m.metallic;
     st.translucency = m.translucency;
-    st.normal = st.geoNormal;
     st.normal = lerp3(st.geoNormal, st.normal, 0.2f);
     rd.curDiffuse = isDiffuse;
     if (rd.depth == 0) {

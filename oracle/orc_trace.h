@@ -14,13 +14,22 @@ struct Reservoir {  // DIReservoir (RestirCommon.h:6-12)
 };
 static_assert(sizeof(Reservoir) == 20, "reservoir is 20 B");
 
-struct Material {  // MaterialParameter subset (SystemParameter.h:11-38), untextured
+struct Material {  // MaterialParameter subset (SystemParameter.h:11-38)
     F3 albedo{1, 1, 1};
     float roughness = 0.5f;
     bool metallic = false;
     float translucency = 0.0f;
     int materialId = -1;
     bool isEmissive = false, isThinfilm = false;
+    int tex[4] = {-1, -1, -1, -1};  // albedo, normal, roughness, metallic texture (-1 = none)
+    float uvScale = 1.0f;
+    bool worldGridUV = false;
+};
+
+// A texture: RGBA8 mip chain (TextureManager.cu:216-259), level l at texels[off[l]], edge size >> l
+struct Texture {
+    int size = 0, maxLod = 0;
+    std::vector<unsigned> off;
 };
 
 struct DenoiseParams {  // DenoisingParams (GlobalSettings.h:82-141) with yaml values
@@ -59,6 +68,8 @@ struct Scene {
     // the pass after a geometry change: prevTopObject = 0 (OptixRenderer.cpp:916-919, 464), so the
     // ReSTIR temporal visibility rays (closesthit.cu:736-755) traverse no scene and see the light
     bool prevSceneEmpty = false;
+    std::vector<uint8_t> texels;      // RGBA8 of every texture's mip chain
+    std::vector<Texture> textures;    // empty: untextured shading
 };
 
 // One 1-spp trace pass (OptixRenderer::render, OptixRenderer.cpp:411-485),

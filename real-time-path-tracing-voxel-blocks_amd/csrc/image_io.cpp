@@ -228,6 +228,19 @@ float ssim(const Image &a, const Image &b) {
 
 }  // namespace
 
+namespace vx {
+// PNG decode for the texture loader (8-bit grey / grey+alpha / RGB / RGBA / palette -> RGB)
+bool decode_png(const std::string &path, int &w, int &h, int &ch, std::vector<uint8_t> &px) {
+    Image im;
+    if (!read_png(path, im)) return false;
+    w = im.w;
+    h = im.h;
+    ch = im.ch;
+    px.swap(im.px);
+    return true;
+}
+}  // namespace vx
+
 extern "C" {
 
 int vxpt_write_png_rgba32f(const char *path, int w, int h, const float *rgba) {

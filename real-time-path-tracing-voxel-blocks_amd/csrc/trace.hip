@@ -343,7 +343,8 @@ VX_D void path_end(const TraceArgs &a, int px, int py, V3 radiance, float primar
 VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segRad, V3 bop, float pdf, bool terminate,
                   bool curDiffuse) {
     const WaveBufs &w = a.wb;
-    V3 thr = xyz(w.pThr[s]), rad = xyz(w.pRad[s]);
+    const float4 rad4 = w.pRad[s];
+    V3 thr = xyz(w.pThr[s]), rad = xyz(rad4);
     rad += thr * segRad;
     const bool cont = !(terminate || pdf <= 0.0f || is_null(bop));
     if (cont) thr *= bop;
@@ -356,7 +357,7 @@ VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segR
         meta.x &= ~(F_ALIVE | F_NEE | F_RESTIR);
     } else {
         w.pThr[s] = f4(thr, 0.0f);
-        w.pRad[s] = f4(rad, 0.0f);
+        w.pRad[s] = f4(rad, rad4.w);  // .w: the path's travelled distance (ray cone)
     }
 }
 
@@ -440,13 +441,23 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     SurfS sf;
     sf.geoNormal = ng;
     sf.wo = wo;
-    sf.albedo = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
-    sf.roughness = m.roughness;
+    sf.metallic = m.metallic != 0;
+    if (a.texEnabled) {
+        // ray cone (closesthit.cu:194-195): width = spread * the path's travelled distance
+        const float travelled = w.pRad[s].w + h.t;
+        w.pRad[s].w = travelled;
+        sf.albedo = V3(m.albedo[0], m.albedo[1], m.albedo[2]);
+        sf.roughness = m.roughness;
+        apply_textures(a.texels, a.tex, m, frontPos, ng, wo, ray_cone_spread(a.cam, px, py) * travelled, sf.albedo,
+                       sf.roughness, sf.metallic, sf.normal);
+    } else {
+        sf.albedo = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
+        sf.roughness = m.roughness;
+        sf.normal = lerp3(ng, ng, 0.2f);
+    }
     if (meta.x & F_HFD) sf.roughness = fminf(sf.roughness * 2.0f + 0.1f, 1.0f);
     const bool isDiffuse = sf.roughness > kRoughThresh;
-    sf.metallic = m.metallic != 0;
     sf.translucency = m.translucency;
-    sf.normal = lerp3(ng, ng, 0.2f);
     if (seg == 0) {
         a.cur.material[pi] = (float)m.materialId;
         a.cur.normalRough[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, sf.roughness);

@@ -699,5 +699,84 @@ VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
     return emission;
 }
 
+// ---------------------------------------------------------------- textures
+// tex2DLod on an RGBA8 mip chain (TextureManager.cu:228-246: wrap addressing, linear filter,
+// linear mip filter, normalized coordinates, unorm reads, lod clamped to [0, maxLod]).  The
+// hardware's 8-bit fixed-point filter weights are float weights here (the oracle does the same).
+VX_D float4 texel_f(const uchar4 *t, unsigned off, int S, int x, int y) {
+    const uchar4 v = t[off + (unsigned)(y * S + x)];
+    return make_float4(v.x / 255.0f, v.y / 255.0f, v.z / 255.0f, v.w / 255.0f);
+}
+VX_D int wrap_i(int i, int S) {
+    const int m = i % S;
+    return m < 0 ? m + S : m;
+}
+VX_D V4 tex_bilinear(const uchar4 *t, const TexInfo &ti, int l, float u, float v) {
+    const int S = ti.size >> l;
+    const float x = u * (float)S - 0.5f, y = v * (float)S - 0.5f;
+    const float fx = floorf(x), fy = floorf(y);
+    const float ax = x - fx, ay = y - fy;
+    const int x0 = wrap_i((int)fx, S), x1 = wrap_i((int)fx + 1, S);
+    const int y0 = wrap_i((int)fy, S), y1 = wrap_i((int)fy + 1, S);
+    const unsigned o = ti.off[l];
+    const float4 a = texel_f(t, o, S, x0, y0), b = texel_f(t, o, S, x1, y0);
+    const float4 c = texel_f(t, o, S, x0, y1), d = texel_f(t, o, S, x1, y1);
+    const float w00 = (1.0f - ax) * (1.0f - ay), w10 = ax * (1.0f - ay), w01 = (1.0f - ax) * ay, w11 = ax * ay;
+    return V4(a.x * w00 + b.x * w10 + c.x * w01 + d.x * w11, a.y * w00 + b.y * w10 + c.y * w01 + d.y * w11,
+              a.z * w00 + b.z * w10 + c.z * w01 + d.z * w11, a.w * w00 + b.w * w10 + c.w * w01 + d.w * w11);
+}
+VX_D V4 tex_lod(const uchar4 *t, const TexInfo &ti, float u, float v, float lod) {
+    lod = fminf(fmaxf(lod, 0.0f), (float)ti.maxLod);
+    const int l0 = (int)floorf(lod);
+    const float fl = lod - (float)l0;
+    const V4 c0 = tex_bilinear(t, ti, l0, u, v);
+    if (!(fl > 0.0f)) return c0;
+    const V4 c1 = tex_bilinear(t, ti, min(l0 + 1, ti.maxLod), u, v);
+    return c0 * (1.0f - fl) + c1 * fl;
+}
+
+// Camera::getRayConeWidth (Camera.h:133-149): the angle one pixel subtends
+VX_D float ray_cone_spread(const CamDev &cam, int px, int py) {
+    const V2 pc = (V2((float)px, (float)py) + 0.5f) - cam.res / 2.0f;
+    const V2 po(copysignf(0.5f, pc.x), copysignf(0.5f, pc.y));
+    const V2 uvN = (pc - po) * cam.invRes * 2.0f, uvF = (pc + po) * cam.invRes * 2.0f;
+    const V2 pN = uvN * cam.tanHalfFov, pF = uvF * cam.tanHalfFov;
+    return atanf(sqrtf(pF.x * pF.x + pF.y * pF.y)) - atanf(sqrtf(pN.x * pN.x + pN.y * pN.y));
+}
+
+// Textured MaterialState (closesthit.cu:167-254): world-grid uv of the front position, ray-cone
+// lod, albedo x texture, roughness / metallic from textures, tangent-space normal map aligned to
+// the face and blended at strength 0.2.  coneWidth = the ray cone's width at this hit.
+VX_D void apply_textures(const uchar4 *texels, const TexInfo *tex, const MatDev &m, V3 pos, V3 ng, V3 wo,
+                         float coneWidth, V3 &albedo, float &roughness, bool &metallic, V3 &normal) {
+    V2 tc(0.0f, 0.0f);
+    if (m.worldGridUV) {
+        if (fabsf(ng.x) > 0.9f) tc = V2(fmodf(pos.z, m.uvScale), fmodf(pos.y, m.uvScale));
+        else if (fabsf(ng.y) > 0.9f) tc = V2(fmodf(pos.x, m.uvScale), fmodf(pos.z, m.uvScale));
+        else if (fabsf(ng.z) > 0.9f) tc = V2(fmodf(pos.x, m.uvScale), fmodf(pos.y, m.uvScale));
+    }
+    tc = tc / m.uvScale;
+    const float mip0 = sqrtf(1024.0f * 1024.0f + 1024.0f * 1024.0f);  // MaterialParameter::texSize (1024, 1024)
+    const float lod = log2f(coneWidth / fmaxf(dot(ng, wo), 0.2f) / m.uvScale * 2.0f * mip0) - 3.0f;
+    if (m.tex[0] >= 0) {
+        const V4 c = tex_lod(texels, tex[m.tex[0]], tc.x, tc.y, lod);
+        albedo = albedo * V3(c.x, c.y, c.z);
+    }
+    albedo = max3(albedo, V3(0.001f));
+    if (m.tex[2] >= 0) roughness = tex_lod(texels, tex[m.tex[2]], tc.x, tc.y, lod).x;
+    if (m.tex[3] >= 0) metallic = tex_lod(texels, tex[m.tex[3]], tc.x, tc.y, lod).x > 0.5f;
+    if (m.tex[1] >= 0) {
+        const V4 c = tex_lod(texels, tex[m.tex[1]], tc.x, tc.y, lod);
+        V3 n = normalize(V3(c.x - 0.5f, c.y - 0.5f, c.z - 0.5f));
+        n.x = -n.x;
+        n.y = -n.y;
+        align_vector(ng, n);
+        normal = n;
+    } else {
+        normal = ng;
+    }
+    normal = lerp3(ng, normal, 0.2f);
+}
+
 }  // namespace
 }  // namespace vx

@@ -20,13 +20,24 @@ struct CamDev {
     }
 };
 
-struct MatDev {  // per block id, untextured MaterialParameter subset
+struct MatDev {  // per block id, MaterialParameter subset (SystemParameter.h:11-38)
     float albedo[3];
     float roughness;
     float translucency;
     int metallic;
     int materialId;
     int thin;
+    int tex[4] = {-1, -1, -1, -1};  // albedo, normal, roughness, metallic texture (-1 = none)
+    float uvScale = 1.0f;
+    int worldGridUV = 0;
+};
+
+// One texture's RGBA8 mip chain in the texel buffer (TextureManager.cu:216-259 layout: square,
+// power of two, levels 0..maxLod = log2(size) - 2); off[l] = first texel of level l
+constexpr int kMaxTexLevels = 14;
+struct TexInfo {
+    int size, maxLod;
+    unsigned off[kMaxTexLevels];
 };
 
 struct AliasBin { float q, p; int alias; };
@@ -138,6 +149,9 @@ struct TraceArgs {
     int numCU;                  // compute units of the device (traversal grid sizing)
     int iterCap, iterCap2;      // outer DDA iterations before a ray moves to the level-1 / level-2 straggler queue
     int prevSceneEmpty;         // the pass after a voxel edit: temporal visibility rays see no previous scene
+    const TexInfo *tex;         // texture table (nullptr: no textures loaded)
+    const uchar4 *texels;       // every texture's mip chain, RGBA8
+    int texEnabled;
 };
 
 // kernel launchers (defined in the .hip translation units)
@@ -217,6 +231,7 @@ struct PostArgs {
     float sunU, sunV, sunLuminance;
 };
 hipError_t launch_postprocess(const PostArgs &a, hipStream_t st);
+bool decode_png(const std::string &path, int &w, int &h, int &ch, std::vector<uint8_t> &px);
 
 hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st);

@@ -169,6 +169,15 @@ struct vxpt_ctx {
     DBuf<float> solar, limb;
     bool skyReady = false;
 
+    // textures (materials.yaml `textures`, TextureManager): per block the albedo / normal /
+    // roughness / metallic paths, the loaded RGBA8 mip chains and their table
+    std::string texPath[13][4];
+    DBuf<uchar4> texels;
+    DBuf<TexInfo> texTable;
+    std::vector<TexInfo> hTex;
+    size_t nTexels = 0;
+    int texEnabled = 0;
+
     // blue noise
     DBuf<uint8_t> bnSobol, bnScramble, bnRank;
 
@@ -460,6 +469,7 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_CELL_MASKS: p = c->cellMask.p; bytes = (size_t)c->nBricks * 8; return !forWrite && c->cellMask.p;
         case VXPT_BUF_BRICK_IDS: p = c->bricks.p; bytes = (size_t)c->nBricks * 64; return !forWrite && c->bricks.p;
         case VXPT_BUF_MACRO_MASKS: p = c->macro.p; bytes = (size_t)c->nBricks / 64 * 8; return !forWrite && c->macro.p;
+        case VXPT_BUF_TEXELS: p = c->texels.p; bytes = c->nTexels * 4; return !forWrite && c->texels.p;
         default: return false;
     }
 }
@@ -640,6 +650,9 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
     a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
     a.prevSceneEmpty = c->prevSceneEmpty;
+    a.tex = c->texTable.p;
+    a.texels = c->texels.p;
+    a.texEnabled = (c->texEnabled && c->texTable.p) ? 1 : 0;
     c->prevSceneEmpty = 0;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_trace(a, c->stream, c->haloPending ? c->haloDone : nullptr));
@@ -1107,11 +1120,18 @@ int vxpt_load_settings(vxpt_ctx *c) {
     std::ifstream fm(c->dataDir + "/assets/materials.yaml");
     if (!fm) return fail(c, VXPT_ERR_IO, "missing assets/materials.yaml");
     std::vector<std::string> ids;
-    std::vector<std::map<std::string, std::string>> props;
+    std::vector<std::map<std::string, std::string>> props, texs;
     while (std::getline(fm, line)) {
         const std::string tl = trim(line);
-        if (tl.rfind("- id:", 0) == 0) { ids.push_back(trim(tl.substr(5))); props.emplace_back(); }
-        else if (tl.rfind("properties:", 0) == 0 && !props.empty()) props.back() = parse_flow_map(tl);
+        if (tl.rfind("- id:", 0) == 0) {
+            ids.push_back(trim(tl.substr(5)));
+            props.emplace_back();
+            texs.emplace_back();
+        } else if (tl.rfind("properties:", 0) == 0 && !props.empty()) {
+            props.back() = parse_flow_map(tl);
+        } else if (tl.rfind("textures:", 0) == 0 && !texs.empty()) {
+            texs.back() = parse_flow_map(tl);
+        }
     }
     std::ifstream fb(c->dataDir + "/assets/blocks.yaml");
     if (!fb) return fail(c, VXPT_ERR_IO, "missing assets/blocks.yaml");
@@ -1134,6 +1154,10 @@ int vxpt_load_settings(vxpt_ctx *c) {
             auto v = parse_list(p["albedo"]);
             if (v.size() == 3) { md.albedo[0] = v[0]; md.albedo[1] = v[1]; md.albedo[2] = v[2]; }
         }
+        if (p.count("uv_scale")) md.uvScale = (float)std::atof(p["uv_scale"].c_str());
+        if (p.count("use_world_grid_uv")) md.worldGridUV = as_bool(p["use_world_grid_uv"]) ? 1 : 0;
+        static const char *kTexKeys[4] = {"albedo", "normal", "roughness", "metallic"};
+        for (int k = 0; k < 4; ++k) c->texPath[bid][k] = texs[mi].count(kTexKeys[k]) ? texs[mi][kTexKeys[k]] : "";
         c->mats[bid] = md;
     }
     return VXPT_OK;
@@ -1282,6 +1306,103 @@ int vxpt_set_camera(vxpt_ctx *c, const vxpt_camera *cur, const vxpt_camera *prev
     if (!c || !cur) return VXPT_ERR_ARG;
     c->cam = make_camera(c->W, c->H, *cur, &c->camYaw, &c->camPitch);
     c->prevCam = make_camera(c->W, c->H, prev ? *prev : *cur, nullptr, nullptr);
+    return VXPT_OK;
+}
+
+// TextureManager::initWithMaterialPaths + LoadTexturesFromPaths (TextureManager.cu:133-330):
+// every texture the cube materials name, in sorted path order (= texture id); decoded, square
+// power-of-two, expanded to RGBA8 (1 channel -> (v,0,0,1), 2 -> (v,a,0,1), 3 -> (r,g,b,1): the
+// unorm reads of the BC4/BC5/BC7 formats), levels 0..log2(size)-2 by 2x2 box averages truncated
+// to 8 bits (fillMipmapKernel, :82-117, and its CPU twin, :390-414).  BC7 itself is not
+// reproduced (NVTT): the texels are the uncompressed ones.
+int vxpt_load_textures(vxpt_ctx *c, const char *root, int *loaded) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    const std::string base = root ? root : c->dataDir;
+    std::vector<std::string> paths;
+    for (int b = 1; b <= 12; ++b)
+        for (int k = 0; k < 4; ++k)
+            if (!c->texPath[b][k].empty()) paths.push_back(c->texPath[b][k]);
+    std::sort(paths.begin(), paths.end());
+    paths.erase(std::unique(paths.begin(), paths.end()), paths.end());
+    std::vector<uchar4> texels;
+    std::vector<TexInfo> table;
+    std::map<std::string, int> idOf;
+    for (const std::string &pth : paths) {
+        int w, h, ch;
+        std::vector<uint8_t> px;
+        if (!decode_png(base + "/" + pth, w, h, ch, px)) continue;  // the reference skips it too (:180-187)
+        if (w != h || w < 4 || (w & (w - 1)) != 0) continue;
+        int maxLod = 0;
+        while ((4 << maxLod) < w) ++maxLod;  // log2(w) - 2
+        if (maxLod >= kMaxTexLevels) continue;
+        TexInfo ti{};
+        ti.size = w;
+        ti.maxLod = maxLod;
+        ti.off[0] = (unsigned)texels.size();
+        texels.resize(texels.size() + (size_t)w * w);
+        uchar4 *l0 = texels.data() + ti.off[0];
+        for (size_t i = 0; i < (size_t)w * w; ++i) {
+            const uint8_t *q = px.data() + i * ch;
+            l0[i] = ch == 1 ? make_uchar4(q[0], 0, 0, 255)
+                  : ch == 2 ? make_uchar4(q[0], q[1], 0, 255)
+                  : ch == 3 ? make_uchar4(q[0], q[1], q[2], 255) : make_uchar4(q[0], q[1], q[2], q[3]);
+        }
+        for (int l = 1; l <= maxLod; ++l) {
+            const int S = w >> l, P = S * 2;
+            ti.off[l] = (unsigned)texels.size();
+            texels.resize(texels.size() + (size_t)S * S);
+            const uchar4 *src = texels.data() + ti.off[l - 1];
+            uchar4 *dst = texels.data() + ti.off[l];
+            for (int y = 0; y < S; ++y)
+                for (int x = 0; x < S; ++x) {
+                    const uchar4 a = src[(2 * y) * P + 2 * x], b2 = src[(2 * y) * P + 2 * x + 1];
+                    const uchar4 c2 = src[(2 * y + 1) * P + 2 * x], d = src[(2 * y + 1) * P + 2 * x + 1];
+                    dst[y * S + x] = make_uchar4((a.x + b2.x + c2.x + d.x) >> 2, (a.y + b2.y + c2.y + d.y) >> 2,
+                                                 (a.z + b2.z + c2.z + d.z) >> 2, (a.w + b2.w + c2.w + d.w) >> 2);
+                }
+        }
+        idOf[pth] = (int)table.size();
+        table.push_back(ti);
+    }
+    for (int b = 1; b <= 12; ++b)
+        for (int k = 0; k < 4; ++k) {
+            const auto it = idOf.find(c->texPath[b][k]);
+            c->mats[b].tex[k] = it == idOf.end() ? -1 : it->second;
+        }
+    c->hTex = table;
+    c->nTexels = texels.size();
+    if (!table.empty()) {
+        if (int r = upload_vec(c, c->texels, texels.data(), texels.size())) return r;
+        if (int r = upload_vec(c, c->texTable, table.data(), table.size())) return r;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    c->texEnabled = table.empty() ? 0 : 1;
+    if (loaded) *loaded = (int)table.size();
+    return VXPT_OK;
+}
+
+int vxpt_enable_textures(vxpt_ctx *c, int on) {
+    if (!c) return VXPT_ERR_ARG;
+    c->texEnabled = (on && !c->hTex.empty()) ? 1 : 0;
+    return VXPT_OK;
+}
+
+// the loaded table: per texture size, maxLod, then maxLod + 1 level offsets (in texels)
+int vxpt_texture_table(vxpt_ctx *c, int32_t *out, int cap, int *n_textures, int64_t *n_texels) {
+    if (!c) return VXPT_ERR_ARG;
+    int k = 0;
+    for (const TexInfo &t : c->hTex) {
+        if (out && k + 2 + t.maxLod + 1 > cap) return VXPT_ERR_ARG;
+        if (out) {
+            out[k] = t.size;
+            out[k + 1] = t.maxLod;
+            for (int l = 0; l <= t.maxLod; ++l) out[k + 2 + l] = (int32_t)t.off[l];
+        }
+        k += 2 + t.maxLod + 1;
+    }
+    if (n_textures) *n_textures = (int)c->hTex.size();
+    if (n_texels) *n_texels = (int64_t)c->nTexels;
     return VXPT_OK;
 }
 

@@ -48,6 +48,7 @@ struct Options {
     std::string dataDir = "data";
     std::string perfReport;
     bool testSequence = false, removal20 = false, removalCircle = false;
+    bool textures = true;
 };
 
 void usage(const char *argv0) {
@@ -71,6 +72,7 @@ void usage(const char *argv0) {
               << "  --device <int>         HIP device (default: 0)\n"
               << "  --data <dir>           Data directory: settings/, assets/, tables/ (default: data)\n"
               << "  --perf-report <file>   Performance report path (default: <output>_performance_report.txt)\n"
+              << "  --no-textures          Untextured materials (textures load from <data>/textures when present)\n"
               << "  --help, -h             Show this help message\n";
 }
 
@@ -109,6 +111,7 @@ int parse(int argc, char **argv, Options &o) {
         else if (a == "--device") { if (!(v = next("--device"))) return -1; o.device = std::atoi(v); }
         else if (a == "--data") { if (!(v = next("--data"))) return -1; o.dataDir = v; }
         else if (a == "--perf-report") { if (!(v = next("--perf-report"))) return -1; o.perfReport = v; }
+        else if (a == "--no-textures") o.textures = false;
         else if (a == "--test-sequence") o.testSequence = true;
         else if (a == "--test-remove20") o.removal20 = true;
         else if (a == "--test-remove-circle") o.removalCircle = true;
@@ -193,6 +196,11 @@ int main(int argc, char **argv) {
 
     // mainOffline.cpp:140-198: settings, assets, the voxel world
     if (vxpt_load_settings(ctx) != VXPT_OK) return fail("loading settings");
+    if (o.textures) {  // TextureManager::initWithMaterialPaths: every material texture found is used
+        int nTex = 0;
+        if (vxpt_load_textures(ctx, nullptr, &nTex) != VXPT_OK) return fail("loading textures");
+        std::cout << "Textures loaded: " << nTex << (nTex ? "" : " (untextured materials)") << std::endl;
+    }
     if (vxpt_generate_terrain(ctx, o.chunks[0], o.chunks[1], o.chunks[2], 32.0f, 32.0f * o.chunks[0], 0) != VXPT_OK)
         return fail("generating terrain");
 

@@ -23,7 +23,7 @@ BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERI
            PREV_NORMAL_ROUGH=8, PREV_GEO_NORMAL_THIN=9, PREV_ALBEDO=10, PREV_MAT_PARAM=11, PREV_DEPTH=12,
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
            PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38,
-           OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42)
+           OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42, TEXELS=43)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
@@ -119,6 +119,9 @@ def load_library(path=LIB_PATH):
         "vxpt_get_camera": (I, [P, I, P]),
         "vxpt_set_camera_angles": (I, [P, P, F, F, F]),
         "vxpt_pick_block": (I, [P, P]),
+        "vxpt_load_textures": (I, [P, ctypes.c_char_p, P]),
+        "vxpt_enable_textures": (I, [P, I]),
+        "vxpt_texture_table": (I, [P, P, I, P, P]),
         "vxpt_set_block": (I, [P, I, I, I, I]),
         "vxpt_click_block": (I, [P, I, P]),
         "vxpt_save_world": (I, [P, ctypes.c_char_p, ctypes.c_char_p]),
@@ -246,6 +249,32 @@ class Renderer:
         self._chk(self.lib.vxpt_set_camera_angles(self.ctx, _ptr(p), float(yaw), float(pitch), float(fov)),
                   "vxpt_set_camera_angles")
 
+    # --- textures (TextureManager; closesthit.cu:167-254) ---
+    def load_textures(self, root=None):
+        n = ctypes.c_int(0)
+        self._chk(self.lib.vxpt_load_textures(self.ctx, str(root).encode() if root else None, ctypes.byref(n)),
+                  "vxpt_load_textures")
+        return n.value
+
+    def enable_textures(self, on=True):
+        self._chk(self.lib.vxpt_enable_textures(self.ctx, int(bool(on))), "vxpt_enable_textures")
+
+    def texture_table(self):
+        """[(size, maxLod, [level offsets in texels])], total texels."""
+        n, nt = ctypes.c_int(0), ctypes.c_int64(0)
+        self._chk(self.lib.vxpt_texture_table(self.ctx, None, 0, ctypes.byref(n), ctypes.byref(nt)),
+                  "vxpt_texture_table")
+        out = np.zeros(16 * max(n.value, 1), np.int32)
+        self._chk(self.lib.vxpt_texture_table(self.ctx, _ptr(out), len(out), ctypes.byref(n), ctypes.byref(nt)),
+                  "vxpt_texture_table")
+        tabs, k = [], 0
+        for _ in range(n.value):
+            size, ml = int(out[k]), int(out[k + 1])
+            tabs.append((size, ml, [int(v) for v in out[k + 2:k + 3 + ml]]))
+            k += 3 + ml
+        self._ntexels = nt.value
+        return tabs, nt.value
+
     # --- voxel edits (VoxelEngine click path) and world files (WorldSceneManager) ---
     @staticmethod
     def _pick_dict(o):
@@ -372,6 +401,8 @@ class Renderer:
         if which == BUF["VOXELS"]:
             cx, cy, cz = self.chunks
             return np.zeros(cx * cy * cz * 32768, np.uint8)
+        if which == BUF["TEXELS"]:
+            return np.zeros((self.texture_table()[1], 4), np.uint8)
         if which in (BUF["OCTANT_TABLES"], BUF["CELL_MASKS"], BUF["BRICK_IDS"], BUF["MACRO_MASKS"]):
             nb = int(np.prod(self.chunks)) * 512
             return {BUF["OCTANT_TABLES"]: np.zeros(8 * nb, np.uint8), BUF["CELL_MASKS"]: np.zeros(nb, np.uint64),
