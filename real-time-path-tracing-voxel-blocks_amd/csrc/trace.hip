@@ -714,11 +714,15 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     unsigned cached = 0;
     int selLoop = -1;
     float tapM0 = 0, tapM1 = 0, tapM2 = 0;
+    const V2 jit(bn_rand(a.bn, px, py, a.iterationIndex - 1, 0), bn_rand(a.bn, px, py, a.iterationIndex - 1, 1));
+    V3 vd0(0.0f), vd1(0.0f), vd2(0.0f);  // the accepted taps' view directions, for the bias correction
     for (int i = 0; i < 3; ++i) {
         const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
         const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
         SurfS ts;
-        if (!prev_surface(a, px, py, ts, x, y)) continue;
+        V3 vd;
+        if (!prev_surface(a, jit, ts, x, y, nullptr, &vd)) continue;
+        if (i == 0) vd0 = vd; else if (i == 1) vd1 = vd; else vd2 = vd;
         const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
         const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
         const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
@@ -741,15 +745,16 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     qr.id0 = 4 * s;
     qr.d = ls.position;
     qr.tmax = kRayMax;
+    LSample sel = invalid_ls();  // the combined reservoir's light (the same for every tap)
+    if (rr.lightData != 0) light_from_res(k, sel, rr);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (rr.lightData != 0 && (cached & (1u << i))) {
             const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
             const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
             SurfS ts;
-            prev_surface(a, px, py, ts, x, y);
-            LSample sel = invalid_ls();
-            light_from_res(k, sel, rr);
+            const V3 vdi = i == 0 ? vd0 : (i == 1 ? vd1 : vd2);
+            prev_surface(a, jit, ts, x, y, &vdi, nullptr);
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;
             // prevSceneEmpty: OptiX's null prevTopObject -- the ray misses, the sample is visible

@@ -643,16 +643,23 @@ VX_D int reflect_view(int p, int n) {
     return p;
 }
 
-VX_D bool prev_surface(const TraceArgs &a, int px, int py, SurfS &sf, int x, int y) {
+// GetPrevSurface (Restir.h): the previous pass's G-buffer at (x, y).  j = the previous pass's
+// camera jitter of the shading pixel (bn_rand(px, py, iterationIndex - 1, 0 / 1): the same for
+// every tap); vd = the tap's view direction, computed when vdIn is null and returned in vdOut.
+VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const V3 *vdIn, V3 *vdOut) {
     if (x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y) return false;
     const size_t i = (size_t)y * a.W + x;
     sf.depth = a.prev.depth[i];
     if (sf.depth == kRayMax) return false;
     const float4 nr = a.prev.normalRough[i], gt = a.prev.geoNormalThin[i], mp = a.prev.matParam[i];
-    const float j0 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 0);
-    const float j1 = bn_rand(a.bn, px, py, a.iterationIndex - 1, 1);
-    const V2 uv = (V2((float)x, (float)y) + V2(j0, j1)) * a.prevCam.invRes;
-    const V3 vd = a.prevCam.uv_to_dir(uv);
+    V3 vd;
+    if (vdIn) {
+        vd = *vdIn;
+    } else {
+        const V2 uv = (V2((float)x, (float)y) + j) * a.prevCam.invRes;
+        vd = a.prevCam.uv_to_dir(uv);
+    }
+    if (vdOut) *vdOut = vd;
     sf.pos = a.prevCam.pos + vd * sf.depth;
     sf.wo = -vd;
     sf.normal = V3(nr.x, nr.y, nr.z);
