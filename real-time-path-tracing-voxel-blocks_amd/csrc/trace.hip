@@ -504,8 +504,8 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         const LSample cand = sun_ls(k, idx);
         const int sx = idx % k.sunW, sy = idx / k.sunW;
         const V2 uv((sx + 0.5f) / float(k.sunW), (sy + 0.5f) / float(k.sunH));
-        const float blended = mis_weight(sf, cand, src, sunMis, brdfMis);
-        const float tp = target_pdf(cand, sf);
+        float blended, tp;
+        mis_and_target(sf, cand, src, sunMis, brdfMis, blended, tp);
         const float rr = rng.next();
         if (stream_sample(sunRes, kSunLight, uv, rr, tp, 1.0f / blended)) sunSel = idx;
     }
@@ -520,8 +520,8 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         const LSample cand = sky_ls(k, idx);
         const int sx = idx % k.skyW, sy = idx / k.skyW;
         const V2 uv((sx + 0.5f) / float(k.skyW), (sy + 0.5f) / float(k.skyH));
-        const float blended = mis_weight(sf, cand, src, skyMis, brdfMis);
-        const float tp = target_pdf(cand, sf);
+        float blended, tp;
+        mis_and_target(sf, cand, src, skyMis, brdfMis, blended, tp);
         const float rr = rng.next();
         if (stream_sample(skyRes, kSkyLight, uv, rr, tp, 1.0f / blended)) skySel = idx;
     }
@@ -622,9 +622,9 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
             }
         }
         if (lightSrcPdf != 0.0f) {
-            const float tp = target_pdf(cand, sf);
             const float misW = (li == kSkyLight) ? skyMis : ((li == kSunLight) ? sunMis : 0.0f);
-            const float blended = mis_weight(sf, cand, lightSrcPdf, misW, brdfMis);
+            float blended, tp;
+            mis_and_target(sf, cand, lightSrcPdf, misW, brdfMis, blended, tp);
             const float rr = rng.next();
             if (stream_sample(brdfRes, li, uv, rr, tp, 1.0f / blended)) brdfLs = cand;
         }

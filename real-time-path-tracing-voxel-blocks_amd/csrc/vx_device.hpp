@@ -598,6 +598,20 @@ VX_D float mis_weight(const SurfS &sf, const LSample &ls, float selPdf, float li
     disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, bp);
     return (lightMis * (selPdf * sa) + brdfMis * bp) / sa;
 }
+// mis_weight and target_pdf of one candidate with a single BSDF evaluation (both evaluate the
+// same Disney lobe for the same surface and direction; results identical to the two calls)
+VX_D void mis_and_target(const SurfS &sf, const LSample &ls, float selPdf, float lightMis, float brdfMis,
+                         float &blended, float &tp) {
+    const float sa = ls.solidAnglePdf;
+    const bool tpEval = !(sa <= 0 || ls.type == LtInvalid);
+    const bool misEval = !(brdfMis == 0.0f || sa <= 0.0f || isinf(sa) || isnan(sa));
+    V3 fr(0.0f);
+    float bp = 0.0f;
+    if (tpEval || misEval)
+        disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, bp);
+    blended = misEval ? (lightMis * (selPdf * sa) + brdfMis * bp) / sa : lightMis * selPdf;
+    tp = tpEval ? luminance(ls.radiance * fr * fabsf(dot(ls.position, sf.normal)) / ls.solidAnglePdf) : 0.0f;
+}
 VX_D bool stream_sample(Reservoir &r, uint32_t light, V2 uv, float rnd, float target, float invSrc) {
     const float w = target * invSrc;
     r.M += 1;
