@@ -807,7 +807,16 @@ char *buffer_rows(vxpt_ctx *c, int which, int y, size_t &rowBytes) {
 // for it (do_trace); the trace passes touch neither the sent rows nor the
 // received ones before that kernel (they write the other G-buffer slot and
 // reservoir parity).
+// several buffers with their own halo depths in one group (one RCCL launch, one sync point)
+int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, int>> &bufRows, bool overlap = false);
+
 int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows, bool overlap = false) {
+    std::vector<std::pair<int, int>> br;
+    for (int b : bufs) br.emplace_back(b, rows);
+    return exchange_set(cs, br, overlap);
+}
+
+int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, int>> &bufRows, bool overlap) {
     if (cs.size() == 1 && cs[0]->comm) {
         vxpt_ctx *c = cs[0];
         hipStream_t st = c->stream;
@@ -817,8 +826,9 @@ int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows
             st = c->commStream;
         }
         if (ncclGroupStart() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupStart");
-        for (int b : bufs)
-            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, rows)) {
+        for (const auto &br : bufRows)
+            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, br.second)) {
+                const int b = br.first;
                 size_t rb;
                 char *send = buffer_rows(c, b, h.sy, rb);
                 char *recv = buffer_rows(c, b, h.ry, rb);
@@ -836,8 +846,9 @@ int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows
     // (never written by an exchange), after every band finished the producing pass
     for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
     for (vxpt_ctx *c : cs)
-        for (int b : bufs)
-            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, rows)) {
+        for (const auto &br : bufRows)
+            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, br.second)) {
+                const int b = br.first;
                 size_t rb;
                 char *dst = buffer_rows(c, b, h.ry, rb);
                 const char *src = buffer_rows(cs[h.peer], b, h.ry, rb);
@@ -864,23 +875,29 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
         FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp));
-        std::vector<int> bufs(std::begin(kGbufBufs), std::end(kGbufBufs));
-        bufs.push_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN);
-        // all but the last pass: overlapped with the next pass up to its temporal reuse
-        BANDCHK(exchange(cs, bufs, kTraceHalo, s + 1 < spp));
+        std::vector<std::pair<int, int>> br;
+        for (int b : kGbufBufs) br.emplace_back(b, kTraceHalo);
+        br.emplace_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, kTraceHalo);
+        if (s + 1 < spp) {
+            // all but the last pass: overlapped with the next pass up to its temporal reuse
+            BANDCHK(exchange_set(cs, br, true));
+        } else {
+            // the last pass's rows travel with the denoiser input's (radiance, or the spp average)
+            for (vxpt_ctx *c : cs) c->denoiseInputIsAccum = spp > 1;
+            br.emplace_back(VXPT_BUF_ILLUM, 2);
+            BANDCHK(exchange_set(cs, br, false));
+        }
     }
     for (vxpt_ctx *c : cs) {
         c->denoiseInputIsAccum = spp > 1;
         HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
         HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     }
-    BANDCHK(exchange(cs, {VXPT_BUF_ILLUM}, 2));
     const int it = it0 + spp, used = it > 0 ? it - 1 : 0;
     FOR_BANDS(run_pass(c, p, 11, 0, 0));
     if (p->enable_firefly_filter) {
         FOR_BANDS(run_pass(c, p, 0, used & 1, 0));
-        BANDCHK(exchange(cs, {(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN}, kTraceHalo));
-        BANDCHK(exchange(cs, {VXPT_BUF_ILLUM}, 2));
+        BANDCHK(exchange_set(cs, {{(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, kTraceHalo}, {VXPT_BUF_ILLUM, 2}}));
     }
     const std::vector<int> hist(std::begin(kHistoryBufs), std::end(kHistoryBufs));
     if (frame == 0) {
@@ -890,8 +907,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     int fin = 0;
     if (p->enable_temporal_accumulation && frame > 0) {
         FOR_BANDS(run_pass(c, p, 2, 0, 0));
-        BANDCHK(exchange(cs, {VXPT_BUF_PING}, 34));  // HistoryFix taps: 2 x (2^3 + 1) rows
-        BANDCHK(exchange(cs, {VXPT_BUF_PONG}, 2));
+        // HistoryFix taps: 2 x (2^3 + 1) rows of ping; pong for its 2-row stencils
+        BANDCHK(exchange_set(cs, {{VXPT_BUF_PING, 34}, {VXPT_BUF_PONG, 2}}));
         fin = 1;
         if (p->enable_history_fix) {
             FOR_BANDS(run_pass(c, p, 3, 0, 0));
