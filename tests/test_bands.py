@@ -141,12 +141,14 @@ def test_gpu_bands_match_single_context():
 
 
 @pytest.mark.gpu
-def test_gpu_library_band_schedule_matches_single_context():
+@pytest.mark.parametrize("n,w,h", [(2, 64, 160), (8, 640, 640)])
+def test_gpu_library_band_schedule_matches_single_context(n, w, h):
     """The library's own band schedule (vxpt_band_link / vxpt_render_frame_linked: the one
     vxpt_band_comm_init runs over RCCL, with device copies between the contexts as the
-    transport) equals the single-context render bit for bit."""
+    transport) equals the single-context render bit for bit; 8 bands simulate the 8-GPU
+    partition on one device (bands of 80 rows, wider than the 72-row trace halo)."""
     import vxpt
-    w, h, spp = 64, 160, 4
+    spp = 4
     cam = C1_CAMERA
 
     def make():
@@ -159,9 +161,9 @@ def test_gpu_library_band_schedule_matches_single_context():
 
     p = vxpt.DenoiseParams.defaults()
     single = make()
-    rs = [make(), make()]
+    rs = [make() for _ in range(n)]
     linked = vxpt.LinkedBands(rs)
-    rows = [bands.band_rows(h, 2, k) for k in range(2)]
+    rows = [bands.band_rows(h, n, k) for k in range(n)]
     for f in range(3):
         single.render_frame(f, spp, p)
         linked.render_frame(f, spp, p)
