@@ -107,6 +107,7 @@ bool read_png(const std::string &path, Image &im) {
         p += 12 + len;
     }
     if (w <= 0 || h <= 0 || depth != 8 || interlace != 0) return false;
+    if (w > 32768 || h > 32768) return false;  // corrupt or hostile header: no multi-GB allocation
     const int fch = ct == 0 ? 1 : (ct == 2 ? 3 : (ct == 3 ? 1 : (ct == 4 ? 2 : (ct == 6 ? 4 : 0))));
     if (!fch) return false;
     const size_t stride = (size_t)w * fch;
