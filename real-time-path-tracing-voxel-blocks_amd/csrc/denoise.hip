@@ -549,16 +549,17 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
 }
 
 // One workgroup per 16x16 tile, over the tile's list from k_temporal: a
-// sparse list (<= 4 pixels, the steady state) gets one wave per pixel,
-// a dense one (history just reset) one lane per pixel.
+// sparse list (<= 64 pixels, the steady state) is walked one pixel per wave at
+// a time, a dense one (history just reset) gets one lane per pixel.
 __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
     const unsigned tile = blockIdx.y * ((a.W + 15) / 16) + blockIdx.x;
     const unsigned n = a.hfCount[tile];
     const unsigned wv = threadIdx.x >> 6;
-    if (n <= 4) {
-        if (wv >= n) return;
-        const size_t i = a.hfList[tile * 256 + wv];
-        history_fix_wave(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i, threadIdx.x & 63);
+    if (n <= 64) {  // sparse (steady state): each wave takes every 4th listed pixel, its taps in parallel
+        for (unsigned k = wv; k < n; k += 4) {
+            const size_t i = a.hfList[tile * 256 + k];
+            history_fix_wave(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i, threadIdx.x & 63);
+        }
         return;
     }
     if (threadIdx.x >= n) return;
