@@ -110,9 +110,10 @@ __global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int parity) {
     const int W = a.W, H = a.H;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int l32 = lane & 31;
-    const int x = blockIdx.x * 8 + (l32 & 7);
-    // band starts on an 8-row boundary, so the 8x4 tiles stay aligned
-    const int y = a.y0 + blockIdx.y * 32 + wv * 8 + (lane >> 5) * 4 + (l32 >> 3);
+    // a wave = two 8x4 tiles side by side, a block = 64 x 4 pixels: row segments of 64 pixels
+    // (the tiles are the reference's 8x4 ones; the band starts on an 8-row boundary)
+    const int x = blockIdx.x * 64 + wv * 16 + (lane >> 5) * 8 + (l32 & 7);
+    const int y = a.y0 + blockIdx.y * 4 + (l32 >> 3);
     const bool inb = x < W && y < a.y1;
     const size_t i = (size_t)y * W + x;
     const float cd = inb ? a.depth[i] : 0.0f;
@@ -916,7 +917,7 @@ hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st) {
     const int used = 0;
     (void)used;
     // parity is baked into a.reservoir by the host
-    hipLaunchKernelGGL(k_firefly, dim3((a.W + 7) / 8, (a.y1 - a.y0 + 31) / 32), dim3(256), 0, st, a, 0);
+    hipLaunchKernelGGL(k_firefly, dim3((a.W + 63) / 64, (a.y1 - a.y0 + 3) / 4), dim3(256), 0, st, a, 0);
     hipLaunchKernelGGL(k_firefly_apply, dim3(64), dim3(256), 0, st, a);
     return hipGetLastError();
 }
