@@ -354,7 +354,7 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
             avgN += ld4(a.normalRough, W, H, x + ax, y + by).xyz();
         }
     avgN /= 9.0f;
-    const V2 pixelUv = (V2((float)x, (float)y) + 0.5f) * V2(1.0f / (float)W, 1.0f / (float)H);
+    const V2 pixelUv = (V2((float)x, (float)y) + 0.5f) * V2(a.invW, a.invH);
     const V2 curUV = (V2((float)x, (float)y) + 0.5f) * cam.invRes;
     const V3 view = cam.uv_to_dir(curUV);
     const V3 cWP = wp(a, x, y);
@@ -375,15 +375,13 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
         par2 = sqrtf(d2.x * d2.x + d2.y * d2.y);
     }
     const float parMax = fmaxf(par1, par2);
-    const float thrB = a.p.disocclusionThreshold + (1.5f / (float)H);
-    const float thrA = a.p.disocclusionThresholdAlternate + (1.5f / (float)H);
-    const float thr = lerpf(thrB, thrA, 0.0f);
+    const float thr = lerpf(a.thrB, a.thrA, 0.0f);
     // loadSurfaceMotionBasedPrevData
     const V3 nIn = normalize(avgN);
     const float estDepth = length(prevWP - pc.pos);
     const V2 ppf(prevUV.x * (float)W, prevUV.y * (float)H);
     const int ox = (int)floorf(ppf.x - 0.5f), oy = (int)floorf(ppf.y - 0.5f);
-    const float frustum = (cam.tanHalfFov.x / (cam.res.x / 2)) * z * (float)(W < H ? W : H);
+    const float frustum = (a.frustumK * z) * (float)(W < H ? W : H);
     const double slope = 1.0 / (double)lerpf(lerpf(0.05f, 1.0f, NoV), 1.0f, saturate(parMax / 30.0f));
     const float t0 = saturate((float)((double)thr * slope)) * frustum;
     V4 thr4(t0);
@@ -445,8 +443,8 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
         hist = fmaxf(hist, 1.0f);
     }
     hist = fminf(hist, a.p.maxAcc);
-    const float alpha = (found > 0) ? fmaxf(1.0f / (a.p.maxAcc + 1.0f), 1.0f / hist) : 1.0f;
-    const float alphaR = (found > 0) ? fmaxf(1.0f / (a.p.maxFast + 1.0f), 1.0f / hist) : 1.0f;
+    const float alpha = (found > 0) ? fmaxf(a.invAcc1, 1.0f / hist) : 1.0f;
+    const float alphaR = (found > 0) ? fmaxf(a.invFast1, 1.0f / hist) : 1.0f;
     const V4 acc = lerp4(prevI, V4(illum, m2), alpha);
     const V3 accR = lerp3(prevF, illum, alphaR);
     a.ping[i] = tf(acc);

@@ -196,6 +196,11 @@ struct DenoiseArgs {
     uint32_t *ffIndex;
     float4 *ffColor;
     Reservoir *ffRes;
+    // launch-uniform terms of the temporal pass, computed once on the host with the same IEEE
+    // operations (a division per wave each on the device): 1/W, 1/H, the two disocclusion
+    // thresholds, the frustum scale tanHalfFov.x / (res.x / 2), 1/(maxAcc+1),
+    // 1/(maxFast+1)
+    float invW, invH, thrB, thrA, frustumK, invAcc1, invFast1;
 };
 
 // post-processing (postprocess.hip; ToneMappingParams + PostProcessingPipelineParams, GlobalSettings.h:10-186)

@@ -401,6 +401,12 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.ffCount = c->ffCount; a.ffIndex = c->ffIndex; a.ffColor = c->ffColor; a.ffRes = c->ffRes;
     a.hfList = c->hfList; a.hfCount = c->hfCount;
     a.wpos = c->wpos;
+    a.invW = 1.0f / (float)c->W; a.invH = 1.0f / (float)c->H;
+    a.thrB = a.p.disocclusionThreshold + (1.5f / (float)c->H);
+    a.thrA = a.p.disocclusionThresholdAlternate + (1.5f / (float)c->H);
+    a.frustumK = c->cam.tanHalfFov.x / (c->cam.res.x / 2);
+    a.invAcc1 = 1.0f / (a.p.maxAcc + 1.0f);
+    a.invFast1 = 1.0f / (a.p.maxFast + 1.0f);
 }
 
 // GlobalSettings.h:10-186 defaults (the reference yaml overrides most of them: vxpt_load_settings)
