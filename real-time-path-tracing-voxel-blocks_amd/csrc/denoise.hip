@@ -241,8 +241,9 @@ __global__ __launch_bounds__(256) void k_frame0(DenoiseArgs a) {
 // launch grid is grid_xcd(a); false = the grid's padding.  Measured: the 3 a-trous passes
 // 57/55/71 -> 49/45/67 us; on the VALU-bound stencils (TA, HC, ASmem) the strips' uneven
 // sky/ground mix across XCDs cost more than the L2 gained, so they keep raster tiles.
+template <int TS = 16>
 VX_D bool xcd_tile(const DenoiseArgs &a, int &tx, int &ty) {
-    const int tilesX = (a.W + 15) / 16, tilesY = (a.y1 - a.y0 + 15) / 16;
+    const int tilesX = (a.W + TS - 1) / TS, tilesY = (a.y1 - a.y0 + TS - 1) / TS;
     const int g = blockIdx.y * gridDim.x + blockIdx.x, k = g % 8, l = g / 8;
     const int sx0 = k * tilesX / 8, sw = (k + 1) * tilesX / 8 - sx0;
     if (sw <= 0 || l >= sw * tilesY) return false;
@@ -753,9 +754,9 @@ struct GlobalTaps {
     VX_D V3 nrm(int px, int py, int W) const { return pN[py * W + px].xyz(); }
     VX_D V4 val(int px, int py, int W) const { return pI[py * W + px]; }
 };
-template <int R>
-struct TileTaps {  // the 16x16 tile at (x0, y0) with an R-pixel apron, zeros outside the frame
-    static constexpr int T = 16 + 2 * R;
+template <int R, int TS = 16>
+struct TileTaps {  // the TSxTS tile at (x0, y0) with an R-pixel apron, zeros outside the frame
+    static constexpr int T = TS + 2 * R;
     const float4 *sP, *sI;
     const float *sNx, *sNy, *sNz;
     int x0, y0;
@@ -853,17 +854,17 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
 }
 
 // the tile and its apron staged once in LDS (steps 2 and 4, R = step: 49 -> 36 and 46 -> 36 us)
-template <int R>
-__global__ __launch_bounds__(256) void k_atrous_tile(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
-                                                     unsigned frameIndex, int final) {
-    constexpr int T = TileTaps<R>::T;
+template <int R, int TS>
+__global__ __launch_bounds__(TS * TS) void k_atrous_tile(DenoiseArgs a, const float4 *in, float4 *out,
+                                                         unsigned step, unsigned frameIndex, int final) {
+    constexpr int T = TileTaps<R, TS>::T;
     __shared__ float4 sP[T * T], sI[T * T];
     __shared__ float sNx[T * T], sNy[T * T], sNz[T * T];
     int tx, ty;
-    if (!xcd_tile(a, tx, ty)) return;
+    if (!xcd_tile<TS>(a, tx, ty)) return;
     const int W = a.W, H = a.H;
-    const int x0 = tx * 16, y0 = a.y0 + ty * 16;
-    for (int k = threadIdx.x; k < T * T; k += 256) {
+    const int x0 = tx * TS, y0 = a.y0 + ty * TS;
+    for (int k = threadIdx.x; k < T * T; k += TS * TS) {
         const int gx = x0 - R + k % T, gy = y0 - R + k / T;
         float4 p = make_float4(0.f, 0.f, 0.f, 0.f), n = p, v = p;
         if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
@@ -877,9 +878,9 @@ __global__ __launch_bounds__(256) void k_atrous_tile(DenoiseArgs a, const float4
         sNx[k] = n.x; sNy[k] = n.y; sNz[k] = n.z;
     }
     __syncthreads();
-    const int x = x0 + (threadIdx.x & 15), y = y0 + (threadIdx.x >> 4);
+    const int x = x0 + (int)(threadIdx.x % TS), y = y0 + (int)(threadIdx.x / TS);
     if (x >= W || y >= a.y1) return;
-    const TileTaps<R> src{sP, sI, sNx, sNy, sNz, x0, y0};
+    const TileTaps<R, TS> src{sP, sI, sNx, sNy, sNz, x0, y0};
     atrous_px(a, src, in, out, step, frameIndex, final, x, y);
 }
 
@@ -896,9 +897,10 @@ __global__ __launch_bounds__(256) void k_copy_output(DenoiseArgs a, const float4
 
 // 16x16 tiles over the band rows [y0, y1)
 inline dim3 grid16(const DenoiseArgs &a) { return dim3((a.W + 15) / 16, (a.y1 - a.y0 + 15) / 16); }
-// xcd_tile's grid: 8 strips x the widest strip's tiles
+// xcd_tile<TS>'s grid: 8 strips x the widest strip's tiles
+template <int TS = 16>
 inline dim3 grid_xcd(const DenoiseArgs &a) {
-    const dim3 g = grid16(a);
+    const dim3 g((a.W + TS - 1) / TS, (a.y1 - a.y0 + TS - 1) / TS);
     const unsigned per = (g.x + 7) / 8 * g.y;
     return dim3(g.x, (8 * per + g.x - 1) / g.x);
 }
@@ -942,12 +944,16 @@ hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st) {
 }
 hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex,
                          bool final, hipStream_t st) {
+    // 32x32 tiles (1024 threads, apron load factor 1.27 / 1.56 / 2.64 instead of 1.56 / 2.25 / 5.1)
+    // were measured slower for every step: 41 / 41 / 70 us against 36 / 36 / 64 -- the passes are
+    // VALU bound on the weights, not on filling the tile
+    const int f = final ? 1 : 0;
     if (step == 2)
-        hipLaunchKernelGGL(k_atrous_tile<2>, grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, final ? 1 : 0);
+        hipLaunchKernelGGL((k_atrous_tile<2, 16>), grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, f);
     else if (step == 4)
-        hipLaunchKernelGGL(k_atrous_tile<4>, grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, final ? 1 : 0);
+        hipLaunchKernelGGL((k_atrous_tile<4, 16>), grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, f);
     else  // step 8: a 34x34 staged apron for 16x16 pixels was measured slower (71 vs 65 us) than the taps
-        hipLaunchKernelGGL(k_atrous, grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, final ? 1 : 0);
+        hipLaunchKernelGGL(k_atrous, grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, f);
     return hipGetLastError();
 }
 hipError_t launch_copy_output(const DenoiseArgs &a, const float4 *in, hipStream_t st) {
