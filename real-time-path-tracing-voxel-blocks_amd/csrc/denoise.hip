@@ -118,8 +118,9 @@ __global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int parity) {
     const size_t i = (size_t)y * W + x;
     const float cd = inb ? a.depth[i] : 0.0f;
     const bool sky = inb && cd > kRange;
+    // the reservoir is read beside the depth (not behind the sky test): one memory round trip
     Reservoir r = Reservoir{0u, 0u, 0.f, 0.f, 0.f};
-    if (inb && !sky) r = a.reservoir[i];
+    if (inb) r = a.reservoir[i];
     const bool valid = inb && !sky && r.lightData != 0 && isfinite(r.weightSum) && r.weightSum > 0.0f;
     float v = valid ? r.weightSum : 0.0f;
     unsigned cnt = valid ? 1u : 0u;
