@@ -54,7 +54,10 @@ enum vxpt_buffer {
     VXPT_BUF_CELL_MASKS = 40,    /* nBricks u64: cube-cell bits of each 4^3 brick             */
     VXPT_BUF_BRICK_IDS = 41,     /* nBricks x 64 u8: ids in brick-major order                 */
     VXPT_BUF_MACRO_MASKS = 42,   /* nBricks/64 u64: occupied-brick bits of each 16^3 cell      */
-    VXPT_BUF_TEXELS = 43         /* every loaded texture's RGBA8 mip chain (vxpt_texture_table) */
+    VXPT_BUF_TEXELS = 43,        /* every loaded texture's RGBA8 mip chain (vxpt_texture_table) */
+    /* emissive-triangle lights of the instanced meshes (vxpt_load_models / vxpt_get_lights) */
+    VXPT_BUF_LIGHTS = 44,        /* nLights x 32 B LightInfo (Light.h:13-23)                     */
+    VXPT_BUF_LIGHT_ALIAS = 45    /* nLights x {f32 q, f32 p, i32 alias} (AliasTable.h bins)      */
 };
 
 typedef struct vxpt_config {
@@ -168,6 +171,26 @@ int vxpt_enable_textures(vxpt_ctx *ctx, int on);
 /* texture table: per texture size, maxLod, maxLod + 1 level offsets in texels (parity hook) */
 int vxpt_texture_table(vxpt_ctx *ctx, int32_t *out, int cap, int *n_textures, int64_t *n_texels);
 
+/* ---- instanced block meshes + emissive triangle lights ---- */
+/* BlockManager / ModelManager / VoxelEngine::{collectInstanceTransforms, generateInstanceLights}
+ * (BlockManager.cpp:7-160, ModelManager.cpp:172-226, ObjUtils.cpp:13-120, VoxelEngine.cu:53-192,
+ * 323-520): read blocks 13..29 from assets/blocks.yaml, their models from assets/models.yaml and
+ * the OBJ files under root (NULL = data_dir; a missing file leaves the block with no triangles),
+ * collect the instances of the current world and build the light table + its alias table.  Both
+ * are rebuilt by every later world upload and by edits that place or remove an instanced block.
+ * *loaded = block types whose mesh loaded.  The DDA still treats instanced cells as empty. */
+int vxpt_load_models(vxpt_ctx *ctx, const char *root, int *loaded);
+/* a block type's mesh as loaded: 9 floats (3 corners) and 6 floats (3 texcoords) per triangle */
+int vxpt_get_model(vxpt_ctx *ctx, int block_id, float *pos, float *uv, int cap_triangles, int *n_triangles);
+/* instances, 5 x int32 each: object id (= block - 1), instance id, cell x, y, z; ordered by object,
+ * then instance id (Scene::geometryInstanceIdMap) */
+int vxpt_get_instances(vxpt_ctx *ctx, int32_t *out, int cap, int *n_instances);
+/* light table summary: per emissive instance (instance id, first light, triangles)
+ * (Scene::instanceLightMapping), the light count and the weights' sum
+ * (accumulatedLocalLightLuminance); the records are VXPT_BUF_LIGHTS / VXPT_BUF_LIGHT_ALIAS */
+int vxpt_get_lights(vxpt_ctx *ctx, uint32_t *mapping, int cap, int *n_mapped, uint32_t *n_lights,
+                    float *local_luminance);
+
 /* ---- voxel edits (VoxelEngine::update click path, VoxelEngine.cu:855-975, 1040-1346) ---- */
 /* performRayTraversal (:1040-1166) of the current camera ray on the world.  out: hit, hit x, y, z,
  * hit id, has space to place, place x, y, z, cells walked */
@@ -225,6 +248,10 @@ int vxpt_postprocess(vxpt_ctx *ctx, const vxpt_post_params *p, float dt_ms);
 int vxpt_write_png_rgba32f(const char *path, int w, int h, const float *rgba);
 /* 8-bit PNG reader (query with pixels = NULL, then read w*h*channels bytes) */
 int vxpt_read_png(const char *path, int *w, int *h, int *channels, uint8_t *pixels, size_t cap);
+/* ObjUtils::extractMeshFromOBJ (ObjUtils.cpp:13-120), no context: one vertex per face corner,
+ * 9 floats (positions) and 6 floats (texcoords) per triangle; *n_triangles = the file's count,
+ * at most cap_triangles written.  VXPT_ERR_IO when the file is missing or a face corner is bad */
+int vxpt_read_obj(const char *path, float *pos, float *uv, int cap_triangles, int *n_triangles);
 /* ImageDiff::compare / generateDiffImage (renderer/util/ImageDiff.cpp:94-185): the canonical-image
  * gate of mainOffline --test-canonical (mainOffline.cpp:450-497) */
 int vxpt_image_diff(const char *png_a, const char *png_b, vxpt_image_diff_result *out);

@@ -73,6 +73,11 @@ def lib():
             "orc_rand": (F, [P, I, I, I, I]),
             "orc_perlin": (F, [F, F, I]),
             "orc_dda": (None, [P, I, P, P, P, I]),
+            "orc_f32_to_f16": (ctypes.c_uint32, [F]),
+            "orc_f16_to_f32": (F, [ctypes.c_uint32]),
+            "orc_oct_encode": (ctypes.c_uint32, [P]),
+            "orc_oct_decode": (None, [ctypes.c_uint32, P]),
+            "orc_tri_lights": (None, [P, I, P, I, P, P, P]),
         }
         for k, (r, a) in sig.items():
             fn = getattr(L, k)
@@ -248,3 +253,123 @@ def postprocess(frame_in, depth, params, state, dt_ms, sun=None, sun_luminance=1
                       float(dt_ms), int(on), int(px), int(py), float(u), float(v), float(sun_luminance),
                       out.ctypes.data)
     return out
+
+
+# ---------------------------------------------------------------- instanced meshes + lights
+# (restatements of BlockManager, VoxelEngine::collectInstanceTransforms,
+# generateInstanceLights and AliasTable::update -- the C part is orc_lights.cpp)
+N_BLOCK_TYPES = 30  # BlockTypeNum (generated/voxelengine/BlockType.h:39)
+
+
+def parse_obj(path):
+    """ObjUtils::extractMeshFromOBJ (ObjUtils.cpp:13-120): (pos [T,3,3], uv [T,3,2]) float32, one
+    vertex per face corner; the first three corners of a face; 1-based indices clamped at the
+    first element, a missing texcoord index reads element 0.  Floats through strtof, as the
+    stream extraction does (no double rounding)."""
+    libc = ctypes.CDLL(None)
+    libc.strtof.restype = ctypes.c_float
+    libc.strtof.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p)]
+
+    def f32(tok):
+        return libc.strtof(tok.encode(), None)
+
+    def lead_int(s):
+        k = 0
+        if k < len(s) and s[k] in "+-":
+            k += 1
+        while k < len(s) and s[k].isdigit():
+            k += 1
+        digits = s[:k]
+        return (int(digits), k) if digits.lstrip("+-") else (None, 0)
+
+    vp, vt, pi, ti = [], [], [], []
+    for line in open(path):
+        t = line.split()
+        if not t:
+            continue
+        if t[0] == "v":
+            vp.append([f32(t[k + 1]) if k + 1 < len(t) else 0.0 for k in range(3)])
+        elif t[0] == "vt":
+            vt.append([f32(t[k + 1]) if k + 1 < len(t) else 0.0 for k in range(2)])
+        elif t[0] == "f":
+            for c in t[1:4]:
+                v, p = lead_int(c)
+                if v is None:
+                    raise ValueError("bad face corner " + c)
+                if p < len(c) and c[p] == "/":
+                    p += 1
+                tx = 0
+                if p >= len(c) or c[p] != "/":
+                    tv, _ = lead_int(c[p:])
+                    tx = tv if tv is not None else 0
+                pi.append(max(v - 1, 0))
+                ti.append(max(tx - 1, 0))
+    n = len(pi) - len(pi) % 3
+    pos = np.array([vp[i] if i < len(vp) else [0.0] * 3 for i in pi[:n]], np.float32).reshape(-1, 3, 3)
+    uv = np.array([vt[i] if i < len(vt) else [0.0] * 2 for i in ti[:n]], np.float32).reshape(-1, 3, 2)
+    return pos, uv
+
+
+def collect_instances(ids, chunks, blocks):
+    """VoxelEngine::collectInstanceTransforms (VoxelEngine.cu:323-384) on a chunk-major id grid.
+    blocks: {block id: dict(instanced=bool, light_base=int)}.  Returns int32 [N, 5] rows
+    (object, instance id, x, y, z) ordered by object then instance id; for a repeated instance
+    id the last cell in x, y, z order wins."""
+    cx, cy, cz = chunks
+    W, H, D = cx * 32, cy * 32, cz * 32
+    g = ids.reshape(cy, cz, cx, 32, 32, 32)  # chunk (y, z, x), then cell (y, z, x)
+    grid = g.transpose(2, 5, 0, 3, 1, 4).reshape(W, H, D)  # [x, y, z]
+    inst = [b for b in range(N_BLOCK_TYPES) if blocks.get(b, {}).get("instanced")]
+    first = inst[0] if inst else N_BLOCK_TYPES
+    by_obj = {}
+
+    def iid(obj, x, y, z):
+        x, y, z = min(x, W - 1), min(y, W - 1), min(z, W - 1)
+        return first + obj * W * W * W + (x + W * (z + W * y))
+
+    for obj in range(first - 1, N_BLOCK_TYPES - 1):
+        block = obj + 1
+        base = blocks.get(block, {}).get("light_base", 0)
+        hit = (grid == block) | ((grid == base) if base else False)
+        for x, y, z in zip(*np.nonzero(hit)):  # x, y, z lexicographic
+            x, y, z = int(x), int(y), int(z)
+            by_obj.setdefault(obj, {})[iid(obj, x, y, z)] = (x, y, z)
+            if base and grid[x, y, z] == block:
+                by_obj.setdefault(base - 1, {})[iid(base - 1, x, y, z)] = (x, y, z)
+    rows = [(o, i) + by_obj[o][i] for o in sorted(by_obj) for i in sorted(by_obj[o])]
+    return np.array(rows, np.int32).reshape(-1, 5)
+
+
+def tri_lights(tri, cells, radiance):
+    """generateLightInfosKernel + extractRadianceKernel: (records uint32 [I*T, 8], weights f32)."""
+    tri = np.ascontiguousarray(tri, np.float32).reshape(-1, 9)
+    cells = np.ascontiguousarray(cells, np.int32).reshape(-1, 3)
+    rad = np.ascontiguousarray(radiance, np.float32)
+    out = np.zeros((len(tri) * len(cells), 8), np.uint32)
+    w = np.zeros(len(tri) * len(cells), np.float32)
+    if len(out):
+        lib().orc_tri_lights(_p(tri), len(tri), _p(cells), len(cells), _p(rad), _p(out), _p(w))
+    return out, w
+
+
+def alias_table(weights):
+    """AliasTable::update's CPU build (AliasTable.cu:58-131) in binary32: p = w / sum,
+    scaled = p * n, FIFO small/large queues; the sum accumulated in binary64 and rounded once
+    (the library's choice for thrust::reduce's unspecified order).  Returns (q, p, alias, sum)."""
+    from collections import deque
+    w = np.asarray(weights, np.float32)
+    n = len(w)
+    s = np.float32(np.sum(w.astype(np.float64)))
+    prob = (w / s).astype(np.float32)
+    scaled = (prob * np.float32(n)).astype(np.float32)
+    alias = np.full(n, -1, np.int32)
+    small = deque(i for i in range(n) if scaled[i] < np.float32(1.0))
+    large = deque(i for i in range(n) if not scaled[i] < np.float32(1.0))
+    while small and large:
+        si, li = small.popleft(), large.popleft()
+        alias[si] = li
+        scaled[li] = np.float32(scaled[li] - np.float32(np.float32(1.0) - scaled[si]))
+        (small if scaled[li] < np.float32(1.0) else large).append(li)
+    for i in list(small) + list(large):
+        scaled[i] = np.float32(1.0)
+    return scaled, prob, alias, s

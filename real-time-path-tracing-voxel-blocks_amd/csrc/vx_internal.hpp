@@ -237,6 +237,23 @@ struct PostArgs {
 };
 hipError_t launch_postprocess(const PostArgs &a, hipStream_t st);
 bool decode_png(const std::string &path, int &w, int &h, int &ch, std::vector<uint8_t> &px);
+bool load_obj(const std::string &path, std::vector<float> &pos, std::vector<float> &uv);
+
+// Emissive-triangle light record, 32 B (renderer/shaders/Light.h:13-23): centroid, the two
+// edge lengths as f16 (lo = edge1), radiance as 4 x f16, the edge directions octahedral
+// unorm16x2 encoded
+struct LightInfo {
+    float center[3];
+    uint32_t scalars;
+    uint32_t radiance[2];
+    uint32_t direction1, direction2;
+};
+// One emissive block type's lights: every (instance, triangle) of its mesh, instance-major
+// (VoxelEngine.cu:53-116), written from out[0]; weight[k] = luminance(radiance) * area of the
+// decoded record (extractRadianceKernel, :139-147).  tri: 9 floats per triangle (object
+// space), inst: 3 ints per instance (the cell = the translation of its 3x4 transform).
+hipError_t launch_tri_lights(const float *tri, int nTri, const int *inst, int nInst, V3 radiance, LightInfo *out,
+                             float *weight, hipStream_t st);
 
 hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st);

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
@@ -131,6 +132,8 @@ bool as_bool(const std::string &s) { return s == "true" || s == "1" || s == "Tru
 
 }  // namespace
 
+constexpr int kBlockTypes = 30;  // BlockTypeNum (generated/voxelengine/BlockType.h:39)
+
 struct vxpt_ctx {
     int W = 0, H = 0, dev = 0, rowBegin = 0, rowEnd = 0;
     int totalBounce = 3, diffuseBounce = 1;
@@ -177,6 +180,26 @@ struct vxpt_ctx {
     std::vector<TexInfo> hTex;
     size_t nTexels = 0;
     int texEnabled = 0;
+
+    // instanced block meshes and their emissive-triangle lights
+    struct BlockDef {
+        std::string model;
+        bool instanced = false, baseLight = false, emissive = false;
+        int lightBase = 0;
+        float emission[3] = {0.f, 0.f, 0.f};
+        int triangles = 0;             // of the loaded mesh (0: missing file)
+        std::vector<float> pos, uv;    // 9 / 6 floats per triangle, object space
+    };
+    bool modelsLoaded = false;
+    BlockDef blocks[kBlockTypes];
+    std::vector<int32_t> instances;    // (objectId, instanceId, x, y, z) by object, then instance id
+    std::vector<uint32_t> lightMap;    // (instanceId, first light, triangles) per emissive instance
+    DBuf<LightInfo> lights;
+    DBuf<AliasBin> lightAlias;
+    DBuf<float> lightTri, lightWeight;
+    DBuf<int> lightInst;
+    unsigned nLights = 0;
+    float localLightLum = 0.0f;
 
     // blue noise
     DBuf<uint8_t> bnSobol, bnScramble, bnRank;
@@ -476,6 +499,9 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_BRICK_IDS: p = c->bricks.p; bytes = (size_t)c->nBricks * 64; return !forWrite && c->bricks.p;
         case VXPT_BUF_MACRO_MASKS: p = c->macro.p; bytes = (size_t)c->nBricks / 64 * 8; return !forWrite && c->macro.p;
         case VXPT_BUF_TEXELS: p = c->texels.p; bytes = c->nTexels * 4; return !forWrite && c->texels.p;
+        case VXPT_BUF_LIGHTS: p = c->lights.p; bytes = (size_t)c->nLights * sizeof(LightInfo); return !forWrite && c->nLights;
+        case VXPT_BUF_LIGHT_ALIAS:
+            p = c->lightAlias.p; bytes = (size_t)c->nLights * sizeof(AliasBin); return !forWrite && c->nLights;
         default: return false;
     }
 }
@@ -1250,6 +1276,8 @@ int vxpt_generate_terrain(vxpt_ctx *c, int cxn, int cyn, int czn, float heightSc
     return vxpt_upload_voxels(c, ids.data(), cxn, cyn, czn);
 }
 
+int refresh_instances(vxpt_ctx *c);  // instanced meshes + lights, after the grid changed
+
 int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int czn) {
     if (!c || !ids || cxn <= 0 || cyn <= 0 || czn <= 0) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
@@ -1259,7 +1287,7 @@ int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int cz
     if (int r = upload_vec(c, c->voxels, c->hIds.data(), n)) return r;
     if (int r = build_occupancy(c, c->hIds.data())) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return VXPT_OK;
+    return refresh_instances(c);
 }
 
 int vxpt_upload_materials(vxpt_ctx *c, const vxpt_material *m, int n) {
@@ -1405,6 +1433,217 @@ int vxpt_load_textures(vxpt_ctx *c, const char *root, int *loaded) {
     return VXPT_OK;
 }
 
+// ---------------------------------------------------------------- instanced meshes + lights
+namespace {
+
+// VoxelEngine::collectInstanceTransforms (VoxelEngine.cu:323-384): for every instanced
+// object (block 13..29 -> object id = block - 1), every cell holding the block -- or, for a
+// light with a paired base, holding the base block -- is an instance of the object; a light
+// cell also registers an instance of its base.  Instance id = PositionToInstanceId
+// (VoxelMath.h:120-133: first instanced block + object * W^3 + x + W * (z + W * y), every
+// coordinate clamped to W - 1, W = the world's x extent); ids are kept in a set per object
+// (Scene.h:77) and a later cell with the same id overwrites the transform.
+void collect_instances(vxpt_ctx *c) {
+    c->instances.clear();
+    if (c->hIds.empty()) return;
+    int first = kBlockTypes;
+    for (int b = 0; b < kBlockTypes; ++b)
+        if (c->blocks[b].instanced) { first = b; break; }
+    const unsigned W = (unsigned)c->cx * 32u, H = (unsigned)c->cy * 32u, D = (unsigned)c->cz * 32u;
+    std::map<int, std::map<unsigned, std::array<unsigned, 3>>> byObject;
+    auto inst_id = [&](unsigned obj, unsigned x, unsigned y, unsigned z) {
+        x = x < W - 1 ? x : W - 1;
+        y = y < W - 1 ? y : W - 1;
+        z = z < W - 1 ? z : W - 1;
+        return (unsigned)first + obj * W * W * W + (x + W * (z + W * y));
+    };
+    // one pass over the cells: what each block id contributes (its own object; a base block
+    // also the objects of the lights paired with it; a paired light also its base's object)
+    std::vector<int> contrib[kBlockTypes];
+    for (int obj = first - 1; obj < kBlockTypes - 1; ++obj) {
+        const int block = obj + 1, base = c->blocks[block].lightBase;
+        contrib[block].push_back(obj);
+        if (base > 0 && base < kBlockTypes) {
+            contrib[base].push_back(obj);
+            contrib[block].push_back(base - 1);
+        }
+    }
+    for (unsigned x = 0; x < W; ++x)  // the reference's x, y, z order (last write wins)
+        for (unsigned y = 0; y < H; ++y)
+            for (unsigned z = 0; z < D; ++z) {
+                const size_t ch = (x >> 5) + (size_t)c->cx * ((z >> 5) + (size_t)c->cz * (y >> 5));
+                const int id = c->hIds[ch * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
+                if (id < first || id >= kBlockTypes) continue;
+                for (int obj : contrib[id]) byObject[obj][inst_id(obj, x, y, z)] = {x, y, z};
+            }
+    for (const auto &o : byObject)
+        for (const auto &i : o.second)
+            c->instances.insert(c->instances.end(),
+                                {o.first, (int32_t)i.first, (int32_t)i.second[0], (int32_t)i.second[1], (int32_t)i.second[2]});
+}
+
+// VoxelEngine::countLightTriangles / generateInstanceLights (VoxelEngine.cu:386-520) and
+// buildAliasTable (:150-192): the emissive objects in object order, each instance's
+// triangles in a row, one launch per object; then the weights' alias table (build_alias,
+// the same construction as the sky's) and their sum (accumulatedLocalLightLuminance).
+int build_lights(vxpt_ctx *c) {
+    c->lightMap.clear();
+    c->nLights = 0;
+    c->localLightLum = 0.0f;
+    size_t total = 0;
+    for (size_t k = 0; k < c->instances.size(); k += 5) {
+        const auto &bd = c->blocks[c->instances[k] + 1];
+        if (bd.emissive) total += (size_t)bd.triangles;
+    }
+    if (total == 0) return VXPT_OK;
+    if (c->lights.n < total) {
+        if (dalloc(c, c->lights.p, total)) return VXPT_ERR_HIP;
+        c->lights.n = total;
+    }
+    if (c->lightWeight.n < total) {
+        if (dalloc(c, c->lightWeight.p, total)) return VXPT_ERR_HIP;
+        c->lightWeight.n = total;
+    }
+    // all emissive meshes' triangles and instance cells, uploaded once
+    std::vector<float> tri;
+    std::vector<int> cells;
+    struct Run { size_t tri, cell; int nTri, nInst; V3 rad; };
+    std::vector<Run> runs;
+    for (size_t k = 0; k < c->instances.size();) {
+        const int obj = c->instances[k];
+        const auto &bd = c->blocks[obj + 1];
+        size_t e = k;
+        while (e < c->instances.size() && c->instances[e] == obj) e += 5;
+        if (bd.emissive && bd.triangles > 0) {
+            Run r{tri.size(), cells.size(), bd.triangles, (int)((e - k) / 5),
+                  V3(bd.emission[0], bd.emission[1], bd.emission[2])};
+            tri.insert(tri.end(), bd.pos.begin(), bd.pos.end());
+            for (size_t i = k; i < e; i += 5) {
+                cells.insert(cells.end(), {c->instances[i + 2], c->instances[i + 3], c->instances[i + 4]});
+                c->lightMap.insert(c->lightMap.end(),
+                                   {(uint32_t)c->instances[i + 1], (uint32_t)c->nLights, (uint32_t)bd.triangles});
+                c->nLights += (unsigned)bd.triangles;
+            }
+            runs.push_back(r);
+        }
+        k = e;
+    }
+    if (int r = upload_vec(c, c->lightTri, tri.data(), tri.size())) return r;
+    if (int r = upload_vec(c, c->lightInst, cells.data(), cells.size())) return r;
+    size_t off = 0;
+    for (const Run &r : runs) {
+        HIPCHK(c, launch_tri_lights(c->lightTri.p + r.tri, r.nTri, c->lightInst.p + r.cell, r.nInst, r.rad,
+                                    c->lights.p + off, c->lightWeight.p + off, c->stream));
+        off += (size_t)r.nTri * r.nInst;
+    }
+    std::vector<float> w(total);
+    HIPCHK(c, hipMemcpyAsync(w.data(), c->lightWeight.p, total * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const std::vector<AliasBin> bins = build_alias(w, c->localLightLum);
+    if (int r = upload_vec(c, c->lightAlias, bins.data(), bins.size())) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VXPT_OK;
+}
+
+}  // namespace
+
+int refresh_instances(vxpt_ctx *c) {
+    if (!c->modelsLoaded) return VXPT_OK;
+    collect_instances(c);
+    return build_lights(c);
+}
+
+// blocks.yaml (ids 13..29) + models.yaml + materials.yaml emission, then the OBJ meshes
+int vxpt_load_models(vxpt_ctx *c, const char *root, int *loaded) {
+    if (!c) return VXPT_ERR_ARG;
+    const std::string dir = root ? root : c->dataDir;
+    std::string line;
+    std::map<std::string, std::string> modelFile;
+    {
+        std::ifstream f(c->dataDir + "/assets/models.yaml");
+        if (!f) return fail(c, VXPT_ERR_IO, "missing assets/models.yaml");
+        while (std::getline(f, line)) {
+            const std::string tl = trim(line);
+            if (tl.rfind("- {", 0) != 0) continue;
+            auto m = parse_flow_map(tl);
+            modelFile[m["id"]] = m["file"];
+        }
+    }
+    std::map<std::string, std::map<std::string, std::string>> matProps;
+    {
+        std::ifstream f(c->dataDir + "/assets/materials.yaml");
+        if (!f) return fail(c, VXPT_ERR_IO, "missing assets/materials.yaml");
+        std::string cur;
+        while (std::getline(f, line)) {
+            const std::string tl = trim(line);
+            if (tl.rfind("- id:", 0) == 0) cur = trim(tl.substr(5));
+            else if (tl.rfind("properties:", 0) == 0) matProps[cur] = parse_flow_map(tl);
+        }
+    }
+    std::ifstream fb(c->dataDir + "/assets/blocks.yaml");
+    if (!fb) return fail(c, VXPT_ERR_IO, "missing assets/blocks.yaml");
+    for (auto &b : c->blocks) b = vxpt_ctx::BlockDef{};
+    int nLoaded = 0;
+    while (std::getline(fb, line)) {
+        const std::string tl = trim(line);
+        if (tl.rfind("- {", 0) != 0) continue;
+        auto m = parse_flow_map(tl);
+        const int bid = std::atoi(m["id"].c_str());
+        if (bid < 1 || bid >= kBlockTypes) continue;
+        auto &bd = c->blocks[bid];
+        bd.instanced = as_bool(m["instanced"]);
+        bd.baseLight = as_bool(m["base_light"]);
+        bd.lightBase = m.count("light_base") ? std::atoi(m["light_base"].c_str()) : 0;
+        bd.model = m.count("model") ? m["model"] : "";
+        // BlockManager::isEmissive: the block's flag or its material's; radiance from the material
+        auto &mp = matProps[m["material"]];
+        bd.emissive = as_bool(m["emissive"]) || as_bool(mp["is_emissive"]);
+        if (as_bool(mp["is_emissive"]) && mp.count("emissive_radiance")) {
+            const auto v = parse_list(mp["emissive_radiance"]);
+            if (v.size() == 3) std::copy(v.begin(), v.end(), bd.emission);
+        }
+        if (!bd.instanced || bd.model.empty() || !modelFile.count(bd.model)) continue;
+        if (load_obj(dir + "/" + modelFile[bd.model], bd.pos, bd.uv)) {
+            bd.triangles = (int)(bd.pos.size() / 9);
+            bd.pos.resize((size_t)bd.triangles * 9);
+            bd.uv.resize((size_t)bd.triangles * 6);
+            if (bd.triangles > 0) ++nLoaded;
+        }
+    }
+    c->modelsLoaded = true;
+    if (loaded) *loaded = nLoaded;
+    HIPCHK(c, hipSetDevice(c->dev));
+    return refresh_instances(c);
+}
+
+int vxpt_get_model(vxpt_ctx *c, int block_id, float *pos, float *uv, int cap_triangles, int *n_triangles) {
+    if (!c || block_id < 0 || block_id >= kBlockTypes) return VXPT_ERR_ARG;
+    const auto &bd = c->blocks[block_id];
+    if (n_triangles) *n_triangles = bd.triangles;
+    const int n = std::min(cap_triangles, bd.triangles);
+    if (pos && n > 0) std::copy(bd.pos.begin(), bd.pos.begin() + (size_t)n * 9, pos);
+    if (uv && n > 0) std::copy(bd.uv.begin(), bd.uv.begin() + (size_t)n * 6, uv);
+    return VXPT_OK;
+}
+
+int vxpt_get_instances(vxpt_ctx *c, int32_t *out, int cap, int *n_instances) {
+    if (!c) return VXPT_ERR_ARG;
+    const int n = (int)(c->instances.size() / 5);
+    if (n_instances) *n_instances = n;
+    if (out) std::copy(c->instances.begin(), c->instances.begin() + (size_t)std::min(cap, n) * 5, out);
+    return VXPT_OK;
+}
+
+int vxpt_get_lights(vxpt_ctx *c, uint32_t *mapping, int cap, int *n_mapped, uint32_t *n_lights, float *local_luminance) {
+    if (!c) return VXPT_ERR_ARG;
+    const int n = (int)(c->lightMap.size() / 3);
+    if (n_mapped) *n_mapped = n;
+    if (mapping) std::copy(c->lightMap.begin(), c->lightMap.begin() + (size_t)std::min(cap, n) * 3, mapping);
+    if (n_lights) *n_lights = c->nLights;
+    if (local_luminance) *local_luminance = c->localLightLum;
+    return VXPT_OK;
+}
+
 int vxpt_enable_textures(vxpt_ctx *c, int on) {
     if (!c) return VXPT_ERR_ARG;
     c->texEnabled = (on && !c->hTex.empty()) ? 1 : 0;
@@ -1487,7 +1726,15 @@ int vxpt_set_block(vxpt_ctx *c, int x, int y, int z, int block_id) {
     if (!c) return VXPT_ERR_ARG;
     if (c->hIds.empty()) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
     HIPCHK(c, hipSetDevice(c->dev));
-    return set_block(c, x, y, z, block_id);
+    int old = 0;
+    if (x >= 0 && y >= 0 && z >= 0 && x < c->cx * 32 && y < c->cy * 32 && z < c->cz * 32) {
+        const size_t ch = (size_t)(x >> 5) + (size_t)c->cx * ((z >> 5) + (size_t)c->cz * (y >> 5));
+        old = c->hIds[ch * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
+    }
+    if (int r = set_block(c, x, y, z, block_id)) return r;
+    // the instance set (and the light table) only changes with an instanced block
+    const auto inst = [&](int id) { return id > 0 && id < kBlockTypes && c->blocks[id].instanced; };
+    return (inst(old) || inst(block_id)) ? refresh_instances(c) : VXPT_OK;
 }
 
 // VoxelEngine::update's click (VoxelEngine.cu:906-975): block 0 deletes the picked block,

@@ -23,10 +23,12 @@ BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERI
            PREV_NORMAL_ROUGH=8, PREV_GEO_NORMAL_THIN=9, PREV_ALBEDO=10, PREV_MAT_PARAM=11, PREV_DEPTH=12,
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
            PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38,
-           OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42, TEXELS=43)
+           OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42, TEXELS=43, LIGHTS=44,
+           LIGHT_ALIAS=45)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
+ALIAS_DTYPE = np.dtype([("q", "<f4"), ("p", "<f4"), ("alias", "<i4")])
 TRACE_PRIMARY_ONLY = 1
 
 
@@ -122,6 +124,11 @@ def load_library(path=LIB_PATH):
         "vxpt_load_textures": (I, [P, ctypes.c_char_p, P]),
         "vxpt_enable_textures": (I, [P, I]),
         "vxpt_texture_table": (I, [P, P, I, P, P]),
+        "vxpt_load_models": (I, [P, ctypes.c_char_p, P]),
+        "vxpt_read_obj": (I, [ctypes.c_char_p, P, P, I, P]),
+        "vxpt_get_model": (I, [P, I, P, P, I, P]),
+        "vxpt_get_instances": (I, [P, P, I, P]),
+        "vxpt_get_lights": (I, [P, P, I, P, P, P]),
         "vxpt_set_block": (I, [P, I, I, I, I]),
         "vxpt_click_block": (I, [P, I, P]),
         "vxpt_save_world": (I, [P, ctypes.c_char_p, ctypes.c_char_p]),
@@ -274,6 +281,49 @@ class Renderer:
             k += 3 + ml
         self._ntexels = nt.value
         return tabs, nt.value
+
+    # --- instanced meshes + emissive triangle lights ---
+    def load_models(self, root=None):
+        """blocks 13..29 + models.yaml + the OBJ files under root; returns block types loaded."""
+        n = ctypes.c_int(0)
+        self._chk(self.lib.vxpt_load_models(self.ctx, str(root).encode() if root else None, ctypes.byref(n)),
+                  "vxpt_load_models")
+        return n.value
+
+    def model(self, block_id):
+        """(pos [T,3,3], uv [T,3,2]) of a block type's loaded mesh."""
+        n = ctypes.c_int(0)
+        self._chk(self.lib.vxpt_get_model(self.ctx, int(block_id), None, None, 0, ctypes.byref(n)), "vxpt_get_model")
+        pos, uv = np.zeros((n.value, 3, 3), np.float32), np.zeros((n.value, 3, 2), np.float32)
+        if n.value:
+            self._chk(self.lib.vxpt_get_model(self.ctx, int(block_id), _ptr(pos), _ptr(uv), n.value, ctypes.byref(n)),
+                      "vxpt_get_model")
+        return pos, uv
+
+    def instances(self):
+        """int32 [N, 5]: object id, instance id, x, y, z."""
+        n = ctypes.c_int(0)
+        self._chk(self.lib.vxpt_get_instances(self.ctx, None, 0, ctypes.byref(n)), "vxpt_get_instances")
+        out = np.zeros((n.value, 5), np.int32)
+        if n.value:
+            self._chk(self.lib.vxpt_get_instances(self.ctx, _ptr(out), n.value, ctypes.byref(n)), "vxpt_get_instances")
+        return out
+
+    def lights(self):
+        """(mapping uint32 [M, 3], LightInfo records uint8 [L, 32], alias bins [L], local luminance)."""
+        n, nl, lum = ctypes.c_int(0), ctypes.c_uint32(0), ctypes.c_float(0)
+        self._chk(self.lib.vxpt_get_lights(self.ctx, None, 0, ctypes.byref(n), ctypes.byref(nl), ctypes.byref(lum)),
+                  "vxpt_get_lights")
+        mp = np.zeros((n.value, 3), np.uint32)
+        if n.value:
+            self._chk(self.lib.vxpt_get_lights(self.ctx, _ptr(mp), n.value, ctypes.byref(n), None, None),
+                      "vxpt_get_lights")
+        recs = np.zeros((nl.value, 32), np.uint8)
+        bins = np.zeros(nl.value, ALIAS_DTYPE)
+        if nl.value:
+            self._chk(self.lib.vxpt_readback(self.ctx, BUF["LIGHTS"], _ptr(recs), recs.nbytes), "vxpt_readback")
+            self._chk(self.lib.vxpt_readback(self.ctx, BUF["LIGHT_ALIAS"], _ptr(bins), bins.nbytes), "vxpt_readback")
+        return mp, recs, bins, lum.value
 
     # --- voxel edits (VoxelEngine click path) and world files (WorldSceneManager) ---
     @staticmethod
@@ -514,3 +564,15 @@ def image_diff(a, b, diff_png=None):
     if diff_png and lib.vxpt_image_diff_png(os.fsencode(a), os.fsencode(b), os.fsencode(diff_png)) != 0:
         raise VxptError("diff image failed")
     return {f: getattr(r, f) for f, _ in r._fields_}
+
+
+def read_obj(path):
+    """The library's OBJ reader (no GPU needed): (pos [T,3,3], uv [T,3,2])."""
+    L = load_library()
+    n = ctypes.c_int(0)
+    if L.vxpt_read_obj(str(path).encode(), None, None, 0, ctypes.byref(n)) != 0:
+        raise IOError("vxpt_read_obj failed: %s" % path)
+    pos, uv = np.zeros((n.value, 3, 3), np.float32), np.zeros((n.value, 3, 2), np.float32)
+    if n.value:
+        L.vxpt_read_obj(str(path).encode(), _ptr(pos), _ptr(uv), n.value, ctypes.byref(n))
+    return pos, uv

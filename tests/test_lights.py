@@ -1,0 +1,176 @@
+"""Instanced block meshes and their emissive-triangle lights (first slice):
+the OBJ reader (ObjUtils.cpp:13-120), the instance set of a world (BlockManager +
+VoxelEngine::collectInstanceTransforms, VoxelEngine.cu:323-384), the light records
+(generateLightInfosKernel + TriangleLight::Store, VoxelEngine.cu:53-116, Light.h:124-137) and
+their alias table (buildAliasTable / AliasTable::update, VoxelEngine.cu:150-192,
+AliasTable.cu:58-131).
+
+The reference's OBJ assets are not shipped here: the meshes are synthetic OBJ files written by
+the tests (a lantern-like emissive prism and a base), so the light table is pinned by the
+oracle restatement (oracle/orc_lights.cpp, oracle.collect_instances / alias_table) and by
+known answers (IEEE f16 rounding against numpy, octahedral encodings of the axes).
+Bit-exact: instance rows, light records, weights and alias bins.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import vxpt
+
+CH = (2, 1, 2)
+LIGHT, BASE = 16, 15
+BLOCKS = {b: dict(instanced=True, light_base=(BASE if b == LIGHT else 0)) for b in range(13, 30)}
+
+
+def _idx(x, y, z, chunks=CH):
+    cx, cy, cz = chunks
+    return ((x >> 5) + cx * ((z >> 5) + cz * (y >> 5))) * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))
+
+
+def _prism_obj(path, lo=0.28, hi=0.72, y0=0.07, y1=0.62):
+    """An open four-sided prism (8 triangles, like the lantern's light) with texcoords."""
+    v = [(lo, y0, lo), (hi, y0, lo), (hi, y0, hi), (lo, y0, hi), (lo, y1, lo), (hi, y1, lo), (hi, y1, hi), (lo, y1, hi)]
+    faces = []
+    for a, b in ((0, 1), (1, 2), (2, 3), (3, 0)):
+        faces += [(a, b, b + 4), (a, b + 4, a + 4)]
+    with open(path, "w") as f:
+        f.write("# synthetic emissive prism\n")
+        for p in v:
+            f.write("v %.6f %.6f %.6f\n" % p)
+        f.write("vt 0.375 0.5\nvt 0.625 0.5\n")
+        for k, (a, b, c) in enumerate(faces):
+            f.write("f %d/1 %d/2 %d/%d\n" % (a + 1, b + 1, c + 1, 1 + k % 2))
+
+
+def _base_obj(path):
+    """A flat quad (2 triangles) with `v//n` corners."""
+    with open(path, "w") as f:
+        f.write("v 0 0 0\nv 1 0 0\nv 1 0 1\nv 0 0 1\nvn 0 1 0\nf 1//1 3//1 2//1\nf 1//1 4//1 3//1\n")
+
+
+@pytest.fixture
+def model_root(tmp_path):
+    os.makedirs(tmp_path / "models")
+    _prism_obj(str(tmp_path / "models" / "lanternLight.obj"))
+    _base_obj(str(tmp_path / "models" / "lanternBase.obj"))
+    return tmp_path
+
+
+# ---------------------------------------------------------------- CPU
+def test_f16_rounding_matches_ieee():
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.standard_normal(20000).astype(np.float32) * np.float32(300),
+                        rng.random(20000).astype(np.float32) * np.float32(1e-4),
+                        np.array([65504, 65519, 65520, 2.0 ** -25, 2.0 ** -24, 3 * 2.0 ** -26, -0.0, np.inf], np.float32)])
+    L = oracle.lib()
+    got = np.array([L.orc_f32_to_f16(float(v)) for v in x], np.uint32)
+    with np.errstate(over="ignore"):
+        want = x.astype(np.float16).view(np.uint16).astype(np.uint32)
+    assert np.array_equal(got, want)
+    back = np.array([L.orc_f16_to_f32(int(h)) for h in want], np.float32)
+    assert np.array_equal(back.view(np.uint32), want.astype(np.uint16).view(np.float16).astype(np.float32).view(np.uint32))
+
+
+def test_octahedral_known_answers_and_round_trip():
+    L = oracle.lib()
+    enc = lambda n: L.orc_oct_encode(oracle._p(np.array(n, np.float32)))  # noqa: E731
+    assert enc([0, 0, 1]) == 32767 | (32767 << 16)
+    assert enc([1, 0, 0]) == 65534 | (32767 << 16)
+    assert enc([0, -1, 0]) == 32767
+    rng = np.random.default_rng(9)
+    out = np.zeros(3, np.float32)
+    for _ in range(2000):
+        n = rng.standard_normal(3).astype(np.float32)
+        n /= np.float32(np.linalg.norm(n))
+        L.orc_oct_decode(enc(n), oracle._p(out))
+        assert np.abs(out - n).max() < 2e-4  # 16-bit octahedral quantisation
+
+
+def test_obj_reader_matches_oracle(tmp_path):
+    p = str(tmp_path / "m.obj")
+    with open(p, "w") as f:
+        f.write("v 0.1 0.2 0.3\nv 1.0000001 -2.5e-3 7\nv 0.333333343 0.5 0.25\nv 9 9 9\nvt 0.25 0.75\nvt 1 0\n"
+                "f 1/1 2/2 3/1\nf 1//3 2//1 3//2\nf 1 2 3 4\nf 2/2/1 3/1/1 4/5/1\nf -1/1 0/0 7/2\n")
+    a, b = vxpt.read_obj(p), oracle.parse_obj(p)
+    assert a[0].shape == (5, 3, 3)
+    for x, y in zip(a, b):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    _prism_obj(str(tmp_path / "prism.obj"))
+    a, b = vxpt.read_obj(str(tmp_path / "prism.obj")), oracle.parse_obj(str(tmp_path / "prism.obj"))
+    assert a[0].shape == (8, 3, 3) and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    with open(p, "w") as f:
+        f.write("v 0 0 0\nf x/1 1 1\n")
+    with pytest.raises(IOError):
+        vxpt.read_obj(p)
+
+
+def test_instance_collection_known_answer():
+    ids = np.zeros(int(np.prod(CH)) * 32768, np.uint8)
+    ids[_idx(3, 4, 5)] = LIGHT   # a lantern: its light and its base
+    ids[_idx(40, 2, 7)] = BASE   # a bare base: its base and (quirk) a light instance
+    ids[_idx(10, 9, 60)] = 14    # leaves
+    rows = oracle.collect_instances(ids, CH, BLOCKS)
+    W = 64
+    iid = lambda obj, x, y, z: 13 + obj * W ** 3 + x + W * (z + W * y)  # noqa: E731
+    want = sorted([(13, iid(13, 10, 9, 60), 10, 9, 60),
+                   (14, iid(14, 3, 4, 5), 3, 4, 5), (14, iid(14, 40, 2, 7), 40, 2, 7),
+                   (15, iid(15, 3, 4, 5), 3, 4, 5), (15, iid(15, 40, 2, 7), 40, 2, 7)])
+    assert [tuple(r) for r in rows] == want
+
+
+def test_alias_table_reproduces_the_distribution():
+    w = np.random.default_rng(3).random(37).astype(np.float32) * np.float32(5)
+    q, p, alias, s = oracle.alias_table(w)
+    n = len(w)
+    got = q.astype(np.float64) / n
+    for j in range(n):
+        if alias[j] >= 0:
+            got[alias[j]] += (1.0 - q[j]) / n
+    assert np.allclose(got, w / w.sum(), atol=1e-6)
+
+
+# ---------------------------------------------------------------- GPU
+def _expected(r, root):
+    """The oracle's instance rows, light records, weights and alias bins for r's world."""
+    ids = r.read("VOXELS")
+    rows = oracle.collect_instances(ids, CH, BLOCKS)
+    tri, _ = oracle.parse_obj(str(root / "models" / "lanternLight.obj"))
+    cells = rows[rows[:, 0] == LIGHT - 1][:, 2:5]
+    recs, w = oracle.tri_lights(tri, cells, [3.737, 2.718, 1.189])
+    return rows, recs, w
+
+
+@pytest.mark.gpu
+def test_light_table_matches_oracle(model_root):
+    r = vxpt.Renderer(64, 64)
+    r.load_settings()
+    r.generate_terrain(CH, height_scale=32.0)
+    assert r.load_models(str(model_root)) == 2  # the prism and the base; the rest are missing
+    assert np.array_equal(r.model(LIGHT)[0], oracle.parse_obj(str(model_root / "models" / "lanternLight.obj"))[0])
+    mp, recs, bins, lum = r.lights()
+    assert len(r.instances()) == 0 and len(recs) == 0 and lum == 0.0
+    cells = [(3, 20, 5), (40, 18, 7), (63, 31, 63), (0, 25, 0), (17, 22, 41)]
+    for c in cells:
+        r.set_block(*c, LIGHT)
+    r.set_block(30, 21, 30, BASE)
+    rows, want, w = _expected(r, model_root)
+    assert np.array_equal(r.instances(), rows)
+    mp, recs, bins, lum = r.lights()
+    nl = len(cells) + 1  # the bare base carries a light instance too (collectInstanceTransforms)
+    assert len(recs) == 8 * nl and len(mp) == nl
+    light_rows = rows[rows[:, 0] == LIGHT - 1]
+    assert np.array_equal(mp, np.stack([light_rows[:, 1], np.arange(nl) * 8, np.full(nl, 8)], 1).astype(np.uint32))
+    assert np.array_equal(recs.view(np.uint32).reshape(-1, 8), want)
+    q, p, alias, s = oracle.alias_table(w)
+    assert np.array_equal(bins["q"].view(np.uint32), q.view(np.uint32))
+    assert np.array_equal(bins["p"].view(np.uint32), p.view(np.uint32))
+    assert np.array_equal(bins["alias"], alias)
+    assert np.float32(lum).view(np.uint32) == s.view(np.uint32)
+    # removing every lantern empties the table; a later world upload rebuilds it
+    for c in cells:
+        r.set_block(*c, 0)
+    r.set_block(30, 21, 30, 0)
+    assert len(r.instances()) == 0 and len(r.lights()[1]) == 0
+    r.close()
