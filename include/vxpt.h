@@ -57,7 +57,8 @@ enum vxpt_buffer {
     VXPT_BUF_TEXELS = 43,        /* every loaded texture's RGBA8 mip chain (vxpt_texture_table) */
     /* emissive-triangle lights of the instanced meshes (vxpt_load_models / vxpt_get_lights) */
     VXPT_BUF_LIGHTS = 44,        /* nLights x 32 B LightInfo (Light.h:13-23)                     */
-    VXPT_BUF_LIGHT_ALIAS = 45    /* nLights x {f32 q, f32 p, i32 alias} (AliasTable.h bins)      */
+    VXPT_BUF_LIGHT_ALIAS = 45,   /* nLights x {f32 q, f32 p, i32 alias} (AliasTable.h bins)      */
+    VXPT_BUF_BLOOM = 46          /* post-process: the horizontally blurred bloom, Float4 per pixel */
 };
 
 typedef struct vxpt_config {
@@ -243,6 +244,10 @@ int vxpt_get_post_params(vxpt_ctx *ctx, vxpt_post_params *out);
  * pixel x, y, uv, and the accumulated sun luminance (parity hook) */
 int vxpt_get_sun_projection(vxpt_ctx *ctx, float out6[6]);
 int vxpt_postprocess(vxpt_ctx *ctx, const vxpt_post_params *p, float dt_ms);
+/* vxpt_postprocess over the bands of vxpt_band_link'ed contexts of one process (the 1-GPU stand-in
+ * for the RCCL band path, which vxpt_postprocess takes by itself on a context with a communicator):
+ * the denoiser output's 1-row halo, the histogram summed over the bands, the bloom's halo */
+int vxpt_postprocess_linked(vxpt_ctx **ctxs, int n, const vxpt_post_params *p, float dt_ms);
 /* OfflineBackend::writeFrameBufferToPNG (OfflineBackend.cpp:191-221): rgba = W*H float4 (the
  * frame), clamped to [0,1], x255 truncated, rows flipped, written as 8-bit RGB PNG */
 int vxpt_write_png_rgba32f(const char *path, int w, int h, const float *rgba);

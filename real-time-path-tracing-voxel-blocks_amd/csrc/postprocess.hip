@@ -61,8 +61,8 @@ __global__ __launch_bounds__(256) void k_lum_bloom(PostArgs a, int doHist, int d
     __shared__ float sC[TY][CW][3];
     __shared__ unsigned sH[kBins];
     const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
-    const int W = a.W, H = a.H;
+    const int x0 = blockIdx.x * TX, y0 = a.y0 + blockIdx.y * TY;
+    const int W = a.W, H = a.H, y1 = a.y1;  // rows [y0, y1) are this band's; y0 - 1 and y1 its halo
     sH[tid] = 0u;
     __syncthreads();
     for (int i = tid; i < (TY + 2) * LW; i += 256) {
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void k_lum_bloom(PostArgs a, int doHist, int d
         if (gx >= 0 && gx < W && gy >= 0 && gy < H) {
             const V3 c = ld3(a.input, W, gx, gy);
             l = lum_ref(c);
-            if (ly >= 1 && ly <= TY && lx >= 1 && lx <= CW) {
+            if (ly >= 1 && ly <= TY && lx >= 1 && lx <= CW && gy < y1) {
                 sC[ly - 1][lx - 1][0] = c.x;
                 sC[ly - 1][lx - 1][1] = c.y;
                 sC[ly - 1][lx - 1][2] = c.z;
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_lum_bloom(PostArgs a, int doHist, int d
     for (int i = tid; i < TY * CW; i += 256) {
         const int ey = i / CW, ex = i - ey * CW;
         const int gx = x0 - kHalo + ex, gy = y0 + ey;
-        if (gx < 0 || gx >= W || gy >= H) continue;
+        if (gx < 0 || gx >= W || gy >= y1) continue;
         const int lx = ex + 1, ly = ey + 1;
         const float n[4] = {sL[ly][lx - 1], sL[ly][lx + 1], sL[ly - 1][lx], sL[ly + 1][lx]};
         const V3 e = bloom_extract(V3(sC[ey][ex][0], sC[ey][ex][1], sC[ey][ex][2]), sL[ly][lx], n, thr);
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void k_lum_bloom(PostArgs a, int doHist, int d
     for (int i = tid; i < TY * TX; i += 256) {
         const int ey = i / TX, ex = i - ey * TX;
         const int x = x0 + ex, y = y0 + ey;
-        if (x >= W || y >= H) continue;
+        if (x >= W || y >= y1) continue;
         V3 r(0.0f);
         float tw = 0.0f;
         for (int k = -half; k <= half; k++) {  // edge-clamped taps; a clamped tap stays in the apron
@@ -182,8 +182,8 @@ __global__ __launch_bounds__(64) void k_exposure(PostArgs a) {
 
 // Bloom for radii wider than the LDS apron: extract -> bloomA, horizontal blur -> bloomB
 __global__ __launch_bounds__(256) void k_bloom_extract(PostArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.y1) return;
     const V3 c = ld3(a.input, a.W, x, y);
     float n[4];
     const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
@@ -194,8 +194,8 @@ __global__ __launch_bounds__(256) void k_bloom_extract(PostArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_bloom_blur_h(PostArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.y1) return;
     const int half = blur_half(a.p);
     V3 r(0.0f);
     float tw = 0.0f;
@@ -284,8 +284,8 @@ VX_D float srgb(float c) { return (c <= 0.0031308f) ? 12.92f * c : 1.055f * powf
 // VignetteKernel, FilmicToneMapping (:58-117), DrawCrosshair (PostProcessor.cu:14-46),
 // CopyToInteropBuffer (:48-63).  64-wide rows: the vertical taps are coalesced row reads.
 __global__ __launch_bounds__(256) void k_compose(PostArgs a, int flare) {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= a.W || y >= a.H) return;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = a.y0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= a.W || y >= a.y1) return;
     const PostParamsDev &p = a.p;
     V3 c = ld3(a.input, a.W, x, y);
     if (p.enableBloom) {
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void k_compose(PostArgs a, int flare) {
         if (tw > 0.0f) r /= tw;
         c = c + r * p.bloomIntensity;
     }
-    if (flare && a.depth[(size_t)a.sunPy * a.W + a.sunPx] >= 1.0e26f) c = c + lens_flare(a, x, y);
+    if (flare && a.hist[kBins] != 0u) c = c + lens_flare(a, x, y);  // the sun pixel is sky (k_sun_flag)
     if (p.enableVignette) c *= vignette(p, a.W, a.H, x, y);
     c *= p.enableAutoExposure ? a.state[1] : p.manualExposure;
     V3 t;
@@ -327,25 +327,46 @@ __global__ __launch_bounds__(256) void k_compose(PostArgs a, int flare) {
     a.frame[(size_t)y * a.W + x] = make_float4(t.x, t.y, t.z, 0.0f);
 }
 
+// The lens flare's sun test (depth of the sun's pixel is sky) as a flag beside the histogram,
+// written by the band that owns the pixel (0 elsewhere), so that a band all-reduce of the
+// histogram carries it to every band
+__global__ void k_sun_flag(PostArgs a) {
+    const bool own = a.sunPy >= a.y0 && a.sunPy < a.y1;
+    a.hist[kBins] = (own && a.depth[(size_t)a.sunPy * a.W + a.sunPx] >= 1.0e26f) ? 1u : 0u;
+}
+
 }  // namespace
+
+int post_bloom_half(const PostArgs &a) { return a.p.enableBloom ? blur_half(a.p) : 0; }
 
 // HBM traffic per pixel with bloom on: pass 1 reads 16 B (+ apron) and writes 16 B of bloomB,
 // pass 3 reads 16 B input + 16 B bloomB (+ taps from cache) and writes 16 B: 80 B per pixel.
-hipError_t launch_postprocess(const PostArgs &a, hipStream_t st) {
+// Phase 1: histogram + bloom of the band's rows (reads input rows y0 - 1 .. y1) and the sun flag;
+// phase 2 (after a banded frame's histogram all-reduce and bloomB halo): exposure + compose.
+hipError_t launch_post_phase1(const PostArgs &a, hipStream_t st) {
+    const int rows = a.y1 - a.y0;
     const bool lds = blur_half(a.p) <= kHalo;
     const int hist = a.p.enableAutoExposure ? 1 : 0, bloomLds = a.p.enableBloom && lds ? 1 : 0;
     if (hist || bloomLds)
-        hipLaunchKernelGGL(k_lum_bloom, dim3((a.W + TX - 1) / TX, (a.H + TY - 1) / TY), dim3(256), 0, st, a, hist,
+        hipLaunchKernelGGL(k_lum_bloom, dim3((a.W + TX - 1) / TX, (rows + TY - 1) / TY), dim3(256), 0, st, a, hist,
                            bloomLds);
     if (a.p.enableBloom && !lds) {
-        const dim3 g((a.W + 15) / 16, (a.H + 15) / 16);
+        const dim3 g((a.W + 15) / 16, (rows + 15) / 16);
         hipLaunchKernelGGL(k_bloom_extract, g, dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_bloom_blur_h, g, dim3(256), 0, st, a);
     }
-    if (hist) hipLaunchKernelGGL(k_exposure, dim3(1), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(k_compose, dim3((a.W + 63) / 64, (a.H + 3) / 4), dim3(256), 0, st, a,
+    if (a.p.enableLensFlare && a.sunOnScreen) hipLaunchKernelGGL(k_sun_flag, dim3(1), dim3(1), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_post_phase2(const PostArgs &a, hipStream_t st) {
+    if (a.p.enableAutoExposure) hipLaunchKernelGGL(k_exposure, dim3(1), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_compose, dim3((a.W + 63) / 64, (a.y1 - a.y0 + 3) / 4), dim3(256), 0, st, a,
                        a.p.enableLensFlare && a.sunOnScreen ? 1 : 0);
     return hipGetLastError();
+}
+hipError_t launch_postprocess(const PostArgs &a, hipStream_t st) {
+    if (hipError_t e = launch_post_phase1(a, st)) return e;
+    return launch_post_phase2(a, st);
 }
 
 }  // namespace vx

@@ -229,13 +229,17 @@ struct PostArgs {
     float4 *bloomA, *bloomB;        // bloom extract (wide-radius path) / horizontally blurred bloom
     float4 *frame;                  // result: Float4(sRGB colour, 0) (CopyToInteropBuffer)
     const float *depth;             // lens-flare sun visibility
-    unsigned *hist;                 // 256 luminance bins (integer counts, cleared by k_exposure)
+    unsigned *hist;                 // 256 luminance bins (integer counts, cleared by k_exposure) + the sun flag
+    int y0, y1;                     // the rows this context composes (its band; 0, H unbanded)
     float *state;                   // [0] current average luminance, [1] exposure of this frame
     float dtMs;                     // frame time for the exposure adaptation (Timer::getDeltaTime, ms)
     int sunOnScreen, sunPx, sunPy;  // ProjectSunToScreen (PostProcessingPipeline.cu:187-206)
     float sunU, sunV, sunLuminance;
 };
 hipError_t launch_postprocess(const PostArgs &a, hipStream_t st);
+hipError_t launch_post_phase1(const PostArgs &a, hipStream_t st);
+hipError_t launch_post_phase2(const PostArgs &a, hipStream_t st);
+int post_bloom_half(const PostArgs &a);  // rows of bloomB the compose pass taps above and below
 bool decode_png(const std::string &path, int &w, int &h, int &ch, std::vector<uint8_t> &px);
 bool load_obj(const std::string &path, std::vector<float> &pos, std::vector<float> &uv);
 

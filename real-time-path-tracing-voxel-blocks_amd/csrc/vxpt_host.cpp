@@ -132,7 +132,8 @@ bool as_bool(const std::string &s) { return s == "true" || s == "1" || s == "Tru
 
 }  // namespace
 
-constexpr int kBlockTypes = 30;  // BlockTypeNum (generated/voxelengine/BlockType.h:39)
+constexpr int kBlockTypes = 30;
+constexpr int kPostHist = 257;   // 256 luminance bins + the lens flare's sun flag  // BlockTypeNum (generated/voxelengine/BlockType.h:39)
 
 struct vxpt_ctx {
     int W = 0, H = 0, dev = 0, rowBegin = 0, rowEnd = 0;
@@ -499,6 +500,7 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_BRICK_IDS: p = c->bricks.p; bytes = (size_t)c->nBricks * 64; return !forWrite && c->bricks.p;
         case VXPT_BUF_MACRO_MASKS: p = c->macro.p; bytes = (size_t)c->nBricks / 64 * 8; return !forWrite && c->macro.p;
         case VXPT_BUF_TEXELS: p = c->texels.p; bytes = c->nTexels * 4; return !forWrite && c->texels.p;
+        case VXPT_BUF_BLOOM: p = c->bloomB; bytes = n * 16; return c->bloomB != nullptr;
         case VXPT_BUF_LIGHTS: p = c->lights.p; bytes = (size_t)c->nLights * sizeof(LightInfo); return !forWrite && c->nLights;
         case VXPT_BUF_LIGHT_ALIAS:
             p = c->lightAlias.p; bytes = (size_t)c->nLights * sizeof(AliasBin); return !forWrite && c->nLights;
@@ -1998,22 +2000,24 @@ int vxpt_get_post_params(vxpt_ctx *c, vxpt_post_params *out) {
     return VXPT_OK;
 }
 
-int vxpt_postprocess(vxpt_ctx *c, const vxpt_post_params *pp, float dtMs) {
-    if (!c) return VXPT_ERR_ARG;
+namespace {
+
+// the context's post-process arguments (allocating its buffers on first use)
+int post_args(vxpt_ctx *c, const vxpt_post_params *pp, float dtMs, PostArgs &a) {
     if (!pp) pp = &c->yamlPost;
-    HIPCHK(c, hipSetDevice(c->dev));
     const size_t n = (size_t)c->W * c->H;
     if (!c->frame) {
         if (dalloc(c, c->bloomA, n) || dalloc(c, c->bloomB, n) ||
-            dalloc(c, c->frame, n) || dalloc(c, c->postHist, 256) || dalloc(c, c->postState, 4))
+            dalloc(c, c->frame, n) || dalloc(c, c->postHist, kPostHist) || dalloc(c, c->postState, 4))
             return VXPT_ERR_HIP;
         const float init[4] = {0.18f, 1.0f, 0.0f, 0.0f};  // m_currentAvgLuminance (PostProcessingPipeline.cu:433)
         HIPCHK(c, hipMemcpyAsync(c->postState, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemsetAsync(c->postHist, 0, 256 * sizeof(unsigned), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->postHist, 0, kPostHist * sizeof(unsigned), c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    PostArgs a{};
+    a = PostArgs{};
     a.W = c->W; a.H = c->H;
+    a.y0 = c->rowBegin; a.y1 = c->rowEnd;
     a.p = {pp->manual_exposure, pp->tone_mapping_curve, pp->white_point, pp->contrast, pp->saturation, pp->lift,
            pp->gain, pp->enable_bloom, pp->bloom_threshold, pp->bloom_intensity, pp->bloom_radius,
            pp->enable_auto_exposure, pp->exposure_speed, pp->exposure_min, pp->exposure_max,
@@ -2029,7 +2033,69 @@ int vxpt_postprocess(vxpt_ctx *c, const vxpt_post_params *pp, float dtMs) {
     a.state = c->postState;
     a.dtMs = dtMs;
     sun_projection(c, a.sunOnScreen, a.sunPx, a.sunPy, a.sunU, a.sunV, a.sunLuminance);
+    return VXPT_OK;
+}
+
+// A banded frame's post-process (PostProcessingPipeline::Execute over bands): the denoiser
+// output's 1-row halo (the bloom extract's vertical neighbours), each band's histogram + bloom
+// rows, the histogram (+ sun flag) summed over the bands -- an RCCL all-reduce of 257 u32, or a
+// host sum for linked contexts -- so that every band adapts the same exposure, the horizontally
+// blurred bloom's halo for the vertical taps, then exposure + compose of the band's rows.
+int band_post(std::vector<vxpt_ctx *> &cs, const vxpt_post_params *pp, float dtMs) {
+    std::vector<PostArgs> as(cs.size());
+    for (size_t k = 0; k < cs.size(); ++k) BANDCHK(post_args(cs[k], pp, dtMs, as[k]));
+    const int half = post_bloom_half(as[0]);
+    if (half > 0 && half > cs[0]->rowEnd - cs[0]->rowBegin)
+        return fail(cs[0], VXPT_ERR_ARG, "bloom radius exceeds the band height");
+    BANDCHK(exchange_set(cs, {{VXPT_BUF_OUTPUT, 1}}));
+    for (size_t k = 0; k < cs.size(); ++k) HIPCHK(cs[k], launch_post_phase1(as[k], cs[k]->stream));
+    const bool reduce = as[0].p.enableAutoExposure || (as[0].p.enableLensFlare && as[0].sunOnScreen);
+    if (reduce) {
+        if (cs.size() == 1 && cs[0]->comm) {
+            vxpt_ctx *c = cs[0];
+            if (ncclAllReduce(c->postHist, c->postHist, kPostHist, ncclUint32, ncclSum, c->comm, c->stream) != ncclSuccess)
+                return fail(c, VXPT_ERR_HIP, "ncclAllReduce (post histogram)");
+        } else {
+            std::vector<unsigned> sum(kPostHist, 0u), h(kPostHist);
+            for (vxpt_ctx *c : cs) {
+                HIPCHK(c, hipMemcpyAsync(h.data(), c->postHist, kPostHist * 4, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                for (int i = 0; i < kPostHist; ++i) sum[i] += h[i];
+            }
+            for (vxpt_ctx *c : cs) {
+                HIPCHK(c, hipMemcpyAsync(c->postHist, sum.data(), kPostHist * 4, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+            }
+        }
+    }
+    if (half > 0) BANDCHK(exchange_set(cs, {{VXPT_BUF_BLOOM, half}}));
+    for (size_t k = 0; k < cs.size(); ++k) HIPCHK(cs[k], launch_post_phase2(as[k], cs[k]->stream));
+    return VXPT_OK;
+}
+
+}  // namespace
+
+int vxpt_postprocess(vxpt_ctx *c, const vxpt_post_params *pp, float dtMs) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    if (c->comm && c->nranks > 1) {
+        std::vector<vxpt_ctx *> cs{c};
+        return band_post(cs, pp, dtMs);
+    }
+    PostArgs a;
+    if (int r = post_args(c, pp, dtMs, a)) return r;
     HIPCHK(c, launch_postprocess(a, c->stream));
+    return VXPT_OK;
+}
+
+int vxpt_postprocess_linked(vxpt_ctx **cs, int n, const vxpt_post_params *pp, float dtMs) {
+    if (!cs || n < 1) return VXPT_ERR_ARG;
+    std::vector<vxpt_ctx *> v(cs, cs + n);
+    for (int k = 0; k < n; ++k)
+        if (!cs[k] || cs[k]->rank != k || cs[k]->nranks != n) return VXPT_ERR_STATE;
+    HIPCHK(cs[0], hipSetDevice(cs[0]->dev));
+    if (int r = band_post(v, pp, dtMs)) return r;
+    for (vxpt_ctx *c : v) HIPCHK(c, hipStreamSynchronize(c->stream));
     return VXPT_OK;
 }
 

@@ -24,7 +24,7 @@ BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERI
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
            PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38,
            OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42, TEXELS=43, LIGHTS=44,
-           LIGHT_ALIAS=45)
+           LIGHT_ALIAS=45, BLOOM=46)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
@@ -151,6 +151,7 @@ def load_library(path=LIB_PATH):
         "vxpt_copy_rows": (I, [P, I, I, I, P, I]),
         "vxpt_get_post_params": (I, [P, ctypes.POINTER(PostParams)]),
         "vxpt_postprocess": (I, [P, ctypes.POINTER(PostParams), F]),
+        "vxpt_postprocess_linked": (I, [ctypes.POINTER(P), I, ctypes.POINTER(PostParams), F]),
         "vxpt_get_sun_projection": (I, [P, P]),
         "vxpt_get_denoise_params": (I, [P, ctypes.POINTER(DenoiseParams)]),
         "vxpt_write_png_rgba32f": (I, [ctypes.c_char_p, I, I, P]),
@@ -534,6 +535,12 @@ class LinkedBands:
         p = params or DenoiseParams.defaults()
         if self.lib.vxpt_render_frame_linked(self._arr, len(self.rs), ctypes.byref(p), frame_num, spp) != 0:
             raise VxptError("vxpt_render_frame_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
+
+    def postprocess(self, params=None, dt_ms=16.6667):
+        """vxpt_postprocess over the bands (histogram summed over them, 1-row and bloom halos)."""
+        if self.lib.vxpt_postprocess_linked(self._arr, len(self.rs), ctypes.byref(params) if params is not None else None,
+                                            float(dt_ms)) != 0:
+            raise VxptError("vxpt_postprocess_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
 
 
 def write_png(path, frame):

@@ -170,3 +170,40 @@ def test_gpu_library_band_schedule_matches_single_context(n, w, h):
         ref = single.read("OUTPUT")
         out = np.concatenate([r.read("OUTPUT")[y0:y1] for r, (y0, y1) in zip(rs, rows)])
         np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,w,h,variant", [(2, 96, 160, "yaml"), (2, 96, 160, "wide_bloom_flare"),
+                                           (8, 640, 640, "yaml")])
+def test_gpu_band_postprocess_matches_single_context(n, w, h, variant):
+    """A banded frame's post-process (vxpt_postprocess_linked: the denoiser output's 1-row halo,
+    the histogram + sun flag summed over the bands, the bloom's halo; the RCCL path differs
+    only in the transport) equals the single-context post-process bit for bit over 3 frames
+    (the auto exposure's state carries across frames)."""
+    import vxpt
+    cam = C1_CAMERA
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    single = make()
+    pp = single.post_params()
+    if variant == "wide_bloom_flare":  # the 2-pass bloom (radius past the LDS apron), lens flare, vignette
+        pp.bloom_radius, pp.bloom_threshold, pp.enable_lens_flare, pp.enable_vignette = 10.0, 0.05, 1, 1
+    rs = [make() for _ in range(n)]
+    linked = vxpt.LinkedBands(rs)
+    rows = [bands.band_rows(h, n, k) for k in range(n)]
+    for f in range(3):
+        single.render_frame(f, 1, p)
+        linked.render_frame(f, 1, p)
+        single.postprocess(pp, 16.0)
+        linked.postprocess(pp, 16.0)
+        ref = single.read("FRAME")
+        out = np.concatenate([r.read("FRAME")[y0:y1] for r, (y0, y1) in zip(rs, rows)])
+        np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
