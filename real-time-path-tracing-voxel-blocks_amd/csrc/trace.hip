@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int 
 // stop after cap more iterations and the unfinished ones move on to the next
 // level, same shard, one atomic per wave.
 template <bool OCC>
-__global__ __launch_bounds__(256) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
     const WaveBufs &w = a.wb;
     const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
     const int shard = wv % kShards, step = gridDim.x * 256 / kShards;
@@ -559,7 +559,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.pMeta[s] = meta;
 }
 
-__global__ __launch_bounds__(256) void k_shade(TraceArgs a, int seg) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_shade(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
     shade_slot(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
