@@ -191,6 +191,12 @@ int vxpt_get_instances(vxpt_ctx *ctx, int32_t *out, int cap, int *n_instances);
  * (accumulatedLocalLightLuminance); the records are VXPT_BUF_LIGHTS / VXPT_BUF_LIGHT_ALIAS */
 int vxpt_get_lights(vxpt_ctx *ctx, uint32_t *mapping, int cap, int *n_mapped, uint32_t *n_lights,
                     float *local_luminance);
+/* closest hit against the instanced meshes (the IAS the reference's rays traverse besides the
+ * voxel faces; meshes.hip): n rays of 8 floats (origin, tmin, direction, tmax); out 4 floats per ray
+ * (t, u, v barycentrics, hit 0/1), ids 2 int32 (instance row of vxpt_get_instances, triangle);
+ * cull = 1 skips back faces (radiance rays), 0 not (visibility rays).  Ties: smaller t, then row,
+ * then triangle.  Parity hook: the path kernels do not consult the meshes yet */
+int vxpt_mesh_probe(vxpt_ctx *ctx, const float *rays, int n, int cull, float *out, int32_t *ids);
 
 /* ---- voxel edits (VoxelEngine::update click path, VoxelEngine.cu:855-975, 1040-1346) ---- */
 /* performRayTraversal (:1040-1166) of the current camera ray on the world.  out: hit, hit x, y, z,

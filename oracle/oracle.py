@@ -78,6 +78,7 @@ def lib():
             "orc_oct_encode": (ctypes.c_uint32, [P]),
             "orc_oct_decode": (None, [ctypes.c_uint32, P]),
             "orc_tri_lights": (None, [P, I, P, I, P, P, P]),
+            "orc_mesh_probe": (None, [P, P, P, P, I, P, I, I, P, P]),
         }
         for k, (r, a) in sig.items():
             fn = getattr(L, k)
@@ -373,3 +374,27 @@ def alias_table(weights):
     for i in list(small) + list(large):
         scaled[i] = np.float32(1.0)
     return scaled, prob, alias, s
+
+
+def mesh_probe(models, rows, rays, cull):
+    """Closest instanced-mesh hit by brute force (orc_mesh_probe).  models: {block: pos [T,3,3]};
+    rows: vxpt_get_instances rows (object, id, x, y, z); rays [N, 8].  Returns (out [N,4], ids [N,2])."""
+    rows = np.asarray(rows, np.int32).reshape(-1, 5)
+    tris, off, cnt = [], [], []
+    acc = 0
+    for r in rows:
+        pos = models.get(int(r[0]) + 1)
+        k = 0 if pos is None else len(pos)
+        off.append(acc)
+        cnt.append(k)
+        if k:
+            tris.append(np.asarray(pos, np.float32).reshape(-1, 9))
+        acc += k
+    tris = np.ascontiguousarray(np.concatenate(tris) if tris else np.zeros((1, 9), np.float32), np.float32)
+    off, cnt = np.array(off + [0], np.int32), np.array(cnt + [0], np.int32)
+    cells = np.ascontiguousarray(rows[:, 2:5].astype(np.float32).reshape(-1) if len(rows) else np.zeros(3, np.float32))
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+    out, ids = np.zeros((len(rays), 4), np.float32), np.zeros((len(rays), 2), np.int32)
+    lib().orc_mesh_probe(_p(tris), _p(off), _p(cnt), _p(cells), len(rows), _p(rays), len(rays), int(cull), _p(out),
+                         _p(ids))
+    return out, ids

@@ -129,4 +129,47 @@ void orc_tri_lights(const float *tri, int nTri, const int *inst, int nInst, cons
         }
 }
 
+// Instanced-mesh closest hit by brute force (the reference's IAS query; meshes.hip walks a BVH
+// and must agree exactly): every instance row in order, the ray origin translated by -cell
+// (the instance transform), Moller-Trumbore with plain IEEE arithmetic in the kernel's order,
+// the first strictly closer hit wins (= ties to the smaller row, then triangle).
+void orc_mesh_probe(const float *tris, const int *triOff, const int *triCnt, const float *cells, int nInst,
+                    const float *rays, int n, int cull, float *out, int *ids) {
+    auto dt3 = [](const F3 &a, const F3 &b) { return a.x * b.x + a.y * b.y + a.z * b.z; };
+    auto cr3 = [](const F3 &a, const F3 &b) {
+        return F3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    };
+    for (int r = 0; r < n; ++r) {
+        const float *ry = rays + (size_t)r * 8;
+        const F3 o(ry[0], ry[1], ry[2]), d(ry[4], ry[5], ry[6]);
+        const float tmin = ry[3];
+        float bt = ry[7], bu = 0.0f, bv = 0.0f;
+        int bi = -1, bk = -1;
+        for (int i = 0; i < nInst; ++i) {
+            const F3 oo(o.x - cells[i * 3], o.y - cells[i * 3 + 1], o.z - cells[i * 3 + 2]);
+            for (int k = 0; k < triCnt[i]; ++k) {
+                const float *t9 = tris + ((size_t)triOff[i] + k) * 9;
+                const F3 v0(t9[0], t9[1], t9[2]), v1(t9[3], t9[4], t9[5]), v2(t9[6], t9[7], t9[8]);
+                const F3 e1 = v1 - v0, e2 = v2 - v0;
+                const F3 p = cr3(d, e2);
+                const float det = dt3(e1, p);
+                if (cull ? !(det > 0.0f) : !(det != 0.0f)) continue;
+                const float inv = 1.0f / det;
+                const F3 s = oo - v0;
+                const float u = dt3(s, p) * inv;
+                if (!(u >= 0.0f && u <= 1.0f)) continue;
+                const F3 q = cr3(s, e1);
+                const float v = dt3(d, q) * inv;
+                if (!(v >= 0.0f && u + v <= 1.0f)) continue;
+                const float t = dt3(e2, q) * inv;
+                if (!(t >= tmin && t <= bt)) continue;
+                if (bi >= 0 && !(t < bt)) continue;
+                bt = t; bu = u; bv = v; bi = i; bk = k;
+            }
+        }
+        out[r * 4] = bt; out[r * 4 + 1] = bu; out[r * 4 + 2] = bv; out[r * 4 + 3] = bi >= 0 ? 1.0f : 0.0f;
+        ids[r * 2] = bi; ids[r * 2 + 1] = bk;
+    }
+}
+
 }  // extern "C"

@@ -256,6 +256,35 @@ struct LightInfo {
 // (VoxelEngine.cu:53-116), written from out[0]; weight[k] = luminance(radiance) * area of the
 // decoded record (extractRadianceKernel, :139-147).  tri: 9 floats per triangle (object
 // space), inst: 3 ints per instance (the cell = the translation of its 3x4 transform).
+// Instanced-mesh ray queries (the geometry half): two-level BVH -- a TLAS over
+// the instances' world boxes, one BLAS per block type's mesh in object space (the instance
+// transform is a translation by its cell, VoxelEngine.cu:364-369).  Node boxes are widened at
+// build time so that box culling can only drop triangles the exact test would also reject.
+// Inner node: count = 0, children left and left + 1; leaf: count primitives from left.
+struct BvhNode {
+    float lo[3];
+    int left;
+    float hi[3];
+    int count;
+};
+struct MeshInst {
+    float cell[3];
+    int block;  // block type -> its BLAS
+    int row;    // the instance's row in vxpt_get_instances
+};
+struct MeshDev {
+    const BvhNode *tlas;    // over instances (primitive = MeshInst index)
+    const MeshInst *inst;
+    const BvhNode *blas;    // every block type's BLAS, concatenated
+    const float *tri;       // 9 floats per triangle in BLAS leaf order (object space)
+    const int *triId;       // the mesh's own triangle index of each
+    const int2 *root;       // per block type: (first BLAS node, first triangle); -1 = no mesh
+    int nInst;
+};
+// closest hit (tie: smaller t, then instance, then triangle) of n rays (o.xyz, tmin, d.xyz, tmax);
+// out: t, u, v, hit flag per ray; ids: instance, triangle.  cull = skip back faces (radiance rays)
+hipError_t launch_mesh_probe(const MeshDev &m, const float *rays, int n, int cull, float *out, int *ids,
+                             hipStream_t st);
 hipError_t launch_tri_lights(const float *tri, int nTri, const int *inst, int nInst, V3 radiance, LightInfo *out,
                              float *weight, hipStream_t st);
 

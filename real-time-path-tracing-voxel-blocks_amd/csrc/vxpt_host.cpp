@@ -201,6 +201,17 @@ struct vxpt_ctx {
     DBuf<int> lightInst;
     unsigned nLights = 0;
     float localLightLum = 0.0f;
+    // two-level BVH of the instanced meshes (meshes.hip): BLAS per block type, TLAS per world
+    std::vector<BvhNode> hBlas;
+    std::vector<float> hBlasTri;
+    std::vector<int> hBlasTriId;
+    std::vector<int2> hRoot;  // per block type: (first node, first triangle), -1 = no mesh
+    DBuf<BvhNode> blas, tlas;
+    DBuf<float> blasTri;
+    DBuf<int> blasTriId;
+    DBuf<int2> blasRoot;
+    DBuf<MeshInst> meshInst;
+    int nMeshInst = 0;
 
     // blue noise
     DBuf<uint8_t> bnSobol, bnScramble, bnRank;
@@ -1549,10 +1560,155 @@ int build_lights(vxpt_ctx *c) {
 
 }  // namespace
 
+// Median-split BVH over boxes (lo xyz, hi xyz per primitive): nodes[0] = root, children of an
+// inner node adjacent, leaves of at most leafMax primitives (order = primitive order in the
+// leaves).  Node boxes are widened by 1e-4 (1 + |coordinate|), far above the slab test's
+// rounding, so box culling is conservative.  Fails past a depth of 40 (the walk's stack is 48).
+bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> &nodes, std::vector<int> &order) {
+    const int n = (int)(box.size() / 6);
+    order.resize(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    nodes.assign(1, BvhNode{});
+    if (n == 0) return true;
+    struct Job { int node, b, e, depth; };
+    std::vector<Job> jobs{{0, 0, n, 0}};
+    while (!jobs.empty()) {
+        const Job j = jobs.back();
+        jobs.pop_back();
+        if (j.depth > 40) return false;
+        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        float clo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, chi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (int i = j.b; i < j.e; ++i) {
+            const float *bx = &box[(size_t)order[i] * 6];
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = std::min(lo[k], bx[k]);
+                hi[k] = std::max(hi[k], bx[k + 3]);
+                const float cc = 0.5f * (bx[k] + bx[k + 3]);
+                clo[k] = std::min(clo[k], cc);
+                chi[k] = std::max(chi[k], cc);
+            }
+        }
+        BvhNode &nd = nodes[j.node];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo[k] = lo[k] - 1e-4f * (1.0f + std::fabs(lo[k]));
+            nd.hi[k] = hi[k] + 1e-4f * (1.0f + std::fabs(hi[k]));
+        }
+        if (j.e - j.b <= leafMax) {
+            nd.left = j.b;
+            nd.count = j.e - j.b;
+            continue;
+        }
+        int axis = 0;
+        for (int k = 1; k < 3; ++k)
+            if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+        const int mid = (j.b + j.e) / 2;
+        std::nth_element(order.begin() + j.b, order.begin() + mid, order.begin() + j.e, [&](int x, int y) {
+            const float cx = box[(size_t)x * 6 + axis] + box[(size_t)x * 6 + axis + 3];
+            const float cy = box[(size_t)y * 6 + axis] + box[(size_t)y * 6 + axis + 3];
+            return cx < cy || (cx == cy && x < y);
+        });
+        const int left = (int)nodes.size();
+        nodes[j.node].left = left;
+        nodes[j.node].count = 0;
+        nodes.push_back(BvhNode{});
+        nodes.push_back(BvhNode{});
+        jobs.push_back({left, j.b, mid, j.depth + 1});
+        jobs.push_back({left + 1, mid, j.e, j.depth + 1});
+    }
+    return true;
+}
+
+// every loaded mesh's BLAS (object space), concatenated
+int build_blas(vxpt_ctx *c) {
+    c->hBlas.clear();
+    c->hBlasTri.clear();
+    c->hBlasTriId.clear();
+    c->hRoot.assign(kBlockTypes, make_int2(-1, -1));
+    for (int b = 0; b < kBlockTypes; ++b) {
+        const auto &bd = c->blocks[b];
+        if (!bd.instanced || bd.triangles == 0) continue;
+        std::vector<float> box((size_t)bd.triangles * 6);
+        for (int t = 0; t < bd.triangles; ++t)
+            for (int k = 0; k < 3; ++k) {
+                const float *v = &bd.pos[(size_t)t * 9];
+                box[(size_t)t * 6 + k] = std::min(v[k], std::min(v[3 + k], v[6 + k]));
+                box[(size_t)t * 6 + 3 + k] = std::max(v[k], std::max(v[3 + k], v[6 + k]));
+            }
+        std::vector<BvhNode> nodes;
+        std::vector<int> order;
+        if (!build_bvh(box, 4, nodes, order)) return fail(c, VXPT_ERR_STATE, "mesh BVH too deep");
+        c->hRoot[b] = make_int2((int)c->hBlas.size(), (int)c->hBlasTriId.size());
+        c->hBlas.insert(c->hBlas.end(), nodes.begin(), nodes.end());
+        for (int t : order) {
+            c->hBlasTri.insert(c->hBlasTri.end(), bd.pos.begin() + (size_t)t * 9, bd.pos.begin() + (size_t)t * 9 + 9);
+            c->hBlasTriId.push_back(t);
+        }
+    }
+    if (!c->hBlas.empty()) {
+        if (int r = upload_vec(c, c->blas, c->hBlas.data(), c->hBlas.size())) return r;
+        if (int r = upload_vec(c, c->blasTri, c->hBlasTri.data(), c->hBlasTri.size())) return r;
+        if (int r = upload_vec(c, c->blasTriId, c->hBlasTriId.data(), c->hBlasTriId.size())) return r;
+    }
+    return upload_vec(c, c->blasRoot, c->hRoot.data(), c->hRoot.size());
+}
+
+// the world's TLAS over the instances whose block type has a mesh
+int build_tlas(vxpt_ctx *c) {
+    std::vector<MeshInst> mi;
+    std::vector<float> box;
+    for (size_t k = 0; k < c->instances.size(); k += 5) {
+        const int block = c->instances[k] + 1;
+        const int2 r = c->hRoot.empty() ? make_int2(-1, -1) : c->hRoot[block];
+        if (r.x < 0) continue;
+        const BvhNode &root = c->hBlas[r.x];
+        const float cell[3] = {(float)c->instances[k + 2], (float)c->instances[k + 3], (float)c->instances[k + 4]};
+        mi.push_back(MeshInst{{cell[0], cell[1], cell[2]}, block, (int)(k / 5)});
+        for (int a = 0; a < 3; ++a) box.push_back(root.lo[a] + cell[a]);
+        for (int a = 0; a < 3; ++a) box.push_back(root.hi[a] + cell[a]);
+    }
+    std::vector<BvhNode> nodes;
+    std::vector<int> order;
+    if (!build_bvh(box, 2, nodes, order)) return fail(c, VXPT_ERR_STATE, "instance BVH too deep");
+    std::vector<MeshInst> sorted;
+    for (int i : order) sorted.push_back(mi[i]);
+    c->nMeshInst = (int)sorted.size();
+    if (c->nMeshInst == 0) return VXPT_OK;
+    if (int r = upload_vec(c, c->tlas, nodes.data(), nodes.size())) return r;
+    return upload_vec(c, c->meshInst, sorted.data(), sorted.size());
+}
+
 int refresh_instances(vxpt_ctx *c) {
     if (!c->modelsLoaded) return VXPT_OK;
     collect_instances(c);
+    if (int r = build_tlas(c)) return r;
     return build_lights(c);
+}
+
+// closest instanced-mesh hit of n rays (8 floats each: o, tmin, d, tmax): out 4 floats (t, u, v,
+// hit), ids 2 ints (instance row, triangle)
+int vxpt_mesh_probe(vxpt_ctx *c, const float *rays, int n, int cull, float *out, int32_t *ids) {
+    if (!c || !rays || !out || !ids || n < 0) return VXPT_ERR_ARG;
+    if (n == 0) return VXPT_OK;
+    HIPCHK(c, hipSetDevice(c->dev));
+    if (c->hRoot.empty()) c->hRoot.assign(kBlockTypes, make_int2(-1, -1));
+    if (!c->blasRoot.p)
+        if (int r = upload_vec(c, c->blasRoot, c->hRoot.data(), c->hRoot.size())) return r;
+    float *dr = nullptr, *dout = nullptr;
+    int *dids = nullptr;
+    // scratch of this call only (freed below; dalloc's buffers live as long as the context)
+    HIPCHK(c, hipMalloc((void **)&dr, (size_t)n * 32));
+    HIPCHK(c, hipMalloc((void **)&dout, (size_t)n * 16));
+    HIPCHK(c, hipMalloc((void **)&dids, (size_t)n * 8));
+    HIPCHK(c, hipMemcpyAsync(dr, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    const MeshDev m{c->tlas.p, c->meshInst.p, c->blas.p, c->blasTri.p, c->blasTriId.p, c->blasRoot.p, c->nMeshInst};
+    HIPCHK(c, launch_mesh_probe(m, dr, n, cull, dout, dids, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ids, dids, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(dr);
+    hipFree(dout);
+    hipFree(dids);
+    return VXPT_OK;
 }
 
 // blocks.yaml (ids 13..29) + models.yaml + materials.yaml emission, then the OBJ meshes
@@ -1615,6 +1771,7 @@ int vxpt_load_models(vxpt_ctx *c, const char *root, int *loaded) {
     c->modelsLoaded = true;
     if (loaded) *loaded = nLoaded;
     HIPCHK(c, hipSetDevice(c->dev));
+    if (int r = build_blas(c)) return r;
     return refresh_instances(c);
 }
 

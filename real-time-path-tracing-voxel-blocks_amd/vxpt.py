@@ -129,6 +129,7 @@ def load_library(path=LIB_PATH):
         "vxpt_get_model": (I, [P, I, P, P, I, P]),
         "vxpt_get_instances": (I, [P, P, I, P]),
         "vxpt_get_lights": (I, [P, P, I, P, P, P]),
+        "vxpt_mesh_probe": (I, [P, P, I, I, P, P]),
         "vxpt_set_block": (I, [P, I, I, I, I]),
         "vxpt_click_block": (I, [P, I, P]),
         "vxpt_save_world": (I, [P, ctypes.c_char_p, ctypes.c_char_p]),
@@ -309,6 +310,14 @@ class Renderer:
         if n.value:
             self._chk(self.lib.vxpt_get_instances(self.ctx, _ptr(out), n.value, ctypes.byref(n)), "vxpt_get_instances")
         return out
+
+    def mesh_probe(self, rays, cull=False):
+        """Closest instanced-mesh hit of rays [N, 8] (o, tmin, d, tmax): (out [N,4] t,u,v,hit; ids [N,2])."""
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out, ids = np.zeros((len(r), 4), np.float32), np.zeros((len(r), 2), np.int32)
+        self._chk(self.lib.vxpt_mesh_probe(self.ctx, _ptr(r), len(r), int(bool(cull)), _ptr(out), _ptr(ids)),
+                  "vxpt_mesh_probe")
+        return out, ids
 
     def lights(self):
         """(mapping uint32 [M, 3], LightInfo records uint8 [L, 32], alias bins [L], local luminance)."""

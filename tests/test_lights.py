@@ -44,6 +44,19 @@ def _prism_obj(path, lo=0.28, hi=0.72, y0=0.07, y1=0.62):
             f.write("f %d/1 %d/2 %d/%d\n" % (a + 1, b + 1, c + 1, 1 + k % 2))
 
 
+def _random_mesh_obj(path, n=600, seed=4):
+    """n random triangles inside the leaves' overhanging box (-0.05 .. 1.07), some tiny, some large."""
+    rng = np.random.default_rng(seed)
+    with open(path, "w") as f:
+        for t in range(n):
+            c = rng.uniform(-0.05, 1.07, 3)
+            for k in range(3):
+                v = np.clip(c + rng.normal(0, 0.02 if t % 3 else 0.3, 3), -0.05, 1.07)
+                f.write("v %.7f %.7f %.7f\n" % tuple(v))
+        for t in range(n):
+            f.write("f %d %d %d\n" % (3 * t + 1, 3 * t + 2, 3 * t + 3))
+
+
 def _base_obj(path):
     """A flat quad (2 triangles) with `v//n` corners."""
     with open(path, "w") as f:
@@ -55,6 +68,7 @@ def model_root(tmp_path):
     os.makedirs(tmp_path / "models")
     _prism_obj(str(tmp_path / "models" / "lanternLight.obj"))
     _base_obj(str(tmp_path / "models" / "lanternBase.obj"))
+    _random_mesh_obj(str(tmp_path / "models" / "leavesCube4.obj"))
     return tmp_path
 
 
@@ -147,7 +161,7 @@ def test_light_table_matches_oracle(model_root):
     r = vxpt.Renderer(64, 64)
     r.load_settings()
     r.generate_terrain(CH, height_scale=32.0)
-    assert r.load_models(str(model_root)) == 2  # the prism and the base; the rest are missing
+    assert r.load_models(str(model_root)) == 3  # the prism, the base, the leaves; the rest are missing
     assert np.array_equal(r.model(LIGHT)[0], oracle.parse_obj(str(model_root / "models" / "lanternLight.obj"))[0])
     mp, recs, bins, lum = r.lights()
     assert len(r.instances()) == 0 and len(recs) == 0 and lum == 0.0
@@ -173,4 +187,41 @@ def test_light_table_matches_oracle(model_root):
         r.set_block(*c, 0)
     r.set_block(30, 21, 30, 0)
     assert len(r.instances()) == 0 and len(r.lights()[1]) == 0
+    r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cull", [0, 1])
+def test_mesh_probe_matches_brute_force(model_root, cull):
+    """The two-level BVH walk (meshes.hip) equals the oracle's brute-force loop over every
+    instance and triangle bit for bit: t, barycentrics, instance row and triangle."""
+    r = vxpt.Renderer(64, 64)
+    r.load_settings()
+    r.generate_terrain(CH, height_scale=32.0)
+    r.load_models(str(model_root))
+    rng = np.random.default_rng(11 + cull)
+    cells = set()
+    while len(cells) < 90:
+        cells.add((int(rng.integers(0, 64)), int(rng.integers(0, 32)), int(rng.integers(0, 64))))
+    for k, c in enumerate(sorted(cells)):
+        r.set_block(*c, (14, 14, 14, 14, 16, 15)[k % 6])
+    rows = r.instances()
+    models = {b: oracle.parse_obj(str(model_root / "models" / f))[0]
+              for b, f in ((14, "leavesCube4.obj"), (15, "lanternBase.obj"), (16, "lanternLight.obj"))}
+    n = 6000
+    o = rng.uniform([0, 0, 0], [64, 32, 64], (n, 3))
+    d = rng.normal(size=(n, 3))
+    aim = rows[rng.integers(0, len(rows), n // 2), 2:5] + rng.uniform(-0.05, 1.07, (n // 2, 3))
+    d[: n // 2] = aim - o[: n // 2]  # half the rays aim into an instance's cell
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d[::97, 1] = 0.0  # axis-parallel components
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3], rays[:, 4:7] = o, d
+    rays[:, 3] = np.where(np.arange(n) % 5 == 0, 0.5, 0.0)
+    rays[:, 7] = np.where(np.arange(n) % 7 == 0, 20.0, 1e27)
+    got, gid = r.mesh_probe(rays, cull)
+    want, wid = oracle.mesh_probe(models, rows, rays, cull)
+    assert 0.2 < want[:, 3].mean() < 0.95
+    np.testing.assert_array_equal(gid, wid)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
     r.close()
