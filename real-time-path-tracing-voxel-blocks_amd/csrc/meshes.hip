@@ -42,7 +42,7 @@ VX_D bool tri_hit(V3 o, V3 d, const float *t9, float tmin, float tmax, int cull,
 }
 
 // slab test against a widened box; an axis the ray does not move along only checks the origin
-VX_D bool box_hit(const BvhNode &n, V3 o, V3 inv, V3 d, float tmin, float tmax) {
+VX_D bool box_hit(const BvhNode &n, V3 o, V3 inv, V3 d, float tmin, float tmax, float &tEnter) {
     float t0 = tmin, t1 = tmax;
     const float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z}, dd[3] = {d.x, d.y, d.z};
 #pragma unroll
@@ -55,7 +55,26 @@ VX_D bool box_hit(const BvhNode &n, V3 o, V3 inv, V3 d, float tmin, float tmax) 
         t0 = fmaxf(t0, fminf(a, b));
         t1 = fminf(t1, fmaxf(a, b));
     }
+    tEnter = t0;
     return t0 <= t1;
+}
+
+// push the children of an inner node, the nearer one on top (visited first, so the closest hit
+// shrinks the interval early); a child whose box the ray misses is not pushed
+VX_D void push_children(const BvhNode *nodes, int base, int left, V3 o, V3 inv, V3 d, float tmin, float tmax,
+                        int *stack, int &sp) {
+    float ta, tb;
+    const bool ha = box_hit(nodes[base + left], o, inv, d, tmin, tmax, ta);
+    const bool hb = box_hit(nodes[base + left + 1], o, inv, d, tmin, tmax, tb);
+    if (ha && hb) {
+        const bool aFirst = ta <= tb;
+        stack[sp++] = base + (aFirst ? left + 1 : left);
+        stack[sp++] = base + (aFirst ? left : left + 1);
+    } else if (ha) {
+        stack[sp++] = base + left;
+    } else if (hb) {
+        stack[sp++] = base + left + 1;
+    }
 }
 
 struct Best {
@@ -66,7 +85,7 @@ struct Best {
     }
 };
 
-constexpr int kStack = 48;
+constexpr int kStack = 44;  // > the builder's depth limit (40) + 2
 
 VX_D void blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b) {
     const int2 r = m.root[block];
@@ -76,12 +95,10 @@ VX_D void blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, fl
     stack[sp++] = r.x;
     while (sp > 0) {
         const BvhNode n = m.blas[stack[--sp]];
-        if (!box_hit(n, o, inv, d, tmin, b.t)) continue;
+        float te;
+        if (!box_hit(n, o, inv, d, tmin, b.t, te)) continue;
         if (n.count == 0) {
-            if (sp + 2 <= kStack) {
-                stack[sp++] = r.x + n.left;
-                stack[sp++] = r.x + n.left + 1;
-            }
+            push_children(m.blas, r.x, n.left, o, inv, d, tmin, b.t, stack, sp);
             continue;
         }
         for (int k = 0; k < n.count; ++k) {
@@ -109,12 +126,10 @@ __global__ __launch_bounds__(256) void k_mesh_probe(MeshDev m, const float *rays
         stack[sp++] = 0;
         while (sp > 0) {
             const BvhNode nd = m.tlas[stack[--sp]];
-            if (!box_hit(nd, o, inv, d, tmin, b.t)) continue;
+            float te;
+            if (!box_hit(nd, o, inv, d, tmin, b.t, te)) continue;
             if (nd.count == 0) {
-                if (sp + 2 <= kStack) {
-                    stack[sp++] = nd.left;
-                    stack[sp++] = nd.left + 1;
-                }
+                push_children(m.tlas, 0, nd.left, o, inv, d, tmin, b.t, stack, sp);
                 continue;
             }
             for (int k = 0; k < nd.count; ++k) {
