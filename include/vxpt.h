@@ -197,6 +197,10 @@ int vxpt_get_lights(vxpt_ctx *ctx, uint32_t *mapping, int cap, int *n_mapped, ui
  * cull = 1 skips back faces (radiance rays), 0 not (visibility rays).  Ties: smaller t, then row,
  * then triangle.  Parity hook: the path kernels do not consult the meshes yet */
 int vxpt_mesh_probe(vxpt_ctx *ctx, const float *rays, int n, int cull, float *out, int32_t *ids);
+/* the visibility-ray form of the same query (optixTraverse with OPTIX_RAY_FLAG_DISABLE_CLOSESTHIT,
+ * no culling, closesthit.cu:616-625 / 752 / 808): occluded[i] = 1 iff some instanced-mesh
+ * triangle, either face, lies in [tmin, tmax] of ray i; the walk stops at the first one */
+int vxpt_mesh_occluded(vxpt_ctx *ctx, const float *rays, int n, uint8_t *occluded);
 
 /* ---- voxel edits (VoxelEngine::update click path, VoxelEngine.cu:855-975, 1040-1346) ---- */
 /* performRayTraversal (:1040-1166) of the current camera ray on the world.  out: hit, hit x, y, z,

@@ -61,8 +61,9 @@ VX_D bool box_hit(const BvhNode &n, V3 o, V3 inv, V3 d, float tmin, float tmax, 
 
 // push the children of an inner node, the nearer one on top (visited first, so the closest hit
 // shrinks the interval early); a child whose box the ray misses is not pushed
+template <class S>
 VX_D void push_children(const BvhNode *nodes, int base, int left, V3 o, V3 inv, V3 d, float tmin, float tmax,
-                        int *stack, int &sp) {
+                        S &stack, int &sp) {
     float ta, tb;
     const bool ha = box_hit(nodes[base + left], o, inv, d, tmin, tmax, ta);
     const bool hb = box_hit(nodes[base + left + 1], o, inv, d, tmin, tmax, tb);
@@ -77,6 +78,17 @@ VX_D void push_children(const BvhNode *nodes, int base, int left, V3 o, V3 inv, 
     }
 }
 
+// The walk keeps ONE per-thread stack for both levels: a BLAS walk runs on the entries above the
+// TLAS's pending ones and is done before the TLAS walk pops again (live entries <= tlasDepth +
+// blasDepth + 1).  It lives in scratch: a 24-entry LDS stack (entry k of lane t at
+// lds[k * 256 + t], conflict-free) was measured 4 % slower on tools/mesh_probe_bench.py (16.0 vs
+// 15.4 ms) -- 24 KiB per block cut occupancy from 8 to 6 waves/SIMD, and the walk is bound by
+// the node and triangle loads, not by the stack.
+struct ScratchStack {
+    int s[84];  // 2 x (the builder's depth limit 40 + 2)
+    VX_D int &operator[](int k) { return s[k]; }
+};
+
 struct Best {
     float t, u, v;
     int inst, tri;
@@ -85,15 +97,14 @@ struct Best {
     }
 };
 
-constexpr int kStack = 44;  // > the builder's depth limit (40) + 2
-
-VX_D void blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b) {
+template <bool kAny, class S>
+VX_D bool blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b,
+                    S &stack, const int sp0) {
     const int2 r = m.root[block];
-    if (r.x < 0) return;
-    int stack[kStack];
-    int sp = 0;
+    if (r.x < 0) return false;
+    int sp = sp0;
     stack[sp++] = r.x;
-    while (sp > 0) {
+    while (sp > sp0) {
         const BvhNode n = m.blas[stack[--sp]];
         float te;
         if (!box_hit(n, o, inv, d, tmin, b.t, te)) continue;
@@ -106,8 +117,30 @@ VX_D void blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, fl
             float t, u, v;
             if (tri_hit(o, d, m.tri + (size_t)ti * 9, tmin, b.t, cull, t, u, v)) {
                 const int id = m.triId[ti];
+                if (kAny) { b.t = t; b.u = u; b.v = v; b.inst = row; b.tri = id; return true; }
                 if (b.better(t, row, id)) { b.t = t; b.u = u; b.v = v; b.inst = row; b.tri = id; }
             }
+        }
+    }
+    return false;
+}
+
+template <bool kAny, class S>
+VX_D void mesh_walk(const MeshDev &m, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b, S &stack) {
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const BvhNode nd = m.tlas[stack[--sp]];
+        float te;
+        if (!box_hit(nd, o, inv, d, tmin, b.t, te)) continue;
+        if (nd.count == 0) {
+            push_children(m.tlas, 0, nd.left, o, inv, d, tmin, b.t, stack, sp);
+            continue;
+        }
+        for (int k = 0; k < nd.count; ++k) {
+            const MeshInst mi = m.inst[nd.left + k];
+            const V3 oo(o.x - mi.cell[0], o.y - mi.cell[1], o.z - mi.cell[2]);
+            if (blas_walk<kAny>(m, mi.row, mi.block, oo, d, inv, tmin, cull, b, stack, sp)) return;
         }
     }
 }
@@ -121,23 +154,8 @@ __global__ __launch_bounds__(256) void k_mesh_probe(MeshDev m, const float *rays
     const V3 inv(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     Best b{r[7], 0.0f, 0.0f, -1, -1};
     if (m.nInst > 0) {
-        int stack[kStack];
-        int sp = 0;
-        stack[sp++] = 0;
-        while (sp > 0) {
-            const BvhNode nd = m.tlas[stack[--sp]];
-            float te;
-            if (!box_hit(nd, o, inv, d, tmin, b.t, te)) continue;
-            if (nd.count == 0) {
-                push_children(m.tlas, 0, nd.left, o, inv, d, tmin, b.t, stack, sp);
-                continue;
-            }
-            for (int k = 0; k < nd.count; ++k) {
-                const MeshInst mi = m.inst[nd.left + k];
-                const V3 oo(o.x - mi.cell[0], o.y - mi.cell[1], o.z - mi.cell[2]);
-                blas_walk(m, mi.row, mi.block, oo, d, inv, tmin, cull, b);
-            }
-        }
+        ScratchStack st;
+        mesh_walk<false>(m, o, d, inv, tmin, cull, b, st);
     }
     out[(size_t)i * 4] = b.t;
     out[(size_t)i * 4 + 1] = b.u;
@@ -147,7 +165,29 @@ __global__ __launch_bounds__(256) void k_mesh_probe(MeshDev m, const float *rays
     ids[(size_t)i * 2 + 1] = b.tri;
 }
 
+// visibility: occluded[i] = 1 iff some instanced-mesh triangle (both faces) lies in [tmin, tmax]
+__global__ __launch_bounds__(256) void k_mesh_occluded(MeshDev m, const float *rays, int n, unsigned char *occluded) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float *r = rays + (size_t)i * 8;
+    const V3 o(r[0], r[1], r[2]), d(r[4], r[5], r[6]);
+    const float tmin = r[3];
+    const V3 inv(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    Best b{r[7], 0.0f, 0.0f, -1, -1};
+    if (m.nInst > 0) {
+        ScratchStack st;
+        mesh_walk<true>(m, o, d, inv, tmin, 0, b, st);
+    }
+    occluded[i] = b.inst >= 0 ? 1 : 0;
+}
+
 }  // namespace
+
+hipError_t launch_mesh_occluded(const MeshDev &m, const float *rays, int n, unsigned char *occluded, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mesh_occluded, dim3((n + 255) / 256), dim3(256), 0, st, m, rays, n, occluded);
+    return hipGetLastError();
+}
 
 hipError_t launch_mesh_probe(const MeshDev &m, const float *rays, int n, int cull, float *out, int *ids,
                              hipStream_t st) {

@@ -285,6 +285,8 @@ struct MeshDev {
 // out: t, u, v, hit flag per ray; ids: instance, triangle.  cull = skip back faces (radiance rays)
 hipError_t launch_mesh_probe(const MeshDev &m, const float *rays, int n, int cull, float *out, int *ids,
                              hipStream_t st);
+// any hit, both faces (visibility rays): occluded 1/0 per ray
+hipError_t launch_mesh_occluded(const MeshDev &m, const float *rays, int n, unsigned char *occluded, hipStream_t st);
 hipError_t launch_tri_lights(const float *tri, int nTri, const int *inst, int nInst, V3 radiance, LightInfo *out,
                              float *weight, hipStream_t st);
 

@@ -1563,12 +1563,15 @@ int build_lights(vxpt_ctx *c) {
 // Median-split BVH over boxes (lo xyz, hi xyz per primitive): nodes[0] = root, children of an
 // inner node adjacent, leaves of at most leafMax primitives (order = primitive order in the
 // leaves).  Node boxes are widened by 1e-4 (1 + |coordinate|), far above the slab test's
-// rounding, so box culling is conservative.  Fails past a depth of 40 (the walk's stack is 48).
-bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> &nodes, std::vector<int> &order) {
+// rounding, so box culling is conservative.  Fails past a depth of 40 (the walk's one stack holds
+// 84 entries, TLAS and BLAS together); *maxDepth = the deepest leaf.
+bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> &nodes, std::vector<int> &order,
+               int *maxDepth) {
     const int n = (int)(box.size() / 6);
     order.resize(n);
     for (int i = 0; i < n; ++i) order[i] = i;
     nodes.assign(1, BvhNode{});
+    *maxDepth = 0;
     if (n == 0) return true;
     struct Job { int node, b, e, depth; };
     std::vector<Job> jobs{{0, 0, n, 0}};
@@ -1576,6 +1579,7 @@ bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> 
         const Job j = jobs.back();
         jobs.pop_back();
         if (j.depth > 40) return false;
+        *maxDepth = std::max(*maxDepth, j.depth);
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
         float clo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, chi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
         for (int i = j.b; i < j.e; ++i) {
@@ -1636,7 +1640,8 @@ int build_blas(vxpt_ctx *c) {
             }
         std::vector<BvhNode> nodes;
         std::vector<int> order;
-        if (!build_bvh(box, 4, nodes, order)) return fail(c, VXPT_ERR_STATE, "mesh BVH too deep");
+        int depth = 0;
+        if (!build_bvh(box, 4, nodes, order, &depth)) return fail(c, VXPT_ERR_STATE, "mesh BVH too deep");
         c->hRoot[b] = make_int2((int)c->hBlas.size(), (int)c->hBlasTriId.size());
         c->hBlas.insert(c->hBlas.end(), nodes.begin(), nodes.end());
         for (int t : order) {
@@ -1668,7 +1673,8 @@ int build_tlas(vxpt_ctx *c) {
     }
     std::vector<BvhNode> nodes;
     std::vector<int> order;
-    if (!build_bvh(box, 2, nodes, order)) return fail(c, VXPT_ERR_STATE, "instance BVH too deep");
+    int depth = 0;
+    if (!build_bvh(box, 2, nodes, order, &depth)) return fail(c, VXPT_ERR_STATE, "instance BVH too deep");
     std::vector<MeshInst> sorted;
     for (int i : order) sorted.push_back(mi[i]);
     c->nMeshInst = (int)sorted.size();
@@ -1682,6 +1688,10 @@ int refresh_instances(vxpt_ctx *c) {
     collect_instances(c);
     if (int r = build_tlas(c)) return r;
     return build_lights(c);
+}
+
+static MeshDev mesh_dev(const vxpt_ctx *c) {
+    return MeshDev{c->tlas.p, c->meshInst.p, c->blas.p, c->blasTri.p, c->blasTriId.p, c->blasRoot.p, c->nMeshInst};
 }
 
 // closest instanced-mesh hit of n rays (8 floats each: o, tmin, d, tmax): out 4 floats (t, u, v,
@@ -1700,7 +1710,7 @@ int vxpt_mesh_probe(vxpt_ctx *c, const float *rays, int n, int cull, float *out,
     HIPCHK(c, hipMalloc((void **)&dout, (size_t)n * 16));
     HIPCHK(c, hipMalloc((void **)&dids, (size_t)n * 8));
     HIPCHK(c, hipMemcpyAsync(dr, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    const MeshDev m{c->tlas.p, c->meshInst.p, c->blas.p, c->blasTri.p, c->blasTriId.p, c->blasRoot.p, c->nMeshInst};
+    const MeshDev m = mesh_dev(c);
     HIPCHK(c, launch_mesh_probe(m, dr, n, cull, dout, dids, c->stream));
     HIPCHK(c, hipMemcpyAsync(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(ids, dids, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1708,6 +1718,28 @@ int vxpt_mesh_probe(vxpt_ctx *c, const float *rays, int n, int cull, float *out,
     hipFree(dr);
     hipFree(dout);
     hipFree(dids);
+    return VXPT_OK;
+}
+
+// visibility rays against the instanced meshes: occluded[i] = 1 iff any triangle, either face,
+// lies in [tmin, tmax] of ray i (8 floats: o, tmin, d, tmax)
+int vxpt_mesh_occluded(vxpt_ctx *c, const float *rays, int n, uint8_t *occluded) {
+    if (!c || !rays || !occluded || n < 0) return VXPT_ERR_ARG;
+    if (n == 0) return VXPT_OK;
+    HIPCHK(c, hipSetDevice(c->dev));
+    if (c->hRoot.empty()) c->hRoot.assign(kBlockTypes, make_int2(-1, -1));
+    if (!c->blasRoot.p)
+        if (int r = upload_vec(c, c->blasRoot, c->hRoot.data(), c->hRoot.size())) return r;
+    float *dr = nullptr;
+    unsigned char *dout = nullptr;
+    HIPCHK(c, hipMalloc((void **)&dr, (size_t)n * 32));
+    HIPCHK(c, hipMalloc((void **)&dout, (size_t)n));
+    HIPCHK(c, hipMemcpyAsync(dr, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_mesh_occluded(mesh_dev(c), dr, n, dout, c->stream));
+    HIPCHK(c, hipMemcpyAsync(occluded, dout, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(dr);
+    hipFree(dout);
     return VXPT_OK;
 }
 

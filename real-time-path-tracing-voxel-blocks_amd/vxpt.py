@@ -130,6 +130,7 @@ def load_library(path=LIB_PATH):
         "vxpt_get_instances": (I, [P, P, I, P]),
         "vxpt_get_lights": (I, [P, P, I, P, P, P]),
         "vxpt_mesh_probe": (I, [P, P, I, I, P, P]),
+        "vxpt_mesh_occluded": (I, [P, P, I, P]),
         "vxpt_set_block": (I, [P, I, I, I, I]),
         "vxpt_click_block": (I, [P, I, P]),
         "vxpt_save_world": (I, [P, ctypes.c_char_p, ctypes.c_char_p]),
@@ -318,6 +319,14 @@ class Renderer:
         self._chk(self.lib.vxpt_mesh_probe(self.ctx, _ptr(r), len(r), int(bool(cull)), _ptr(out), _ptr(ids)),
                   "vxpt_mesh_probe")
         return out, ids
+
+    def mesh_occluded(self, rays):
+        """Visibility rays [N, 8] (o, tmin, d, tmax) against the instanced meshes, both faces:
+        uint8 [N], 1 = some triangle lies in [tmin, tmax] (closesthit.cu:616-625)."""
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        occ = np.zeros(len(r), np.uint8)
+        self._chk(self.lib.vxpt_mesh_occluded(self.ctx, _ptr(r), len(r), _ptr(occ)), "vxpt_mesh_occluded")
+        return occ
 
     def lights(self):
         """(mapping uint32 [M, 3], LightInfo records uint8 [L, 32], alias bins [L], local luminance)."""

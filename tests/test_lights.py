@@ -194,7 +194,9 @@ def test_light_table_matches_oracle(model_root):
 @pytest.mark.parametrize("cull", [0, 1])
 def test_mesh_probe_matches_brute_force(model_root, cull):
     """The two-level BVH walk (meshes.hip) equals the oracle's brute-force loop over every
-    instance and triangle bit for bit: t, barycentrics, instance row and triangle."""
+    instance and triangle bit for bit: t, barycentrics, instance row and triangle.  The any-hit
+    walk of visibility rays (vxpt_mesh_occluded) reports exactly the rays the brute-force loop
+    finds any triangle for, both faces (closesthit.cu:616-625 traces them without culling)."""
     r = vxpt.Renderer(64, 64)
     r.load_settings()
     r.generate_terrain(CH, height_scale=32.0)
@@ -224,4 +226,8 @@ def test_mesh_probe_matches_brute_force(model_root, cull):
     assert 0.2 < want[:, 3].mean() < 0.95
     np.testing.assert_array_equal(gid, wid)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    if not cull:
+        occ = r.mesh_occluded(rays)
+        assert occ.dtype == np.uint8 and 0 < occ.sum() < len(occ)
+        np.testing.assert_array_equal(occ, want[:, 3].astype(np.uint8))
     r.close()

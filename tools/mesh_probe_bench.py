@@ -52,3 +52,10 @@ for cull in (0, 1, 1):
     dt = time.time() - t0
 print("instances %d (%d triangles each), rays %d: hit fraction %.3f, call %.1f ms incl. copies"
       % (len(r.instances()), 600, n_rays, out[:, 3].mean(), dt * 1e3))
+for _ in range(2):  # visibility form (k_mesh_occluded): any hit, both faces
+    t0 = time.time()
+    occ = r.mesh_occluded(rays)
+    dt = time.time() - t0
+closest, _ = r.mesh_probe(rays, 0)
+assert (occ == closest[:, 3].astype(np.uint8)).all(), "any-hit and closest-hit disagree"
+print("occluded: fraction %.3f, call %.1f ms incl. copies" % (occ.mean(), dt * 1e3))
