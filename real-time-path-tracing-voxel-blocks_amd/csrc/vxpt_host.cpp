@@ -1560,7 +1560,7 @@ int build_lights(vxpt_ctx *c) {
 
 }  // namespace
 
-// Median-split BVH over boxes (lo xyz, hi xyz per primitive): nodes[0] = root, children of an
+// Binned-SAH BVH over boxes (lo xyz, hi xyz per primitive): nodes[0] = root, children of an
 // inner node adjacent, leaves of at most leafMax primitives (order = primitive order in the
 // leaves).  Node boxes are widened by 1e-4 (1 + |coordinate|), far above the slab test's
 // rounding, so box culling is conservative.  Fails past a depth of 40 (the walk's one stack holds
@@ -1602,15 +1602,73 @@ bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> 
             nd.count = j.e - j.b;
             continue;
         }
+        // binned SAH split (16 centroid bins per axis, cost = area x count on either side); the
+        // median of the widest axis when no bin boundary separates the primitives, and from depth
+        // 24 on, so the depth limit holds for any primitive count the median builder accepted
         int axis = 0;
         for (int k = 1; k < 3; ++k)
             if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
-        const int mid = (j.b + j.e) / 2;
-        std::nth_element(order.begin() + j.b, order.begin() + mid, order.begin() + j.e, [&](int x, int y) {
-            const float cx = box[(size_t)x * 6 + axis] + box[(size_t)x * 6 + axis + 3];
-            const float cy = box[(size_t)y * 6 + axis] + box[(size_t)y * 6 + axis + 3];
-            return cx < cy || (cx == cy && x < y);
-        });
+        int mid = -1;
+        if (j.depth < 24) {
+            constexpr int kBins = 16;
+            float bestCost = FLT_MAX;
+            int bestAxis = -1, bestBin = 0;
+            for (int k = 0; k < 3; ++k) {
+                const float ext = chi[k] - clo[k];
+                if (!(ext > 0.0f)) continue;
+                float blo[kBins][3], bhi[kBins][3];
+                int cnt[kBins] = {};
+                for (int q = 0; q < kBins; ++q)
+                    for (int a = 0; a < 3; ++a) { blo[q][a] = FLT_MAX; bhi[q][a] = -FLT_MAX; }
+                for (int i = j.b; i < j.e; ++i) {
+                    const float *bx = &box[(size_t)order[i] * 6];
+                    const int q = std::min(kBins - 1, (int)((0.5f * (bx[k] + bx[k + 3]) - clo[k]) / ext * kBins));
+                    cnt[q]++;
+                    for (int a = 0; a < 3; ++a) {
+                        blo[q][a] = std::min(blo[q][a], bx[a]);
+                        bhi[q][a] = std::max(bhi[q][a], bx[a + 3]);
+                    }
+                }
+                auto area = [](const float *lo3, const float *hi3) {
+                    const float dx = hi3[0] - lo3[0], dy = hi3[1] - lo3[1], dz = hi3[2] - lo3[2];
+                    return dx * dy + dy * dz + dz * dx;
+                };
+                float rArea[kBins];
+                int rCnt[kBins];
+                float rl[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, rh[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                for (int q = kBins - 1, c = 0; q > 0; --q) {
+                    c += cnt[q];
+                    for (int a = 0; a < 3; ++a) { rl[a] = std::min(rl[a], blo[q][a]); rh[a] = std::max(rh[a], bhi[q][a]); }
+                    rCnt[q] = c;
+                    rArea[q] = c ? area(rl, rh) : 0.0f;
+                }
+                float ll[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lh[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                for (int q = 0, c = 0; q < kBins - 1; ++q) {  // split between bins q and q + 1
+                    c += cnt[q];
+                    for (int a = 0; a < 3; ++a) { ll[a] = std::min(ll[a], blo[q][a]); lh[a] = std::max(lh[a], bhi[q][a]); }
+                    if (c == 0 || rCnt[q + 1] == 0) continue;
+                    const float cost = area(ll, lh) * c + rArea[q + 1] * rCnt[q + 1];
+                    if (cost < bestCost) { bestCost = cost; bestAxis = k; bestBin = q; }
+                }
+            }
+            if (bestAxis >= 0) {
+                const float ext = chi[bestAxis] - clo[bestAxis], c0 = clo[bestAxis];
+                auto it = std::stable_partition(order.begin() + j.b, order.begin() + j.e, [&](int x) {
+                    const float *bx = &box[(size_t)x * 6];
+                    const int q = std::min(kBins - 1, (int)((0.5f * (bx[bestAxis] + bx[bestAxis + 3]) - c0) / ext * kBins));
+                    return q <= bestBin;
+                });
+                mid = (int)(it - order.begin());
+            }
+        }
+        if (mid <= j.b || mid >= j.e) {
+            mid = (j.b + j.e) / 2;
+            std::nth_element(order.begin() + j.b, order.begin() + mid, order.begin() + j.e, [&](int x, int y) {
+                const float cx = box[(size_t)x * 6 + axis] + box[(size_t)x * 6 + axis + 3];
+                const float cy = box[(size_t)y * 6 + axis] + box[(size_t)y * 6 + axis + 3];
+                return cx < cy || (cx == cy && x < y);
+            });
+        }
         const int left = (int)nodes.size();
         nodes[j.node].left = left;
         nodes[j.node].count = 0;
