@@ -309,11 +309,18 @@ int vxpt_timings(vxpt_ctx *ctx, vxpt_timing *out);
 int vxpt_sync(vxpt_ctx *ctx);
 /* raw stream handle (hipStream_t) for hosts that enqueue their own work */
 void *vxpt_stream(vxpt_ctx *ctx);
-/* DDA probe: n rays (o3 d3 tmin tmax) -> n x (hit x y z face id) + t; mode 0 closest, 2 occluded */
+/* DDA probe: n rays (o3 d3 tmin tmax) -> n x (hit x y z face id) + t; mode 0 closest, 2 occluded;
+ * mode | 4: the same walks handed over through the straggler save/resume state after every iteration */
 int vxpt_probe_rays(vxpt_ctx *ctx, int n, const float *rays, int32_t *out6, float *t, int mode);
 /* blue-noise sampler probe: n queries (pixel x, pixel y, iterationIndex, dimension) ->
  * BlueNoiseRandGenerator::rand (RandGen.h:21-45) as the trace kernel evaluates it */
 int vxpt_probe_rng(vxpt_ctx *ctx, int n, const int32_t *q4, float *out);
+/* ray-queue counters of the last trace pass (no reference counterpart: the wavefront's
+ * own instrumentation, read after the pass): for each of the 16 queues q (4*segment + kind,
+ * kind 1 BRDF-candidate closest-hit rays, 2 NEE visibility rays, 3 ReSTIR visibility rays)
+ * out[3q] = rays queued, out[3q+1] = walks deferred to the straggler queue (level 1),
+ * out[3q+2] = walks deferred again (level 2).  cap >= 48 */
+int vxpt_trace_counters(vxpt_ctx *ctx, uint32_t *out, int cap);
 
 #ifdef __cplusplus
 }

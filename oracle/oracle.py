@@ -116,6 +116,13 @@ class Oracle:
             self.L.orc_set_material(self.h, b, 1.0, 1.0, 1.0, r, 0, 0.0, b - 1)
         self.chunks = None
 
+    def set_materials(self, mats):
+        """Same list as vxpt.Renderer.upload_materials (block ids 1..len)."""
+        for b, m in enumerate(mats, start=1):
+            al = m.get("albedo", (1.0, 1.0, 1.0))
+            self.L.orc_set_material(self.h, b, al[0], al[1], al[2], m.get("roughness", 0.8),
+                                    int(m.get("metallic", 0)), m.get("translucency", 0.0), m.get("material_id", b - 1))
+
     def __del__(self):
         if getattr(self, "h", None):
             self.L.orc_destroy(self.h)

@@ -15,6 +15,15 @@
 // because the variance / second-moment channel depends on it.
 #include "vx_internal.hpp"
 
+#ifdef VX_EXACT_DENOISE
+// experiment build (libvxpt_exact.so): the reference's compensated dots and IEEE sqrt/exp in
+// every weight, to separate the deliberate numeric deviations from other differences
+#define dot_fast dot
+#define luminance_fast luminance
+#define __expf expf
+#define __builtin_amdgcn_sqrtf sqrtf
+#endif
+
 namespace vx {
 namespace {
 

@@ -874,6 +874,30 @@ __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *r
     const float *r = rays + 8 * i;
     const V3 o(r[0], r[1], r[2]), d(r[3], r[4], r[5]);
     int *q = out + 6 * i;
+    if (mode & 4) {
+        // the straggler path: every iteration goes through dda_save / dda_resume (the state
+        // k_queue and k_resume hand over between launches), one iteration per "launch"
+        Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+        Dda st;
+        const bool occ = (mode & 2) != 0;
+        const float tmin = occ ? r[6] : 0.0f;
+        int rc = occ ? dda_begin<true>(w, o, d, tmin, r[7], st, h) : dda_begin<false>(w, o, d, 0.0f, r[7], st, h);
+        while (rc == DdaRun) {
+            const DdaSaved sv = dda_save(st, i);
+            dda_resume(w, o, d, tmin, r[7], sv, st);
+            rc = occ ? dda_iter<true>(w, st, h) : dda_iter<false>(w, st, h);
+        }
+        if (occ) {
+            q[0] = rc == DdaEvent ? 1 : 0;
+            q[1] = q[2] = q[3] = q[4] = q[5] = 0;
+            t[i] = 0.0f;
+            return;
+        }
+        if (rc != DdaEvent) h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
+        q[0] = h.hit; q[1] = h.x; q[2] = h.y; q[3] = h.z; q[4] = h.face; q[5] = h.id;
+        t[i] = h.t;
+        return;
+    }
     if (mode == 2) {
         q[0] = dda_occluded(w, o, d, r[6], r[7]) ? 1 : 0;
         q[1] = q[2] = q[3] = q[4] = q[5] = 0;

@@ -441,6 +441,42 @@ VX_D bool lobes(V3 albedo, float metalness, float cosForF, Lobes &L) {
     return true;
 }
 
+// EvaluateFresnelDielectric (Bsdf.h:40-65)
+VX_D float fresnel_dielectric(float et, float cosIn) {
+    const float cosi = fabsf(cosIn);
+    float sint = 1.0f - cosi * cosi;
+    sint = (0.0f < sint) ? sqrtf(sint) / et : 0.0f;
+    if (1.0f < sint) return 1.0f;
+    float cost = 1.0f - sint * sint;
+    cost = (0.0f < cost) ? sqrtf(cost) : 0.0f;
+    const float ec = et * cosi, ect = et * cost;
+    const float rPerp = (cosi - ect) / (cosi + ect);
+    const float rPar = (ec - cost) / (ec + cost);
+    const float r = (rPar * rPar + rPerp * rPerp) * 0.5f;
+    return r <= 1.0f ? r : 1.0f;
+}
+// refract (LinearMath.h:1483-1513): false on total internal reflection
+VX_D bool refract3(V3 &r, V3 i, V3 n, float ior) {
+    float neg = dot(i, n), eta;
+    if (neg > 0.0f) { eta = ior; n = -n; neg = -neg; } else eta = 1.0f / ior;
+    const float k = 1.0f - eta * eta * (1.0f - neg * neg);
+    if (k < 0.0f) { r = V3(0.0f); return false; }
+    r = normalize(eta * i - (eta * neg + sqrtf(k)) * n);
+    return true;
+}
+// SpecularReflectionTransmissionSample (Bsdf.h:218-245), ior 1.4; the
+// transmission flag only matters for thin films (closesthit.cu:293)
+VX_D void spec_refl_trans_sample(float u, V3 n, V3 ng, V3 wo, V3 albedo, V3 &wi, V3 &bop, float &pdf) {
+    const float ior = 1.4f;
+    const float eta = dot(wo, ng) > 0.0f ? ior / 1.0f : 1.0f / ior;
+    const V3 wr = reflect3(-wo, n);
+    V3 wt;
+    float R = 1.0f;
+    if (refract3(wt, -wo, n, eta)) R = fresnel_dielectric(eta, dot(wo, n));
+    if (u <= R) { wi = wr; pdf = R; } else { wi = wt; pdf = 1.0f - R; }
+    bop = albedo / pdf;
+}
+
 // DisneyBSDFSample for rough surfaces (Bsdf.h:401-534); specular branch of
 // the reference only for roughness < 1e-5 (:403-425).
 VX_D void disney_sample(float u0, float u1, float u2, float u3, V3 n, V3 ng, V3 wo, V3 albedo, bool metallic,
@@ -452,8 +488,12 @@ VX_D void disney_sample(float u0, float u1, float u2, float u3, V3 n, V3 ng, V3 
             else { bop = albedo; pdf = 1.0f; }
             pdf = fmaxf(pdf, kMinPdf);
             bop = clamp_throughput(bop);
+        } else if (translucency > 1.0f - kTranslThresh) {
+            spec_refl_trans_sample(u0, n, ng, wo, albedo, wi, bop, pdf);
+            pdf = fmaxf(pdf, kMinPdf);
+            bop = clamp_throughput(bop);
         } else {
-            bop = V3(0.0f);  // refractive specular: not in the cube material table
+            bop = V3(0.0f);
             pdf = 0.0f;
         }
         return;

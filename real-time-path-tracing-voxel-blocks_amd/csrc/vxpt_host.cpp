@@ -2483,6 +2483,24 @@ extern "C" int vxpt_probe_rays(vxpt_ctx *c, int n, const float *rays, int32_t *o
     return VXPT_OK;
 }
 
+extern "C" int vxpt_trace_counters(vxpt_ctx *c, uint32_t *out, int cap) {
+    if (!c || !out || cap < 48) return VXPT_ERR_ARG;
+    if (!c->wb.qCount) return fail(c, VXPT_ERR_STATE, "no trace buffers");
+    HIPCHK(c, hipSetDevice(c->dev));
+    std::vector<uint32_t> q(64 + 3 * 16 * 8 * 16);
+    HIPCHK(c, hipMemcpyAsync(q.data(), c->wb.qCount, q.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 16; ++k) {
+        out[3 * k] = q[k];
+        for (int level = 1; level <= 2; ++level) {
+            uint32_t n = 0;
+            for (int sh = 0; sh < 8; ++sh) n += q[64 + (((level - 1) * 16 + k) * 8 + sh) * 16];
+            out[3 * k + level] = n;
+        }
+    }
+    return VXPT_OK;
+}
+
 extern "C" int vxpt_probe_rng(vxpt_ctx *c, int n, const int32_t *q4, float *out) {
     if (!c || n <= 0 || !q4 || !out) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));

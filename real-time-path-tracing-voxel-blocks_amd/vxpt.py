@@ -148,6 +148,7 @@ def load_library(path=LIB_PATH):
         "vxpt_stream": (P, [P]),
         "vxpt_probe_rays": (I, [P, I, P, P, P, I]),
         "vxpt_probe_rng": (I, [P, I, P, P]),
+        "vxpt_trace_counters": (I, [P, P, I]),
         "vxpt_set_band": (I, [P, I, I]),
         "vxpt_row_bytes": (I, [P, I]),
         "vxpt_copy_rows": (I, [P, I, I, I, P, I]),
@@ -507,6 +508,23 @@ class Renderer:
         t = np.zeros(n, np.float32)
         self._chk(self.lib.vxpt_probe_rays(self.ctx, n, _ptr(rays), _ptr(out), _ptr(t), mode), "vxpt_probe_rays")
         return out, t
+
+    def trace_counters(self):
+        """Queue counters of the last trace pass: (16, 3) array of (rays queued,
+        level-1 stragglers, level-2 stragglers) per queue 4*segment + kind."""
+        out = np.zeros(48, np.uint32)
+        self._chk(self.lib.vxpt_trace_counters(self.ctx, _ptr(out), 48), "vxpt_trace_counters")
+        return out.reshape(16, 3)
+
+    def upload_materials(self, mats):
+        """mats: list of 12 dicts (block ids 1..12) with albedo, roughness, translucency,
+        metallic, material_id, thinfilm (MaterialManager GPU table)."""
+        arr = (Material * len(mats))()
+        for i, m in enumerate(mats):
+            arr[i] = Material((ctypes.c_float * 3)(*m.get("albedo", (1.0, 1.0, 1.0))), m.get("roughness", 0.8),
+                              m.get("translucency", 0.0), int(m.get("metallic", 0)), m.get("material_id", i),
+                              int(m.get("thinfilm", 0)))
+        self._chk(self.lib.vxpt_upload_materials(self.ctx, arr, len(mats)), "vxpt_upload_materials")
 
     def probe_rng(self, queries):
         """queries: (n, 4) int32 of (px, py, iterationIndex, dim) -> n floats."""

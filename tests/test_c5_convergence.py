@@ -1,12 +1,13 @@
 """C5 (the canonical-render gate): 64 frames x 1 spp of the C1 scene at
 256x256 (the reference's CPU config), the HIP path against the oracle.  The canonical PNG
 the reference's --test-canonical compares with is not shipped, so the gate is the
-oracle's 64-frame render: relative RMS of the denoised output over non-sky pixels < 1e-3
-(north_star's per-pixel L2 bar, untextured), radiance < 1e-5."""
+oracle's 64-frame render: north_star's per-pixel L2 bar (1e-3) on the denoised output and the
+last frame's radiance, over every pixel (check_radiance), plus the relative RMS over non-sky
+pixels (output < 1e-3, radiance < 1e-5)."""
 import numpy as np
 import pytest
 
-from test_gpu_parity import _setup, _inject_sky, _dn_params
+from test_gpu_parity import _setup, _inject_sky, _dn_params, check_radiance
 
 
 @pytest.mark.gpu
@@ -28,4 +29,8 @@ def test_c5_64_frames_match_oracle():
         rms = np.sqrt(((g - c) ** 2).mean()) / np.sqrt((c ** 2).mean())
         print("%s relative RMS %.3e" % (name, rms))
         assert rms < bar, (name, rms)
+        # 64 frames of history accumulation: a few pixels take another branch of a denoiser
+        # threshold test after ulp-level differences (measured: 99.93 % within 1e-3)
+        check_radiance(r.read(name), o.read(which), "C5 %s after %d frames" % (name, frames), frac_tight=0.98,
+                       frac_l2=0.999)
     r.close()

@@ -8,8 +8,8 @@ Bars (DESIGN.md "Parity"):
   ray t, G-buffer normals/albedo/depth): bit-exact or <= 1 ulp;
 - radiance: transcendentals come from different libms (ocml vs glibc), so a
   path may take another branch after a 1-ulp difference in a threshold test.
-  Per-pixel relative tolerance RTOL_RAD on >= PIX_FRAC of pixels and an
-  image-mean tolerance MEAN_TOL;
+  Per-pixel relative L2 error (check_radiance) on nearly every pixel and an
+  image-mean tolerance;
 - denoiser on identical injected inputs: RTOL_DN elementwise.
 """
 import numpy as np
@@ -23,9 +23,6 @@ from test_oracle import _random_rays
 pytestmark = pytest.mark.gpu
 
 W, H = 128, 96
-RTOL_RAD = 2e-3
-PIX_FRAC = 0.97
-MEAN_TOL = 2e-3
 RTOL_DN = 1e-4
 DN_FLOATS = [30, 6, 2, 0.5, 0.15, 0.003, 0.01, 0.05, 500000]
 DN_INTS = [1, 1, 1, 1, 1, 1]
@@ -138,18 +135,34 @@ def test_primary_gbuffer(pair):
     np.testing.assert_allclose(g, c, rtol=1e-5, atol=1e-6)
 
 
-def _compare_radiance(g, c, what):
-    lum = lambda x: x[..., 0] * 0.2126 + x[..., 1] * 0.7152 + x[..., 2] * 0.0722
-    lg, lc = lum(g), lum(c)
-    rel = _rel(lg, lc)
-    frac = (rel < RTOL_RAD).mean()
-    mean_rel = abs(lg.mean() - lc.mean()) / max(lc.mean(), 1e-6)
-    msg = "%s: frac within %.0e = %.4f, image-mean rel diff = %.2e, max rel = %.3f" % (
-        what, RTOL_RAD, frac, mean_rel, rel.max())
-    print(msg)
+# Radiance bars (per pixel, RGB): relative L2 error e = |g - c|_2 / max(|c|_2, 1e-3).
+# North_star's per-pixel L2 tolerance is 1e-3; ocml vs glibc transcendentals can flip a
+# threshold test on a handful of pixels, so: >= 99.9 % of pixels with e < 1e-4, >= 99.95 %
+# with e < 1e-3, image mean within 1e-5 (measured: 100 %, max e ~1e-4, mean ~1e-7).
+E_TIGHT, FRAC_TIGHT = 1e-4, 0.999
+E_L2, FRAC_L2 = 1e-3, 0.9995
+MEAN_TOL_L2 = 1e-5
+
+
+def pixel_l2(g, c):
+    g, c = g[..., :3].astype(np.float64), c[..., :3].astype(np.float64)
+    return np.linalg.norm(g - c, axis=-1) / np.maximum(np.linalg.norm(c, axis=-1), 1e-3)
+
+
+def check_radiance(g, c, what, frac_tight=FRAC_TIGHT, frac_l2=FRAC_L2):
     assert np.isfinite(g).all(), what
-    assert frac >= PIX_FRAC, msg
-    assert mean_rel < MEAN_TOL, msg
+    e = pixel_l2(g, c)
+    ft, fl = (e < E_TIGHT).mean(), (e < E_L2).mean()
+    mean_rel = abs(g[..., :3].mean() - c[..., :3].mean()) / max(abs(c[..., :3].mean()), 1e-6)
+    msg = "%s: e<1e-4 %.5f, e<1e-3 %.5f, max e %.3g, mean rel %.2e" % (what, ft, fl, e.max(), mean_rel)
+    print(msg)
+    assert ft >= frac_tight and fl >= frac_l2, msg
+    assert mean_rel < MEAN_TOL_L2, msg
+    return e
+
+
+def _compare_radiance(g, c, what):
+    check_radiance(g, c, what)
 
 
 def test_full_trace_frame0(pair):
