@@ -62,7 +62,9 @@ enum vxpt_buffer {
 };
 
 typedef struct vxpt_config {
-    int32_t width, height;   /* frame size; must be multiples of 8 (Atrous.h has no bounds guard) */
+    int32_t width, height;   /* frame size, any positive size.  The reference's Atrous has no bounds guard:
+                                 its threads past a frame edge store to the clamped edge pixels (a race
+                                 when the size is not a multiple of 16); here those threads are masked */
     int32_t device;          /* HIP device ordinal                                                */
     int32_t row_begin, row_end; /* band of rows this context traces (multi-GPU); 0,0 = all      */
     int32_t total_bounce_limit;   /* RayGen.cu:146 (3)  */

@@ -1015,7 +1015,7 @@ const char *vxpt_last_error(const vxpt_ctx *c) { return c ? c->err.c_str() : "nu
 int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (!cfg || !out) return VXPT_ERR_ARG;
     *out = nullptr;
-    if (cfg->width <= 0 || cfg->height <= 0 || cfg->width % 8 || cfg->height % 8) return VXPT_ERR_ARG;
+    if (cfg->width <= 0 || cfg->height <= 0) return VXPT_ERR_ARG;  // any size: partial 8x8 trace tiles and 16x16 denoise tiles are masked
     // the trace pass keeps 4 ray-queue counters per path segment, 64 in all
     if (cfg->total_bounce_limit > 16 || cfg->diffuse_bounce_limit > 16) return VXPT_ERR_ARG;
     int ndev = 0;

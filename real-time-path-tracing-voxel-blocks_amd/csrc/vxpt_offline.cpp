@@ -80,46 +80,50 @@ void usage(const char *argv0) {
 int parse(int argc, char **argv, Options &o) {
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
+        // mainOffline.cpp:57-133 reads a flag's value only when one follows (`&& i + 1 < argc`)
+        // and skips anything it does not know: a trailing valueless flag and unknown
+        // arguments are ignored here too (with a note on stderr), so reference scripts run as-is
         auto next = [&](const char *what) -> const char * {
             if (i + 1 >= argc) {
-                std::cerr << "missing value for " << what << "\n";
+                std::cerr << "note: " << what << " without a value ignored\n";
                 return nullptr;
             }
             return argv[++i];
         };
         const char *v = nullptr;
-        if (a == "--width") { if (!(v = next("--width"))) return -1; o.width = std::atoi(v); }
-        else if (a == "--height") { if (!(v = next("--height"))) return -1; o.height = std::atoi(v); }
-        else if (a == "--output") { if (!(v = next("--output"))) return -1; o.outputPrefix = v; }
-        else if (a == "--scene") { if (!(v = next("--scene"))) return -1; o.sceneFile = v; }
+        if (a == "--width") { if ((v = next("--width"))) { o.width = std::atoi(v); } }
+        else if (a == "--height") { if ((v = next("--height"))) { o.height = std::atoi(v); } }
+        else if (a == "--output") { if ((v = next("--output"))) { o.outputPrefix = v; } }
+        else if (a == "--scene") { if ((v = next("--scene"))) { o.sceneFile = v; } }
         else if (a == "--test-canonical" || a == "--test") o.testCanonical = true;
         else if (a == "--update-canonical") o.updateCanonical = true;
-        else if (a == "--canonical-image") { if (!(v = next("--canonical-image"))) return -1; o.canonicalImagePath = v; }
-        else if (a == "--comment") { if (!(v = next("--comment"))) return -1; o.runComment = v; }
+        else if (a == "--canonical-image") { if ((v = next("--canonical-image"))) { o.canonicalImagePath = v; } }
+        else if (a == "--comment") { if ((v = next("--comment"))) { o.runComment = v; } }
         else if (a == "--frames") {
-            if (!(v = next("--frames"))) return -1;
-            o.totalFrames = std::atoi(v);
-            if (o.totalFrames == 1) o.savedFrames = {1};  // mainOffline.cpp:108-111
+            if ((v = next("--frames"))) {
+                o.totalFrames = std::atoi(v);
+                if (o.totalFrames == 1) o.savedFrames = {1};  // mainOffline.cpp:108-111
+            }
         }
-        else if (a == "--spp") { if (!(v = next("--spp"))) return -1; o.spp = std::atoi(v); }
+        else if (a == "--spp") { if ((v = next("--spp"))) { o.spp = std::atoi(v); } }
         else if (a == "--chunks") {
             for (int k = 0; k < 3; k++) {
-                if (!(v = next("--chunks"))) return -1;
+                if (!(v = next("--chunks"))) return -1;  // an extension flag: all three values required
                 o.chunks[k] = std::atoi(v);
             }
         }
-        else if (a == "--device") { if (!(v = next("--device"))) return -1; o.device = std::atoi(v); }
-        else if (a == "--data") { if (!(v = next("--data"))) return -1; o.dataDir = v; }
-        else if (a == "--perf-report") { if (!(v = next("--perf-report"))) return -1; o.perfReport = v; }
+        else if (a == "--device") { if ((v = next("--device"))) { o.device = std::atoi(v); } }
+        else if (a == "--data") { if ((v = next("--data"))) { o.dataDir = v; } }
+        else if (a == "--perf-report") { if ((v = next("--perf-report"))) { o.perfReport = v; } }
         else if (a == "--no-textures") o.textures = false;
         else if (a == "--test-sequence") o.testSequence = true;
         else if (a == "--test-remove20") o.removal20 = true;
         else if (a == "--test-remove-circle") o.removalCircle = true;
         else if (a == "--help" || a == "-h") { usage(argv[0]); return 0; }
-        else { std::cerr << "unknown option " << a << "\n"; return -1; }
+        else std::cerr << "note: unknown option " << a << " ignored\n";
     }
-    if (o.width <= 0 || o.height <= 0 || o.width % 8 || o.height % 8) {
-        std::cerr << "width and height must be positive multiples of 8\n";
+    if (o.width <= 0 || o.height <= 0) {
+        std::cerr << "width and height must be positive\n";
         return -1;
     }
     if (o.totalFrames <= 0 || o.spp <= 0 || o.chunks[0] <= 0 || o.chunks[1] <= 0 || o.chunks[2] <= 0) {

@@ -192,6 +192,24 @@ def test_frames_end_to_end():
     r.close()
 
 
+@pytest.mark.parametrize("w,h", [(100, 62), (37, 29)])
+def test_frames_at_sizes_off_the_tile_grid(w, h):
+    """Frame sizes that are not multiples of the 8x8 trace / 16x16 denoise tiles (the
+    reference renders any size): partial tiles are masked, results equal the oracle."""
+    r, o = _setup(w, h)
+    _inject_sky(r, o)
+    p = _dn_params()
+    for f in range(3):
+        r.trace(f)
+        r.denoise(f, f + 1, p)
+        o.trace(f)
+        o.post_trace()
+        o.denoise(f, f + 1)
+        _compare_radiance(r.read("ILLUM"), o.read(0), "%dx%d frame%d illum" % (w, h, f))
+        _compare_radiance(r.read("OUTPUT"), o.read(21), "%dx%d frame%d output" % (w, h, f))
+    r.close()
+
+
 def _inject_frame(r, o):
     # previous-frame planes (the denoiser's history slot), then the current ones
     for name in ("PREV_NORMAL_ROUGH", "PREV_DEPTH", "PREV_MATERIAL", "PREV_ILLUM", "PREV_FAST", "PREV_HIST_LEN",

@@ -7,6 +7,7 @@ numpy restatement, the oracle post-process on a synthetic frame (exposure,
 bloom, tone curve sanity).  GPU: the HIP post-process chain against the oracle
 on a rendered frame, with the sun on screen (lens flare) and off.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -109,10 +110,11 @@ VARIANTS = {
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("look_at_sun,variant", [(False, "defaults"), (True, "defaults"),
-                                                 (False, "wide_bloom_uncharted2"), (True, "manual_reinhard")])
-def test_gpu_postprocess_matches_oracle(look_at_sun, variant, tmp_path):
-    w, h = 128, 96
+@pytest.mark.parametrize("look_at_sun,variant,w,h", [(False, "defaults", 128, 96), (True, "defaults", 128, 96),
+                                                     (False, "wide_bloom_uncharted2", 128, 96),
+                                                     (True, "manual_reinhard", 128, 96), (False, "defaults", 100, 62),
+                                                     (True, "wide_bloom_uncharted2", 37, 29)])
+def test_gpu_postprocess_matches_oracle(look_at_sun, variant, w, h, tmp_path):
     r = vxpt.Renderer(w, h)
     r.load_settings()
     r.generate_terrain((2, 1, 2))
@@ -143,3 +145,36 @@ def test_gpu_postprocess_matches_oracle(look_at_sun, variant, tmp_path):
     px = vxpt.read_png(path)
     assert px.shape == (h, w, 3)
     r.close()
+
+
+def _golden_imagediff():
+    import json
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(d, "imagediff_ref.json")) as f:
+        return os.path.join(d, "imagediff"), json.load(f)
+
+
+@pytest.mark.parametrize("case", sorted(_golden_imagediff()[1]))
+def test_image_diff_matches_reference_imagediff(case, tmp_path):
+    """vxpt_image_diff / vxpt_image_diff_png against the reference's own ImageDiff
+    (ImageDiff.cpp:94-372, compiled from its sources; fixtures by
+    tests/golden/make_imagediff_golden.py): pixel counts, verdicts and the diff image exact,
+    RMSE and SSIM to float rounding."""
+    root, ref = _golden_imagediff()
+    ref = ref[case]
+    pa, pb = os.path.join(root, case + "_a.png"), os.path.join(root, case + "_b.png")
+    pd = str(tmp_path / "diff.png")
+    if ref["total_pixels"] == 0:
+        # size mismatch: the reference returns an empty result (every verdict false); the ABI
+        # zeroes the result the same way and returns VXPT_ERR_ARG
+        res = vxpt.ImageDiffResult()
+        rc = vxpt.load_library().vxpt_image_diff(pa.encode(), pb.encode(), ctypes.byref(res))
+        assert rc != 0 and res.total_pixels == 0 and not (res.is_identical or res.is_very_close or res.is_close)
+        return
+    r = vxpt.image_diff(pa, pb, pd if ref["diff_png"] else None)
+    for k in ("different_pixels", "total_pixels", "is_identical", "is_very_close", "is_close"):
+        assert int(r[k]) == ref[k], (k, r[k], ref[k])
+    for k in ("pixel_difference_ratio", "rmse", "ssim"):
+        assert abs(r[k] - ref[k]) <= 2e-6 * max(1.0, abs(ref[k])), (k, r[k], ref[k])
+    if ref["diff_png"]:
+        np.testing.assert_array_equal(vxpt.read_png(pd), vxpt.read_png(os.path.join(root, ref["diff_png"])))
