@@ -24,6 +24,7 @@ import argparse
 import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -43,7 +44,28 @@ def scene_args(a):
     return chunks, 32.0 * scale, 64.0 * scale, pos
 
 
+def native_oracle():
+    """Build the oracle for this host with -march=native (the CPU baseline's
+    flags) into oracle/_native/ -- the prebuilt liboracle.so targets x86-64-v3 because it is
+    compiled in another container.  Returns (library path, march label)."""
+    src = os.path.join(REPO, "oracle")
+    out_dir = os.path.join(src, "_native")
+    lib = os.path.join(out_dir, "liboracle_native.so")
+    try:
+        os.makedirs(out_dir, exist_ok=True)
+        srcs = [os.path.join(src, f) for f in ("orc_scene.cpp", "orc_sky.cpp", "orc_trace.cpp", "orc_denoise.cpp",
+                                               "orc_post.cpp", "orc_lights.cpp", "orc_api.cpp")]
+        subprocess.run(["g++", "-O3", "-march=native", "-fopenmp", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
+                        "-std=c++17", "-shared", "-o", lib] + srcs, check=True, timeout=120,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        return lib, "native"
+    except (OSError, subprocess.SubprocessError):
+        return os.path.join(src, "liboracle.so"), "x86-64-v3"
+
+
 def cpu_baseline(a, target_s):
+    lib, march = native_oracle()
+    os.environ["ORACLE_LIB"] = lib
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     chunks, hs, fd, pos = scene_args(a)
@@ -69,9 +91,26 @@ def cpu_baseline(a, target_s):
         else:
             passes = int(passes * grow) + 1
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": passes * rows * a.width / dt / 1e6, "unit": "Mpaths/s", "cores": cores, "kind": "port",
-            "sample": "oracle trace of rows [%d,%d) x %d pass(es) at %dx%d, 1 spp each, %s, same scene (%.1f s)" % (
-                y0, y0 + rows, passes, a.width, a.height, "primary rays only" if a.primary_only else "full path", dt)}
+    res = {"value": passes * rows * a.width / dt / 1e6, "unit": "Mpaths/s", "cores": cores, "kind": "port",
+           "march": march,
+           "sample": "oracle trace of rows [%d,%d) x %d pass(es) at %dx%d, 1 spp each, %s, same scene (%.1f s)" % (
+               y0, y0 + rows, passes, a.width, a.height, "primary rays only" if a.primary_only else "full path", dt)}
+    if not a.primary_only:
+        # the denoiser chain on the CPU: whole-frame trace passes feed two
+        # frames; the second (steady state: temporal accumulation, history fix and clamping,
+        # a-trous 1 + 3 on the ReLAX defaults) is timed
+        o.set_denoise_params([30, 6, 2, 0.5, 0.15, 0.003, 0.01, 0.05, 500000], [1, 1, 1, 1, 1, 1])
+        o.trace(0)
+        o.post_trace()
+        o.denoise(0, 1)
+        o.set_camera(pos, C1_DIR, 90.0, which=1)
+        o.trace(1)
+        o.post_trace()
+        t0 = time.perf_counter()
+        o.denoise(1, 2)
+        res["denoise_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+        res["denoise_sample"] = "oracle ReLAX chain, one steady-state %dx%d frame (frame 1)" % (a.width, a.height)
+    return res
 
 
 def main():

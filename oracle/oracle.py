@@ -21,7 +21,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB = os.path.join(HERE, "liboracle.so")
+# ORACLE_LIB: another build of the same sources (bench.py's CPU baseline builds one with
+# -march=native for the host it runs on)
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 TABLES = os.path.join(REPO, "data", "tables")
 
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),

@@ -58,11 +58,13 @@ def frame_ops(frame, spp, p):
     yield ("exchange", ["ILLUM"], 2)
     it = it0 + spp
     used = it - 1 if it > 0 else 0
-    yield ("pass", 11, 0, 0)
     if p["firefly"]:
+        # the firefly pass writes the world-position plane too (pass 11 alone otherwise)
         yield ("pass", 0, used & 1, 0)
         yield ("exchange", [RES[used & 1]], TRACE_HALO)
         yield ("exchange", ["ILLUM"], 2)
+    else:
+        yield ("pass", 11, 0, 0)
     if frame == 0:
         yield ("pass", 12, 0, 0)
         yield ("exchange", HISTORY, 2)

@@ -47,17 +47,12 @@ VX_D V3 world_pos(const CamDev &c, int x, int y, float depth) {
 VX_D V3 xyz4(float4 v) { return V3(v.x, v.y, v.z); }
 // world position of the (edge-clamped) pixel's hit, from the per-frame plane
 VX_D V3 wp(const DenoiseArgs &a, int x, int y) { return xyz4(a.wpos[(size_t)cl(y, a.H) * a.W + cl(x, a.W)]); }
-__global__ __launch_bounds__(256) void k_world_pos(DenoiseArgs a) {
-    // the first pass of every denoise: zero the firefly list counter
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) a.ffCount[threadIdx.x] = 0u;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = a.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.y1) return;
-    const size_t i = (size_t)y * a.W + x;
-    const float z = a.depth[i];
+// the packed plane's value of a pixel: world position of its primary hit and, in w, its 16-bit
+// material read (Load2DUshort1 quirk, ld_ushort) for the a-trous / history-fix material tests,
+// -1 for sky (no tap weight)
+VX_D float4 wpos_px(const DenoiseArgs &a, int x, int y, float z) {
     const V3 p = world_pos(a.cam, x, y, z);
-    // w: the pixel's 16-bit material read (Load2DUshort1 quirk, ld_ushort) for
-    // the a-trous / history-fix material tests, -1 for sky (no tap weight)
-    a.wpos[i] = make_float4(p.x, p.y, p.z, z > kRange ? -1.0f : ld_ushort(a.material, a.W, a.H, x, y));
+    return make_float4(p.x, p.y, p.z, z > kRange ? -1.0f : ld_ushort(a.material, a.W, a.H, x, y));
 }
 VX_D float smooth_step10(float x) {  // SmoothStep(1, 0, x)
     // (x - 1) / (0 - 1): dividing by -1 is exact and round-to-nearest is sign
@@ -113,99 +108,105 @@ VX_D uint32_t explode(uint32_t x) {
 }
 
 // ---------------------------------------------------------------- firefly
-// 256-thread workgroups over 8x32 pixels; each wave covers two 8x4 tiles
-// (one per 32-lane half of the wave).
-__global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int parity) {
+// 256-thread workgroups over 64x4 pixels; each wave covers two 8x4 tiles (one per 32-lane half of
+// the wave).  The same launch writes the packed world-position plane (wpos_px) over rows
+// [wy0, wy1) -- the band and the halo rows the later stencils read -- so the filter's own
+// neighbour positions come from the depth directly (the same world_pos arithmetic).
+// Detected pixels are listed (ffCand) for k_firefly_filter; filtered pixels are listed per 16x16
+// tile of the band (ffCount[tile], entries at tile*256):
+// k_temporal applies its tile's entries before reading the radiance (or k_firefly_apply does,
+// when no temporal pass follows), so every read of this pass sees the pre-filter values (the
+// reference's in-place write races).
+// The filter of one detected firefly (FireflyFilter.h:131-220), by a whole wave: lane k < 8 fetches
+// and tests neighbour k (row-major 3x3 without the centre) in parallel, then every lane combines the
+// eight results in the reference's order (the same arithmetic as the loop over neighbours), and
+// lane 0 lists the filtered pixel for its 16x16 tile.  The candidate's values are wave-uniform.
+VX_D void firefly_filter_wave(const DenoiseArgs &a, int lane, int x, int y, float cd, const Reservoir &r,
+                              float nSum, int nCnt) {
     const int W = a.W, H = a.H;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int l32 = lane & 31;
-    // a wave = two 8x4 tiles side by side, a block = 64 x 4 pixels: row segments of 64 pixels
-    // (the tiles are the reference's 8x4 ones; the band starts on an 8-row boundary)
-    const int x = blockIdx.x * 64 + wv * 16 + (lane >> 5) * 8 + (l32 & 7);
-    const int y = a.y0 + blockIdx.y * 4 + (l32 >> 3);
-    const bool inb = x < W && y < a.y1;
     const size_t i = (size_t)y * W + x;
-    const float cd = inb ? a.depth[i] : 0.0f;
-    const bool sky = inb && cd > kRange;
-    // the reservoir is read beside the depth (not behind the sky test): one memory round trip
-    Reservoir r = Reservoir{0u, 0u, 0.f, 0.f, 0.f};
-    if (inb) r = a.reservoir[i];
-    const bool valid = inb && !sky && r.lightData != 0 && isfinite(r.weightSum) && r.weightSum > 0.0f;
-    float v = valid ? r.weightSum : 0.0f;
-    unsigned cnt = valid ? 1u : 0u;
-    for (int off = 16; off > 0; off >>= 1) {
-        v += __shfl_down(v, off, 32);
-        cnt += __shfl_down(cnt, off, 32);
-    }
-    const float tileSum = __shfl(v, 0, 32);
-    const unsigned tileCnt = __shfl(cnt, 0, 32);
-    if (!valid) return;
     const float cw = r.weightSum;
-    const float nSum = tileSum - cw;
-    const int nCnt = (int)tileCnt - 1;
     const float minWeight = 5.0f, wThr = 80.0f, nThr = 0.8f, depthSigma = 0.02f;
-    bool firefly = false;
-    if (cw >= minWeight) {
-        if (nCnt <= 0) firefly = true;
-        else {
-            const float avg = nSum / float(nCnt);
-            if (avg > 0.0f && cw > avg * wThr) firefly = true;
-        }
-    }
-    if (!firefly) return;
     const V4 cc4 = f4(a.illum[i]);
     const float cLum = luminance(cc4.xyz());
     V3 cN = f4(a.normalRough[i]).xyz();
     const float cl_ = length(cN);
     if (cl_ > 0.0f) cN /= cl_; else cN = V3(0.0f, 1.0f, 0.0f);
     const float cMat = a.material[i];
-    const V3 cWP = wp(a, x, y);
+    const V3 cWP = world_pos(a.cam, x, y, cd);
     const float g[3] = {1.0f, 2.0f, 1.0f};
+    const float depthScale = fmaxf(fabsf(cd), 1.0f);
+    const float nwp = normal_weight_param(1.0f, 0.25f);
+    // this lane's neighbour
+    const int t = lane < 4 ? lane : lane + 1;
+    const int sx = x + t % 3 - 1, sy = y + t / 3 - 1;
+    const int inF = lane < 8 && sx >= 0 && sy >= 0 && sx < W && sy < H;
+    V4 sc4;
+    float tw = 0.0f, score = 0.0f;
+    int useTw = 0, cand = 0;
+    Reservoir nr = Reservoir{0u, 0u, 0.f, 0.f, 0.f};
+    if (inF) {
+        const size_t j = (size_t)sy * W + sx;
+        sc4 = f4(a.illum[j]);
+        const float sd = a.depth[j];
+        const V3 sN0 = f4(a.normalRough[j]).xyz();
+        const float sMat = a.material[j];
+        nr = a.reservoir[j];
+        const float gw = g[abs(t % 3 - 1)] * g[abs(t / 3 - 1)];
+        do {  // the reference's tests in order; a failed test drops the neighbour from both weights
+            if (sd > kRange) break;
+            V3 sN = sN0;
+            const float sl = length(sN);
+            if (sl <= 0.0f) break;
+            sN /= sl;
+            const float nd = dot(cN, sN);
+            if (nd < nThr) break;
+            if (fabsf(sMat - cMat) > 0.5f) break;
+            const V3 sWP = world_pos(a.cam, sx, sy, sd);
+            if (plane_w(cWP, cN, sWP, depthSigma * depthScale) <= 0.0f) break;
+            const float nw = nonexp_w(acos_approx(clampf(nd, -1.0f, 1.0f)), nwp);
+            const float dw = expf(-fabsf(sd - cd) / (depthScale * depthSigma + 1e-6f));
+            const float lw = expf(-fabsf(luminance(sc4.xyz()) - cLum) * a.p.phiL);
+            tw = gw * 1.0f * nw * dw * lw;
+            useTw = tw > 1e-5f;
+            if (nr.lightData != 0 && isfinite(nr.weightSum) && nr.weightSum > 0.0f && nr.weightSum < cw) {
+                cand = 1;
+                score = fabsf(sd - cd) / (depthScale + 1e-6f) + (1.0f - clampf(nd, 0.0f, 1.0f)) +
+                        0.25f * fabsf(nr.weightSum - cw);
+            }
+        } while (false);
+    }
     V4 filt = cc4;
     float filtW = 1.0f;
     V4 fb = cc4 * (g[0] * g[0]);
     float fbW = g[0] * g[0];
-    const float depthScale = fmaxf(fabsf(cd), 1.0f);
-    const float nwp = normal_weight_param(1.0f, 0.25f);
     Reservoir best = r;
     float bestScore = 3.402823466e+38f;
     bool repl = false;
-    for (int dy = -1; dy <= 1; ++dy)
-        for (int dx = -1; dx <= 1; ++dx) {
-            if (dx == 0 && dy == 0) continue;
-            const int sx = x + dx, sy = y + dy;
-            if (sx < 0 || sy < 0 || sx >= W || sy >= H) continue;
-            const float gw = g[abs(dx)] * g[abs(dy)];
-            const size_t j = (size_t)sy * W + sx;
-            const V4 sc4 = f4(a.illum[j]);
-            fb += sc4 * gw;
-            fbW += gw;
-            const float sd = a.depth[j];
-            if (sd > kRange) continue;
-            V3 sN = f4(a.normalRough[j]).xyz();
-            const float sl = length(sN);
-            if (sl <= 0.0f) continue;
-            sN /= sl;
-            const float nd = dot(cN, sN);
-            if (nd < nThr) continue;
-            if (fabsf(a.material[j] - cMat) > 0.5f) continue;
-            const V3 sWP = wp(a, sx, sy);
-            if (plane_w(cWP, cN, sWP, depthSigma * depthScale) <= 0.0f) continue;
-            const float nw = nonexp_w(acos_approx(clampf(nd, -1.0f, 1.0f)), nwp);
-            const float dw = expf(-fabsf(sd - cd) / (depthScale * depthSigma + 1e-6f));
-            const float lw = expf(-fabsf(luminance(sc4.xyz()) - cLum) * a.p.phiL);
-            const float tw = gw * 1.0f * nw * dw * lw;
-            if (tw > 1e-5f) {
-                filt += sc4 * tw;
-                filtW += tw;
-            }
-            const Reservoir nr = a.reservoir[j];
-            if (nr.lightData != 0 && isfinite(nr.weightSum) && nr.weightSum > 0.0f && nr.weightSum < cw) {
-                const float score = fabsf(sd - cd) / (depthScale + 1e-6f) + (1.0f - clampf(nd, 0.0f, 1.0f)) +
-                                    0.25f * fabsf(nr.weightSum - cw);
-                if (score < bestScore) { bestScore = score; best = nr; repl = true; }
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+        if (!__shfl(inF, k)) continue;
+        const int tk = k < 4 ? k : k + 1;
+        const float gw = g[abs(tk % 3 - 1)] * g[abs(tk / 3 - 1)];
+        const V4 s4(__shfl(sc4.x, k), __shfl(sc4.y, k), __shfl(sc4.z, k), __shfl(sc4.w, k));
+        fb += s4 * gw;
+        fbW += gw;
+        if (__shfl(useTw, k)) {
+            const float twk = __shfl(tw, k);
+            filt += s4 * twk;
+            filtW += twk;
+        }
+        if (__shfl(cand, k)) {
+            const float sk = __shfl(score, k);
+            if (sk < bestScore) {
+                bestScore = sk;
+                best = Reservoir{(uint32_t)__shfl((int)nr.lightData, k), (uint32_t)__shfl((int)nr.uvData, k),
+                                 __shfl(nr.weightSum, k), __shfl(nr.targetPdf, k), __shfl(nr.M, k)};
+                repl = true;
             }
         }
+    }
+    if (lane != 0) return;
     V4 outc;
     if (filtW > 0.0f) outc = filt / filtW;
     else if (fbW > 0.0f) outc = fb / fbW;
@@ -219,19 +220,90 @@ __global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int parity) {
         tgt = fmaxf(tgt, minWeight);
         dst.weightSum = fminf(dst.weightSum, tgt);
     }
-    const uint32_t slot = atomicAdd(a.ffCount, 1u);
-    a.ffIndex[slot] = (uint32_t)i;
+    const int by = y - a.y0;
+    const uint32_t tile = (uint32_t)((by >> 4) * ((W + 15) / 16) + (x >> 4));
+    const uint32_t slot = tile * 256u + atomicAdd(a.ffCount + tile, 1u);
+    a.ffIndex[slot] = (uint32_t)((by & 15) * 16 + (x & 15));
     a.ffColor[slot] = tf(outc);
     a.ffRes[slot] = dst;
 }
 
-__global__ __launch_bounds__(256) void k_firefly_apply(DenoiseArgs a) {
-    const uint32_t n = *a.ffCount;
-    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
-        const uint32_t i = a.ffIndex[s];
-        a.illum[i] = a.ffColor[s];
-        a.reservoir[i] = a.ffRes[s];
+__global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int wy0, int wy1, int detect) {
+    const int W = a.W, H = a.H;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int l32 = lane & 31;
+    // a wave = two 8x4 tiles side by side, a block = 64 x 4 pixels: row segments of 64 pixels
+    // (the tiles are the reference's 8x4 ones; the band and wy0 start on 8-row boundaries)
+    const int x = blockIdx.x * 64 + wv * 16 + (lane >> 5) * 8 + (l32 & 7);
+    const int y = wy0 + blockIdx.y * 4 + (l32 >> 3);
+    const bool inb = x < W && y < wy1;
+    const size_t i = (size_t)y * W + x;
+    const float cd = inb ? a.depth[i] : 0.0f;
+    const bool sky = inb && cd > kRange;
+    const bool inBand = detect && inb && y >= a.y0 && y < a.y1;
+    // the reservoir is read beside the depth (not behind the sky test): one memory round trip
+    Reservoir r = Reservoir{0u, 0u, 0.f, 0.f, 0.f};
+    if (inBand) r = a.reservoir[i];
+    if (inb) a.wpos[i] = wpos_px(a, x, y, cd);
+    const bool valid = inBand && !sky && r.lightData != 0 && isfinite(r.weightSum) && r.weightSum > 0.0f;
+    float v = valid ? r.weightSum : 0.0f;
+    unsigned cnt = valid ? 1u : 0u;
+    for (int off = 16; off > 0; off >>= 1) {
+        v += __shfl_down(v, off, 32);
+        cnt += __shfl_down(cnt, off, 32);
     }
+    const float tileSum = __shfl(v, 0, 32);
+    const unsigned tileCnt = __shfl(cnt, 0, 32);
+    const float cw = r.weightSum;
+    const float nSum = tileSum - cw;
+    const int nCnt = (int)tileCnt - 1;
+    const float minWeight = 5.0f, wThr = 80.0f;
+    bool firefly = false;
+    if (valid && cw >= minWeight) {
+        if (nCnt <= 0) firefly = true;
+        else {
+            const float avg = nSum / float(nCnt);
+            if (avg > 0.0f && cw > avg * wThr) firefly = true;
+        }
+    }
+    // detected pixels are filtered by k_firefly_filter, a wave per pixel: the filter's registers
+    // would cut this pass's occupancy (32 -> 84 VGPRs inline)
+    if (firefly) a.ffCand[atomicAdd(a.ffCandCount, 1u)] = make_uint4((uint32_t)i, __float_as_uint(nSum), (uint32_t)nCnt, 0u);
+}
+
+// the detected fireflies (~100 on the bench scene at 1080p): one wave per pixel, grid-stride
+__global__ __launch_bounds__(64) void k_firefly_filter(DenoiseArgs a) {
+    const uint32_t n = *a.ffCandCount;
+    for (uint32_t s = blockIdx.x; s < n; s += gridDim.x) {
+        const uint4 c = a.ffCand[s];
+        const size_t i = c.x;
+        firefly_filter_wave(a, threadIdx.x, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), a.depth[i], a.reservoir[i],
+                            __uint_as_float(c.y), (int)c.z);
+    }
+}
+
+// a tile's firefly list entry k: written back to the radiance and reservoir planes
+VX_D size_t ff_apply(const DenoiseArgs &a, unsigned tile, unsigned k, float4 &col) {
+    const unsigned tilesX = (a.W + 15) / 16, s = tile * 256 + k, p = a.ffIndex[s];
+    const size_t i = (size_t)(a.y0 + (tile / tilesX) * 16 + (p >> 4)) * a.W + (tile % tilesX) * 16 + (p & 15);
+    col = a.ffColor[s];
+    a.illum[i] = col;
+    a.reservoir[i] = a.ffRes[s];
+    return i;
+}
+
+// the lists' consumer when no temporal pass runs (frame 0, temporal accumulation off, or a band
+// whose filtered rows travel to its neighbours before the next pass): one workgroup per tile;
+// the count is reset for the next frame
+__global__ __launch_bounds__(256) void k_firefly_apply(DenoiseArgs a) {
+    const unsigned tile = blockIdx.y * ((a.W + 15) / 16) + blockIdx.x;
+    if (tile == 0 && threadIdx.x == 0) *a.ffCandCount = 0u;  // k_firefly_filter has finished
+    const unsigned n = a.ffCount[tile];
+    if (n == 0) return;
+    float4 col;
+    if (threadIdx.x < n) ff_apply(a, tile, threadIdx.x, col);
+    __syncthreads();
+    if (threadIdx.x == 0) a.ffCount[tile] = 0u;
 }
 
 // ---------------------------------------------------------------- frame 0
@@ -316,7 +388,8 @@ VX_D V4 bilinear_custom4(const float4 *b, int W, int H, V2 uv, const float cw[4]
     out /= sum;
     return out;
 }
-VX_D float bilinear_custom1(const float *b, int W, int H, V2 uv, const float cw[4]) {
+// v[k]: the plane at the bilinear taps (x0 + (k & 1), y0 + (k >> 1)), edge-clamped
+VX_D float bilinear_custom1(const float v[4], int W, int H, V2 uv, const float cw[4]) {
     int x0, y0;
     float w[4];
     bilinear_taps(W, H, uv, x0, y0, w);
@@ -326,7 +399,7 @@ VX_D float bilinear_custom1(const float *b, int W, int H, V2 uv, const float cw[
         const float wt = w[k] * cw[k];
         const float weight = (wt < 1e-6f) ? 1e-6f : wt;
         sum += weight;
-        out += ld1(b, W, H, x0 + (k & 1), y0 + (k >> 1)) * weight;
+        out += v[k] * weight;
     }
     return out / sum;
 }
@@ -351,7 +424,7 @@ VX_D V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
 
 // Returns whether the history fix must filter the pixel (HistoryFix.h:20-22:
 // non-sky and history <= 4; pixels past the denoising range keep last frame's length).
-VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
+VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol) {
     const int W = a.W, H = a.H;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
@@ -373,7 +446,7 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
     const float NoV = fabsf(dot(cN, Vv));
     const V3 prevWP = cWP + f4(a.motion[i]).xyz();
     const V2 prevUV = pc.dir_to_uv(normalize(prevWP - pc.pos));
-    const V3 illum = f4(a.illum[i]).xyz();
+    const V3 illum = f4(ffCol ? *ffCol : a.illum[i]).xyz();
     const float m1 = luminance(illum), m2 = m1 * m1;
     const V3 camDelta = pc.pos - cam.pos;
     float par1, par2;
@@ -440,7 +513,10 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
     if ((taps[0] * 1.0f + taps[1] * 1.0f + taps[2] * 1.0f + taps[3] * 1.0f) == 0.0f) {
         found = 0.0f; quality = 0.0f; hist = 0.0f;
     } else {
-        hist = bilinear_custom1(a.prevHistLen, W, H, prevUV, taps);
+        float histTap[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) histTap[k] = ld1(a.prevHistLen, W, H, ox + (k & 1), oy + (k >> 1));
+        hist = bilinear_custom1(histTap, W, H, prevUV, taps);
     }
     hist = hist + 1.0f;
     const V3 Vp = normalize(prevWP - pc.pos);
@@ -467,16 +543,44 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y) {
 // The pixels the history fix must filter (rare once history has built up)
 // are listed per 16x16 tile: hfList[tile*256 + k] = pixel index, hfCount[tile]
 // = k's; no atomics, and the history-fix launch only works on listed pixels.
-__global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
-    __shared__ unsigned sTot[4];
+// The tile's firefly list (k_firefly) is applied first: its entries go back to the radiance and
+// reservoir planes, and the filtered values of the tile's own pixels are handed over in LDS.
+#ifdef VX_EXP_TEMPORAL_LB5
+#define VX_TEMPORAL_LB __launch_bounds__(256, 5)
+#else
+#define VX_TEMPORAL_LB __launch_bounds__(256)
+#endif
+__global__ VX_TEMPORAL_LB void k_temporal(DenoiseArgs a, Qt rot) {
+    __shared__ unsigned sTot[4], sFFn, sFFmask[8];
+    __shared__ float4 sFF[256];
     const int tx = blockIdx.x, ty = blockIdx.y;
+    const unsigned tile = ty * ((a.W + 15) / 16) + tx;
+    if (threadIdx.x == 0) {
+        const unsigned n = a.ffCount[tile];
+        sFFn = n;
+        if (n) a.ffCount[tile] = 0u;
+        if (tile == 0) *a.ffCandCount = 0u;  // k_firefly_filter has finished
+    }
+    if (threadIdx.x < 8) sFFmask[threadIdx.x] = 0u;
+    __syncthreads();
+    const unsigned nff = sFFn;
+    if (nff) {
+        if (threadIdx.x < nff) {
+            float4 col;
+            ff_apply(a, tile, threadIdx.x, col);
+            const unsigned p = a.ffIndex[tile * 256 + threadIdx.x];
+            sFF[p] = col;
+            atomicOr(&sFFmask[p >> 5], 1u << (p & 31));
+        }
+        __syncthreads();
+    }
+    const bool own = nff && ((sFFmask[threadIdx.x >> 5] >> (threadIdx.x & 31)) & 1u);
     const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);
-    const bool fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y);
+    const bool fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr);
     const unsigned long long m = __ballot(fix);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0) sTot[wv] = (unsigned)__popcll(m);
     __syncthreads();
-    const unsigned tile = ty * ((a.W + 15) / 16) + tx;
     unsigned off = 0;
     for (int k = 0; k < wv; ++k) off += sTot[k];
     if (fix) a.hfList[tile * 256 + off + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)((size_t)y * a.W + x);
@@ -514,11 +618,11 @@ VX_D void history_fix_px(const DenoiseArgs &a, int W, int H, int x, int y, size_
     a.pong[i] = tf(sum / wsum);
 }
 
-// One pixel per wave: lane t < 25 takes tap t of the 5x5 pattern (t = 12 is
-// the centre, weight 1), so all 24 sparse taps are fetched at once instead of
-// one dependent round trip after another; the sums are combined across lanes
-// (the V4 operators keep the reference's w-from-z behaviour).
-VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, size_t i, int lane) {
+// One pixel per 32-lane half-wave: lane t < 25 of the half takes tap t of the 5x5 pattern (t = 12
+// is the centre, weight 1), so all 24 sparse taps are fetched at once instead of one dependent
+// round trip after another; the sums are combined across the half's lanes (the V4 operators keep
+// the reference's w-from-z behaviour).
+VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, size_t i, int lane, bool store) {
     const float z = a.depth[i], hist = a.histLen[i];
     const float cMat = ld_ushort(a.material, W, H, x, y);
     const V3 cN = f4(a.normalRough[i]).xyz();
@@ -548,14 +652,14 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
             }
         }
     }
-    for (int o = 16; o > 0; o >>= 1) {  // lanes 0..31 hold every tap
+    for (int o = 16; o > 0; o >>= 1) {  // the half's 32 lanes hold every tap
         sum.x += __shfl_xor(sum.x, o);
         sum.y += __shfl_xor(sum.y, o);
         sum.z += __shfl_xor(sum.z, o);
         sum.w += __shfl_xor(sum.w, o);
         wsum += __shfl_xor(wsum, o);
     }
-    if (lane == 0) a.pong[i] = tf(sum / wsum);
+    if (lane == 0 && store) a.pong[i] = tf(sum / wsum);
 }
 
 // One workgroup per 16x16 tile, over the tile's list from k_temporal: a
@@ -565,10 +669,13 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
     const unsigned tile = blockIdx.y * ((a.W + 15) / 16) + blockIdx.x;
     const unsigned n = a.hfCount[tile];
     const unsigned wv = threadIdx.x >> 6;
-    if (n <= 64) {  // sparse (steady state): each wave takes every 4th listed pixel, its taps in parallel
-        for (unsigned k = wv; k < n; k += 4) {
-            const size_t i = a.hfList[tile * 256 + k];
-            history_fix_wave(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i, threadIdx.x & 63);
+    if (n <= 64) {  // sparse (steady state): each half-wave takes every 8th listed pixel, its taps in parallel
+        const unsigned half = wv * 2 + ((threadIdx.x >> 5) & 1);
+        for (unsigned k0 = wv * 2; k0 < n; k0 += 8) {  // wave-uniform trip count; the halves share the shuffles
+            const unsigned k = k0 + (half & 1);
+            const bool has = k < n;
+            const size_t i = a.hfList[tile * 256 + (has ? k : k0)];
+            history_fix_wave(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i, threadIdx.x & 31, has);
         }
         return;
     }
@@ -601,7 +708,13 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
     const float hist = a.histLen[i];
     V3 m1(0.0f), m2(0.0f), nm1(0.0f);
     float nm2 = 0.0f;
+    // one column of taps per iteration: fully unrolled, the 25 taps' LDS values were all held in
+    // registers (118 VGPRs, 4 waves/SIMD); a column at a time runs at 65 (7 waves), 61 -> 50 us.
+    // Precomputing the per-pixel moment terms in the staging loop (3 float4 planes in LDS) was
+    // slower (59 us at 44 or 87 VGPRs).
+#pragma unroll 1
     for (int dx = -2; dx <= 2; ++dx)
+#pragma unroll
         for (int dy = -2; dy <= 2; ++dy) {
             const int k = (ty + 2 + dy) * 20 + (tx + 2 + dx);
             const V3 s(sY[0][k], sY[1][k], sY[2][k]);
@@ -617,8 +730,11 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
                    sqrtf(fmaxf(0.0f, m2.z - m1.z * m1.z)));
     V3 cmin = m1 - 2.0f * sigma, cmax = m1 + 2.0f * sigma;
     const V3 center = rgb_to_ycocg(f4(a.pong[i]).xyz());
-    cmin = (cmin.x < center.x) ? cmin : center;  // LinearMath.h template min on Float3 (x-compare)
-    cmax = (cmax.x > center.x) ? cmax : center;
+    // LinearMath.h template min / max on Float3 (x-compare), as component selects (a select of whole
+    // vectors went through scratch memory)
+    const bool useMin = cmin.x < center.x, useMax = cmax.x > center.x;
+    cmin = V3(useMin ? cmin.x : center.x, useMin ? cmin.y : center.y, useMin ? cmin.z : center.z);
+    cmax = V3(useMax ? cmax.x : center.x, useMax ? cmax.y : center.y, useMax ? cmax.z : center.z);
     const V4 pi = f4(a.ping[i]);
     const V3 dY = rgb_to_ycocg(pi.xyz());
     const V3 cY(clampf(dY.x, cmin.x, cmax.x), clampf(dY.y, cmin.y, cmax.y), clampf(dY.z, cmin.z, cmax.z));
@@ -702,6 +818,8 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
         float sumW = 0.0f;
         V4 sum;
         const float dthr = a.p.depthThreshold * z;
+        // a column of taps per iteration (126 -> 64 VGPRs: 4 -> 8 waves/SIMD)
+#pragma unroll 1
         for (int cx = -1; cx <= 1; ++cx)
             for (int cy = -1; cy <= 1; ++cy) {
                 const int px = x + cx, py = y + cy;
@@ -730,6 +848,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
         float sw = 0.0f, s1 = 0.0f, s2 = 0.0f;
         V3 si(0.0f);
         const float nwp = normal_weight_param(1.0f, a.p.lobeAngleFraction);
+#pragma unroll 1
         for (int cx = -2; cx <= 2; ++cx)
             for (int cy = -2; cy <= 2; ++cy) {
                 const int k = (ty + 2 + cy) * 20 + tx + 2 + cx;
@@ -759,6 +878,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
 // descriptors (any step, jitter) or an LDS tile with a step-wide apron (steps 2 and 4).  The
 // arithmetic is the same code for both.
 struct GlobalTaps {
+    static constexpr bool kBatch = true;  // every tap fetched up front (one round trip)
     Plane4 pW, pN, pI;
     VX_D V4 wpos(int px, int py, int W) const { return pW[py * W + px]; }
     VX_D V3 nrm(int px, int py, int W) const { return pN[py * W + px].xyz(); }
@@ -767,6 +887,7 @@ struct GlobalTaps {
 template <int R, int TS = 16>
 struct TileTaps {  // the TSxTS tile at (x0, y0) with an R-pixel apron, zeros outside the frame
     static constexpr int T = TS + 2 * R;
+    static constexpr bool kBatch = false;  // LDS taps: read where used
     const float4 *sP, *sI;
     const float *sNx, *sNy, *sNz;
     int x0, y0;
@@ -789,20 +910,6 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
         if (final) a.output[i] = a.illum[i];  // BufferCopySky
         return;
     }
-    const V4 cP = src.wpos(x, y, W);
-    const float cMat = cP.w;
-    const V3 cN = src.nrm(x, y, W);
-    const V3 cWP = cP.xyz();
-    const float hist = a.histLen[i];
-    float lobe = a.p.lobeAngleFraction / sqrtf((float)step);
-    lobe = lerpf(0.99f, lobe, saturate(hist / 5.0f));
-    const V4 c = src.val(x, y, W);
-    const float cLum = luminance_fast(c.xyz());
-    const float phiInv = 1.0f / fmaxf(1.0e-4f, a.p.phiL * sqrtf(c.w));
-    const float nwp = normal_weight_param(1.0f, lobe);
-    float sumW = 0.44198f * 0.44198f;
-    V4 sum = c * V4(V3(sumW), sumW * sumW);
-    const float dthr = a.p.depthThreshold * z;
     int ofx = 0, ofy = 0;
     if (step > 4) {
         const uint32_t lin = explode((uint32_t)x) | (explode((uint32_t)y) << 1);
@@ -817,34 +924,69 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
         ofx = (int)o.x;
         ofy = (int)o.y;
     }
-    const float k3[2] = {0.44198f, 0.27901f};
-    for (int yy = -1; yy <= 1; ++yy)
-        for (int xx = -1; xx <= 1; ++xx) {
-            if (xx == 0 && yy == 0) continue;
+    // every tap's position, normal and value is fetched before the first weight: one memory round
+    // trip for the whole stencil (a value read behind its tap's weight test was a second one; the
+    // packed tap holds world position + 16-bit material, -1 = sky: weight 0 like the reference's
+    // depth test; out-of-frame taps read 0 and get weight 0 below)
+    V4 tP[8], tV[8];
+    V3 tN[8];
+    if (Src::kBatch) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int t = k < 4 ? k : k + 1, xx = t % 3 - 1, yy = t / 3 - 1;
             const int px = x + ofx + xx * (int)step, py = y + ofy + yy * (int)step;
-            const bool inside = px >= 0 && py >= 0 && px < W && py < H;
-            const float kernel = k3[abs(xx)] * k3[abs(yy)];
-            // packed tap: world position + 16-bit material (-1 = sky: weight 0 like the
-            // reference's depth test); out-of-frame taps get weight 0 below
-            const V4 sP = src.wpos(px, py, W);
-            const V3 sN = src.nrm(px, py, W);
-            const float sMat = sP.w;
-            const V3 sWP = sP.xyz();
-            float geo = plane_w_fast(cWP, cN, sWP, dthr);
-            geo *= kernel;
-            geo *= float(inside);
-            const float nw = nonexp_w(acos_approx_fast(dot_fast(cN, sN)), nwp);
-            float w = geo * nw;
-            w *= (float)(sMat == cMat);
-            if (w > 1e-4f) {
-                const V4 sv = src.val(px, py, W);
-                float lw = fabsf(cLum - luminance_fast(sv.xyz())) * phiInv;
-                lw = fminf(INFINITY, lw);
-                w *= __expf(-lw);
-                sumW += w;
-                sum += V4(V3(w), w * w) * sv;
-            }
+            tP[k] = src.wpos(px, py, W);
+            tN[k] = src.nrm(px, py, W);
+#ifndef VX_EXP_ATROUS_B
+            tV[k] = src.val(px, py, W);
+#endif
         }
+    }
+    const V4 cP = src.wpos(x, y, W);
+    const float cMat = cP.w;
+    const V3 cN = src.nrm(x, y, W);
+    const V3 cWP = cP.xyz();
+    const float hist = a.histLen[i];
+    float lobe = a.p.lobeAngleFraction / sqrtf((float)step);
+    lobe = lerpf(0.99f, lobe, saturate(hist / 5.0f));
+    const V4 c = src.val(x, y, W);
+    const float cLum = luminance_fast(c.xyz());
+    const float phiInv = 1.0f / fmaxf(1.0e-4f, a.p.phiL * sqrtf(c.w));
+    const float nwp = normal_weight_param(1.0f, lobe);
+    float sumW = 0.44198f * 0.44198f;
+    V4 sum = c * V4(V3(sumW), sumW * sumW);
+    const float dthr = a.p.depthThreshold * z;
+    const float k3[2] = {0.44198f, 0.27901f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // row-major over the 3x3 taps without the centre (Atrous.h order)
+        const int t = k < 4 ? k : k + 1, xx = t % 3 - 1, yy = t / 3 - 1;
+        const int px = x + ofx + xx * (int)step, py = y + ofy + yy * (int)step;
+        const bool inside = px >= 0 && py >= 0 && px < W && py < H;
+        const float kernel = k3[abs(xx)] * k3[abs(yy)];
+        if (!Src::kBatch) {
+            tP[k] = src.wpos(px, py, W);
+            tN[k] = src.nrm(px, py, W);
+        }
+        const float sMat = tP[k].w;
+        float geo = plane_w_fast(cWP, cN, tP[k].xyz(), dthr);
+        geo *= kernel;
+        geo *= float(inside);
+        const float nw = nonexp_w(acos_approx_fast(dot_fast(cN, tN[k])), nwp);
+        float w = geo * nw;
+        w *= (float)(sMat == cMat);
+        if (w > 1e-4f) {
+#ifdef VX_EXP_ATROUS_B
+            const V4 sv = src.val(px, py, W);
+#else
+            const V4 sv = Src::kBatch ? tV[k] : src.val(px, py, W);
+#endif
+            float lw = fabsf(cLum - luminance_fast(sv.xyz())) * phiInv;
+            lw = fminf(INFINITY, lw);
+            w *= __expf(-lw);
+            sumW += w;
+            sum += V4(V3(w), w * w) * sv;
+        }
+    }
     const V4 res = sum / V4(V3(sumW), sumW * sumW);
     out[i] = tf(res);
     if (final) {
@@ -853,8 +995,13 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
     }
 }
 
-__global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
-                                                unsigned frameIndex, int final) {
+#ifdef VX_EXP_ATROUS_C
+#define VX_ATROUS_LB __launch_bounds__(256, 6)
+#else
+#define VX_ATROUS_LB __launch_bounds__(256)
+#endif
+__global__ VX_ATROUS_LB void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
+                                      unsigned frameIndex, int final) {
     int tx, ty;
     if (!xcd_tile(a, tx, ty)) return;
     const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);
@@ -918,17 +1065,14 @@ inline dim3 grid1d(const DenoiseArgs &a) { return dim3((unsigned)(((size_t)(a.y1
 
 }  // namespace
 
-hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_world_pos, grid16(a), dim3(256), 0, st, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st) {
-    const int used = 0;
-    (void)used;
-    // parity is baked into a.reservoir by the host
-    hipLaunchKernelGGL(k_firefly, dim3((a.W + 63) / 64, (a.y1 - a.y0 + 3) / 4), dim3(256), 0, st, a, 0);
-    hipLaunchKernelGGL(k_firefly_apply, dim3(64), dim3(256), 0, st, a);
+// world positions over rows [wy0, wy1); with `detect` also the firefly filter over the band (its
+// reservoir parity is baked into a.reservoir by the host); with `apply` the filtered pixels are
+// written back here rather than by the next k_temporal
+hipError_t launch_firefly(const DenoiseArgs &a, int wy0, int wy1, bool detect, bool apply, hipStream_t st) {
+    hipLaunchKernelGGL(k_firefly, dim3((a.W + 63) / 64, (wy1 - wy0 + 3) / 4), dim3(256), 0, st, a, wy0, wy1,
+                       detect ? 1 : 0);
+    if (detect) hipLaunchKernelGGL(k_firefly_filter, dim3(1024), dim3(64), 0, st, a);
+    if (detect && apply) hipLaunchKernelGGL(k_firefly_apply, grid16(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st) {

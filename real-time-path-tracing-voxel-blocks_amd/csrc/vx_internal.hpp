@@ -184,16 +184,21 @@ struct DenoiseArgs {
     // persistent denoiser state
     float4 *ping, *pong, *prevIllum, *prevFast, *output;
     float *histLen, *prevHistLen;
-    // world position of every pixel's primary hit (world_pos of depth), built
-    // once per frame by k_world_pos: the stencil passes read it instead of
-    // re-deriving a camera ray per tap
+    // world position of every pixel's primary hit (world_pos of depth) + 16-bit material, built
+    // once per frame by k_firefly: the stencil passes read it instead of re-deriving a camera
+    // ray per tap
     float4 *wpos;
     // history-fix lists (k_temporal -> k_history_fix), per 16x16 tile of the band's
     // grid: up to 256 pixel indices at tile*256, count in hfCount[tile]
     uint32_t *hfList, *hfCount;
-    // firefly scratch; ffCount[0..3] are zeroed by k_world_pos
+    // firefly lists per 16x16 tile of the band: ffCount[tile] entries at tile*256 (local pixel
+    // index, filtered radiance, replacement reservoir); the consumer resets the count
     uint32_t *ffCount;
     uint32_t *ffIndex;
+    // detected fireflies for k_firefly_filter: {pixel, neighbour weight sum, neighbour count}; the
+    // count is reset by the lists' consumer (k_temporal or k_firefly_apply)
+    uint4 *ffCand;
+    uint32_t *ffCandCount;
     float4 *ffColor;
     Reservoir *ffRes;
     // launch-uniform terms of the temporal pass, computed once on the host with the same IEEE
@@ -290,8 +295,7 @@ hipError_t launch_mesh_occluded(const MeshDev &m, const float *rays, int n, unsi
 hipError_t launch_tri_lights(const float *tri, int nTri, const int *inst, int nInst, V3 radiance, LightInfo *out,
                              float *weight, hipStream_t st);
 
-hipError_t launch_firefly(const DenoiseArgs &a, hipStream_t st);
-hipError_t launch_world_pos(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_firefly(const DenoiseArgs &a, int wy0, int wy1, bool detect, bool apply, hipStream_t st);
 hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st);

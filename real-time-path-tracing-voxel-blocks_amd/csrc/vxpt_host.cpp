@@ -230,7 +230,8 @@ struct vxpt_ctx {
     float4 *ping = nullptr, *pong = nullptr, *prevIllum = nullptr, *prevFast = nullptr, *output = nullptr;
     float *histLen = nullptr, *prevHistLen = nullptr;
     float4 *wpos = nullptr;
-    uint32_t *ffCount = nullptr, *ffIndex = nullptr, *hfList = nullptr, *hfCount = nullptr;
+    uint32_t *ffCount = nullptr, *ffIndex = nullptr, *hfList = nullptr, *hfCount = nullptr, *ffCandCount = nullptr;
+    uint4 *ffCand = nullptr;
     float4 *ffColor = nullptr;
     Reservoir *ffRes = nullptr;
     bool denoiseInputIsAccum = false;
@@ -434,6 +435,7 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.output = c->output;
     a.histLen = c->histLen; a.prevHistLen = c->prevHistLen;
     a.ffCount = c->ffCount; a.ffIndex = c->ffIndex; a.ffColor = c->ffColor; a.ffRes = c->ffRes;
+    a.ffCand = c->ffCand; a.ffCandCount = c->ffCandCount;
     a.hfList = c->hfList; a.hfCount = c->hfCount;
     a.wpos = c->wpos;
     a.invW = 1.0f / (float)c->W; a.invH = 1.0f / (float)c->H;
@@ -717,13 +719,12 @@ hipError_t history_copies(vxpt_ctx *c) {
 }
 
 // world positions for the band and kWposHalo rows either side (the widest
-// stencil, HistoryFix at 2 x 17 rows, reads them there)
+// stencil, HistoryFix at 2 x 17 rows, reads them there), in the firefly pass's
+// launch (`detect`: the filter over the band; `apply`: write the filtered pixels
+// back in this launch rather than in the next k_temporal)
 constexpr int kWposHalo = 40;
-hipError_t world_pos_band(const DenoiseArgs &a, hipStream_t st) {
-    DenoiseArgs e = a;
-    e.y0 = std::max(0, a.y0 - kWposHalo);
-    e.y1 = std::min(a.H, a.y1 + kWposHalo);
-    return launch_world_pos(e, st);
+hipError_t firefly_band(const DenoiseArgs &a, bool detect, bool apply, hipStream_t st) {
+    return launch_firefly(a, std::max(0, a.y0 - kWposHalo), std::min(a.H, a.y1 + kWposHalo), detect, apply, st);
 }
 
 int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) {
@@ -732,8 +733,9 @@ int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) 
     DenoiseArgs a{};
     fill_denoise(c, p, a, used & 1);
     HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
-    HIPCHK(c, world_pos_band(a, c->stream));
-    if (p->enable_firefly_filter) HIPCHK(c, launch_firefly(a, c->stream));
+    // the temporal pass applies the firefly lists when it runs
+    const bool ffFold = p->enable_temporal_accumulation && frameNum > 0;
+    HIPCHK(c, firefly_band(a, p->enable_firefly_filter, !ffFold, c->stream));
     if (frameNum == 0) HIPCHK(c, launch_frame0_init(a, c->stream));
     int fin = 0;  // 0 illum, 1 ping, 2 pong, 3 prevIllum
     if (p->enable_temporal_accumulation && frameNum > 0) {
@@ -775,7 +777,7 @@ int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int a
     DenoiseArgs a{};
     fill_denoise(c, p, a, pass == 0 ? (arg & 1) : 0);
     switch (pass) {
-        case 0: HIPCHK(c, launch_firefly(a, c->stream)); break;
+        case 0: HIPCHK(c, firefly_band(a, true, true, c->stream)); break;  // + world positions
         case 2: HIPCHK(c, launch_temporal(a, c->stream)); break;
         case 3: HIPCHK(c, launch_history_fix(a, c->stream)); break;
         case 4: HIPCHK(c, launch_history_clamp(a, c->stream)); break;
@@ -783,7 +785,7 @@ int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int a
         case 6: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
         case 7: HIPCHK(c, launch_atrous(a, a.pong, a.ping, (unsigned)arg, (unsigned)arg2, false, c->stream)); break;
         case 10: HIPCHK(c, launch_atrous(a, a.ping, a.pong, (unsigned)arg, (unsigned)arg2, true, c->stream)); break;
-        case 11: HIPCHK(c, world_pos_band(a, c->stream)); break;
+        case 11: HIPCHK(c, firefly_band(a, false, false, c->stream)); break;
         case 12: HIPCHK(c, launch_frame0_init(a, c->stream)); break;
         case 13: {
             const float4 *src = arg == 1 ? a.ping : (arg == 2 ? a.pong : (arg == 3 ? a.prevIllum : a.illum));
@@ -939,8 +941,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     }
     const int it = it0 + spp, used = it > 0 ? it - 1 : 0;
-    FOR_BANDS(run_pass(c, p, 11, 0, 0));
-    if (p->enable_firefly_filter) {
+    if (!p->enable_firefly_filter) FOR_BANDS(run_pass(c, p, 11, 0, 0));
+    if (p->enable_firefly_filter) {  // + world positions
         FOR_BANDS(run_pass(c, p, 0, used & 1, 0));
         BANDCHK(exchange_set(cs, {{(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, kTraceHalo}, {VXPT_BUF_ILLUM, 2}}));
     }
@@ -1033,8 +1035,11 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(c, hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->dev));
-    for (auto &e : c->ev) HIPCHK(c, hipEventCreate(&e));
+    // timing markers only (every read of them follows a stream synchronisation): no system-scope
+    // fence, so a marker neither writes back / invalidates the L2 nor delays the next kernel
+    for (auto &e : c->ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     const size_t n = (size_t)c->W * c->H;
+    const size_t tiles16 = (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16);  // denoiser tiles
     for (auto &g : c->gb) {
         if (dalloc(c, g.normalRough, n) || dalloc(c, g.geoNormalThin, n) || dalloc(c, g.albedo, n) ||
             dalloc(c, g.matParam, n) || dalloc(c, g.depth, n) || dalloc(c, g.material, n))
@@ -1043,9 +1048,10 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (dalloc(c, c->illum, n) || dalloc(c, c->accum, n) || dalloc(c, c->motion, n) || dalloc(c, c->res, 2 * n) ||
         dalloc(c, c->ping, n) || dalloc(c, c->pong, n) || dalloc(c, c->prevIllum, n) || dalloc(c, c->prevFast, n) ||
         dalloc(c, c->output, n) || dalloc(c, c->histLen, n) || dalloc(c, c->prevHistLen, n) ||
-        dalloc(c, c->ffCount, 4) || dalloc(c, c->wpos, n) || dalloc(c, c->ffIndex, n) || dalloc(c, c->ffColor, n) || dalloc(c, c->ffRes, n) ||
-        dalloc(c, c->hfList, (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16) * 256) ||
-        dalloc(c, c->hfCount, (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16)))
+        dalloc(c, c->wpos, n) || dalloc(c, c->ffCount, tiles16) || dalloc(c, c->ffIndex, tiles16 * 256) ||
+        dalloc(c, c->ffColor, tiles16 * 256) || dalloc(c, c->ffRes, tiles16 * 256) ||
+        dalloc(c, c->ffCand, tiles16 * 256) || dalloc(c, c->ffCandCount, 1) ||
+        dalloc(c, c->hfList, tiles16 * 256) || dalloc(c, c->hfCount, tiles16))
         return VXPT_ERR_HIP;
     {   // wavefront trace state: one slot per pixel (8x8 tiles), 4 visibility rays per slot
         const size_t ns = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64;

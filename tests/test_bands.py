@@ -56,11 +56,14 @@ def test_band_rows_and_plan():
 def test_frame_ops_cover_every_pass():
     ops = list(bands.frame_ops(1, 4, P))
     passes = [o[1] for o in ops if o[0] == "pass"]
-    assert passes == [11, 0, 2, 3, 4, 5, 6, 7, 10, 14]
+    # pass 0 (firefly) writes the world-position plane too; pass 11 alone when the filter is off
+    assert passes == [0, 2, 3, 4, 5, 6, 7, 10, 14]
     assert sum(1 for o in ops if o[0] == "trace") == 4
     assert [o[2] for o in ops if o[0] == "trace"] == [2 | 4 | 1024, 2 | 1024, 2 | 1024, 2 | 1024]
     first = list(bands.frame_ops(0, 1, P))
-    assert [o[1] for o in first if o[0] == "pass"] == [11, 0, 12, 5, 6, 7, 10, 14]
+    assert [o[1] for o in first if o[0] == "pass"] == [0, 12, 5, 6, 7, 10, 14]
+    nofire = list(bands.frame_ops(1, 1, dict(P, firefly=False)))
+    assert [o[1] for o in nofire if o[0] == "pass"] == [11, 2, 3, 4, 5, 6, 7, 10, 14]
 
 
 def test_oracle_bands_in_process():
