@@ -343,8 +343,9 @@ void pass_temporal(const Scene &s, Frame &f, const DenoiseParams &p) {
             int ox = (int)std::floor(ppf.x - 0.5f), oy = (int)std::floor(ppf.y - 0.5f);
             float pixelSize = cam.pixel_world_size_scale() * z;
             float frustum = pixelSize * (float)(W < H ? W : H);
-            double slope = 1.0 / (double)lerpf(lerpf(0.05f, 1.0f, NoV), 1.0f, saturate(parMax / 30.0f));
-            float t0 = saturate((float)((double)thr * slope)) * frustum;
+            // TemporalAccumulation.h:82-83: `float disocclusionThresholdSlopeScale = 1.0 / lerp(...)`
+            float slope = (float)(1.0 / (double)lerpf(lerpf(0.05f, 1.0f, NoV), 1.0f, saturate(parMax / 30.0f)));
+            float t0 = saturate(thr * slope) * frustum;
             F4 thr4(t0);
             {  // IsInScreenBilinear with the Float4 quirk (DenoiserCommon.h:82-104)
                 float r[4] = {ox >= 0 ? 1.f : 0.f, oy >= 0 ? 1.f : 0.f, ox + 1 >= 0 ? 1.f : 0.f, oy + 1 >= 0 ? 1.f : 0.f};

@@ -466,8 +466,10 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const f
     const V2 ppf(prevUV.x * (float)W, prevUV.y * (float)H);
     const int ox = (int)floorf(ppf.x - 0.5f), oy = (int)floorf(ppf.y - 0.5f);
     const float frustum = (a.frustumK * z) * (float)(W < H ? W : H);
-    const double slope = 1.0 / (double)lerpf(lerpf(0.05f, 1.0f, NoV), 1.0f, saturate(parMax / 30.0f));
-    const float t0 = saturate((float)((double)thr * slope)) * frustum;
+    // TemporalAccumulation.h:82-83: the slope scale is a float (its double quotient rounded to float
+    // equals the float quotient: double rounding is innocuous for a division)
+    const float slope = 1.0f / lerpf(lerpf(0.05f, 1.0f, NoV), 1.0f, saturate(parMax / 30.0f));
+    const float t0 = saturate(thr * slope) * frustum;
     V4 thr4(t0);
     {
         float r[4] = {ox >= 0 ? 1.f : 0.f, oy >= 0 ? 1.f : 0.f, ox + 1 >= 0 ? 1.f : 0.f, oy + 1 >= 0 ? 1.f : 0.f};
@@ -545,12 +547,10 @@ VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const f
 // = k's; no atomics, and the history-fix launch only works on listed pixels.
 // The tile's firefly list (k_firefly) is applied first: its entries go back to the radiance and
 // reservoir planes, and the filtered values of the tile's own pixels are handed over in LDS.
-#ifdef VX_EXP_TEMPORAL_LB5
-#define VX_TEMPORAL_LB __launch_bounds__(256, 5)
-#else
-#define VX_TEMPORAL_LB __launch_bounds__(256)
-#endif
-__global__ VX_TEMPORAL_LB void k_temporal(DenoiseArgs a, Qt rot) {
+// 123 VGPRs (4 waves/SIMD); bounding it to 5 waves spills 80-116 B/lane and was slower (89 -> 105 us),
+// and fetching the pixel's inputs before the depth test or the history taps with the depth taps
+// raised it to 130 (3 waves: 100-103 us)
+__global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
     __shared__ unsigned sTot[4], sFFn, sFFmask[8];
     __shared__ float4 sFF[256];
     const int tx = blockIdx.x, ty = blockIdx.y;
@@ -690,7 +690,8 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
 __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
     const int W = a.W, H = a.H;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int x0 = blockIdx.x * 16, y0 = a.y0 + blockIdx.y * 16;
+    const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
+    const int x0 = btx * 16, y0 = a.y0 + bty * 16;
     const int x = x0 + tx, y = y0 + ty;
     __shared__ float sY[3][400], sR[3][400];
     for (int k = threadIdx.x; k < 400; k += 256) {
@@ -779,7 +780,8 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
 __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
     const int W = a.W, H = a.H;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int x0 = blockIdx.x * 16, y0 = a.y0 + blockIdx.y * 16;
+    const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
+    const int x0 = btx * 16, y0 = a.y0 + bty * 16;
     const int x = x0 + tx, y = y0 + ty;
     __shared__ float4 sI[400];
     __shared__ float sNx[400], sNy[400], sNz[400], sM[400], sPx[400], sPy[400], sPz[400];
@@ -937,9 +939,7 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
             const int px = x + ofx + xx * (int)step, py = y + ofy + yy * (int)step;
             tP[k] = src.wpos(px, py, W);
             tN[k] = src.nrm(px, py, W);
-#ifndef VX_EXP_ATROUS_B
             tV[k] = src.val(px, py, W);
-#endif
         }
     }
     const V4 cP = src.wpos(x, y, W);
@@ -975,11 +975,7 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
         float w = geo * nw;
         w *= (float)(sMat == cMat);
         if (w > 1e-4f) {
-#ifdef VX_EXP_ATROUS_B
-            const V4 sv = src.val(px, py, W);
-#else
             const V4 sv = Src::kBatch ? tV[k] : src.val(px, py, W);
-#endif
             float lw = fabsf(cLum - luminance_fast(sv.xyz())) * phiInv;
             lw = fminf(INFINITY, lw);
             w *= __expf(-lw);
@@ -995,12 +991,7 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
     }
 }
 
-#ifdef VX_EXP_ATROUS_C
-#define VX_ATROUS_LB __launch_bounds__(256, 6)
-#else
-#define VX_ATROUS_LB __launch_bounds__(256)
-#endif
-__global__ VX_ATROUS_LB void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
+__global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
                                       unsigned frameIndex, int final) {
     int tx, ty;
     if (!xcd_tile(a, tx, ty)) return;

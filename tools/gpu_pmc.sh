@@ -1,11 +1,15 @@
 #!/bin/bash
 # PMC passes (each counter group in its own rocprofv3 run, no trace domains) + kernel trace,
-# steady-state frames.  Usage: tools/gpu_pmc.sh TAG   -> gpurun_out/TAG_*.{db,json}
+# steady-state frames, and the FETCH_SIZE / WRITE_SIZE calibration per access width.
+# Usage: tools/gpu_pmc.sh TAG   -> gpurun_out/TAG_*.{db,json,txt}
 TAG=${1:-pmc}
 export TMPDIR=/tmp
 cd /tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 ARGS="--warmup 8 --steps 4 --no-cpu-baseline"
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -f csv rocpd -d gpurun_out/${TAG}_cfetch -o run -- ./tools/calib/pmc_calib > gpurun_out/${TAG}_cfetch.log 2>&1 || { echo "calib fetch failed"; exit 1; }
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -f csv rocpd -d gpurun_out/${TAG}_cwrite -o run -- ./tools/calib/pmc_calib > gpurun_out/${TAG}_cwrite.log 2>&1 || { echo "calib write failed"; exit 1; }
+python tools/pmc_calib.py gpurun_out/${TAG}_cfetch/run_results.db gpurun_out/${TAG}_cwrite/run_results.db gpurun_out/${TAG}_pmc_calib.json
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv rocpd -d gpurun_out/${TAG}_kt -o run -- python bench.py $ARGS > gpurun_out/${TAG}_kt.log 2>&1 || { echo "kernel-trace pass failed"; exit 1; }
 echo kt ok
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -f csv rocpd -d gpurun_out/${TAG}_fetch -o run -- python bench.py $ARGS > gpurun_out/${TAG}_fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
@@ -14,6 +18,6 @@ timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -f csv rocpd -d gpurun_out/${TAG}_w
 echo write ok
 timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES -f csv rocpd -d gpurun_out/${TAG}_sq -o run -- python bench.py $ARGS > gpurun_out/${TAG}_sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
 echo sq ok
-python tools/pmc_traffic.py gpurun_out/${TAG}_fetch/run_results.db gpurun_out/${TAG}_write/run_results.db gpurun_out/${TAG}_kt/run_results.db 4 gpurun_out/${TAG}_pmc_denoise.json
+python tools/pmc_traffic.py gpurun_out/${TAG}_fetch/run_results.db gpurun_out/${TAG}_write/run_results.db gpurun_out/${TAG}_kt/run_results.db 4 gpurun_out/${TAG}_pmc_denoise.json gpurun_out/${TAG}_pmc_calib.json
 python tools/pmcsum.py gpurun_out/${TAG}_sq/run_results.db gpurun_out/${TAG}_fetch/run_results.db gpurun_out/${TAG}_write/run_results.db > gpurun_out/${TAG}_pmc.txt
 python tools/profsum.py gpurun_out/${TAG}_kt/run_results.db > gpurun_out/${TAG}_kernel_stats.txt
