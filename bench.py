@@ -54,7 +54,7 @@ def native_oracle():
     try:
         os.makedirs(out_dir, exist_ok=True)
         srcs = [os.path.join(src, f) for f in ("orc_scene.cpp", "orc_sky.cpp", "orc_trace.cpp", "orc_denoise.cpp",
-                                               "orc_post.cpp", "orc_lights.cpp", "orc_api.cpp")]
+                                               "orc_post.cpp", "orc_lights.cpp", "orc_mesh.cpp", "orc_api.cpp")]
         subprocess.run(["g++", "-O3", "-march=native", "-fopenmp", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
                         "-std=c++17", "-shared", "-o", lib] + srcs, check=True, timeout=120,
                        stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)

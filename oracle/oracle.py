@@ -81,6 +81,8 @@ def lib():
             "orc_oct_decode": (None, [ctypes.c_uint32, P]),
             "orc_tri_lights": (None, [P, I, P, I, P, P, P]),
             "orc_mesh_probe": (None, [P, P, P, P, I, P, I, I, P, P]),
+            "orc_set_material_flags": (None, [P, I, I, I, I, F]),
+            "orc_set_meshes": (None, [P, P, P, P, P, I, P, I, P, I, P, P, P]),
         }
         for k, (r, a) in sig.items():
             fn = getattr(L, k)
@@ -124,6 +126,68 @@ class Oracle:
             al = m.get("albedo", (1.0, 1.0, 1.0))
             self.L.orc_set_material(self.h, b, al[0], al[1], al[2], m.get("roughness", 0.8),
                                     int(m.get("metallic", 0)), m.get("translucency", 0.0), m.get("material_id", b - 1))
+
+    def set_material(self, block, albedo=(1.0, 1.0, 1.0), roughness=0.5, metallic=0, translucency=0.0,
+                     material_id=0, emissive=False, thin=False, world_grid=False, uv_scale=1.0):
+        """One block's MaterialParameter (any block id < 32; for an emissive block `albedo` is its
+        radiance, MaterialManager.cpp:162-167)."""
+        self.L.orc_set_material(self.h, block, albedo[0], albedo[1], albedo[2], roughness, int(metallic),
+                                translucency, material_id)
+        self.L.orc_set_material_flags(self.h, block, int(emissive), int(thin), int(world_grid), float(uv_scale))
+
+    def set_meshes(self, models, blocks, rows=None):
+        """The world's instanced meshes.  models: {block: (pos [T,3,3], uv [T,3,2])};
+        blocks: {block: dict(instanced, light_base, emissive, radiance)}; rows: instance rows
+        (object, id, x, y, z), collected from this oracle's voxels when None.  The light records
+        are generated in the library's order (emissive objects by object id, each instance's
+        triangles in a row) and their alias table built as AliasTable::update does."""
+        if rows is None:
+            rows = collect_instances(self.voxels(), self.chunks, blocks)
+        rows = np.asarray(rows, np.int32).reshape(-1, 5)
+        pos, uv, off, cnt = [], [], np.zeros(32, np.int32), np.zeros(32, np.int32)
+        acc = 0
+        for b in range(32):
+            if b in models and len(models[b][0]):
+                p_, u_ = models[b]
+                off[b], cnt[b] = acc, len(p_)
+                pos.append(np.asarray(p_, np.float32).reshape(-1, 9))
+                uv.append(np.asarray(u_, np.float32).reshape(-1, 6))
+                acc += len(p_)
+        pos = np.ascontiguousarray(np.concatenate(pos) if pos else np.zeros((1, 9), np.float32))
+        uv = np.ascontiguousarray(np.concatenate(uv) if uv else np.zeros((1, 6), np.float32))
+        inst = np.zeros((len(rows), 5), np.int32)
+        recs, ws, nl = [], [], 0
+        k = 0
+        while k < len(rows):
+            obj = int(rows[k, 0])
+            e = k
+            while e < len(rows) and rows[e, 0] == obj:
+                e += 1
+            b = obj + 1
+            bd = blocks.get(b, {})
+            t = cnt[b]
+            for i in range(k, e):
+                inst[i] = (b, rows[i, 2], rows[i, 3], rows[i, 4], -1)
+            if bd.get("emissive") and t > 0:
+                r, w = tri_lights(models[b][0], rows[k:e, 2:5], bd.get("radiance", (0.0, 0.0, 0.0)))
+                for i in range(k, e):
+                    inst[i, 4] = nl + (i - k) * t
+                recs.append(r)
+                ws.append(w)
+                nl += t * (e - k)
+            k = e
+        lights = np.ascontiguousarray(np.concatenate(recs) if recs else np.zeros((1, 8), np.uint32))
+        if nl:
+            q, pr, al, _ = alias_table(np.concatenate(ws))
+        else:
+            q, pr, al = np.zeros(1, np.float32), np.zeros(1, np.float32), np.zeros(1, np.int32)
+        q, pr, al = (np.ascontiguousarray(q, np.float32), np.ascontiguousarray(pr, np.float32),
+                     np.ascontiguousarray(al, np.int32))
+        inst = np.ascontiguousarray(inst)
+        self.L.orc_set_meshes(self.h, _p(pos), _p(uv), _p(off), _p(cnt), acc, _p(inst), len(inst), _p(lights), nl,
+                              _p(q), _p(pr), _p(al))
+        self._mesh_keep = (pos, uv, off, cnt, inst, lights, q, pr, al)
+        return inst
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -178,6 +178,38 @@ void orc_set_material_textures(void *p, int blockId, int albedo, int normal, int
     m.uvScale = uvScale;
     m.worldGridUV = worldGrid != 0;
 }
+// emissive / thin-film flags and the world-grid uv set-up of a block's material (instanced
+// meshes: lantern light, leaves, lantern base); for an emissive block the albedo is its radiance
+// (MaterialManager.cpp:162-167)
+void orc_set_material_flags(void *p, int blockId, int emissive, int thin, int worldGrid, float uvScale) {
+    Material &m = static_cast<Ctx *>(p)->s.mats[blockId];
+    m.isEmissive = emissive != 0;
+    m.isThinfilm = thin != 0;
+    m.worldGridUV = worldGrid != 0;
+    m.uvScale = uvScale;
+}
+// The world's instanced meshes: triangles (9 floats) and texcoords (6 floats) per block type,
+// concatenated, with per-block offsets / counts (32 entries); instance rows of 5 ints
+// (block, x, y, z, first light or -1); light records (8 u32 each) and their alias table.
+void orc_set_meshes(void *p, const float *pos, const float *uv, const int *triOff, const int *triCnt, int nTri,
+                    const int *inst, int nInst, const uint32_t *lights, int nLights, const float *aliasQ,
+                    const float *aliasP, const int *aliasA) {
+    MeshSet &m = static_cast<Ctx *>(p)->s.mesh;
+    m.pos.assign(pos, pos + (size_t)nTri * 9);
+    m.uv.assign(uv, uv + (size_t)nTri * 6);
+    for (int b = 0; b < 32; ++b) { m.triOff[b] = triOff[b]; m.triCnt[b] = triCnt[b]; }
+    m.inst.resize(nInst);
+    for (int i = 0; i < nInst; ++i) {
+        const int *r = inst + (size_t)i * 5;
+        m.inst[i].block = r[0];
+        m.inst[i].cell = F3((float)r[1], (float)r[2], (float)r[3]);
+        m.inst[i].lightBase = r[4];
+    }
+    m.numLights = nLights;
+    m.lights.assign(lights, lights + (size_t)nLights * 8);
+    m.lightAlias.resize(nLights);
+    for (int i = 0; i < nLights; ++i) m.lightAlias[i] = AliasBin{aliasQ[i], aliasP[i], aliasA[i]};
+}
 // rows [y0, y1) the denoiser passes compute (multi-GPU band schedule; 0,0 = whole frame)
 void orc_set_band(void *p, int y0, int y1) {
     Frame &f = static_cast<Ctx *>(p)->f;

@@ -5,6 +5,7 @@
 #include "orc_trace.h"
 
 #include <cmath>
+#include <utility>
 
 namespace orc {
 
@@ -261,9 +262,33 @@ LightSample sky_sample(const Scene &s, int idx) {  // Restir.h:256-283
     return ls;
 }
 
+// TriangleLight::calcSample (Light.h:54-82): SampleTriangle (LinearMath.h:2048-2056), PdfAtoW
+LightSample tri_sample(const TriLight &t, F2 uv, const F3 &viewer) {
+    const float sx = std::sqrt(uv.x);
+    const F3 bary(1.0f - sx, sx * (1.0f - uv.y), sx * uv.y);
+    LightSample r;
+    r.position = t.base + t.edge1 * bary.y + t.edge2 * bary.z;
+    F3 L = r.position - viewer;
+    const float Ld = length(L);
+    L /= Ld;
+    const float areaPdf = 1.0f / t.area;
+    const float cosT = saturate(dot(L, -t.normal));
+    r.solidAnglePdf = areaPdf * (Ld * Ld) / cosT;
+    r.radiance = t.radiance;
+    r.type = LtLocal;
+    return r;
+}
+F2 inverse_tri_sample(float u, float v) {  // InverseTriangleSample (LinearMath.h:2059-2064)
+    const F3 b(1.0f - u - v, u, v);
+    const float sx = 1 - b.x;
+    return F2(sx * sx, b.z / sx);
+}
+// the direction a light sample is seen in from p (closesthit.cu:610, 738, 794, 829)
+F3 light_dir(const LightSample &ls, const F3 &p) { return ls.type == LtLocal ? normalize(ls.position - p) : ls.position; }
+
 float target_pdf(const LightSample &ls, const Surf &sf) {  // Restir.h:194-211
     if (ls.solidAnglePdf <= 0 || ls.type == LtInvalid) return 0.0f;
-    F3 wi = ls.position;
+    F3 wi = light_dir(ls, sf.pos);
     F3 fr; float pdf;
     disney_eval(sf.st.normal, sf.st.geoNormal, wi, sf.st.wo, sf.st.albedo, sf.st.metallic, sf.st.translucency,
                 sf.st.roughness, fr, pdf);
@@ -281,8 +306,13 @@ float brdf_pdf(const Surf &sf, const F3 &wi) {
 float mis_weight(const Surf &sf, const LightSample &ls, float selPdf, float lightMis, bool env, float brdfMis) {
     float sa = ls.solidAnglePdf;  // Restir.h:286-328, brdfCutoff == 0
     if (brdfMis == 0.0f || sa <= 0.0f || std::isinf(sa) || std::isnan(sa)) return lightMis * selPdf;
-    F3 dir = ls.position;  // sky/sun only on this path
-    float bp = brdf_pdf(sf, dir);
+    F3 dir = ls.position;
+    if (ls.type == LtLocal) {
+        const F3 toLight = ls.position - sf.pos;
+        const float dist = length(toLight);
+        dir = toLight / dist;
+    }
+    float bp = brdf_pdf(sf, dir);  // brdfCutoff 0: the distance test never drops it
     (void)env;
     float src = selPdf * sa;
     float blended = lightMis * src + brdfMis * bp;
@@ -314,7 +344,8 @@ void finalize(Reservoir &r, float num, float den) {
     r.weightSum = (d == 0.0f) ? 0.0f : (r.weightSum * num) / d;
 }
 
-bool light_from_reservoir(const Scene &s, LightSample &ls, const Reservoir &r) {  // Restir.h:383-415
+bool light_from_reservoir(const Scene &s, LightSample &ls, const Reservoir &r, const Surf &sf,
+                          bool hasLocal) {  // Restir.h:383-415
     uint32_t li = r.lightData & kIndexMask;
     F2 uv = F2((float)(r.uvData & 0xffff), (float)(r.uvData >> 16)) / float(0xffff);
     const Sky &k = s.sky;
@@ -324,6 +355,9 @@ bool light_from_reservoir(const Scene &s, LightSample &ls, const Reservoir &r) {
     } else if (li == kSunLight) {
         int x = clampi(int(uv.x * k.sunW), 0, k.sunW - 1), y = clampi(int(uv.y * k.sunH), 0, k.sunH - 1);
         ls = sun_sample(s, y * k.sunW + x);
+    } else if (hasLocal && li < (uint32_t)s.mesh.numLights) {
+        ls = tri_sample(tri_light(s.mesh, (int)li), uv, sf.pos);
+        return true;
     }
     return li < kInvalidLight;
 }
@@ -374,6 +408,32 @@ void store_reservoir(Px &c, const Reservoir &r) {
 Reservoir load_prev_reservoir(Px &c, int x, int y) {
     size_t p = (size_t)x + (size_t)y * c.f.W + (size_t)((c.it + 1) % 2) * c.f.W * c.f.H;
     return c.f.reservoir[p];
+}
+
+// Closest hit over the voxel faces and the instanced meshes (one IAS in the reference): a mesh
+// hit replaces the voxel hit only when strictly closer (ties go to the voxel face).
+struct AnyHit { Hit vox; MeshHit mesh; bool isMesh = false, hit = false; float t = kRayMax; };
+AnyHit closest_any(const Scene &s, const F3 &o, const F3 &d, float tmax) {
+    AnyHit a;
+    a.vox = dda_closest(s.world, o, d, tmax);
+    a.hit = a.vox.hit;
+    a.t = a.vox.hit ? a.vox.t : kRayMax;
+    if (!s.mesh.inst.empty()) {
+        const MeshHit m = mesh_closest_hit(s.mesh, o, d, a.vox.hit ? a.vox.t : tmax);
+        if (m.hit && (!a.vox.hit || m.t < a.vox.t)) { a.mesh = m; a.isMesh = true; a.hit = true; a.t = m.t; }
+    }
+    return a;
+}
+// visibility (mask 0xFE: every voxel face and every mesh triangle, either side)
+bool occluded_any(const Scene &s, const F3 &o, const F3 &d, float tmin, float tmax) {
+    if (dda_occluded(s.world, o, d, tmin, tmax)) return true;
+    return !s.mesh.inst.empty() && mesh_any_hit(s.mesh, o, d, tmin, tmax);
+}
+// a visibility ray toward a light sample (closesthit.cu:606-633): local lights stop 0.01 short
+bool light_occluded(const Scene &s, const F3 &org, const LightSample &ls, const F3 &p, float extra) {
+    const F3 sd = light_dir(ls, p);
+    const float tmax = ls.type == LtLocal ? length(ls.position - p) - 0.01f - extra : kRayMax;
+    return occluded_any(s, org, sd, extra, tmax);
 }
 
 void on_miss(Px &c, Ray &rd) {  // miss.cu:9-82
@@ -468,38 +528,66 @@ float ray_cone_spread(const Camera &cam, int px, int py) {
     return std::atan(std::sqrt(pF.x * pF.x + pF.y * pF.y)) - std::atan(std::sqrt(pN.x * pN.x + pN.y * pN.y));
 }
 
-void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
+void on_hit(Px &c, Ray &rd, const AnyHit &ah) {  // closesthit.cu:10-852
     const Scene &s = c.s;
     Frame &f = c.f;
     const size_t pi = c.idx();
-    rd.distance = h.t;
-    // hit point on the face plane (OptiX barycentric reconstruction is not reproducible)
-    F3 hp = rd.pos + rd.wi * h.t;
-    {
+    rd.distance = ah.t;
+    F3 frontPos, backPos, geoNormal;
+    int block;
+    if (!ah.isMesh) {
+        const Hit &h = ah.vox;
+        // hit point on the face plane (OptiX barycentric reconstruction is not reproducible)
+        F3 hp = rd.pos + rd.wi * h.t;
         const int axis = (h.face < 2) ? 1 : (h.face < 4 ? 0 : 2);
         const int cell = axis == 0 ? h.x : (axis == 1 ? h.y : h.z);
         const bool high = (h.face == 0 || h.face == 3 || h.face == 4);
         hp[axis] = (float)(cell + (high ? 1 : 0));
+        safe_spawn(h, hp, frontPos, backPos, geoNormal);
+        block = h.id;
+    } else {
+        mesh_spawn(s.mesh, ah.mesh, frontPos, backPos, geoNormal);
+        block = s.mesh.inst[ah.mesh.row].block;
     }
-    F3 frontPos, backPos, geoNormal;
-    safe_spawn(h, hp, frontPos, backPos, geoNormal);
     F3 motionWS = frontPos - frontPos;  // static geometry
     if (rd.depth == 0) f.motion[pi] = F4(motionWS, 0.0f);
     rd.pos = frontPos;
-    const Material &m = s.mats[h.id];
+    bool hitFront = dot(rd.wo, geoNormal) > 0.0f;
+    const Material &m = s.mats[block];
+    if (m.isEmissive) {  // closesthit.cu:107-122
+        if (!rd.hitFirstDiffuse) {
+            rd.radiance = m.albedo;
+            if (rd.depth == 0) {
+                f.albedo[pi] = F4(1.0f);
+                f.material[pi] = (float)0xFFFF;
+                f.normalRough[pi] = F4(0.0f, -1.0f, 0.0f, 0.0f);
+                f.geoNormalThin[pi] = F4(0.0f, -1.0f, 0.0f, 0.0f);
+                f.matParam[pi] = F4(0.0f);
+            }
+        }
+        rd.terminate = true;
+        return;
+    }
+    if (m.isThinfilm && !hitFront) {  // closesthit.cu:124-133: the normal faces the incoming ray
+        geoNormal = -geoNormal;
+        hitFront = true;
+        std::swap(frontPos, backPos);
+    }
     State st;
     st.geoNormal = geoNormal;
     st.wo = rd.wo;
     st.metallic = m.metallic;
     if (!s.textures.empty()) {  // closesthit.cu:167-254
-        rd.travelled += h.t;
+        rd.travelled += ah.t;
         const float cone = ray_cone_spread(s.cam, c.px, c.py) * rd.travelled;
         F2 tc(0.0f, 0.0f);
-        const F3 p = frontPos;
+        const F3 p = rd.pos;  // the front position before the thin-film swap
         if (m.worldGridUV) {
             if (std::fabs(geoNormal.x) > 0.9f) tc = F2(std::fmod(p.z, m.uvScale), std::fmod(p.y, m.uvScale));
             else if (std::fabs(geoNormal.y) > 0.9f) tc = F2(std::fmod(p.x, m.uvScale), std::fmod(p.z, m.uvScale));
             else if (std::fabs(geoNormal.z) > 0.9f) tc = F2(std::fmod(p.x, m.uvScale), std::fmod(p.y, m.uvScale));
+        } else if (ah.isMesh) {
+            tc = mesh_texcoord(s.mesh, ah.mesh);
         }
         tc = tc / m.uvScale;
         const float mip0 = std::sqrt(1024.0f * 1024.0f + 1024.0f * 1024.0f);
@@ -546,7 +634,7 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
     disney_sample(u4, st.normal, st.geoNormal, st.wo, st.albedo, st.metallic, st.translucency, st.roughness, sWi, sBop,
                   sPdf, trans);
     if (sPdf <= 0.0f) rd.terminate = true;
-    rd.pos = frontPos;
+    rd.pos = m.isThinfilm ? (dot(sWi, st.normal) > 0.0f ? frontPos : backPos) : frontPos;  // closesthit.cu:288
     rd.wi = sWi;
     rd.bsdfOverPdf = sBop;
     rd.pdf = sPdf;
@@ -572,13 +660,28 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
     LightSample lightSample;
     Reservoir ris;
     const bool skipSun = !sf.thin && (dot(st.normal, k.sunDir) < 0.0f || dot(st.geoNormal, k.sunDir) < 0.0f);
-    const int nLocal = 0, nSun = skipSun ? 0 : 1, nSky = 1, nBrdf = 1;
+    const int nLocal = s.mesh.numLights > 0 ? 8 : 0, nSun = skipSun ? 0 : 1, nSky = 1, nBrdf = 1;
+    // a ray leaving the surface toward `dir` starts on the side it leaves from (thin films,
+    // closesthit.cu:457, 614, 799)
+    auto spawn = [&](const F3 &dir) { return sf.thin ? (dot(dir, st.normal) > 0.0f ? frontPos : backPos) : frontPos; };
     const int nMis = nLocal + nSun + nSky + nBrdf;
     const float sunMis = float(nSun) / nMis, skyMis = float(nSky) / nMis, brdfMis = float(nBrdf) / nMis;
     const float localMis = float(nLocal) / nMis;
 
     Reservoir localRes;
     LightSample localSample;
+    for (int i = 0; i < nLocal; ++i) {  // closesthit.cu:350-376
+        float srcPdf;
+        const int li = (int)alias_sample(s.mesh.lightAlias, c.rnd(), srcPdf);
+        if (li >= s.mesh.numLights) continue;
+        const F2 uv = c.rnd2();
+        const LightSample cand = tri_sample(tri_light(s.mesh, li), uv, sf.pos);
+        const float blended = mis_weight(sf, cand, srcPdf, localMis, false, brdfMis);
+        const float tp = target_pdf(cand, sf);
+        const float rr = c.rnd();
+        if (blended != 0.0f)
+            if (stream_sample(localRes, (uint32_t)li, uv, rr, tp, 1.0f / blended)) localSample = cand;
+    }
     finalize(localRes, 1.0f, (float)nMis);
     localRes.M = 1;
 
@@ -629,8 +732,20 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
         disney_sample(u, st.normal, st.geoNormal, st.wo, st.albedo, st.metallic, st.translucency, st.roughness, sd,
                       bop, bp, tr);
         if (bp > 0.0f) {
-            Hit bh = dda_closest(s.world, frontPos, sd, FLT_MAX);
-            if (!bh.hit) {
+            const AnyHit bh = closest_any(s, spawn(sd), sd, FLT_MAX);
+            if (bh.isMesh && nLocal > 0) {  // __closesthit__bsdf_light (closesthit.cu:854-900)
+                const MeshInstance &mi = s.mesh.inst[bh.mesh.row];
+                if (s.mats[mi.block].isEmissive && mi.lightBase >= 0) {
+                    li = (uint32_t)(mi.lightBase + bh.mesh.tri);
+                    if (li >= (uint32_t)s.mesh.numLights) {
+                        li = kInvalidLight;
+                    } else {
+                        uv = inverse_tri_sample(bh.mesh.u, bh.mesh.v);
+                        cand = tri_sample(tri_light(s.mesh, (int)li), uv, sf.pos);
+                        lightSrcPdf = s.mesh.lightAlias[li].p;
+                    }
+                }
+            } else if (!bh.hit) {
                 if (equal_area_cone_uv(uv, k.sunDir, sd, kSunCosMax())) {
                     li = kSunLight;
                     int x = (int)(uv.x * k.sunW - 0.5f), y = (int)(uv.y * k.sunH - 0.5f);
@@ -680,7 +795,7 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
 
     bool visible = false;
     if (lightSample.type != LtInvalid && ris.lightData != 0) {
-        visible = !dda_occluded(s.world, frontPos, lightSample.position, 0.0f, kRayMax);
+        visible = !light_occluded(s, spawn(light_dir(lightSample, sf.pos)), lightSample, sf.pos, 0.0f);
         if (!visible) { ris.lightData = 0; ris.weightSum = 0; }
     }
 
@@ -718,7 +833,7 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
             float nw = 0;
             LightSample cand;
             if (pr.lightData != 0) {
-                if (!light_from_reservoir(s, cand, pr)) pr = Reservoir{};
+                if (!light_from_reservoir(s, cand, pr, sf, nLocal > 0)) pr = Reservoir{};
                 nw = target_pdf(cand, sf);
             }
             float rn = c.rnd();
@@ -732,12 +847,11 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
                 Surf ts;
                 prev_surface(c, ts, x, y);
                 LightSample sel;
-                light_from_reservoir(s, sel, rr);
+                light_from_reservoir(s, sel, rr, ts, nLocal > 0);
                 float ps = target_pdf(sel, ts);
                 if (ps > 0 && !(i == 0 && i == selLoop) && !s.prevSceneEmpty) {
                     const float extra = 0.01f + 0.01f * ts.depth;
-                    F3 sd = lightSample.position;
-                    if (dda_occluded(s.world, ts.pos, sd, extra, kRayMax)) ps = 0.0f;
+                    if (light_occluded(s, ts.pos, lightSample, ts.pos, extra)) ps = 0.0f;
                 }
                 Reservoir pr = load_prev_reservoir(c, x, y);
                 if (std::isnan(pr.weightSum) || std::isinf(pr.weightSum)) pr = Reservoir{};
@@ -748,13 +862,13 @@ void on_hit(Px &c, Ray &rd, const Hit &h) {  // closesthit.cu:10-852
             finalize(rr, piv, piSum);
         }
         if (lightSample.type != LtInvalid) {
-            visible = !dda_occluded(s.world, frontPos, lightSample.position, 0.0f, kRayMax);
+            visible = !light_occluded(s, spawn(light_dir(lightSample, sf.pos)), lightSample, sf.pos, 0.0f);
             if (!visible) { rr.lightData = 0; rr.weightSum = 0; }
         }
     }
     const Reservoir &shade = restir ? rr : ris;
     if (lightSample.type != LtInvalid && shade.lightData != 0 && visible) {
-        F3 sd = lightSample.position;
+        F3 sd = light_dir(lightSample, sf.pos);
         F3 alb = skipAlbedo ? F3(1.0f) : st.albedo;
         F3 bsdf; float pdf;
         disney_eval(st.normal, st.geoNormal, sd, st.wo, alb, st.metallic, st.translucency, st.roughness, bsdf, pdf);
@@ -774,7 +888,7 @@ bool trace_next(Px &c, Ray &rd, F3 &radiance, F3 &throughput) {  // RayGen.cu:8-
     rd.terminate = false;
     rd.lastDiffuse = rd.curDiffuse;
     rd.curDiffuse = false;
-    Hit h = dda_closest(c.s.world, rd.pos, rd.wi, kRayMax);
+    const AnyHit h = closest_any(c.s, rd.pos, rd.wi, kRayMax);
     if (h.hit) on_hit(c, rd, h);
     else on_miss(c, rd);
     radiance += throughput * rd.radiance;

@@ -58,11 +58,43 @@ struct Frame {
     void alloc(int w, int h);
 };
 
+// Instanced block meshes of a world: object-space triangles per block type,
+// the instance rows (vxpt_get_instances order: the cell is the instance's translation), the
+// emissive-triangle light records and their alias table.
+struct MeshInstance { int block = 0; F3 cell; int lightBase = -1; };  // lightBase: first light, -1 = not emissive
+struct MeshSet {
+    std::vector<float> pos, uv;           // 9 / 6 floats per triangle, block types concatenated
+    int triOff[32] = {}, triCnt[32] = {};  // per block id
+    std::vector<MeshInstance> inst;
+    std::vector<uint32_t> lights;         // LightInfo records, 8 x u32 each (Light.h:13-23)
+    std::vector<AliasBin> lightAlias;
+    int numLights = 0;
+};
+
+// closest hit of a radiance ray over voxels and meshes; isMesh: row / tri / u / v valid
+struct MeshHit { bool hit = false; int row = -1, tri = -1; float t = kRayMax, u = 0, v = 0; };
+// brute-force mesh queries (the reference's IAS; meshes.hip walks a BVH to the same answer):
+// closest hit with t in [0, tmax], back faces culled, first strictly closer (row, triangle) wins
+MeshHit mesh_closest_hit(const MeshSet &m, const F3 &o, const F3 &d, float tmax);
+// any triangle, either face, with t in [tmin, tmax]
+bool mesh_any_hit(const MeshSet &m, const F3 &o, const F3 &d, float tmin, float tmax);
+// the hit's self-intersection-safe front / back spawn points and world normal
+// (SelfHit.h:178-193 getTrianglePointAndError, :539-563 getSafeTriangleSpawnOffset,
+// :566-656 safeInstancedSpawnOffsetImpl with the instance's translation, :150-164
+// offsetSpawnPoint)
+void mesh_spawn(const MeshSet &m, const MeshHit &h, F3 &front, F3 &back, F3 &normal);
+// texture coordinates at the hit (closesthit.cu:189)
+F2 mesh_texcoord(const MeshSet &m, const MeshHit &h);
+// TriangleLight::Create (Light.h:85-122) of light record k
+struct TriLight { F3 base, edge1, edge2, radiance, normal; float area = 0; };
+TriLight tri_light(const MeshSet &m, int k);
+
 struct Scene {
     World world;
     Sky sky;
     BlueNoise bn;
-    Material mats[13];   // index = block id (1..12); 0 unused
+    Material mats[32];   // index = block id (1..12 cubes, 13..29 instanced meshes); 0 unused
+    MeshSet mesh;
     Camera cam, prevCam;
     int totalBounceLimit = 3, diffuseBounceLimit = 1;  // RayGen.cu:146-147
     // the pass after a geometry change: prevTopObject = 0 (OptixRenderer.cpp:916-919, 464), so the

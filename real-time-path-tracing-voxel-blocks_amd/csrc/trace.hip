@@ -145,13 +145,13 @@ __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
 // {o xyz + tmin, d xyz + tmax, result id}, so the traversal kernels see only
 // live rays.  Result ids: closest-hit rays write cHit/cT[id] (id = slot),
 // visibility rays oHit[id] (id = 4*slot + k).
-struct QRays {  // up to 4 rays of one slot sharing a direction
+struct QRays {  // up to 4 rays of one slot (a local light is seen in a different direction from each origin)
     unsigned mask;
     int id0;
-    V3 d;
-    float tmax;
+    V3 d0, d1, d2, d3;
+    float x0, x1, x2, x3;  // tmax
     V3 o0, o1, o2, o3;
-    float t0, t1, t2, t3;
+    float t0, t1, t2, t3;  // tmin
 };
 
 // Appends every lane's rays (bits of r.mask) to queue q.  Every thread of the
@@ -183,8 +183,10 @@ VX_D void block_enqueue(const TraceArgs &a, int q, const QRays &r) {
         if (!(r.mask & (1u << i))) continue;
         const V3 o = i == 0 ? r.o0 : (i == 1 ? r.o1 : (i == 2 ? r.o2 : r.o3));
         const float tmin = i == 0 ? r.t0 : (i == 1 ? r.t1 : (i == 2 ? r.t2 : r.t3));
+        const V3 d = i == 0 ? r.d0 : (i == 1 ? r.d1 : (i == 2 ? r.d2 : r.d3));
+        const float tmax = i == 0 ? r.x0 : (i == 1 ? r.x1 : (i == 2 ? r.x2 : r.x3));
         w.qO[k] = f4(o, tmin);
-        w.qD[k] = f4(r.d, r.tmax);
+        w.qD[k] = f4(d, tmax);
         w.qId[k] = r.id0 + i;
         ++k;
     }
@@ -361,7 +363,11 @@ VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segR
     }
 }
 
-VX_D SurfS load_surf(const WaveBufs &w, int s, bool &skipAlbedo) {
+// sPos: front spawn point, hit t; sWo.w: skip-albedo flag (1) + thin-film flag (2).  A thin
+// surface's back spawn point is in sBack (w = 1: the surface position -- the path's spawn point
+// -- is the back one, closesthit.cu:288 + 321).  front / back: the spawn points of rays leaving it.
+struct SurfX { V3 front, back; bool thin; };
+VX_D SurfS load_surf(const WaveBufs &w, int s, bool &skipAlbedo, SurfX *x = nullptr) {
     SurfS sf;
     const float4 p = w.sPos[s], n = w.sNrm[s], g = w.sGeo[s], al = w.sAlb[s], wo = w.sWo[s];
     sf.pos = xyz(p); sf.depth = p.w;
@@ -369,15 +375,28 @@ VX_D SurfS load_surf(const WaveBufs &w, int s, bool &skipAlbedo) {
     sf.geoNormal = xyz(g); sf.translucency = g.w;
     sf.albedo = xyz(al); sf.metallic = al.w != 0.0f;
     sf.wo = xyz(wo);
-    skipAlbedo = wo.w != 0.0f;
+    const int fl = (int)wo.w;
+    skipAlbedo = (fl & 1) != 0;
+    if (x) {
+        x->front = sf.pos;
+        x->back = sf.pos;
+        x->thin = (fl & 2) != 0;
+        if (x->thin) {
+            const float4 b = w.sBack[s];
+            x->back = xyz(b);
+            if (b.w != 0.0f) sf.pos = x->back;
+        }
+    }
     return sf;
 }
 
-VX_D void mis_params(const SkyDev &k, const SurfS &sf, int &nSun, int &nMis, float &sunMis, float &skyMis,
-                     float &brdfMis) {
-    const bool skipSun = (dot(sf.normal, k.sunDir) < 0.0f || dot(sf.geoNormal, k.sunDir) < 0.0f);
+// closesthit.cu:328-340: 8 local-light candidates when the scene has lights; the sun is skipped
+// below the horizon of a surface that is not a thin film
+VX_D void mis_params(const SkyDev &k, const SurfS &sf, bool thin, int nLocal, int &nSun, int &nMis, float &sunMis,
+                     float &skyMis, float &brdfMis) {
+    const bool skipSun = !thin && (dot(sf.normal, k.sunDir) < 0.0f || dot(sf.geoNormal, k.sunDir) < 0.0f);
     nSun = skipSun ? 0 : 1;
-    nMis = nSun + 2;
+    nMis = nLocal + nSun + 2;
     sunMis = float(nSun) / nMis;
     skyMis = 1.0f / nMis;
     brdfMis = 1.0f / nMis;
@@ -394,15 +413,61 @@ VX_D LSample load_ls(const WaveBufs &w, int s) {
 VX_D LSample invalid_ls() { return LSample{V3(0.f), V3(0.f), 0.f, LtInvalid}; }
 
 VX_D V3 shade_light(const SurfS &sf, bool skipAlbedo, const LSample &ls, const Reservoir &r) {
-    const V3 alb = skipAlbedo ? V3(1.0f) : sf.albedo;  // closesthit.cu:834
+    const V3 alb = skipAlbedo ? V3(1.0f) : sf.albedo;  // closesthit.cu:829-841
+    const V3 wi = light_dir(ls, sf.pos);
     V3 bsdf;
     float pdf;
-    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, alb, sf.metallic, sf.roughness, bsdf, pdf);
-    const float cosT = fmaxf(0.0f, dot(ls.position, sf.normal));
+    disney_eval(sf.normal, sf.geoNormal, wi, sf.wo, alb, sf.metallic, sf.roughness, bsdf, pdf);
+    const float cosT = fmaxf(0.0f, dot(wi, sf.normal));
     return bsdf * cosT * ls.radiance * r.weightSum / ls.solidAnglePdf;
 }
 
+// The geometry of a closest hit: spawn points, geometric normal, material.  A mesh hit (face 15:
+// x = instance row, y = triangle in BLAS leaf order, z = the mesh's triangle index, id = block)
+// re-runs the walk's triangle test on the same operands for its barycentrics (identical t, u, v).
+struct HitGeo {
+    V3 front, back, ng;
+    float u, v;
+    bool mesh;
+};
+template <bool MESH>
+VX_D HitGeo hit_geometry(const TraceArgs &a, const Hit &h, V3 o, V3 d) {
+    HitGeo g;
+    g.u = g.v = 0.0f;
+    g.mesh = MESH && h.face == 15;
+    if (!g.mesh) {
+        hit_frame(h, o, d, g.front, g.back, g.ng);
+        return g;
+    }
+    const int4 r = a.meshRow[h.x];
+    const V3 cell((float)r.x, (float)r.y, (float)r.z);
+    const float *t9 = a.mesh.tri + (size_t)h.y * 9;
+    float t;
+    tri_hit(V3(o.x - cell.x, o.y - cell.y, o.z - cell.z), d, t9, 0.0f, INFINITY, 1, t, g.u, g.v);
+    mesh_spawn(V3(t9[0], t9[1], t9[2]), V3(t9[3], t9[4], t9[5]), V3(t9[6], t9[7], t9[8]), g.u, g.v, cell, g.front,
+               g.back, g.ng);
+    return g;
+}
+// interpolated texcoords of a mesh hit (closesthit.cu:189)
+VX_D V2 mesh_tc(const TraceArgs &a, const Hit &h, float u, float v) {
+    const float *t6 = a.meshUV + (size_t)h.y * 6;
+    const float alpha = 1.0f - u - v;
+    return V2(t6[0], t6[1]) * alpha + V2(t6[2], t6[3]) * u + V2(t6[4], t6[5]) * v;
+}
+// a ray leaving a thin-film surface toward dir starts on the side it leaves from
+// (closesthit.cu:288, 457, 614, 799); other surfaces spawn at the front point
+VX_D V3 spawn_toward(bool thin, V3 dir, V3 n, V3 front, V3 back) {
+    return thin ? (dot(dir, n) > 0.0f ? front : back) : front;
+}
+// a visibility ray toward a light sample from p (closesthit.cu:606-633, 734-755): local lights
+// are traced to 0.01 short of the sampled point
+VX_D void light_ray(const LSample &ls, V3 p, float extra, V3 &dir, float &tmax) {
+    dir = light_dir(ls, p);
+    tmax = ls.type == LtLocal ? length(ls.position - p) - 0.01f - extra : kRayMax;
+}
+
 // closesthit / miss for the segment's ray; candidate generation for NEE
+template <bool MESH>
 VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
@@ -434,10 +499,35 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
 
     // __closesthit__radiance (closesthit.cu:10-316)
     const V3 wo = -rayD;
-    V3 frontPos, backPos, ng;
-    hit_frame(h, rayO, rayD, frontPos, backPos, ng);
+    const HitGeo g = hit_geometry<MESH>(a, h, rayO, rayD);
+    V3 frontPos = g.front, backPos = g.back, ng = g.ng;
     if (seg == 0) a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const MatDev &m = a.mats[h.id];
+    const MatDev &m = (MESH && g.mesh) ? a.meshMats[h.id] : a.mats[h.id];
+    if (MESH && m.emissive) {  // closesthit.cu:107-122: emits until the first diffuse bounce
+        V3 e(0.0f);
+        if (!(meta.x & F_HFD)) {
+            e = V3(m.albedo[0], m.albedo[1], m.albedo[2]);
+            if (seg == 0) {
+                a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+                a.cur.material[pi] = (float)0xFFFF;
+                a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+                a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+                a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+        }
+        if (seg == 0) w.pPos[s].w = h.t;  // the primary distance (no reservoir is stored)
+        seg_end(a, s, px, py, meta, e, V3(1.0f), 0.0f, true, false);
+        w.pMeta[s] = meta;
+        return;
+    }
+    const bool thin = m.thin != 0;
+    const V3 texPos = frontPos;  // world-grid uv: the front position before a thin-film swap
+    if (MESH && thin && !(dot(wo, ng) > 0.0f)) {  // closesthit.cu:124-133
+        ng = -ng;
+        const V3 t = frontPos;
+        frontPos = backPos;
+        backPos = t;
+    }
     SurfS sf;
     sf.geoNormal = ng;
     sf.wo = wo;
@@ -448,8 +538,9 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         w.pRad[s].w = travelled;
         sf.albedo = V3(m.albedo[0], m.albedo[1], m.albedo[2]);
         sf.roughness = m.roughness;
-        apply_textures(a.texels, a.tex, m, frontPos, ng, wo, ray_cone_spread(a.cam, px, py) * travelled, sf.albedo,
-                       sf.roughness, sf.metallic, sf.normal);
+        apply_textures(a.texels, a.tex, m, texPos, ng, wo, ray_cone_spread(a.cam, px, py) * travelled, sf.albedo,
+                       sf.roughness, sf.metallic, sf.normal, MESH && g.mesh,
+                       (MESH && g.mesh) ? mesh_tc(a, h, g.u, g.v) : V2(0.0f, 0.0f));
     } else {
         sf.albedo = max3(V3(m.albedo[0], m.albedo[1], m.albedo[2]), V3(0.001f));
         sf.roughness = m.roughness;
@@ -461,7 +552,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     if (seg == 0) {
         a.cur.material[pi] = (float)m.materialId;
         a.cur.normalRough[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, sf.roughness);
-        a.cur.geoNormalThin[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, m.thin ? 1.0f : 0.0f);
+        a.cur.geoNormalThin[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, thin ? 1.0f : 0.0f);
         a.cur.matParam[pi] = make_float4(sf.metallic ? 1.0f : 0.0f, sf.translucency, 0.0f, 0.0f);
     }
     V3 swi, sbop;
@@ -479,7 +570,8 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         skipAlbedo = true;
         primaryDist = h.t;
     }
-    w.pPos[s] = f4(frontPos, primaryDist);
+    const V3 spawnPos = spawn_toward(thin, swi, sf.normal, frontPos, backPos);
+    w.pPos[s] = f4(spawnPos, primaryDist);
     w.pDir[s] = f4(swi, spdf);
     if (!isDiffuse) {
         if (seg == 0) a.resCur[pi] = empty_res();
@@ -489,13 +581,36 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         return;
     }
 
-    // NEE candidates: sun and sky from their alias tables (closesthit.cu:318-414)
-    sf.pos = frontPos;
+    // NEE candidates: local lights, sun and sky from their alias tables (closesthit.cu:318-414)
+    sf.pos = spawnPos;
     sf.depth = h.t;
     const SkyDev &k = a.sky;
+    const int nLocal = (MESH && a.numLights > 0) ? 8 : 0;
     int nSun, nMis;
     float sunMis, skyMis, brdfMis;
-    mis_params(k, sf, nSun, nMis, sunMis, skyMis, brdfMis);
+    mis_params(k, sf, thin, nLocal, nSun, nMis, sunMis, skyMis, brdfMis);
+    if (MESH) {
+        Reservoir loc = empty_res();
+        LSample locLs = invalid_ls();
+        const float locMis = float(nLocal) / nMis;
+        for (int i = 0; i < nLocal; ++i) {  // closesthit.cu:350-376
+            float src;
+            const int li = (int)alias_sample(a.lightAlias, a.numLights, rng.next(), src);
+            if (li >= a.numLights) continue;
+            const float ux = rng.next(), uy = rng.next();
+            const LSample cand = tri_sample(tri_light(a.lights[li]), V2(ux, uy), sf.pos);
+            const float blended = mis_weight(sf, cand, src, locMis, brdfMis);
+            const float tp = target_pdf(cand, sf);
+            const float rr = rng.next();
+            if (blended != 0.0f)
+                if (stream_sample(loc, (uint32_t)li, V2(ux, uy), rr, tp, 1.0f / blended)) locLs = cand;
+        }
+        finalize(loc, 1.0f, (float)nMis);
+        loc.M = 1;
+        w.rLoc[s] = loc;
+        w.lLoc0[s] = f4(locLs.position, locLs.solidAnglePdf);
+        w.lLoc1[s] = f4(locLs.radiance, (float)locLs.type);
+    }
     Reservoir sunRes = empty_res();
     int sunSel = -1;
     if (nSun) {
@@ -534,22 +649,24 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         float bp;
         disney_sample(u0, u1, u2, u3, sf.normal, sf.geoNormal, wo, sf.albedo, sf.metallic, sf.translucency,
                       sf.roughness, sd, bop, bp);
-        w.cRayO[s] = f4(frontPos, bp > 0.0f ? kFltMax : -1.0f);
+        const V3 org = spawn_toward(thin, sd, sf.normal, frontPos, backPos);
+        w.cRayO[s] = f4(org, bp > 0.0f ? kFltMax : -1.0f);
         w.cRayD[s] = f4(sd, 0.0f);
         if (bp > 0.0f) {
             qr.mask = 1u;
             qr.id0 = s;
-            qr.o0 = frontPos;
+            qr.o0 = org;
             qr.t0 = 0.0f;
-            qr.d = sd;
-            qr.tmax = kFltMax;
+            qr.d0 = sd;
+            qr.x0 = kFltMax;
         }
     }
     w.sPos[s] = f4(frontPos, h.t);
+    if (thin) w.sBack[s] = f4(backPos, dot(swi, sf.normal) > 0.0f ? 0.0f : 1.0f);
     w.sNrm[s] = f4(sf.normal, sf.roughness);
     w.sGeo[s] = f4(sf.geoNormal, sf.translucency);
     w.sAlb[s] = f4(sf.albedo, sf.metallic ? 1.0f : 0.0f);
-    w.sWo[s] = f4(wo, skipAlbedo ? 1.0f : 0.0f);
+    w.sWo[s] = f4(wo, (skipAlbedo ? 1.0f : 0.0f) + (thin ? 2.0f : 0.0f));
     w.pBop[s] = f4(sbop, terminate ? 1.0f : 0.0f);
     w.rSun[s] = sunRes;
     w.rSky[s] = skyRes;
@@ -559,14 +676,16 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.pMeta[s] = meta;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_shade(TraceArgs a, int seg) {
+template <bool MESH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 3 : 5))) void k_shade(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
-    shade_slot(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
+    shade_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
     block_enqueue(a, 4 * seg + 1, qr);
 }
 
 // BRDF candidate from its traced ray, RIS over {local, sun, sky, BRDF}, visibility ray
+template <bool MESH>
 VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
@@ -574,16 +693,25 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
     int4 meta = w.pMeta[s];
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
-    const SurfS sf = load_surf(w, s, skipAlbedo);
+    SurfX sp;
+    const SurfS sf = load_surf(w, s, skipAlbedo, &sp);
     const SkyDev &k = a.sky;
     Rng rng{&a.bn, px, py, a.iterationIndex, meta.y};
+    const int nLocal = (MESH && a.numLights > 0) ? 8 : 0;
     int nSun, nMis;
     float sunMis, skyMis, brdfMis;
-    mis_params(k, sf, nSun, nMis, sunMis, skyMis, brdfMis);
+    mis_params(k, sf, sp.thin, nLocal, nSun, nMis, sunMis, skyMis, brdfMis);
 
     Reservoir localRes = empty_res();
-    finalize(localRes, 1.0f, (float)nMis);
-    localRes.M = 1;
+    LSample localLs = invalid_ls();
+    if (MESH) {  // the local candidates streamed by k_shade
+        localRes = w.rLoc[s];
+        const float4 l0 = w.lLoc0[s], l1 = w.lLoc1[s];
+        localLs = LSample{xyz(l0), xyz(l1), l0.w, (int)l1.w};
+    } else {
+        finalize(localRes, 1.0f, (float)nMis);
+        localRes.M = 1;
+    }
     const Reservoir sunRes = w.rSun[s], skyRes = w.rSky[s];
     const int4 idx = w.nIdx[s];
     const LSample sunLs = idx.x >= 0 ? sun_ls(k, idx.x) : invalid_ls();
@@ -596,10 +724,30 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
         uint32_t li = kInvalidLight;
         V2 uv(0.0f, 0.0f);
         LSample cand = invalid_ls();
-        if (w.cRayO[s].w >= 0.0f) {
+        const float4 co = w.cRayO[s];
+        if (co.w >= 0.0f) {
             const V3 sd = xyz(w.cRayD[s]);
             const Hit bh = unpack_hit(w.cHit[s], w.cT[s]);
-            if (!bh.hit) {  // __miss__bsdf_light
+            if (MESH && bh.hit && bh.face == 15) {
+                // __closesthit__bsdf_light (closesthit.cu:854-900): an emissive instance's triangle is
+                // light (its first light + the mesh's triangle index)
+                const int base = a.meshRowLight[bh.x];
+                if (nLocal > 0 && a.meshMats[bh.id].emissive && base >= 0) {
+                    li = (uint32_t)(base + bh.z);
+                    if (li >= (uint32_t)a.numLights) {
+                        li = kInvalidLight;
+                    } else {
+                        const int4 r = a.meshRow[bh.x];
+                        const V3 org = xyz(co);
+                        float t, bu, bv;
+                        tri_hit(V3(org.x - (float)r.x, org.y - (float)r.y, org.z - (float)r.z), sd,
+                                a.mesh.tri + (size_t)bh.y * 9, 0.0f, INFINITY, 1, t, bu, bv);
+                        uv = inverse_tri_sample(bu, bv);
+                        cand = tri_sample(tri_light(a.lights[li]), uv, sf.pos);
+                        lightSrcPdf = a.lightAlias[li].p;
+                    }
+                }
+            } else if (!bh.hit) {  // __miss__bsdf_light
                 if (eq_area_cone_uv(uv, k.sunDir, sd, k.sunCosMax)) {
                     li = kSunLight;
                     int x = (int)(uv.x * k.sunW - 0.5f), y = (int)(uv.y * k.sunH - 0.5f);
@@ -622,7 +770,7 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
             }
         }
         if (lightSrcPdf != 0.0f) {
-            const float misW = (li == kSkyLight) ? skyMis : ((li == kSunLight) ? sunMis : 0.0f);
+            const float misW = (li == kSkyLight) ? skyMis : ((li == kSunLight) ? sunMis : float(nLocal) / nMis);
             float blended, tp;
             mis_and_target(sf, cand, lightSrcPdf, misW, brdfMis, blended, tp);
             const float rr = rng.next();
@@ -639,15 +787,18 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
     const bool selBrdf = combine(ris, brdfRes, rng.next(), brdfRes.targetPdf);
     finalize(ris, 1.0f, 1.0f);
     ris.M = 1;
-    const LSample ls = selBrdf ? brdfLs : (selSky ? skyLs : (selSun ? sunLs : invalid_ls()));
+    const LSample ls = selBrdf ? brdfLs : (selSky ? skyLs : (selSun ? sunLs : localLs));
     const bool trace = ls.type != LtInvalid && ris.lightData != 0;
     if (trace) {
+        V3 dir;
+        float tmax;
+        light_ray(ls, sf.pos, 0.0f, dir, tmax);
         qr.mask = 1u;
         qr.id0 = 4 * s;
-        qr.o0 = sf.pos;
+        qr.o0 = spawn_toward(sp.thin, dir, sf.normal, sp.front, sp.back);
         qr.t0 = 0.0f;
-        qr.d = ls.position;
-        qr.tmax = kRayMax;
+        qr.d0 = dir;
+        qr.x0 = tmax;
     }
     w.rRis[s] = ris;
     store_ls(w, s, ls);
@@ -655,15 +806,17 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
     w.pMeta[s] = meta;
 }
 
+template <bool MESH>
 __global__ __launch_bounds__(256) void k_nee(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
-    nee_slot(a, blockIdx.x * 256 + threadIdx.x, qr);
+    nee_slot<MESH>(a, blockIdx.x * 256 + threadIdx.x, qr);
     block_enqueue(a, 4 * seg + 2, qr);
 }
 
 // visibility of the RIS sample; seg 0: ReSTIR temporal reuse (Restir.h:11-415,
 // closesthit.cu:626-851) up to its visibility rays; seg > 0: final shading.
+template <bool MESH>
 VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
@@ -671,8 +824,9 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int4 meta = w.pMeta[s];
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
-    const SurfS sf = load_surf(w, s, skipAlbedo);
-    const SkyDev &k = a.sky;
+    SurfX sp;
+    const SurfS sf = load_surf(w, s, skipAlbedo, &sp);
+    const bool hasLocal = MESH && a.numLights > 0;
     Reservoir ris = w.rRis[s];
     LSample ls = load_ls(w, s);
     bool visible = false;
@@ -735,7 +889,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         float nw = 0.0f;
         LSample cand = invalid_ls();
         if (pr.lightData != 0) {
-            if (!light_from_res(k, cand, pr)) pr = empty_res();
+            if (!light_from_res(a, cand, pr, sf.pos, hasLocal)) pr = empty_res();
             nw = target_pdf(cand, sf);
         }
         if (combine(rr, pr, rng.next(), nw)) { ls = cand; selLoop = i; }
@@ -743,10 +897,8 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     // bias-correction rays: the selected light seen from each accepted tap's surface
     float psv0 = 0, psv1 = 0, psv2 = 0;
     qr.id0 = 4 * s;
-    qr.d = ls.position;
-    qr.tmax = kRayMax;
-    LSample sel = invalid_ls();  // the combined reservoir's light (the same for every tap)
-    if (rr.lightData != 0) light_from_res(k, sel, rr);
+    LSample sel = invalid_ls();  // the combined reservoir's light (environment lights: the same for every tap)
+    if (rr.lightData != 0) light_from_res(a, sel, rr, sf.pos, hasLocal);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (rr.lightData != 0 && (cached & (1u << i))) {
@@ -755,15 +907,19 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             SurfS ts;
             const V3 vdi = i == 0 ? vd0 : (i == 1 ? vd1 : vd2);
             prev_surface(a, jit, ts, x, y, &vdi, nullptr);
+            if (MESH && sel.type == LtLocal) light_from_res(a, sel, rr, ts.pos, hasLocal);  // seen from the tap
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;
             // prevSceneEmpty: OptiX's null prevTopObject -- the ray misses, the sample is visible
             if (psv > 0 && !(i == 0 && i == selLoop) && !a.prevSceneEmpty) {
                 qr.mask |= 2u << i;
                 const float tmin = 0.01f + 0.01f * ts.depth;
-                if (i == 0) { qr.o1 = ts.pos; qr.t1 = tmin; }
-                else if (i == 1) { qr.o2 = ts.pos; qr.t2 = tmin; }
-                else { qr.o3 = ts.pos; qr.t3 = tmin; }
+                V3 dir;
+                float tmax;
+                light_ray(ls, ts.pos, tmin, dir, tmax);
+                if (i == 0) { qr.o1 = ts.pos; qr.t1 = tmin; qr.d1 = dir; qr.x1 = tmax; }
+                else if (i == 1) { qr.o2 = ts.pos; qr.t2 = tmin; qr.d2 = dir; qr.x2 = tmax; }
+                else { qr.o3 = ts.pos; qr.t3 = tmin; qr.d3 = dir; qr.x3 = tmax; }
             }
         }
         w.oHit[4 * s + 1 + i] = 0;
@@ -771,9 +927,14 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     // final visibility: with no tap selected the sample is the RIS one and the
     // ray equals the RIS visibility ray, whose result is already in oHit[4s]
     if (ls.type != LtInvalid && selLoop >= 0) {
+        V3 dir;
+        float tmax;
+        light_ray(ls, sf.pos, 0.0f, dir, tmax);
         qr.mask |= 1u;
-        qr.o0 = sf.pos;
+        qr.o0 = spawn_toward(sp.thin, dir, sf.normal, sp.front, sp.back);
         qr.t0 = 0.0f;
+        qr.d0 = dir;
+        qr.x0 = tmax;
     }
     w.rRR[s] = rr;
     store_ls(w, s, ls);
@@ -784,10 +945,11 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.pMeta[s] = meta;
 }
 
+template <bool MESH>
 __global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
-    restir_slot(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
+    restir_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
     block_enqueue(a, 4 * seg + 3, qr);
 }
 
@@ -801,7 +963,8 @@ __global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
     if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
     const size_t pi = (size_t)py * a.W + px;
     bool skipAlbedo;
-    const SurfS sf = load_surf(w, s, skipAlbedo);
+    SurfX sp;
+    const SurfS sf = load_surf(w, s, skipAlbedo, &sp);
     Reservoir rr = w.rRR[s];
     const LSample ls = load_ls(w, s);
     const int4 idx = w.nIdx[s];
@@ -831,6 +994,63 @@ __global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
     const float4 b = w.pBop[s];
     seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true);
     w.pMeta[s] = meta;
+}
+
+// ----------------------------------------------------------------- instanced meshes
+// The mesh pass of a traversal (launched only when the world has instanced meshes):
+// a closest-hit ray's voxel result is replaced by a strictly closer mesh triangle (ties stay with
+// the voxel face -- the oracle's definition; OptiX leaves the order of equal-t hits unspecified),
+// back faces culled (RayGen.cu:52); a visibility ray is occluded by any triangle, either face, in
+// [tmin, tmax] (closesthit.cu:616-625).  Mesh hit record: face 15, x = instance row, y = the
+// triangle in BLAS leaf order, z = the mesh's triangle index, id = block.
+VX_D bool mesh_closest_update(const TraceArgs &a, V3 o, V3 d, float tmax, int4 &hp, float &t) {
+    const bool vox = ((hp.w >> 12) & 1) != 0;
+    Best b{vox ? t : tmax, 0.0f, 0.0f, -1, -1, -1};
+    ScratchStack st;
+    mesh_walk<false>(a.mesh, o, d, V3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z), 0.0f, 1, b, st);
+    if (b.inst < 0 || (vox && !(b.t < t))) return false;
+    hp = make_int4(b.inst, b.leaf, b.tri, 15 | (a.meshRow[b.inst].w << 4) | (1 << 12));
+    t = b.t;
+    return true;
+}
+// camera (mode 2) and continuing path rays (mode 0), after k_closest
+__global__ __launch_bounds__(256) void k_mesh_slots(TraceArgs a, int mode) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    const WaveBufs &w = a.wb;
+    if (mode == 0 && !(w.pMeta[s].x & F_ALIVE)) return;
+    int4 hp = w.cHit[s];
+    float t = w.cT[s];
+    if (mesh_closest_update(a, xyz(w.pPos[s]), xyz(w.pDir[s]), kRayMax, hp, t)) {
+        w.cHit[s] = hp;
+        w.cT[s] = t;
+    }
+}
+// a ray queue, after its voxel traversal (k_queue + k_resume)
+template <bool OCC>
+__global__ __launch_bounds__(256) void k_mesh_queue(TraceArgs a, int q) {
+    const WaveBufs &w = a.wb;
+    const unsigned n = w.qCount[q];
+    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 ro = w.qO[i], rd = w.qD[i];
+    const int id = w.qId[i];
+    const V3 o = xyz(ro), d = xyz(rd);
+    if (OCC) {
+        if (w.oHit[id]) return;
+        Best b{rd.w, 0.0f, 0.0f, -1, -1, -1};
+        ScratchStack st;
+        mesh_walk<true>(a.mesh, o, d, V3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z), ro.w, 0, b, st);
+        if (b.inst >= 0) w.oHit[id] = 1;
+    } else {
+        int4 hp = w.cHit[id];
+        float t = w.cT[id];
+        if (mesh_closest_update(a, o, d, rd.w, hp, t)) {
+            w.cHit[id] = hp;
+            w.cT[id] = t;
+        }
+    }
 }
 
 // C2 bring-up mode: primary hit G-buffer + sky, no NEE
@@ -940,8 +1160,9 @@ hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, f
 
 hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir) {
     const dim3 g((a.nSlots + 255) / 256), g4((4 * a.nSlots + 255) / 256), b(256);
+    const bool mesh = a.mesh.nInst > 0;
     hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 2);
-    if (a.primaryOnly) {
+    if (a.primaryOnly) {  // C2 bring-up: the voxel G-buffer only
         hipLaunchKernelGGL(k_primary_gbuffer, g, b, 0, st, a);
         return hipGetLastError();
     }
@@ -956,22 +1177,32 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBefor
             hipLaunchKernelGGL(k_queue<true>, gq, b, 0, st, a, q, a.iterCap, shardCap);
             hipLaunchKernelGGL(k_resume<true>, gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
             if (a.iterCap2 > 0) hipLaunchKernelGGL(k_resume<true>, gr, b, 0, st, a, q, 2, shardCap, 0);
+            if (mesh) hipLaunchKernelGGL(k_mesh_queue<true>, gq, b, 0, st, a, q);
         } else {
             hipLaunchKernelGGL(k_queue<false>, gq, b, 0, st, a, q, a.iterCap, shardCap);
             hipLaunchKernelGGL(k_resume<false>, gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
             if (a.iterCap2 > 0) hipLaunchKernelGGL(k_resume<false>, gr, b, 0, st, a, q, 2, shardCap, 0);
+            if (mesh) hipLaunchKernelGGL(k_mesh_queue<false>, gq, b, 0, st, a, q);
         }
     };
+    if (mesh) hipLaunchKernelGGL(k_mesh_slots, g, b, 0, st, a, 2);
     for (int seg = 0; seg < a.segments; ++seg) {
-        if (seg > 0) hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
-        hipLaunchKernelGGL(k_shade, g, b, 0, st, a, seg);
+        if (seg > 0) {
+            hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
+            if (mesh) hipLaunchKernelGGL(k_mesh_slots, g, b, 0, st, a, 0);
+        }
+        // the shading kernels' mesh variants (mesh hits, thin films, local lights) run only with meshes
+        if (mesh) hipLaunchKernelGGL(k_shade<true>, g, b, 0, st, a, seg);
+        else hipLaunchKernelGGL(k_shade<false>, g, b, 0, st, a, seg);
         trav(false, 4 * seg + 1, a.nSlots);
-        hipLaunchKernelGGL(k_nee, g, b, 0, st, a, seg);
+        if (mesh) hipLaunchKernelGGL(k_nee<true>, g, b, 0, st, a, seg);
+        else hipLaunchKernelGGL(k_nee<false>, g, b, 0, st, a, seg);
         trav(true, 4 * seg + 2, a.nSlots);
         // the first reader of the previous pass's G-buffer and reservoirs (temporal taps):
         // a band's halo rows of them may still be in flight on the exchange stream
         if (seg == 0 && waitBeforeRestir) hipStreamWaitEvent(st, waitBeforeRestir, 0);
-        hipLaunchKernelGGL(k_restir, g, b, 0, st, a, seg);
+        if (mesh) hipLaunchKernelGGL(k_restir<true>, g, b, 0, st, a, seg);
+        else hipLaunchKernelGGL(k_restir<false>, g, b, 0, st, a, seg);
         if (seg == 0) {
             trav(true, 4 * seg + 3, 4 * a.nSlots);
             hipLaunchKernelGGL(k_finish, g, b, 0, st, a);

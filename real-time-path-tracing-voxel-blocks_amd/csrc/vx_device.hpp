@@ -2,14 +2,14 @@
 // voxel DDA, safe spawn, Disney BSDF, blue-noise sampler, light sampling,
 // reservoirs, sky lookup.  See trace.hip for the pass structure.
 #pragma once
-#include "vx_internal.hpp"
+#include "vx_mesh.hpp"
 
 namespace vx {
 namespace {
 
 constexpr uint32_t kValidBit = 0x80000000u, kIndexMask = 0x7FFFFFFFu;
 constexpr uint32_t kInvalidLight = 0x7FFFFFFFu, kSkyLight = 0x7FFFFFFEu, kSunLight = 0x7FFFFFFDu;
-enum { LtInvalid = 0, LtSky = 1, LtSun = 2 };
+enum { LtInvalid = 0, LtSky = 1, LtSun = 2, LtLocal = 3 };
 constexpr float kRoughThresh = 0.00001f, kTranslThresh = 0.001f;
 constexpr float kMinPdf = 1e-5f, kMaxThroughput = 32.0f, kMinLobe = 0.05f;
 
@@ -623,25 +623,59 @@ struct SurfS {
     bool metallic;
 };
 
-VX_D float target_pdf(const LSample &ls, const SurfS &sf) {
+// the direction a light sample is seen in from p: local lights by position (closesthit.cu:610,
+// Restir.h:201), environment samples carry it
+VX_D V3 light_dir(const LSample &ls, V3 p) { return ls.type == LtLocal ? normalize(ls.position - p) : ls.position; }
+VX_D float target_pdf(const LSample &ls, const SurfS &sf) {  // Restir.h:194-211
     if (ls.solidAnglePdf <= 0 || ls.type == LtInvalid) return 0.0f;
+    const V3 wi = light_dir(ls, sf.pos);
     V3 fr;
     float pdf;
-    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, pdf);
-    return luminance(ls.radiance * fr * fabsf(dot(ls.position, sf.normal)) / ls.solidAnglePdf);
+    disney_eval(sf.normal, sf.geoNormal, wi, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, pdf);
+    return luminance(ls.radiance * fr * fabsf(dot(wi, sf.normal)) / ls.solidAnglePdf);
 }
 VX_D float mis_weight(const SurfS &sf, const LSample &ls, float selPdf, float lightMis, float brdfMis) {
-    const float sa = ls.solidAnglePdf;
+    const float sa = ls.solidAnglePdf;  // Restir.h:286-328 (brdfCutoff 0)
     if (brdfMis == 0.0f || sa <= 0.0f || isinf(sa) || isnan(sa)) return lightMis * selPdf;
+    V3 dir = ls.position;
+    if (ls.type == LtLocal) {
+        const V3 toLight = ls.position - sf.pos;
+        dir = toLight / length(toLight);
+    }
     V3 fr;
     float bp;
-    disney_eval(sf.normal, sf.geoNormal, ls.position, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, bp);
+    disney_eval(sf.normal, sf.geoNormal, dir, sf.wo, sf.albedo, sf.metallic, sf.roughness, fr, bp);
     return (lightMis * (selPdf * sa) + brdfMis * bp) / sa;
 }
-// mis_weight and target_pdf of one candidate with a single BSDF evaluation (both evaluate the
-// same Disney lobe for the same surface and direction; results identical to the two calls)
+// TriangleLight::calcSample (Light.h:54-82; SampleTriangle LinearMath.h:2048-2056, PdfAtoW :2125)
+VX_D LSample tri_sample(const TriL &t, V2 uv, V3 viewer) {
+    const float sx = sqrtf(uv.x);
+    LSample r;
+    r.position = t.base + t.e1 * (sx * (1.0f - uv.y)) + t.e2 * (sx * uv.y);
+    V3 L = r.position - viewer;
+    const float Ld = length(L);
+    L /= Ld;
+    const float areaPdf = 1.0f / t.area;
+    const float cosT = saturate(dot(L, -t.n));
+    r.solidAnglePdf = areaPdf * (Ld * Ld) / cosT;
+    r.radiance = t.rad;
+    r.type = LtLocal;
+    return r;
+}
+VX_D V2 inverse_tri_sample(float u, float v) {  // InverseTriangleSample (LinearMath.h:2059-2064)
+    const float b0 = 1.0f - u - v, sx = 1 - b0;
+    return V2(sx * sx, v / sx);
+}
+// mis_weight and target_pdf of one environment candidate with a single BSDF evaluation (both
+// evaluate the same Disney lobe for the same surface and direction; results identical to the
+// two calls).  Local lights normalise their direction two ways and go through the two calls.
 VX_D void mis_and_target(const SurfS &sf, const LSample &ls, float selPdf, float lightMis, float brdfMis,
                          float &blended, float &tp) {
+    if (ls.type == LtLocal) {
+        blended = mis_weight(sf, ls, selPdf, lightMis, brdfMis);
+        tp = target_pdf(ls, sf);
+        return;
+    }
     const float sa = ls.solidAnglePdf;
     const bool tpEval = !(sa <= 0 || ls.type == LtInvalid);
     const bool misEval = !(brdfMis == 0.0f || sa <= 0.0f || isinf(sa) || isnan(sa));
@@ -678,7 +712,9 @@ VX_D void finalize(Reservoir &r, float num, float den) {
 }
 VX_D Reservoir empty_res() { return Reservoir{0u, 0u, 0.0f, 0.0f, 0.0f}; }
 
-VX_D bool light_from_res(const SkyDev &k, LSample &ls, const Reservoir &r) {
+// GetLightSampleFromReservoir (Restir.h:383-415); local lights are sampled as seen from `pos`
+VX_D bool light_from_res(const TraceArgs &a, LSample &ls, const Reservoir &r, V3 pos, bool hasLocal) {
+    const SkyDev &k = a.sky;
     const uint32_t li = r.lightData & kIndexMask;
     const float ux = (float)(r.uvData & 0xffff) / float(0xffff), uy = (float)(r.uvData >> 16) / float(0xffff);
     if (li == kSkyLight) {
@@ -687,6 +723,9 @@ VX_D bool light_from_res(const SkyDev &k, LSample &ls, const Reservoir &r) {
     } else if (li == kSunLight) {
         const int x = clampi(int(ux * k.sunW), 0, k.sunW - 1), y = clampi(int(uy * k.sunH), 0, k.sunH - 1);
         ls = sun_ls(k, y * k.sunW + x);
+    } else if (hasLocal && li < (uint32_t)a.numLights) {
+        ls = tri_sample(tri_light(a.lights[li]), V2(ux, uy), pos);
+        return true;
     }
     return li < kInvalidLight;
 }
@@ -808,13 +847,17 @@ VX_D float ray_cone_spread(const CamDev &cam, int px, int py) {
 // Textured MaterialState (closesthit.cu:167-254): world-grid uv of the front position, ray-cone
 // lod, albedo x texture, roughness / metallic from textures, tangent-space normal map aligned to
 // the face and blended at strength 0.2.  coneWidth = the ray cone's width at this hit.
+// vertexTc: the mesh triangle's interpolated texcoords (closesthit.cu:189; useVertexTc = a mesh hit)
 VX_D void apply_textures(const uchar4 *texels, const TexInfo *tex, const MatDev &m, V3 pos, V3 ng, V3 wo,
-                         float coneWidth, V3 &albedo, float &roughness, bool &metallic, V3 &normal) {
+                         float coneWidth, V3 &albedo, float &roughness, bool &metallic, V3 &normal,
+                         bool useVertexTc = false, V2 vertexTc = V2(0.0f, 0.0f)) {
     V2 tc(0.0f, 0.0f);
     if (m.worldGridUV) {
         if (fabsf(ng.x) > 0.9f) tc = V2(fmodf(pos.z, m.uvScale), fmodf(pos.y, m.uvScale));
         else if (fabsf(ng.y) > 0.9f) tc = V2(fmodf(pos.x, m.uvScale), fmodf(pos.z, m.uvScale));
         else if (fabsf(ng.z) > 0.9f) tc = V2(fmodf(pos.x, m.uvScale), fmodf(pos.y, m.uvScale));
+    } else if (useVertexTc) {
+        tc = vertexTc;
     }
     tc = tc / m.uvScale;
     const float mip0 = sqrtf(1024.0f * 1024.0f + 1024.0f * 1024.0f);  // MaterialParameter::texSize (1024, 1024)

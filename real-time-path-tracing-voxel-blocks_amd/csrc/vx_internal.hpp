@@ -30,6 +30,7 @@ struct MatDev {  // per block id, MaterialParameter subset (SystemParameter.h:11
     int tex[4] = {-1, -1, -1, -1};  // albedo, normal, roughness, metallic texture (-1 = none)
     float uvScale = 1.0f;
     int worldGridUV = 0;
+    int emissive = 0;  // MaterialParameter.isEmissive: albedo holds the emitted radiance (MaterialManager.cpp:162-167)
 };
 
 // One texture's RGBA8 mip chain in the texel buffer (TextureManager.cu:216-259 layout: square,
@@ -113,6 +114,12 @@ struct WaveBufs {
     float4 *ls1;    // radiance xyz, light type
     float4 *tapPsv; // target pdf of the selection at the three temporal taps, first-visibility flag
     float4 *tapM;   // the taps' clamped M
+    // instanced meshes: back spawn point of a thin-film surface (xyz, w = thin
+    // flag; rays leaving it on the far side start there), the 8 local-light candidates' reservoir
+    // and selected sample (position xyz + solid-angle pdf, radiance xyz + type)
+    float4 *sBack;
+    Reservoir *rLoc;
+    float4 *lLoc0, *lLoc1;
     // visibility results: 4 rays per slot (0: RIS/final visibility, 1-3: bias-correction taps)
     uint8_t *oHit;
     // compacted ray queue (trace.hip block_enqueue): o xyz + tmin, d xyz + tmax,
@@ -124,6 +131,41 @@ struct WaveBufs {
     int4 *sCell[2];
     float4 *sT[2];
     int2 *sFace[2];
+};
+
+// Emissive-triangle light record, 32 B (renderer/shaders/Light.h:13-23): centroid, the two
+// edge lengths as f16 (lo = edge1), radiance as 4 x f16, the edge directions octahedral
+// unorm16x2 encoded
+struct LightInfo {
+    float center[3];
+    uint32_t scalars;
+    uint32_t radiance[2];
+    uint32_t direction1, direction2;
+};
+// Instanced-mesh ray queries (SURVEY §8f #1, the geometry half): two-level BVH -- a TLAS over
+// the instances' world boxes, one BLAS per block type's mesh in object space (the instance
+// transform is a translation by its cell, VoxelEngine.cu:364-369).  Node boxes are widened at
+// build time so that box culling can only drop triangles the exact test would also reject.
+// Inner node: count = 0, children left and left + 1; leaf: count primitives from left.
+struct BvhNode {
+    float lo[3];
+    int left;
+    float hi[3];
+    int count;
+};
+struct MeshInst {
+    float cell[3];
+    int block;  // block type -> its BLAS
+    int row;    // the instance's row in vxpt_get_instances
+};
+struct MeshDev {
+    const BvhNode *tlas;    // over instances (primitive = MeshInst index)
+    const MeshInst *inst;
+    const BvhNode *blas;    // every block type's BLAS, concatenated
+    const float *tri;       // 9 floats per triangle in BLAS leaf order (object space)
+    const int *triId;       // the mesh's own triangle index of each
+    const int2 *root;       // per block type: (first BLAS node, first triangle); -1 = no mesh
+    int nInst;
 };
 
 struct TraceArgs {
@@ -152,6 +194,15 @@ struct TraceArgs {
     const TexInfo *tex;         // texture table (nullptr: no textures loaded)
     const uchar4 *texels;       // every texture's mip chain, RGBA8
     int texEnabled;
+    // instanced meshes (mesh.nInst == 0: none, and no mesh kernel runs)
+    MeshDev mesh;
+    const float *meshUV;        // 6 floats (3 corners' texcoords) per triangle, BLAS leaf order
+    const int4 *meshRow;        // per instance row: cell xyz, block id
+    const int *meshRowLight;    // per instance row: its first light record, -1 = not emissive
+    const MatDev *meshMats;     // materials by block id (0..31)
+    const LightInfo *lights;    // emissive-triangle lights (VoxelEngine.cu:53-116)
+    const AliasBin *lightAlias;
+    int numLights;
 };
 
 // kernel launchers (defined in the .hip translation units)
@@ -248,50 +299,16 @@ int post_bloom_half(const PostArgs &a);  // rows of bloomB the compose pass taps
 bool decode_png(const std::string &path, int &w, int &h, int &ch, std::vector<uint8_t> &px);
 bool load_obj(const std::string &path, std::vector<float> &pos, std::vector<float> &uv);
 
-// Emissive-triangle light record, 32 B (renderer/shaders/Light.h:13-23): centroid, the two
-// edge lengths as f16 (lo = edge1), radiance as 4 x f16, the edge directions octahedral
-// unorm16x2 encoded
-struct LightInfo {
-    float center[3];
-    uint32_t scalars;
-    uint32_t radiance[2];
-    uint32_t direction1, direction2;
-};
-// One emissive block type's lights: every (instance, triangle) of its mesh, instance-major
-// (VoxelEngine.cu:53-116), written from out[0]; weight[k] = luminance(radiance) * area of the
-// decoded record (extractRadianceKernel, :139-147).  tri: 9 floats per triangle (object
-// space), inst: 3 ints per instance (the cell = the translation of its 3x4 transform).
-// Instanced-mesh ray queries (SURVEY §8f #1, the geometry half): two-level BVH -- a TLAS over
-// the instances' world boxes, one BLAS per block type's mesh in object space (the instance
-// transform is a translation by its cell, VoxelEngine.cu:364-369).  Node boxes are widened at
-// build time so that box culling can only drop triangles the exact test would also reject.
-// Inner node: count = 0, children left and left + 1; leaf: count primitives from left.
-struct BvhNode {
-    float lo[3];
-    int left;
-    float hi[3];
-    int count;
-};
-struct MeshInst {
-    float cell[3];
-    int block;  // block type -> its BLAS
-    int row;    // the instance's row in vxpt_get_instances
-};
-struct MeshDev {
-    const BvhNode *tlas;    // over instances (primitive = MeshInst index)
-    const MeshInst *inst;
-    const BvhNode *blas;    // every block type's BLAS, concatenated
-    const float *tri;       // 9 floats per triangle in BLAS leaf order (object space)
-    const int *triId;       // the mesh's own triangle index of each
-    const int2 *root;       // per block type: (first BLAS node, first triangle); -1 = no mesh
-    int nInst;
-};
 // closest hit (tie: smaller t, then instance, then triangle) of n rays (o.xyz, tmin, d.xyz, tmax);
 // out: t, u, v, hit flag per ray; ids: instance, triangle.  cull = skip back faces (radiance rays)
 hipError_t launch_mesh_probe(const MeshDev &m, const float *rays, int n, int cull, float *out, int *ids,
                              hipStream_t st);
 // any hit, both faces (visibility rays): occluded 1/0 per ray
 hipError_t launch_mesh_occluded(const MeshDev &m, const float *rays, int n, unsigned char *occluded, hipStream_t st);
+// One emissive block type's lights: every (instance, triangle) of its mesh, instance-major
+// (VoxelEngine.cu:53-116), written from out[0]; weight[k] = luminance(radiance) * area of the
+// decoded record (extractRadianceKernel, :139-147).  tri: 9 floats per triangle (object
+// space), inst: 3 ints per instance (the cell = the translation of its 3x4 transform).
 hipError_t launch_tri_lights(const float *tri, int nTri, const int *inst, int nInst, V3 radiance, LightInfo *out,
                              float *weight, hipStream_t st);
 

@@ -159,7 +159,7 @@ struct vxpt_ctx {
     std::vector<uint64_t> hMacro, hCell;
     std::vector<int> topCount;  // cube cells per 64^3 block
     int prevSceneEmpty = 0;     // the next trace pass's temporal visibility sees no previous scene
-    MatDev mats[13] = {};
+    MatDev mats[32] = {};  // by block id: 1..12 cubes (kernel arguments), 13..29 instanced meshes (meshMats)
     CamDev cam{}, prevCam{};
     float camYaw = 0, camPitch = 0;
 
@@ -212,6 +212,13 @@ struct vxpt_ctx {
     DBuf<int2> blasRoot;
     DBuf<MeshInst> meshInst;
     int nMeshInst = 0;
+    // the path kernels' view of the meshes: texcoords in BLAS leaf order, per instance row its cell +
+    // block and first light, materials by block id
+    std::vector<float> hBlasUV;
+    DBuf<float> blasUV;
+    DBuf<int4> meshRow;
+    DBuf<int> meshRowLight;
+    DBuf<MatDev> meshMats;
 
     // blue noise
     DBuf<uint8_t> bnSobol, bnScramble, bnRank;
@@ -655,6 +662,10 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
     return 0;
 }
 
+}  // namespace
+static MeshDev mesh_dev(const vxpt_ctx *c);
+namespace {
+
 int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale) {
     if (!c->voxels.p) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
     if (!c->skyReady) return fail(c, VXPT_ERR_STATE, "sky not set");
@@ -663,6 +674,17 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     fill_sky(c, a.sky);
     a.bn = {c->bnSobol.p, c->bnScramble.p, c->bnRank.p};
     for (int i = 0; i < 13; ++i) a.mats[i] = c->mats[i];
+    if (c->nMeshInst > 0) {
+        if (int r = upload_vec(c, c->meshMats, c->mats, 32)) return r;
+        a.mesh = mesh_dev(c);
+        a.meshUV = c->blasUV.p;
+        a.meshRow = c->meshRow.p;
+        a.meshRowLight = c->meshRowLight.p;
+        a.meshMats = c->meshMats.p;
+        a.lights = c->lights.p;
+        a.lightAlias = c->lightAlias.p;
+        a.numLights = (int)c->nLights;
+    }
     a.cam = c->cam;
     a.prevCam = c->prevCam;
     int next = 0;
@@ -688,6 +710,9 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     // otherwise the later segments' kernels would find no live path.
     bool anySpecular = false;
     for (int b = 1; b <= 12; ++b) anySpecular |= !(c->mats[b].roughness > 0.00001f);
+    if (c->nMeshInst > 0)  // instanced meshes in the world: their materials count too
+        for (int b = 13; b < kBlockTypes; ++b)
+            anySpecular |= c->blocks[b].triangles > 0 && !c->mats[b].emissive && !(c->mats[b].roughness > 0.00001f);
     a.segments = (c->diffuseBounce == 1 && !anySpecular) ? 1 : c->totalBounce;
     a.primaryOnly = (flags & VXPT_TRACE_PRIMARY_ONLY) ? 1 : 0;
     a.wb = c->wb;
@@ -1067,7 +1092,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
             dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, 64 + 3 * 16 * 8 * 16) ||
             dalloc(c, w.sCell[0], 4 * ns + 2048) || dalloc(c, w.sT[0], 4 * ns + 2048) ||
             dalloc(c, w.sFace[0], 4 * ns + 2048) || dalloc(c, w.sCell[1], 4 * ns + 2048) ||
-            dalloc(c, w.sT[1], 4 * ns + 2048) || dalloc(c, w.sFace[1], 4 * ns + 2048))
+            dalloc(c, w.sT[1], 4 * ns + 2048) || dalloc(c, w.sFace[1], 4 * ns + 2048) ||
+            dalloc(c, w.sBack, ns) || dalloc(c, w.rLoc, ns) || dalloc(c, w.lLoc0, ns) || dalloc(c, w.lLoc1, ns))
             return VXPT_ERR_HIP;
     }
     // tables
@@ -1310,11 +1336,17 @@ int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int cz
 }
 
 int vxpt_upload_materials(vxpt_ctx *c, const vxpt_material *m, int n) {
-    if (!c || !m || n < 1 || n > 12) return VXPT_ERR_ARG;
+    if (!c || !m || n < 1 || n >= kBlockTypes) return VXPT_ERR_ARG;
     for (int b = 1; b <= n; ++b) {
         const vxpt_material &s = m[b - 1];
+        const MatDev old = c->mats[b];
         c->mats[b] = MatDev{{s.albedo[0], s.albedo[1], s.albedo[2]}, s.roughness, s.translucency, s.metallic,
                             s.material_id, s.thinfilm};
+        if (b > 12) {  // instanced blocks keep their emissive / world-grid set-up (vxpt_load_models)
+            c->mats[b].emissive = old.emissive;
+            c->mats[b].worldGridUV = old.worldGridUV;
+            c->mats[b].uvScale = old.uvScale;
+        }
     }
     return VXPT_OK;
 }
@@ -1690,6 +1722,7 @@ bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> 
 int build_blas(vxpt_ctx *c) {
     c->hBlas.clear();
     c->hBlasTri.clear();
+    c->hBlasUV.clear();
     c->hBlasTriId.clear();
     c->hRoot.assign(kBlockTypes, make_int2(-1, -1));
     for (int b = 0; b < kBlockTypes; ++b) {
@@ -1710,12 +1743,14 @@ int build_blas(vxpt_ctx *c) {
         c->hBlas.insert(c->hBlas.end(), nodes.begin(), nodes.end());
         for (int t : order) {
             c->hBlasTri.insert(c->hBlasTri.end(), bd.pos.begin() + (size_t)t * 9, bd.pos.begin() + (size_t)t * 9 + 9);
+            c->hBlasUV.insert(c->hBlasUV.end(), bd.uv.begin() + (size_t)t * 6, bd.uv.begin() + (size_t)t * 6 + 6);
             c->hBlasTriId.push_back(t);
         }
     }
     if (!c->hBlas.empty()) {
         if (int r = upload_vec(c, c->blas, c->hBlas.data(), c->hBlas.size())) return r;
         if (int r = upload_vec(c, c->blasTri, c->hBlasTri.data(), c->hBlasTri.size())) return r;
+        if (int r = upload_vec(c, c->blasUV, c->hBlasUV.data(), c->hBlasUV.size())) return r;
         if (int r = upload_vec(c, c->blasTriId, c->hBlasTriId.data(), c->hBlasTriId.size())) return r;
     }
     return upload_vec(c, c->blasRoot, c->hRoot.data(), c->hRoot.size());
@@ -1751,7 +1786,23 @@ int refresh_instances(vxpt_ctx *c) {
     if (!c->modelsLoaded) return VXPT_OK;
     collect_instances(c);
     if (int r = build_tlas(c)) return r;
-    return build_lights(c);
+    if (int r = build_lights(c)) return r;
+    // per instance row: cell + block, and its first light record (-1: not an emissive instance)
+    const size_t n = c->instances.size() / 5;
+    if (n == 0) return VXPT_OK;
+    std::vector<int4> rows(n);
+    std::vector<int> rowLight(n, -1);
+    std::map<uint32_t, int> firstLight;
+    for (size_t k = 0; k < c->lightMap.size(); k += 3) firstLight[c->lightMap[k]] = (int)c->lightMap[k + 1];
+    for (size_t i = 0; i < n; ++i) {
+        const int32_t *r = &c->instances[i * 5];
+        rows[i] = make_int4(r[2], r[3], r[4], r[0] + 1);
+        // the light mapping is by instance id within the emissive object's run (closesthit.cu:869-899)
+        const auto it = firstLight.find((uint32_t)r[1]);
+        if (it != firstLight.end() && c->blocks[r[0] + 1].emissive) rowLight[i] = it->second;
+    }
+    if (int r = upload_vec(c, c->meshRow, rows.data(), rows.size())) return r;
+    return upload_vec(c, c->meshRowLight, rowLight.data(), rowLight.size());
 }
 
 static MeshDev mesh_dev(const vxpt_ctx *c) {
@@ -1824,14 +1875,20 @@ int vxpt_load_models(vxpt_ctx *c, const char *root, int *loaded) {
         }
     }
     std::map<std::string, std::map<std::string, std::string>> matProps;
+    std::map<std::string, int> matIndex;  // MaterialParameter.materialId: the material's index in materials.yaml
     {
         std::ifstream f(c->dataDir + "/assets/materials.yaml");
         if (!f) return fail(c, VXPT_ERR_IO, "missing assets/materials.yaml");
         std::string cur;
         while (std::getline(f, line)) {
             const std::string tl = trim(line);
-            if (tl.rfind("- id:", 0) == 0) cur = trim(tl.substr(5));
-            else if (tl.rfind("properties:", 0) == 0) matProps[cur] = parse_flow_map(tl);
+            if (tl.rfind("- id:", 0) == 0) {
+                cur = trim(tl.substr(5));
+                const int k = (int)matIndex.size();
+                matIndex.emplace(cur, k);
+            } else if (tl.rfind("properties:", 0) == 0) {
+                matProps[cur] = parse_flow_map(tl);
+            }
         }
     }
     std::ifstream fb(c->dataDir + "/assets/blocks.yaml");
@@ -1855,6 +1912,24 @@ int vxpt_load_models(vxpt_ctx *c, const char *root, int *loaded) {
         if (as_bool(mp["is_emissive"]) && mp.count("emissive_radiance")) {
             const auto v = parse_list(mp["emissive_radiance"]);
             if (v.size() == 3) std::copy(v.begin(), v.end(), bd.emission);
+        }
+        if (bd.instanced) {
+            // MaterialManager::createMaterialParameter (MaterialManager.cpp:150-190) for the mesh's
+            // shading: an emissive material's albedo is its radiance (no textures on mesh materials here)
+            MatDev md{{1.f, 1.f, 1.f}, 0.5f, 0.0f, 0, matIndex.count(m["material"]) ? matIndex[m["material"]] : 0, 0};
+            if (mp.count("albedo")) {
+                const auto v = parse_list(mp["albedo"]);
+                if (v.size() == 3) std::copy(v.begin(), v.end(), md.albedo);
+            }
+            if (mp.count("roughness")) md.roughness = (float)std::atof(mp["roughness"].c_str());
+            if (mp.count("metallic")) md.metallic = std::atof(mp["metallic"].c_str()) != 0.0;
+            if (mp.count("translucency")) md.translucency = (float)std::atof(mp["translucency"].c_str());
+            if (mp.count("is_thinfilm")) md.thin = as_bool(mp["is_thinfilm"]);
+            if (mp.count("uv_scale")) md.uvScale = (float)std::atof(mp["uv_scale"].c_str());
+            if (mp.count("use_world_grid_uv")) md.worldGridUV = as_bool(mp["use_world_grid_uv"]) ? 1 : 0;
+            md.emissive = as_bool(mp["is_emissive"]) ? 1 : 0;
+            if (md.emissive) std::copy(bd.emission, bd.emission + 3, md.albedo);
+            c->mats[bid] = md;
         }
         if (!bd.instanced || bd.model.empty() || !modelFile.count(bd.model)) continue;
         if (load_obj(dir + "/" + modelFile[bd.model], bd.pos, bd.uv)) {

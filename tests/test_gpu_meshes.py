@@ -1,0 +1,147 @@
+"""Instanced meshes in the path tracer (the rendering half), GPU vs oracle.
+
+The C1 world with lanterns (emissive light mesh + its base, blocks 16 / 15) and leaves (thin-film
+mesh, block 14) placed on the terrain in front of the C1 camera.  The meshes are the synthetic OBJ
+files of test_lights (the reference's assets are not shipped); the materials are the repo's
+data/assets materials.yaml entries, read here independently of the library (MaterialManager.cpp:
+150-190: materialId = the material's index, an emissive material's albedo is its radiance).
+
+Covered against oracle/orc_mesh.cpp + orc_trace.cpp over 4 frames of trace + denoise:
+  closest hit = min(voxel DDA, mesh BVH walk) with back faces culled, ties to the voxel face;
+  mesh-hit shading with the general self-intersection-safe spawn (SelfHit.h:539-656);
+  emissive hits before the first diffuse bounce (closesthit.cu:107-122);
+  thin-film normal flip and front / back spawn choice (closesthit.cu:124-133, 288, 457, 614);
+  8 local-light NEE candidates from the light alias table (closesthit.cu:350-378);
+  BRDF-candidate rays that hit an emissive triangle (closesthit.cu:518-551, 854-900);
+  visibility rays against voxels and meshes, local lights traced to 0.01 short;
+  ReSTIR temporal reuse of local-light reservoirs (Restir.h:383-415).
+"""
+import os
+
+import numpy as np
+import pytest
+import yaml
+
+import oracle
+import vxpt
+from golden.make_golden import C1_CAMERA
+from test_gpu_parity import DN_FLOATS, DN_INTS, _dn_params, _inject_sky, check_radiance
+from test_lights import _base_obj, _prism_obj, _random_mesh_obj
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CH = (2, 1, 2)
+LIGHT, BASE, LEAVES = 16, 15, 14
+
+
+def _idx(x, y, z):
+    return ((x >> 5) + CH[0] * ((z >> 5) + CH[2] * (y >> 5))) * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))
+
+
+def asset_tables():
+    """blocks.yaml + materials.yaml of the repo data: block defs for the instance / light collection and
+    the MaterialParameter of each instanced block."""
+    with open(os.path.join(REPO, "data", "assets", "blocks.yaml")) as f:
+        blocks = {b["id"]: b for b in yaml.safe_load(f)["blocks"]}
+    with open(os.path.join(REPO, "data", "assets", "materials.yaml")) as f:
+        mats = yaml.safe_load(f)["materials"]
+    index = {m["id"]: i for i, m in enumerate(mats)}
+    props = {m["id"]: m.get("properties", {}) for m in mats}
+    defs, params = {}, {}
+    for b, d in blocks.items():
+        if not d.get("instanced"):
+            continue
+        p = props.get(d.get("material"), {})
+        emissive = bool(d.get("emissive")) or bool(p.get("is_emissive"))
+        rad = tuple(p.get("emissive_radiance", (0.0, 0.0, 0.0))) if p.get("is_emissive") else (0.0, 0.0, 0.0)
+        defs[b] = dict(instanced=True, light_base=d.get("light_base", 0), emissive=emissive, radiance=rad)
+        params[b] = dict(albedo=rad if p.get("is_emissive") else tuple(p.get("albedo", (1.0, 1.0, 1.0))),
+                         roughness=p.get("roughness", 0.5), metallic=int(p.get("metallic", 0.0) != 0),
+                         translucency=p.get("translucency", 0.0), material_id=index.get(d.get("material"), 0),
+                         emissive=bool(p.get("is_emissive")), thin=bool(p.get("is_thinfilm")),
+                         world_grid=bool(p.get("use_world_grid_uv")), uv_scale=p.get("uv_scale", 1.0))
+    return defs, params
+
+
+def place_meshes(ids):
+    """Lanterns and leaves on top of the terrain along the C1 camera's view direction."""
+    pos, d = np.array(C1_CAMERA[0]), np.array(C1_CAMERA[1], np.float64)
+    d /= np.linalg.norm(d)
+    placed = []
+    for k, dist in enumerate([6, 8, 10, 12, 14, 16, 18, 21]):
+        p = pos + d * dist
+        x, z = int(p[0]) + (k % 3) - 1, int(p[2])
+        col = [y for y in range(32) if 1 <= ids[_idx(x, y, z)] <= 12]
+        if not col or max(col) + 1 >= 32:
+            continue
+        y = max(col) + 1
+        ids[_idx(x, y, z)] = LEAVES if k % 2 else LIGHT
+        placed.append((x, y, z, int(ids[_idx(x, y, z)])))
+    return placed
+
+
+@pytest.fixture
+def mesh_scene(tmp_path):
+    os.makedirs(tmp_path / "models")
+    _prism_obj(str(tmp_path / "models" / "lanternLight.obj"))
+    _base_obj(str(tmp_path / "models" / "lanternBase.obj"))
+    _random_mesh_obj(str(tmp_path / "models" / "leavesCube4.obj"), n=120)
+    w, h = 128, 96
+    r = vxpt.Renderer(w, h)
+    r.load_settings()
+    o = oracle.Oracle(w, h)
+    o.terrain(CH)
+    ids = o.voxels()
+    placed = place_meshes(ids)
+    assert sum(1 for p in placed if p[3] == LIGHT) >= 2 and sum(1 for p in placed if p[3] == LEAVES) >= 2, placed
+    o.set_voxels(ids, CH)
+    r.upload_voxels(ids, CH)
+    assert r.load_models(tmp_path) >= 3
+    cam = (C1_CAMERA[0], C1_CAMERA[1], C1_CAMERA[2])
+    r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+    r.set_sky(0.25, 45.0, 0.0, 1.0)
+    o.set_camera(*cam[:2], fov=cam[2])
+    o.set_camera(*cam[:2], fov=cam[2], which=1)
+    o.set_denoise_params(DN_FLOATS, DN_INTS)
+    defs, params = asset_tables()
+    for b, p in params.items():
+        o.set_material(b, **p)
+    models = {b: oracle.parse_obj(str(tmp_path / "models" / f)) for b, f in
+              ((LIGHT, "lanternLight.obj"), (BASE, "lanternBase.obj"), (LEAVES, "leavesCube4.obj"))}
+    rows = o.set_meshes(models, defs)
+    _inject_sky(r, o)
+    yield r, o, rows, placed
+    r.close()
+
+
+def test_mesh_scene_matches_oracle(mesh_scene):
+    r, o, rows, placed = mesh_scene
+    inst = r.instances()
+    # the library's instance rows are the oracle's (object, id, x, y, z); rows here are (block, x, y, z, light)
+    np.testing.assert_array_equal(inst[:, 0] + 1, rows[:, 0])
+    np.testing.assert_array_equal(inst[:, 2:5], rows[:, 1:4])
+    mapping, recs, _, _ = r.lights()
+    assert len(recs) == int((rows[:, 4] >= 0).sum()) * 8 and len(recs) > 0
+    p = _dn_params()
+    for f in range(4):
+        r.trace(f)
+        r.denoise(f, f + 1, p)
+        o.trace(f)
+        o.post_trace()
+        o.denoise(f, f + 1)
+        for name in ("DEPTH", "MATERIAL", "NORMAL_ROUGH", "GEO_NORMAL_THIN", "ALBEDO", "MAT_PARAM"):
+            np.testing.assert_allclose(r.read(name), o.read(vxpt.BUF[name]), rtol=1e-6, atol=1e-7,
+                                       err_msg="frame %d %s" % (f, name))
+        check_radiance(r.read("ILLUM"), o.read(0), "meshes frame%d illum" % f)
+        check_radiance(r.read("OUTPUT"), o.read(21), "meshes frame%d output" % f)
+        res_g, res_o = r.read("RESERVOIRS"), o.read(vxpt.BUF["RESERVOIRS"])
+        np.testing.assert_array_equal(res_g["lightData"], res_o["lightData"], err_msg="frame %d lightData" % f)
+    depth, mat, geo = r.read("DEPTH"), r.read("MATERIAL"), r.read("GEO_NORMAL_THIN")
+    # the primary rays see emissive lantern lights (material 0xFFFF at a finite depth) and the thin leaves
+    assert ((mat == 0xFFFF) & (depth < 1e26)).sum() > 0
+    assert (geo[..., 3] == 1.0).sum() > 0
+    # local lights were selected by the reservoirs (light index < number of lights)
+    res = r.read("RESERVOIRS")
+    li = res["lightData"] & 0x7FFFFFFF
+    assert ((res["lightData"] != 0) & (li < len(recs))).sum() > 0
