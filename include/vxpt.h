@@ -193,6 +193,11 @@ int vxpt_get_instances(vxpt_ctx *ctx, int32_t *out, int cap, int *n_instances);
  * (accumulatedLocalLightLuminance); the records are VXPT_BUF_LIGHTS / VXPT_BUF_LIGHT_ALIAS */
 int vxpt_get_lights(vxpt_ctx *ctx, uint32_t *mapping, int cap, int *n_mapped, uint32_t *n_lights,
                     float *local_luminance);
+/* the last light update's previous -> current light index table (VoxelEngine::buildLightIdMapping /
+ * buildIncrementalLightMapping, VoxelEngine.cu:503-633; -1 = the light is gone), its length (the
+ * light count before the update, Scene::m_prevNumLights) and whether the next trace pass still
+ * applies it to the previous reservoirs (Scene::m_lightsJustUpdated, Restir.h:48-79) */
+int vxpt_get_light_remap(vxpt_ctx *ctx, int32_t *remap, int cap, int *prev_num_lights, int *pending);
 /* closest hit against the instanced meshes (the IAS the reference's rays traverse besides the
  * voxel faces; meshes.hip): n rays of 8 floats (origin, tmin, direction, tmax); out 4 floats per ray
  * (t, u, v barycentrics, hit 0/1), ids 2 int32 (instance row of vxpt_get_instances, triangle);
@@ -284,8 +289,29 @@ int vxpt_row_bytes(vxpt_ctx *ctx, int which);
 /* copy `rows` rows starting at row y between a buffer and device memory `dev`
  * (to_buffer = 1: dev -> buffer), enqueued on the context stream */
 int vxpt_copy_rows(vxpt_ctx *ctx, int which, int y, int rows, void *dev, int to_buffer);
-/* kept for ABI compatibility: no-op (the halo exchanges belong to the band schedule below) */
+/* one halo exchange of the band schedule below, for a host-driven schedule over the context's RCCL
+ * communicator: the buffers of buffer_mask (bit b = buffer id b < 32, per-pixel buffers only),
+ * `rows` rows with each band neighbour (vxpt_halo_plan), grouped ncclSend/ncclRecv on the context
+ * stream.  A no-op for one band; VXPT_ERR_STATE without a communicator. */
 int vxpt_exchange_halo(vxpt_ctx *ctx, uint32_t buffer_mask, int rows);
+/* the band partition's pure functions (no context, no GPU): rows [row_begin, row_end) of `rank`
+ * (8-aligned equal bands, the last takes the rest), and the halo plan of a `rows`-deep exchange:
+ * up to 2 entries of 5 int32 (peer, send row, send rows, receive row, receive rows) for the
+ * neighbours rank -/+ 1, both sides of a border moving min(rows, the two band heights) rows */
+int vxpt_band_rows(int height, int nranks, int rank, int *row_begin, int *row_end);
+int vxpt_halo_plan(int height, int nranks, int rank, int rows, int32_t out[10], int *n_entries);
+/* halo depths a banded frame exchanges for a camera that turned from prev to cur between passes:
+ * trace_rows (ReSTIR temporal taps: 64 rows around the reprojected row, >= 72) and history_rows
+ * (the temporal accumulation's bicubic history taps, >= 2).  VXPT_ERR_STATE when the camera
+ * translated (depth-dependent parallax), part of a band falls behind the previous camera, or the
+ * trace halo is deeper than a band: vxpt_render_frame / _linked refuse such a frame the same way. */
+int vxpt_band_halo_rows(const vxpt_camera *cur, const vxpt_camera *prev, int width, int height, int nranks,
+                        int *trace_rows, int *history_rows);
+/* end-of-frame gather: every band's rows of a per-pixel buffer (e.g. VXPT_BUF_OUTPUT, or
+ * VXPT_BUF_FRAME after vxpt_postprocess) into the root rank's buffer, which then holds the whole
+ * frame (RCCL: ncclSend to the root, ncclRecv per band at the root; blocking) */
+int vxpt_band_gather(vxpt_ctx *ctx, int which, int root);
+int vxpt_band_gather_linked(vxpt_ctx **ctxs, int n, int which, int root);
 
 /* Multi-GPU band partition driven by the library (replaces the single-GPU
  * OfflineBackend::renderFrame, OfflineBackend.cpp:46-89, with one band per GPU).  One process
@@ -293,7 +319,8 @@ int vxpt_exchange_halo(vxpt_ctx *ctx, uint32_t buffer_mask, int rows);
  * it, every rank calls vxpt_band_comm_init.  The context then owns rows band_rows(H, nranks,
  * rank) and vxpt_render_frame renders that band, enqueueing every halo exchange (grouped
  * ncclSend/ncclRecv with the neighbours rank +/- 1, rows moved in place) on the context
- * stream.  Bands must be >= 72 rows tall. */
+ * stream.  Bands must be >= 72 rows tall; a camera that turns between frames deepens the
+ * halos (vxpt_band_halo_rows). */
 int vxpt_band_comm_id(void *id, size_t bytes);
 int vxpt_band_comm_init(vxpt_ctx *ctx, const void *id, size_t bytes, int nranks, int rank);
 /* The same schedule over n contexts of one process (tests, one-GPU boxes): context k owns band

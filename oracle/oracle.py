@@ -83,6 +83,7 @@ def lib():
             "orc_mesh_probe": (None, [P, P, P, P, I, P, I, I, P, P]),
             "orc_set_material_flags": (None, [P, I, I, I, I, F]),
             "orc_set_meshes": (None, [P, P, P, P, P, I, P, I, P, I, P, P, P]),
+            "orc_set_light_remap": (None, [P, P, I, I]),
         }
         for k, (r, a) in sig.items():
             fn = getattr(L, k)
@@ -119,6 +120,10 @@ class Oracle:
         for b, r in enumerate(TERRAIN_ROUGHNESS, start=1):
             self.L.orc_set_material(self.h, b, 1.0, 1.0, 1.0, r, 0, 0.0, b - 1)
         self.chunks = None
+        # Scene's light-update state (Scene.h:91-115): light count, update type, the edit sets and
+        # m_instanceToLightRange (only an incremental update refreshes it)
+        self._lights = dict(num=0, incremental=False, changed=set(), removed=set(), range={})
+        self._lights_dirty = False
 
     def set_materials(self, mats):
         """Same list as vxpt.Renderer.upload_materials (block ids 1..len)."""
@@ -135,12 +140,16 @@ class Oracle:
                                 translucency, material_id)
         self.L.orc_set_material_flags(self.h, block, int(emissive), int(thin), int(world_grid), float(uv_scale))
 
-    def set_meshes(self, models, blocks, rows=None):
+    def set_meshes(self, models, blocks, rows=None, light_update="full"):
         """The world's instanced meshes.  models: {block: (pos [T,3,3], uv [T,3,2])};
         blocks: {block: dict(instanced, light_base, emissive, radiance)}; rows: instance rows
         (object, id, x, y, z), collected from this oracle's voxels when None.  The light records
         are generated in the library's order (emissive objects by object id, each instance's
-        triangles in a row) and their alias table built as AliasTable::update does."""
+        triangles in a row) and their alias table built as AliasTable::update does.  light_update: the
+        light update this is -- "full" (scene init / reload), "update" (after light_edit calls; full
+        or incremental as the edits made it), None (an edit of no emissive block: the light table
+        is unchanged and no remap follows); after an update the next trace pass remaps the previous
+        pass's light indices."""
         if rows is None:
             rows = collect_instances(self.voxels(), self.chunks, blocks)
         rows = np.asarray(rows, np.int32).reshape(-1, 5)
@@ -187,7 +196,50 @@ class Oracle:
         self.L.orc_set_meshes(self.h, _p(pos), _p(uv), _p(off), _p(cnt), acc, _p(inst), len(inst), _p(lights), nl,
                               _p(q), _p(pr), _p(al))
         self._mesh_keep = (pos, uv, off, cnt, inst, lights, q, pr, al)
+        ranges = {int(rows[i, 1]): (int(inst[i, 4]), int(cnt[inst[i, 0]])) for i in range(len(rows)) if inst[i, 4] >= 0}
+        if light_update is not None:
+            self._light_update(ranges, int(nl), light_update == "full")
         return inst
+
+    def light_edit(self, instance, removed):
+        """deleteInstancedBlock / addInstancedBlock of an emissive block (VoxelEngine.cu:1206-1212,
+        1278-1284): the next light update is incremental, with `instance` removed or changed."""
+        st = self._lights
+        st["incremental"] = True
+        (st["removed"] if removed else st["changed"]).add(int(instance))
+
+    def _light_update(self, cur, total, full):
+        """VoxelEngine::updateLight (VoxelEngine.cu:658-709) with buildLightIdMapping (:503-539) and
+        buildIncrementalLightMapping (:541-633): the previous light index -> current index table of
+        the next pass (Restir.h:48-79).  cur: {instance id: (first light, count)} of the new table."""
+        st = self._lights
+        if full:
+            st["incremental"] = False
+        prev_n = st["num"]
+        remap = np.full(max(prev_n, 1), -1, np.int32)
+        if prev_n > 0:
+            if st["incremental"]:
+                owner = [None] * prev_n
+                for iid, (off, cnt) in st["range"].items():
+                    for i in range(cnt):
+                        if off + i < prev_n:
+                            owner[off + i] = iid
+                for p in range(prev_n):
+                    iid = owner[p]
+                    if iid is None or iid in st["removed"] or iid in st["changed"] or iid not in cur:
+                        continue
+                    (po, pc), (co, cc) = st["range"][iid], cur[iid]
+                    rel = p - po
+                    if rel < pc and rel < cc and co + rel < total:
+                        remap[p] = co + rel
+                st["range"] = dict(cur)
+            st["changed"].clear()
+            st["removed"].clear()
+        st["num"] = total
+        self._lights_prev = prev_n
+        self._remap_keep = remap
+        self.L.orc_set_light_remap(self.h, _p(remap), prev_n, 1)
+        self._lights_dirty = True
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -241,6 +293,10 @@ class Oracle:
 
     def trace(self, it, y0=0, y1=None, primary_only=False):
         self.L.orc_trace(self.h, it, y0, self.H if y1 is None else y1, int(primary_only))
+        # the light remap holds for the one pass after a light update (OptixRenderer.cpp:451-458)
+        if self._lights_dirty and (y1 is None or y1 >= self.H):
+            self._lights_dirty = False
+            self.L.orc_set_light_remap(self.h, _p(self._remap_keep), 0, 0)
 
     def set_textures(self, chains):
         """chains: list of mip-level lists (level l = (S>>l, S>>l, 4) uint8 RGBA)."""
@@ -384,6 +440,14 @@ def parse_obj(path):
     return pos, uv
 
 
+def instance_id(first, width, obj, x, y, z):
+    """PositionToInstanceId (VoxelMath.h:120-133): first = the first instanced block id, width = the
+    world's x extent; every coordinate clamped to width - 1."""
+    W = width
+    x, y, z = min(x, W - 1), min(y, W - 1), min(z, W - 1)
+    return first + obj * W * W * W + (x + W * (z + W * y))
+
+
 def collect_instances(ids, chunks, blocks):
     """VoxelEngine::collectInstanceTransforms (VoxelEngine.cu:323-384) on a chunk-major id grid.
     blocks: {block id: dict(instanced=bool, light_base=int)}.  Returns int32 [N, 5] rows
@@ -398,8 +462,7 @@ def collect_instances(ids, chunks, blocks):
     by_obj = {}
 
     def iid(obj, x, y, z):
-        x, y, z = min(x, W - 1), min(y, W - 1), min(z, W - 1)
-        return first + obj * W * W * W + (x + W * (z + W * y))
+        return instance_id(first, W, obj, x, y, z)
 
     for obj in range(first - 1, N_BLOCK_TYPES - 1):
         block = obj + 1

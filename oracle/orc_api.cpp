@@ -158,6 +158,13 @@ void orc_trace(void *p, int it, int y0, int y1, int primaryOnly) {
 }
 void orc_post_trace(void *p) { post_trace_copies(static_cast<Ctx *>(p)->f); }
 void orc_set_prev_scene_empty(void *p, int on) { static_cast<Ctx *>(p)->s.prevSceneEmpty = on != 0; }
+// the light-id remap of the next pass (dirty = 0: the pass after it, no remap)
+void orc_set_light_remap(void *p, const int *remap, int prevNumLights, int dirty) {
+    Scene &s = static_cast<Ctx *>(p)->s;
+    s.prevNumLights = prevNumLights;
+    s.lightRemap.assign(remap, remap + (prevNumLights > 0 ? prevNumLights : 0));
+    s.lightsDirty = dirty != 0;
+}
 // textures: nTex mip chains; info per texture = size, maxLod, then maxLod + 1 level offsets (texels)
 void orc_set_textures(void *p, const uint8_t *texels, size_t nTexels, const int *info, int nTex) {
     Scene &s = static_cast<Ctx *>(p)->s;

@@ -12,6 +12,8 @@
 //     float at x>>1 for even x, the high half for odd x; the byte coordinate
 //     clamps to [0, 4W-2], the row to [0, H-1].
 //   * surface reads clamp to the edge (Sampler.h:134-188).
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include "orc_trace.h"
 
@@ -406,6 +408,14 @@ void pass_temporal(const Scene &s, Frame &f, const DenoiseParams &p) {
             f.ping[i] = acc;
             f.pong[i] = F4(accR, 0.0f);
             f.histLen[i] = hist;
+            if (const char *dbg = std::getenv("ORC_DBG_PX")) {
+                int dx = -1, dy = -1;
+                if (std::sscanf(dbg, "%d,%d", &dx, &dy) == 2 && dx == x && dy == y)
+                    std::printf("ORC px %d %d ox %d oy %d est %.9g t0 %.9g bic %g taps %g %g %g %g found %g q %.9g hist %.9g "
+                                "prevI %.9g %.9g %.9g illum %.9g %.9g %.9g pnr.n %.9g\n", x, y, ox, oy, estDepth, t0, bicValid,
+                                tapsValid[0], tapsValid[1], tapsValid[2], tapsValid[3], found, quality, hist, prevI.x, prevI.y,
+                                prevI.z, illum.x, illum.y, illum.z, dot(nIn, pnr));
+            }
         }
 }
 
@@ -450,7 +460,7 @@ void pass_history_fix(const Scene &s, Frame &f) {
 
 // ---------------------------------------------------------------- D5
 void pass_history_clamp(Frame &f) {
-    const int W = f.W, H = f.H;
+    const int W = f.W;
 #pragma omp parallel for schedule(dynamic, 4)
     for (int y = f.by0(); y < f.by1(); ++y)
         for (int x = 0; x < W; ++x) {

@@ -405,9 +405,22 @@ void store_reservoir(Px &c, const Reservoir &r) {
     size_t p = c.idx() + (size_t)(c.it % 2) * c.f.W * c.f.H;
     c.f.reservoir[p] = r;
 }
+// LoadDIReservoir (Restir.h:48-79): in the pass after a light update the previous pass's local-light
+// indices go through the update's remap; a light that is gone empties the reservoir.  Taken
+// literally: an empty reservoir (lightData 0) reads as index 0 and is remapped as well.
 Reservoir load_prev_reservoir(Px &c, int x, int y) {
     size_t p = (size_t)x + (size_t)y * c.f.W + (size_t)((c.it + 1) % 2) * c.f.W * c.f.H;
-    return c.f.reservoir[p];
+    Reservoir r = c.f.reservoir[p];
+    const Scene &s = c.s;
+    if (!s.lightsDirty) return r;
+    const uint32_t li = r.lightData & 0x7FFFFFFFu;
+    if (li >= 0x7FFFFFFDu) return r;  // sun / sky: unchanged
+    if (s.prevNumLights > 0 && li < (uint32_t)s.prevNumLights) {
+        const int cur = s.lightRemap[li];
+        if (cur < 0 || cur >= s.mesh.numLights) return Reservoir{};
+        r.lightData = (r.lightData & 0x80000000u) | (uint32_t)cur;
+    }
+    return r;
 }
 
 // Closest hit over the voxel faces and the instanced meshes (one IAS in the reference): a mesh

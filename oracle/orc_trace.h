@@ -100,7 +100,12 @@ struct Scene {
     // the pass after a geometry change: prevTopObject = 0 (OptixRenderer.cpp:916-919, 464), so the
     // ReSTIR temporal visibility rays (closesthit.cu:736-755) traverse no scene and see the light
     bool prevSceneEmpty = false;
-    std::vector<uint8_t> texels;      // RGBA8 of every texture's mip chain
+    // the pass after a light update (VoxelEngine.cu:658-709, OptixRenderer.cpp:447-457): the previous
+    // pass's light index i < prevNumLights becomes lightRemap[i] (-1: gone)
+    bool lightsDirty = false;
+    int prevNumLights = 0;
+    std::vector<int> lightRemap;
+    std::vector<uint8_t> texels;     // RGBA8 of every texture's mip chain
     std::vector<Texture> textures;    // empty: untextured shading
 };
 

@@ -20,8 +20,10 @@ with the exchanges inserted:
 
 The rows are moved by a transport: DistExchange (torch.distributed: RCCL over
 xGMI on GPUs, gloo on CPU) or LocalExchange (bands of one process; tests).
-Bands must be at least TRACE_HALO rows tall.  The reprojection offset of the
-temporal taps is assumed <= 8 rows (the offline camera is static).
+Bands must be at least TRACE_HALO rows tall.  This host-driven schedule assumes a
+static camera (reprojection offsets <= 8 rows); the library's own schedule
+(vxpt_render_frame with a communicator, vxpt_render_frame_linked) deepens its halos
+for a camera that turns between frames (vxpt_band_halo_rows).
 """
 import numpy as np
 

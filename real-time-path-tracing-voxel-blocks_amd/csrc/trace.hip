@@ -816,6 +816,20 @@ __global__ __launch_bounds__(256) void k_nee(TraceArgs a, int seg) {
 
 // visibility of the RIS sample; seg 0: ReSTIR temporal reuse (Restir.h:11-415,
 // closesthit.cu:626-851) up to its visibility rays; seg > 0: final shading.
+// LoadDIReservoir (Restir.h:48-79): the previous pass's reservoir, its local-light index remapped
+// in the pass after a light update (a light that is gone empties it).  Taken literally: an empty
+// reservoir (lightData 0) reads as index 0 and is remapped as well.
+VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) {
+    Reservoir r = a.resPrev[i];
+    if (!a.lightsDirty) return r;
+    const uint32_t li = r.lightData & 0x7FFFFFFFu;
+    if (li >= 0x7FFFFFFDu || li >= (uint32_t)a.prevNumLights) return r;  // sun / sky, or not a previous light
+    const int cur = a.lightRemap[li];
+    if (cur < 0 || cur >= a.numLights) return empty_res();
+    r.lightData = (r.lightData & 0x80000000u) | (uint32_t)cur;
+    return r;
+}
+
 template <bool MESH>
 VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
@@ -882,7 +896,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
         if (!(nOk && dOk && rOk)) continue;
         cached |= (1u << i);
-        Reservoir pr = a.resPrev[(size_t)y * a.W + x];
+        Reservoir pr = load_prev_res(a, (size_t)y * a.W + x);
         if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
         if (pr.M > 20.0f) pr.M = 20.0f;
         if (i == 0) tapM0 = pr.M; else if (i == 1) tapM1 = pr.M; else tapM2 = pr.M;

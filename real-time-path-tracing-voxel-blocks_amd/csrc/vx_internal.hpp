@@ -203,6 +203,11 @@ struct TraceArgs {
     const LightInfo *lights;    // emissive-triangle lights (VoxelEngine.cu:53-116)
     const AliasBin *lightAlias;
     int numLights;
+    // LoadDIReservoir's remap (Restir.h:48-79): in the pass after a light update (lightsDirty) the
+    // previous reservoirs' light index i < prevNumLights becomes lightRemap[i] (-1: empty reservoir)
+    const int *lightRemap;
+    int prevNumLights;
+    int lightsDirty;
 };
 
 // kernel launchers (defined in the .hip translation units)

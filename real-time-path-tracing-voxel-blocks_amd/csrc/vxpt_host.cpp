@@ -20,6 +20,7 @@
 #include <map>
 #include <queue>
 #include <random>
+#include <set>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -201,6 +202,14 @@ struct vxpt_ctx {
     DBuf<int> lightInst;
     unsigned nLights = 0;
     float localLightLum = 0.0f;
+    // light-update state (Scene.h:91-115): the update type, the edits' instance sets, the instance ->
+    // (first light, count) table of the last incremental update, and the remap the next pass applies
+    bool lightIncremental = false;
+    std::set<uint32_t> lightChanged, lightRemoved;
+    std::map<uint32_t, std::pair<uint32_t, uint32_t>> instLightRange;
+    unsigned prevNumLights = 0;
+    int lightsDirty = 0;
+    DBuf<int> lightRemap;
     // two-level BVH of the instanced meshes (meshes.hip): BLAS per block type, TLAS per world
     std::vector<BvhNode> hBlas;
     std::vector<float> hBlasTri;
@@ -219,6 +228,10 @@ struct vxpt_ctx {
     DBuf<int4> meshRow;
     DBuf<int> meshRowLight;
     DBuf<MatDev> meshMats;
+    // vxpt_mesh_probe / vxpt_mesh_occluded scratch (grown to the largest call)
+    DBuf<float> probeRays, probeOut;
+    DBuf<int> probeIds;
+    DBuf<unsigned char> probeOcc;
 
     // blue noise
     DBuf<uint8_t> bnSobol, bnScramble, bnRank;
@@ -268,6 +281,7 @@ struct vxpt_ctx {
     // pass up to its temporal-reuse kernel (haloDone: recorded after the exchange)
     hipStream_t commStream = nullptr;
     hipEvent_t haloReady = nullptr, haloDone = nullptr;
+    int haloTraceRows = 72, haloHistRows = 2;  // halo depths the last banded frame exchanged
     bool haloPending = false;
 };
 
@@ -298,6 +312,14 @@ bool read_file(const std::string &p, std::vector<uint8_t> &out) {
     if (!f) return false;
     out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
     return true;
+}
+
+template <class T>
+int grow(vxpt_ctx *c, DBuf<T> &d, size_t n) {
+    if (d.n >= n) return 0;
+    if (dalloc(c, d.p, n)) return 1;
+    d.n = n;
+    return 0;
 }
 
 template <class T>
@@ -722,6 +744,11 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
     a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
     a.prevSceneEmpty = c->prevSceneEmpty;
+    // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
+    a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;
+    a.prevNumLights = (int)c->prevNumLights;
+    a.lightRemap = c->lightRemap.p;
+    c->lightsDirty = 0;
     a.tex = c->texTable.p;
     a.texels = c->texels.p;
     a.texEnabled = (c->texEnabled && c->texTable.p) ? 1 : 0;
@@ -864,6 +891,68 @@ std::vector<Halo> halo_plan(int H, int world, int rank, int rows) {
     return plan;
 }
 
+// Halo depths of a banded frame whose camera moved between passes (cur vs prev).  A band's
+// pixels reproject to rows prevCam.dir_to_uv(cam ray).y * H: the ReSTIR temporal taps read the
+// previous pass's G-buffer and reservoirs within 64 rows of that row (Restir.h:348-381, truncated
+// row), the temporal accumulation its histories within its bicubic footprint (-1..+2 around
+// floor(row - 0.5), TemporalAccumulation.h:29-215).  For a rotation the reprojection does not
+// depend on depth: the extreme rows over the band come from the pixel corners on the band's first
+// and last row boundaries (all columns) plus a 33-column grid over every row; 2 rows of margin
+// cover host/device rounding.  A translated camera makes it depth dependent (unbounded parallax
+// for near surfaces): refused, as is a point behind the previous camera or a halo deeper than a
+// neighbouring band (the plan only reaches ranks r +/- 1).  An unmoved camera keeps the static
+// depths (72 / 2).
+bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, int world, int &traceRows, int &histRows,
+                    std::string &err) {
+    traceRows = kTraceHalo;
+    histRows = 2;
+    if (world <= 1) return true;
+    if (std::memcmp(&cam, &pc, sizeof(CamDev)) == 0) return true;
+    if (cam.pos.x != pc.pos.x || cam.pos.y != pc.pos.y || cam.pos.z != pc.pos.z) {
+        err = "banded frames need a camera that does not translate between passes (depth-dependent reprojection)";
+        return false;
+    }
+    int minBand = H;
+    float reach = 0.0f;  // rows beyond its band any band pixel reprojects to
+    for (int r = 0; r < world; ++r) {
+        int y0, y1;
+        band_rows(H, world, r, y0, y1);
+        if (y1 <= y0) continue;
+        minBand = std::min(minBand, y1 - y0);
+        float lo = 1e30f, hi = -1e30f;
+        bool behind = false;
+        auto sample = [&](float u, float v) {
+            const V3 d = cam.uv_to_dir(V2(u, v));
+            const V3 n = m3_apply(pc.worldToUv, d);
+            if (!(n.z > 0.0f)) { behind = true; return; }
+            const float py = n.y / n.z * (float)H;
+            lo = std::min(lo, py);
+            hi = std::max(hi, py);
+        };
+        for (int x = 0; x <= W; ++x) {
+            sample((float)x / (float)W, (float)y0 / (float)H);
+            sample((float)x / (float)W, (float)y1 / (float)H);
+        }
+        for (int y = y0; y <= y1; ++y)
+            for (int k = 0; k <= 32; ++k) sample((float)k / 32.0f, (float)y / (float)H);
+        if (behind) {
+            err = "the camera turned so far that part of a band lies behind the previous camera";
+            return false;
+        }
+        if (r > 0) reach = std::max(reach, (float)y0 - lo);
+        if (r < world - 1) reach = std::max(reach, hi - (float)y1);
+    }
+    const int d = (int)std::ceil(std::max(reach, 0.0f)) + 2;
+    traceRows = std::max(kTraceHalo, 64 + d + 1);
+    histRows = std::max(2, d + 2);
+    if (traceRows > minBand) {
+        err = "the camera moved " + std::to_string(d) + " rows between passes: a " + std::to_string(traceRows) +
+              "-row halo exceeds the " + std::to_string(minBand) + "-row bands";
+        return false;
+    }
+    return true;
+}
+
 char *buffer_rows(vxpt_ctx *c, int which, int y, size_t &rowBytes) {
     void *p, *mirror;
     size_t n;
@@ -944,12 +1033,32 @@ int atrous_rows(int step) { return step + (step > 4 ? step / 4 : 0); }  // Atrou
 // One banded OfflineBackend::renderFrame over cs (vxpt_render_frame's order).
 int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int frame, int spp) {
     const int it0 = frame * spp;
+    // halo depths for this frame's camera motion; the previous frame exchanged its last pass's
+    // rows and the histories for its own camera: top them up before the first pass reads them
+    int traceRows = kTraceHalo, histRows = 2;
+    {
+        vxpt_ctx *c0 = cs[0];
+        std::string err;
+        if (!band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err))
+            return fail(c0, VXPT_ERR_STATE, err.c_str());
+    }
+    if (frame > 0 && (traceRows > cs[0]->haloTraceRows || histRows > cs[0]->haloHistRows)) {
+        std::vector<std::pair<int, int>> br;
+        for (int b : kGbufBufs) br.emplace_back(b, traceRows);
+        br.emplace_back(((it0 - 1) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows);
+        for (int b : kHistoryBufs) br.emplace_back(b, histRows);
+        BANDCHK(exchange_set(cs, br, false));
+    }
+    for (vxpt_ctx *c : cs) {
+        c->haloTraceRows = traceRows;
+        c->haloHistRows = histRows;
+    }
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
         FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp));
         std::vector<std::pair<int, int>> br;
-        for (int b : kGbufBufs) br.emplace_back(b, kTraceHalo);
-        br.emplace_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, kTraceHalo);
+        for (int b : kGbufBufs) br.emplace_back(b, traceRows);
+        br.emplace_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows);
         if (s + 1 < spp) {
             // all but the last pass: overlapped with the next pass up to its temporal reuse
             BANDCHK(exchange_set(cs, br, true));
@@ -969,12 +1078,12 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     if (!p->enable_firefly_filter) FOR_BANDS(run_pass(c, p, 11, 0, 0));
     if (p->enable_firefly_filter) {  // + world positions
         FOR_BANDS(run_pass(c, p, 0, used & 1, 0));
-        BANDCHK(exchange_set(cs, {{(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, kTraceHalo}, {VXPT_BUF_ILLUM, 2}}));
+        BANDCHK(exchange_set(cs, {{(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows}, {VXPT_BUF_ILLUM, 2}}));
     }
     const std::vector<int> hist(std::begin(kHistoryBufs), std::end(kHistoryBufs));
     if (frame == 0) {
         FOR_BANDS(run_pass(c, p, 12, 0, 0));
-        BANDCHK(exchange(cs, hist, 2));
+        BANDCHK(exchange(cs, hist, histRows));
     }
     int fin = 0;
     if (p->enable_temporal_accumulation && frame > 0) {
@@ -989,7 +1098,7 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         }
         if (p->enable_history_clamping) {
             FOR_BANDS(run_pass(c, p, 4, 0, 0));
-            BANDCHK(exchange(cs, hist, 2));
+            BANDCHK(exchange(cs, hist, histRows));
             fin = 3;
         }
     }
@@ -1321,7 +1430,7 @@ int vxpt_generate_terrain(vxpt_ctx *c, int cxn, int cyn, int czn, float heightSc
     return vxpt_upload_voxels(c, ids.data(), cxn, cyn, czn);
 }
 
-int refresh_instances(vxpt_ctx *c);  // instanced meshes + lights, after the grid changed
+int refresh_instances(vxpt_ctx *c, bool lights, bool full);  // instanced meshes (+ lights), after the grid changed
 
 int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int czn) {
     if (!c || !ids || cxn <= 0 || cyn <= 0 || czn <= 0) return VXPT_ERR_ARG;
@@ -1332,7 +1441,7 @@ int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int cz
     if (int r = upload_vec(c, c->voxels, c->hIds.data(), n)) return r;
     if (int r = build_occupancy(c, c->hIds.data())) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return refresh_instances(c);
+    return refresh_instances(c, true, true);
 }
 
 int vxpt_upload_materials(vxpt_ctx *c, const vxpt_material *m, int n) {
@@ -1494,6 +1603,17 @@ namespace {
 // (VoxelMath.h:120-133: first instanced block + object * W^3 + x + W * (z + W * y), every
 // coordinate clamped to W - 1, W = the world's x extent); ids are kept in a set per object
 // (Scene.h:77) and a later cell with the same id overwrites the transform.
+uint32_t instance_id(const vxpt_ctx *c, unsigned obj, unsigned x, unsigned y, unsigned z) {
+    int first = kBlockTypes;
+    for (int b = 0; b < kBlockTypes; ++b)
+        if (c->blocks[b].instanced) { first = b; break; }
+    const unsigned W = (unsigned)c->cx * 32u;
+    x = x < W - 1 ? x : W - 1;
+    y = y < W - 1 ? y : W - 1;
+    z = z < W - 1 ? z : W - 1;
+    return (unsigned)first + obj * W * W * W + (x + W * (z + W * y));
+}
+
 void collect_instances(vxpt_ctx *c) {
     c->instances.clear();
     if (c->hIds.empty()) return;
@@ -1502,12 +1622,7 @@ void collect_instances(vxpt_ctx *c) {
         if (c->blocks[b].instanced) { first = b; break; }
     const unsigned W = (unsigned)c->cx * 32u, H = (unsigned)c->cy * 32u, D = (unsigned)c->cz * 32u;
     std::map<int, std::map<unsigned, std::array<unsigned, 3>>> byObject;
-    auto inst_id = [&](unsigned obj, unsigned x, unsigned y, unsigned z) {
-        x = x < W - 1 ? x : W - 1;
-        y = y < W - 1 ? y : W - 1;
-        z = z < W - 1 ? z : W - 1;
-        return (unsigned)first + obj * W * W * W + (x + W * (z + W * y));
-    };
+    auto inst_id = [&](unsigned obj, unsigned x, unsigned y, unsigned z) { return instance_id(c, obj, x, y, z); };
     // one pass over the cells: what each block id contributes (its own object; a base block
     // also the objects of the lights paired with it; a paired light also its base's object)
     std::vector<int> contrib[kBlockTypes];
@@ -1782,11 +1897,59 @@ int build_tlas(vxpt_ctx *c) {
     return upload_vec(c, c->meshInst, sorted.data(), sorted.size());
 }
 
-int refresh_instances(vxpt_ctx *c) {
+// VoxelEngine::updateLight (VoxelEngine.cu:658-709) after the light table was rebuilt from
+// prevN lights: buildLightIdMapping (:503-539) -- every previous light unmapped, and for an
+// incremental update buildIncrementalLightMapping (:541-633): a light keeps its position within
+// its instance's run unless the instance was removed or changed; the instance -> range table is
+// only refreshed by an incremental update, so the first one after a full build maps nothing.
+// The edit sets are cleared only when there were previous lights.  The next trace pass applies
+// the table (Restir.h:48-79).
+int light_update(vxpt_ctx *c, unsigned prevN) {
+    std::vector<int> remap(prevN, -1);
+    if (prevN > 0) {
+        if (c->lightIncremental) {
+            std::map<uint32_t, std::pair<uint32_t, uint32_t>> cur;
+            for (size_t k = 0; k < c->lightMap.size(); k += 3)
+                cur[c->lightMap[k]] = {c->lightMap[k + 1], c->lightMap[k + 2]};
+            std::vector<int64_t> owner(prevN, -1);
+            for (const auto &e : c->instLightRange)
+                for (uint32_t i = 0; i < e.second.second; ++i)
+                    if (e.second.first + i < prevN) owner[e.second.first + i] = e.first;
+            for (unsigned p = 0; p < prevN; ++p) {
+                if (owner[p] < 0) continue;
+                const uint32_t id = (uint32_t)owner[p];
+                if (c->lightRemoved.count(id) || c->lightChanged.count(id)) continue;
+                const auto it = cur.find(id);
+                if (it == cur.end()) continue;
+                const auto &pr = c->instLightRange[id];
+                const uint32_t rel = p - pr.first;
+                if (rel < pr.second && rel < it->second.second && it->second.first + rel < c->nLights)
+                    remap[p] = (int)(it->second.first + rel);
+            }
+            c->instLightRange = cur;
+        }
+        c->lightChanged.clear();
+        c->lightRemoved.clear();
+        if (int r = upload_vec(c, c->lightRemap, remap.data(), remap.size())) return r;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    c->prevNumLights = prevN;
+    c->lightsDirty = 1;
+    return VXPT_OK;
+}
+
+// lights: rebuild the light table as a light update (full: scene init / reload; otherwise of the
+// type the edits made it), or keep it (an edit of no emissive block, VoxelEngine.cu:1206, 1278)
+int refresh_instances(vxpt_ctx *c, bool lights, bool full) {
     if (!c->modelsLoaded) return VXPT_OK;
     collect_instances(c);
     if (int r = build_tlas(c)) return r;
-    if (int r = build_lights(c)) return r;
+    if (lights) {
+        if (full) c->lightIncremental = false;
+        const unsigned prevN = c->nLights;
+        if (int r = build_lights(c)) return r;
+        if (int r = light_update(c, prevN)) return r;
+    }
     // per instance row: cell + block, and its first light record (-1: not an emissive instance)
     const size_t n = c->instances.size() / 5;
     if (n == 0) return VXPT_OK;
@@ -1818,21 +1981,13 @@ int vxpt_mesh_probe(vxpt_ctx *c, const float *rays, int n, int cull, float *out,
     if (c->hRoot.empty()) c->hRoot.assign(kBlockTypes, make_int2(-1, -1));
     if (!c->blasRoot.p)
         if (int r = upload_vec(c, c->blasRoot, c->hRoot.data(), c->hRoot.size())) return r;
-    float *dr = nullptr, *dout = nullptr;
-    int *dids = nullptr;
-    // scratch of this call only (freed below; dalloc's buffers live as long as the context)
-    HIPCHK(c, hipMalloc((void **)&dr, (size_t)n * 32));
-    HIPCHK(c, hipMalloc((void **)&dout, (size_t)n * 16));
-    HIPCHK(c, hipMalloc((void **)&dids, (size_t)n * 8));
-    HIPCHK(c, hipMemcpyAsync(dr, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    const MeshDev m = mesh_dev(c);
-    HIPCHK(c, launch_mesh_probe(m, dr, n, cull, dout, dids, c->stream));
-    HIPCHK(c, hipMemcpyAsync(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ids, dids, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    // the probe's scratch grows with the largest call and lives with the context
+    if (int r = upload_vec(c, c->probeRays, rays, (size_t)n * 8)) return r;
+    if (grow(c, c->probeOut, (size_t)n * 4) || grow(c, c->probeIds, (size_t)n * 2)) return VXPT_ERR_HIP;
+    HIPCHK(c, launch_mesh_probe(mesh_dev(c), c->probeRays.p, n, cull, c->probeOut.p, c->probeIds.p, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, c->probeOut.p, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ids, c->probeIds.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    hipFree(dr);
-    hipFree(dout);
-    hipFree(dids);
     return VXPT_OK;
 }
 
@@ -1845,16 +2000,11 @@ int vxpt_mesh_occluded(vxpt_ctx *c, const float *rays, int n, uint8_t *occluded)
     if (c->hRoot.empty()) c->hRoot.assign(kBlockTypes, make_int2(-1, -1));
     if (!c->blasRoot.p)
         if (int r = upload_vec(c, c->blasRoot, c->hRoot.data(), c->hRoot.size())) return r;
-    float *dr = nullptr;
-    unsigned char *dout = nullptr;
-    HIPCHK(c, hipMalloc((void **)&dr, (size_t)n * 32));
-    HIPCHK(c, hipMalloc((void **)&dout, (size_t)n));
-    HIPCHK(c, hipMemcpyAsync(dr, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, launch_mesh_occluded(mesh_dev(c), dr, n, dout, c->stream));
-    HIPCHK(c, hipMemcpyAsync(occluded, dout, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    if (int r = upload_vec(c, c->probeRays, rays, (size_t)n * 8)) return r;
+    if (grow(c, c->probeOcc, (size_t)n)) return VXPT_ERR_HIP;
+    HIPCHK(c, launch_mesh_occluded(mesh_dev(c), c->probeRays.p, n, c->probeOcc.p, c->stream));
+    HIPCHK(c, hipMemcpyAsync(occluded, c->probeOcc.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    hipFree(dr);
-    hipFree(dout);
     return VXPT_OK;
 }
 
@@ -1943,7 +2093,7 @@ int vxpt_load_models(vxpt_ctx *c, const char *root, int *loaded) {
     if (loaded) *loaded = nLoaded;
     HIPCHK(c, hipSetDevice(c->dev));
     if (int r = build_blas(c)) return r;
-    return refresh_instances(c);
+    return refresh_instances(c, true, true);
 }
 
 int vxpt_get_model(vxpt_ctx *c, int block_id, float *pos, float *uv, int cap_triangles, int *n_triangles) {
@@ -1961,6 +2111,19 @@ int vxpt_get_instances(vxpt_ctx *c, int32_t *out, int cap, int *n_instances) {
     const int n = (int)(c->instances.size() / 5);
     if (n_instances) *n_instances = n;
     if (out) std::copy(c->instances.begin(), c->instances.begin() + (size_t)std::min(cap, n) * 5, out);
+    return VXPT_OK;
+}
+
+int vxpt_get_light_remap(vxpt_ctx *c, int32_t *remap, int cap, int *prev_num_lights, int *pending) {
+    if (!c || cap < 0) return VXPT_ERR_ARG;
+    if (prev_num_lights) *prev_num_lights = (int)c->prevNumLights;
+    if (pending) *pending = c->lightsDirty;
+    const int n = std::min(cap, (int)c->prevNumLights);
+    if (remap && n > 0) {
+        HIPCHK(c, hipSetDevice(c->dev));
+        HIPCHK(c, hipMemcpyAsync(remap, c->lightRemap.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     return VXPT_OK;
 }
 
@@ -2062,9 +2225,25 @@ int vxpt_set_block(vxpt_ctx *c, int x, int y, int z, int block_id) {
         old = c->hIds[ch * 32768 + (x & 31) + 32 * ((z & 31) + 32 * (y & 31))];
     }
     if (int r = set_block(c, x, y, z, block_id)) return r;
-    // the instance set (and the light table) only changes with an instanced block
+    // the instance set only changes with an instanced block
     const auto inst = [&](int id) { return id > 0 && id < kBlockTypes && c->blocks[id].instanced; };
-    return (inst(old) || inst(block_id)) ? refresh_instances(c) : VXPT_OK;
+    if (!inst(old) && !inst(block_id)) return VXPT_OK;
+    // deleteInstancedBlock / addInstancedBlock of an emissive block (VoxelEngine.cu:1206-1212,
+    // 1278-1284): an incremental light update with the light instance removed / changed.  A light
+    // base alone also carries its light's instance here (the instance set is always the grid's,
+    // collectInstanceTransforms), so its edit counts as that light's.
+    const auto light_obj = [&](int id) {
+        if (!inst(id) || !c->modelsLoaded) return -1;
+        if (c->blocks[id].emissive) return id - 1;
+        for (int l = 1; l < kBlockTypes; ++l)
+            if (c->blocks[l].instanced && c->blocks[l].emissive && c->blocks[l].lightBase == id) return l - 1;
+        return -1;
+    };
+    const int lo = old != block_id ? light_obj(old) : -1, ln = old != block_id ? light_obj(block_id) : -1;
+    if (lo >= 0) c->lightRemoved.insert(instance_id(c, lo, x, y, z));
+    if (ln >= 0) c->lightChanged.insert(instance_id(c, ln, x, y, z));
+    if (lo >= 0 || ln >= 0) c->lightIncremental = true;
+    return refresh_instances(c, lo >= 0 || ln >= 0, false);
 }
 
 // VoxelEngine::update's click (VoxelEngine.cu:906-975): block 0 deletes the picked block,
@@ -2288,7 +2467,25 @@ int vxpt_copy_rows(vxpt_ctx *c, int which, int y, int rows, void *dev, int to_bu
     return VXPT_OK;
 }
 
-int vxpt_exchange_halo(vxpt_ctx *c, uint32_t, int) { return c ? VXPT_OK : VXPT_ERR_ARG; }
+// the halo exchange of the band schedule for the buffers of `mask` (bit b = buffer id b < 32), over the
+// context's RCCL communicator, enqueued on its stream
+int vxpt_exchange_halo(vxpt_ctx *c, uint32_t mask, int rows) {
+    if (!c || rows < 0) return VXPT_ERR_ARG;
+    if (c->nranks <= 1 || mask == 0 || rows == 0) return VXPT_OK;
+    if (!c->comm) return fail(c, VXPT_ERR_STATE, "no band communicator (vxpt_band_comm_init; linked contexts exchange inside vxpt_render_frame_linked)");
+    std::vector<std::pair<int, int>> br;
+    for (int b = 0; b < 32; ++b) {
+        if (!((mask >> b) & 1u)) continue;
+        void *ptr, *mirror;
+        size_t n;
+        if (!buffer_ptr(c, b, ptr, n, false, &mirror) || b == VXPT_BUF_RESERVOIRS)
+            return fail(c, VXPT_ERR_ARG, "buffer has no row layout");
+        br.emplace_back(b, rows);
+    }
+    HIPCHK(c, hipSetDevice(c->dev));
+    std::vector<vxpt_ctx *> cs{c};
+    return exchange_set(cs, br, false);
+}
 
 // ProjectSunToScreen (PostProcessingPipeline.cu:187-206) on the host, like the reference;
 // sunLuminance = SkyModel::getAccumulatedSunLuminance, 1 when not positive (:569-571)
@@ -2470,6 +2667,99 @@ int vxpt_band_link(vxpt_ctx **cs, int n) {
         if (int r = vxpt_set_band(c, y0, y1)) return r;
     }
     return VXPT_OK;
+}
+
+// Every band's rows of a buffer into the root's buffer (the frame's output for one writer).  RCCL:
+// grouped ncclSend to the root / ncclRecv of each band at the root, on the context streams.
+namespace {
+int band_gather(std::vector<vxpt_ctx *> &cs, int which, int root) {
+    vxpt_ctx *c0 = cs[0];
+    const int world = c0->nranks;
+    if (root < 0 || root >= world) return fail(c0, VXPT_ERR_ARG, "root rank out of range");
+    {
+        void *ptr, *mirror;
+        size_t n;
+        if (!buffer_ptr(c0, which, ptr, n, false, &mirror) || which == VXPT_BUF_RESERVOIRS || (which >= 32 && which <= 34))
+            return fail(c0, VXPT_ERR_ARG, "buffer has no row layout (or is not allocated yet)");
+    }
+    if (cs.size() == 1 && c0->comm) {
+        size_t rb;
+        if (ncclGroupStart() != ncclSuccess) return fail(c0, VXPT_ERR_HIP, "ncclGroupStart");
+        if (c0->rank == root) {
+            for (int r = 0; r < world; ++r) {
+                int y0, y1;
+                band_rows(c0->H, world, r, y0, y1);
+                if (r == root || y1 <= y0) continue;
+                char *dst = buffer_rows(c0, which, y0, rb);
+                ncclRecv(dst, (size_t)(y1 - y0) * rb, ncclUint8, r, c0->comm, c0->stream);
+            }
+        } else if (c0->rowEnd > c0->rowBegin) {
+            char *src = buffer_rows(c0, which, c0->rowBegin, rb);
+            ncclSend(src, (size_t)(c0->rowEnd - c0->rowBegin) * rb, ncclUint8, root, c0->comm, c0->stream);
+        }
+        if (ncclGroupEnd() != ncclSuccess) return fail(c0, VXPT_ERR_HIP, "ncclGroupEnd (gather)");
+        HIPCHK(c0, hipStreamSynchronize(c0->stream));
+        return VXPT_OK;
+    }
+    for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
+    vxpt_ctx *dst = cs[root];
+    for (int r = 0; r < (int)cs.size(); ++r) {
+        if (r == root || cs[r]->rowEnd <= cs[r]->rowBegin) continue;
+        size_t rb;
+        char *d = buffer_rows(dst, which, cs[r]->rowBegin, rb);
+        const char *src = buffer_rows(cs[r], which, cs[r]->rowBegin, rb);
+        HIPCHK(dst, hipMemcpyAsync(d, src, (size_t)(cs[r]->rowEnd - cs[r]->rowBegin) * rb, hipMemcpyDeviceToDevice,
+                                   dst->stream));
+    }
+    HIPCHK(dst, hipStreamSynchronize(dst->stream));
+    return VXPT_OK;
+}
+}  // namespace
+
+int vxpt_band_gather(vxpt_ctx *c, int which, int root) {
+    if (!c) return VXPT_ERR_ARG;
+    if (c->nranks <= 1) return VXPT_OK;
+    if (!c->comm) return fail(c, VXPT_ERR_STATE, "no band communicator (linked contexts: vxpt_band_gather_linked)");
+    HIPCHK(c, hipSetDevice(c->dev));
+    std::vector<vxpt_ctx *> cs{c};
+    return band_gather(cs, which, root);
+}
+
+int vxpt_band_gather_linked(vxpt_ctx **cs, int n, int which, int root) {
+    if (!cs || n < 1) return VXPT_ERR_ARG;
+    for (int k = 0; k < n; ++k)
+        if (!cs[k] || cs[k]->rank != k || cs[k]->nranks != n) return VXPT_ERR_STATE;
+    if (n == 1) return VXPT_OK;
+    HIPCHK(cs[0], hipSetDevice(cs[0]->dev));
+    std::vector<vxpt_ctx *> v(cs, cs + n);
+    return band_gather(v, which, root);
+}
+
+int vxpt_band_rows(int height, int nranks, int rank, int *row_begin, int *row_end) {
+    if (height < 1 || nranks < 1 || rank < 0 || rank >= nranks || !row_begin || !row_end) return VXPT_ERR_ARG;
+    band_rows(height, nranks, rank, *row_begin, *row_end);
+    return VXPT_OK;
+}
+
+int vxpt_halo_plan(int height, int nranks, int rank, int rows, int32_t *out, int *n_entries) {
+    if (height < 1 || nranks < 1 || rank < 0 || rank >= nranks || rows < 0 || !out || !n_entries) return VXPT_ERR_ARG;
+    const std::vector<Halo> plan = halo_plan(height, nranks, rank, rows);
+    for (size_t k = 0; k < plan.size(); ++k) {
+        const Halo &h = plan[k];
+        const int32_t e[5] = {h.peer, h.sy, h.sn, h.ry, h.rn};
+        std::memcpy(out + 5 * k, e, sizeof(e));
+    }
+    *n_entries = (int)plan.size();
+    return VXPT_OK;
+}
+
+int vxpt_band_halo_rows(const vxpt_camera *cur, const vxpt_camera *prev, int width, int height, int nranks,
+                        int *trace_rows, int *history_rows) {
+    if (!cur || width < 1 || height < 1 || nranks < 1 || !trace_rows || !history_rows) return VXPT_ERR_ARG;
+    const CamDev c = make_camera(width, height, *cur, nullptr, nullptr);
+    const CamDev pc = make_camera(width, height, prev ? *prev : *cur, nullptr, nullptr);
+    std::string err;
+    return band_halo_rows(c, pc, width, height, nranks, *trace_rows, *history_rows, err) ? VXPT_OK : VXPT_ERR_STATE;
 }
 
 int vxpt_render_frame_linked(vxpt_ctx **cs, int n, const vxpt_denoise_params *p, int32_t frameNum, int32_t spp) {

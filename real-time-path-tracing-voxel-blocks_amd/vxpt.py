@@ -129,6 +129,7 @@ def load_library(path=LIB_PATH):
         "vxpt_get_model": (I, [P, I, P, P, I, P]),
         "vxpt_get_instances": (I, [P, P, I, P]),
         "vxpt_get_lights": (I, [P, P, I, P, P, P]),
+        "vxpt_get_light_remap": (I, [P, P, I, P, P]),
         "vxpt_mesh_probe": (I, [P, P, I, I, P, P]),
         "vxpt_mesh_occluded": (I, [P, P, I, P]),
         "vxpt_set_block": (I, [P, I, I, I, I]),
@@ -167,6 +168,12 @@ def load_library(path=LIB_PATH):
         "vxpt_band_link": (I, [ctypes.POINTER(P), I]),
         "vxpt_render_frame_linked": (I, [ctypes.POINTER(P), I, ctypes.POINTER(DenoiseParams), ctypes.c_int32,
                                          ctypes.c_int32]),
+        "vxpt_band_rows": (I, [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
+        "vxpt_halo_plan": (I, [I, I, I, I, P, ctypes.POINTER(I)]),
+        "vxpt_band_halo_rows": (I, [ctypes.POINTER(Camera), ctypes.POINTER(Camera), I, I, I, ctypes.POINTER(I),
+                                    ctypes.POINTER(I)]),
+        "vxpt_band_gather": (I, [P, I, I]),
+        "vxpt_band_gather_linked": (I, [ctypes.POINTER(P), I, I, I]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -329,6 +336,16 @@ class Renderer:
         self._chk(self.lib.vxpt_mesh_occluded(self.ctx, _ptr(r), len(r), _ptr(occ)), "vxpt_mesh_occluded")
         return occ
 
+    def light_remap(self):
+        """(previous -> current light index int32 [prevNumLights], pending: the next pass applies it)."""
+        n, pend = ctypes.c_int(0), ctypes.c_int(0)
+        self._chk(self.lib.vxpt_get_light_remap(self.ctx, None, 0, ctypes.byref(n), ctypes.byref(pend)),
+                  "vxpt_get_light_remap")
+        out = np.zeros(n.value, np.int32)
+        if n.value:
+            self._chk(self.lib.vxpt_get_light_remap(self.ctx, _ptr(out), n.value, None, None), "vxpt_get_light_remap")
+        return out, bool(pend.value)
+
     def lights(self):
         """(mapping uint32 [M, 3], LightInfo records uint8 [L, 32], alias bins [L], local luminance)."""
         n, nl, lum = ctypes.c_int(0), ctypes.c_uint32(0), ctypes.c_float(0)
@@ -430,6 +447,18 @@ class Renderer:
     def write_png(self, path):
         """The post-processed frame as the reference's offline PNG."""
         write_png(path, self.read("FRAME"))
+
+    def band_gather(self, name, root=0):
+        """vxpt_band_gather: every band's rows of `name` into the root rank's buffer (RCCL)."""
+        self._chk(self.lib.vxpt_band_gather(self.ctx, BUF[name] if isinstance(name, str) else int(name), root),
+                  "vxpt_band_gather")
+
+    def exchange_halo(self, names, rows):
+        """vxpt_exchange_halo: one RCCL halo exchange of the named buffers with the band neighbours."""
+        mask = 0
+        for n in names:
+            mask |= 1 << (BUF[n] if isinstance(n, str) else int(n))
+        self._chk(self.lib.vxpt_exchange_halo(self.ctx, mask, rows), "vxpt_exchange_halo")
 
     def band_comm_init(self, comm_id, nranks, rank):
         """Attach an RCCL communicator (vxpt_band_comm_init): this context renders band `rank`
@@ -556,6 +585,38 @@ def band_comm_id():
     return buf.raw
 
 
+def band_rows(height, nranks, rank):
+    """vxpt_band_rows: (row_begin, row_end) of `rank` (pure host function, no GPU)."""
+    y0, y1 = ctypes.c_int(0), ctypes.c_int(0)
+    if load_library().vxpt_band_rows(height, nranks, rank, ctypes.byref(y0), ctypes.byref(y1)) != 0:
+        raise VxptError("vxpt_band_rows: bad arguments")
+    return y0.value, y1.value
+
+
+def halo_plan(height, nranks, rank, rows):
+    """vxpt_halo_plan as bands.halo_plan's dict: {peer: ((send y, n), (recv y, n))}."""
+    out, n = np.zeros(10, np.int32), ctypes.c_int(0)
+    if load_library().vxpt_halo_plan(height, nranks, rank, rows, out.ctypes.data, ctypes.byref(n)) != 0:
+        raise VxptError("vxpt_halo_plan: bad arguments")
+    e = out.reshape(2, 5)[:n.value]
+    return {int(p): ((int(sy), int(sn)), (int(ry), int(rn))) for p, sy, sn, ry, rn in e}
+
+
+def band_halo_rows(cur, prev, width, height, nranks):
+    """vxpt_band_halo_rows: (trace rows, history rows) of a banded frame whose camera moved from
+    prev to cur ((pos, dir, fov) each); None when the library refuses the motion."""
+    def cam(c):
+        return Camera((ctypes.c_float * 3)(*c[0]), (ctypes.c_float * 3)(*c[1]), c[2])
+    t, h = ctypes.c_int(0), ctypes.c_int(0)
+    r = load_library().vxpt_band_halo_rows(ctypes.byref(cam(cur)), ctypes.byref(cam(prev)), width, height, nranks,
+                                           ctypes.byref(t), ctypes.byref(h))
+    if r == -4:  # VXPT_ERR_STATE
+        return None
+    if r != 0:
+        raise VxptError("vxpt_band_halo_rows: bad arguments")
+    return t.value, h.value
+
+
 class LinkedBands:
     """n contexts of this process rendering the bands of one frame (vxpt_band_link):
     the library's multi-GPU schedule with device copies as the transport."""
@@ -571,6 +632,12 @@ class LinkedBands:
         p = params or DenoiseParams.defaults()
         if self.lib.vxpt_render_frame_linked(self._arr, len(self.rs), ctypes.byref(p), frame_num, spp) != 0:
             raise VxptError("vxpt_render_frame_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
+
+    def gather(self, name, root=0):
+        """vxpt_band_gather_linked: every band's rows of `name` into band `root`'s buffer."""
+        if self.lib.vxpt_band_gather_linked(self._arr, len(self.rs), BUF[name] if isinstance(name, str) else int(name),
+                                            root) != 0:
+            raise VxptError("vxpt_band_gather_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
 
     def postprocess(self, params=None, dt_ms=16.6667):
         """vxpt_postprocess over the bands (histogram summed over them, 1-row and bloom halos)."""

@@ -210,3 +210,92 @@ def test_gpu_band_postprocess_matches_single_context(n, w, h, variant):
         ref = single.read("FRAME")
         out = np.concatenate([r.read("FRAME")[y0:y1] for r, (y0, y1) in zip(rs, rows)])
         np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+def test_library_band_functions_match_bands_py():
+    """vxpt_band_rows / vxpt_halo_plan (pure host functions of the C ABI) equal bands.py's."""
+    import vxpt
+    for H in (160, 640, 1080, 2160):
+        for n in (1, 2, 3, 8):
+            rows = [bands.band_rows(H, n, r) for r in range(n)]
+            for r in range(n):
+                assert vxpt.band_rows(H, n, r) == rows[r]
+                for depth in (0, 2, 34, 72, 91):
+                    assert vxpt.halo_plan(H, n, r, depth) == bands.halo_plan(rows, r, depth), (H, n, r, depth)
+
+
+def _turn(d, yaw_deg, pitch_deg):
+    import math
+    y = math.atan2(d[0], d[2]) + math.radians(yaw_deg)
+    p = math.asin(max(-1.0, min(1.0, d[1]))) + math.radians(pitch_deg)
+    return (math.sin(y) * math.cos(p), math.sin(p), math.cos(y) * math.cos(p))
+
+
+def test_band_halo_rows_follow_the_camera():
+    """vxpt_band_halo_rows: the static depths for an unmoved camera, deeper halos as the camera turns
+    further, refusal for a translation or a turn past the band height."""
+    import vxpt
+    cam = C1_CAMERA
+    assert vxpt.band_halo_rows(cam, cam, 640, 640, 8) == (72, 2)
+    assert vxpt.band_halo_rows(cam, cam, 640, 640, 1) == (72, 2)
+    moved = ((cam[0][0] + 0.1, cam[0][1], cam[0][2]), cam[1], cam[2])
+    assert vxpt.band_halo_rows(moved, cam, 640, 640, 2) is None
+    last = (72, 2)
+    for pitch in (0.2, 0.5, 1.0, 1.5):
+        got = vxpt.band_halo_rows((cam[0], _turn(cam[1], 0.0, pitch), cam[2]), cam, 640, 640, 2)
+        assert got is not None and got[0] >= last[0] and got[1] >= last[1] and got[1] > 2, (pitch, got)
+        assert got[0] >= 64 + got[1] - 1
+        last = got
+    # 8 bands of 80 rows: a 3-degree pitch needs more than a band
+    assert vxpt.band_halo_rows((cam[0], _turn(cam[1], 0.0, 3.0), cam[2]), cam, 640, 640, 8) is None
+    assert vxpt.band_halo_rows((cam[0], _turn(cam[1], 0.0, 3.0), cam[2]), cam, 640, 640, 2) is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,w,h,turns", [
+    (2, 96, 320, [(0, 0), (2, 0.8), (0, 3), (0, 2), (1, 1)]),
+    (8, 640, 640, [(0, 0), (1, 0.3), (0.5, 0.5), (1.5, 0.4), (0, 1.0)])])
+def test_gpu_linked_bands_follow_a_turning_camera(n, w, h, turns):
+    """A camera that yaws / pitches between frames: the banded frame deepens its halos
+    (vxpt_band_halo_rows: the reprojected rows of the ReSTIR temporal taps and the history taps)
+    and stays bit-exact against one context; the end-of-frame gather leaves the whole frame in
+    band 0; a turn past the band height is refused."""
+    import vxpt
+    spp = 2
+    cam = C1_CAMERA
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    single = make()
+    rs = [make() for _ in range(n)]
+    linked = vxpt.LinkedBands(rs)
+    rows = [bands.band_rows(h, n, k) for k in range(n)]
+    d, prev, deep = cam[1], cam, 0
+    for f, (dy, dp) in enumerate(turns):
+        d = _turn(d, dy, dp)
+        cur = (cam[0], d, cam[2])
+        halo = vxpt.band_halo_rows(cur, prev, w, h, n)
+        assert halo is not None
+        deep += halo != (72, 2)
+        for r in [single] + rs:
+            r.set_camera(*cur[:2], fov=cur[2], prev=prev)
+        single.render_frame(f, spp, p)
+        linked.render_frame(f, spp, p)
+        ref = single.read("OUTPUT")
+        out = np.concatenate([r.read("OUTPUT")[y0:y1] for r, (y0, y1) in zip(rs, rows)])
+        np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32), err_msg="frame %d" % f)
+        linked.gather("OUTPUT", 0)
+        np.testing.assert_array_equal(rs[0].read("OUTPUT").view(np.uint32), ref.view(np.uint32))
+        prev = cur
+    assert deep >= 2
+    far = (cam[0], _turn(d, 0.0, 30.0), cam[2])
+    for r in rs:
+        r.set_camera(*far[:2], fov=far[2], prev=prev)
+    with pytest.raises(vxpt.VxptError):
+        linked.render_frame(len(turns), spp, p)

@@ -14,7 +14,8 @@ Covered against oracle/orc_mesh.cpp + orc_trace.cpp over 4 frames of trace + den
   8 local-light NEE candidates from the light alias table (closesthit.cu:350-378);
   BRDF-candidate rays that hit an emissive triangle (closesthit.cu:518-551, 854-900);
   visibility rays against voxels and meshes, local lights traced to 0.01 short;
-  ReSTIR temporal reuse of local-light reservoirs (Restir.h:383-415).
+  ReSTIR temporal reuse of local-light reservoirs (Restir.h:383-415);
+  the light-id remap across lantern edits (VoxelEngine.cu:503-633, 1192-1284; Restir.h:48-79).
 """
 import os
 
@@ -111,12 +112,12 @@ def mesh_scene(tmp_path):
               ((LIGHT, "lanternLight.obj"), (BASE, "lanternBase.obj"), (LEAVES, "leavesCube4.obj"))}
     rows = o.set_meshes(models, defs)
     _inject_sky(r, o)
-    yield r, o, rows, placed
+    yield r, o, rows, placed, dict(models=models, defs=defs)
     r.close()
 
 
 def test_mesh_scene_matches_oracle(mesh_scene):
-    r, o, rows, placed = mesh_scene
+    r, o, rows, placed, _ = mesh_scene
     inst = r.instances()
     # the library's instance rows are the oracle's (object, id, x, y, z); rows here are (block, x, y, z, light)
     np.testing.assert_array_equal(inst[:, 0] + 1, rows[:, 0])
@@ -145,3 +146,63 @@ def test_mesh_scene_matches_oracle(mesh_scene):
     res = r.read("RESERVOIRS")
     li = res["lightData"] & 0x7FFFFFFF
     assert ((res["lightData"] != 0) & (li < len(recs))).sum() > 0
+
+
+def _frame(r, o, f, p, tag):
+    r.trace(f)
+    r.denoise(f, f + 1, p)
+    o.trace(f)
+    o.set_prev_scene_empty(False)
+    o.post_trace()
+    o.denoise(f, f + 1)
+    res_g, res_o = r.read("RESERVOIRS"), o.read(vxpt.BUF["RESERVOIRS"])
+    np.testing.assert_array_equal(res_g["lightData"], res_o["lightData"], err_msg=tag + " lightData")
+    np.testing.assert_array_equal(res_g["M"], res_o["M"], err_msg=tag + " M")
+    check_radiance(r.read("ILLUM"), o.read(0), tag + " illum")
+    check_radiance(r.read("OUTPUT"), o.read(21), tag + " output")
+    return res_g
+
+
+def test_lantern_edits_remap_reservoirs(mesh_scene):
+    """Remove / re-add lanterns between frames: each edit is an incremental light update whose
+    previous -> current light table (the first one after the scene's full build maps nothing,
+    m_instanceToLightRange being empty until then) is applied to the previous reservoirs in the
+    one pass after it; the library's table and the frames match the oracle's restatement."""
+    r, o, rows, placed, ex = mesh_scene
+    models, defs = ex["models"], ex["defs"]
+    first, width = min(defs), CH[0] * 32
+    lanterns = sorted((p for p in placed if p[3] == LIGHT),
+                      key=lambda p: oracle.instance_id(first, width, LIGHT - 1, *p[:3]))
+    assert len(lanterns) >= 2
+    p = _dn_params()
+    f = 0
+    for _ in range(2):
+        _frame(r, o, f, p, "pre frame%d" % f)
+        f += 1
+    # edit 1 removes the last lantern, edit 2 the first one (the rest shift down), edit 3 re-adds the last
+    edits = [(lanterns[-1], 0), (lanterns[0], 0), (lanterns[-1], LIGHT)]
+    mapped = 0
+    for k, ((x, y, z, _), block) in enumerate(edits):
+        r.set_block(x, y, z, block)
+        ids = r.read("VOXELS")
+        o.set_voxels(ids, CH)
+        o.set_prev_scene_empty(True)
+        o.light_edit(oracle.instance_id(first, width, LIGHT - 1, x, y, z), removed=block == 0)
+        o.set_meshes(models, defs, light_update="update")
+        remap, pending = r.light_remap()
+        exp = o._remap_keep[:len(remap)]
+        assert pending and len(remap) == o._lights_prev, (k, len(remap))
+        np.testing.assert_array_equal(remap, exp, err_msg="edit %d remap" % k)
+        if k == 0:
+            assert (remap == -1).all()  # the first incremental update after the full build
+        else:
+            assert (remap == -1).any() or block != 0
+        mapped += int((remap >= 0).sum())
+        for _ in range(2):
+            res = _frame(r, o, f, p, "edit%d frame%d" % (k, f))
+            f += 1
+        assert not r.light_remap()[1]
+    assert mapped > 0
+    # local-light reservoirs survive the remaps
+    li = res["lightData"] & 0x7FFFFFFF
+    assert ((res["lightData"] != 0) & (li < len(r.lights()[1]))).sum() > 0

@@ -231,3 +231,30 @@ def test_mesh_probe_matches_brute_force(model_root, cull):
         assert occ.dtype == np.uint8 and 0 < occ.sum() < len(occ)
         np.testing.assert_array_equal(occ, want[:, 3].astype(np.uint8))
     r.close()
+
+
+def test_light_id_remap_known_answers():
+    """The oracle's restatement of buildLightIdMapping / buildIncrementalLightMapping
+    (VoxelEngine.cu:503-633) on a hand-derived edit sequence: the full build maps nothing, the
+    first incremental update neither (m_instanceToLightRange still empty), later ones keep a
+    light's position within its instance's run, removed / changed instances map to -1, and a
+    full reload resets the update type without refreshing the instance ranges."""
+    o = oracle.Oracle(8, 8)
+    A, B, C = 101, 202, 303
+    o._light_update({A: (0, 4), B: (4, 4)}, 8, True)
+    assert o._lights_prev == 0
+    o.light_edit(C, removed=False)
+    o._light_update({A: (0, 4), B: (4, 4), C: (8, 4)}, 12, False)
+    assert o._lights_prev == 8 and (o._remap_keep[:8] == -1).all()
+    o.light_edit(A, removed=True)
+    o._light_update({B: (0, 4), C: (4, 4)}, 8, False)
+    assert o._remap_keep.tolist() == [-1] * 4 + [0, 1, 2, 3] + [4, 5, 6, 7]
+    o._light_update({B: (0, 4), C: (4, 4)}, 8, True)  # reload
+    assert (o._remap_keep == -1).all() and not o._lights["incremental"]
+    o.light_edit(B, removed=True)
+    o._light_update({C: (0, 4)}, 4, False)
+    assert o._remap_keep.tolist() == [-1] * 4 + [0, 1, 2, 3]
+    # a changed instance (re-placed lantern) loses its lights too
+    o.light_edit(C, removed=False)
+    o._light_update({C: (0, 4)}, 4, False)
+    assert o._remap_keep.tolist() == [-1] * 4
