@@ -208,6 +208,10 @@ int vxpt_mesh_probe(vxpt_ctx *ctx, const float *rays, int n, int cull, float *ou
  * no culling, closesthit.cu:616-625 / 752 / 808): occluded[i] = 1 iff some instanced-mesh
  * triangle, either face, lies in [tmin, tmax] of ray i; the walk stops at the first one */
 int vxpt_mesh_occluded(vxpt_ctx *ctx, const float *rays, int n, uint8_t *occluded);
+/* the mesh BVH builder on its own (no context, no GPU; test hook): n boxes of 6 floats (lo xyz,
+ * hi xyz), leaves of at most leaf_max primitives -> the deepest leaf's depth (<= 40: the walk's
+ * stack bound) and the node count; VXPT_ERR_STATE if the depth limit cannot be kept */
+int vxpt_bvh_depth(const float *boxes, int n, int leaf_max, int *max_depth, int *n_nodes);
 
 /* ---- voxel edits (VoxelEngine::update click path, VoxelEngine.cu:855-975, 1040-1346) ---- */
 /* performRayTraversal (:1040-1166) of the current camera ray on the world.  out: hit, hit x, y, z,

@@ -47,6 +47,28 @@ VX_D bool box_hit(const BvhNode &n, V3 o, V3 inv, V3 d, float tmin, float tmax, 
     return t0 <= t1;
 }
 
+// The walk keeps ONE per-thread stack for both levels: a BLAS walk runs on the entries above the
+// TLAS's pending ones and is done before the TLAS walk pops again (live entries <= tlasDepth +
+// blasDepth + 1).  An entry is (node, entry distance of its box): a popped node whose box starts
+// past the current closest hit is dropped without loading it, and a node that is loaded is not
+// box-tested again (its test at push time with the then-current interval stays valid: a later,
+// shorter interval that still reaches the entry distance contains the box's entry point).  It lives
+// in scratch: a 24-entry LDS stack (entry k of lane t at lds[k * 256 + t], conflict-free) was
+// measured 4 % slower on tools/mesh_probe_bench.py (16.0 vs 15.4 ms) -- 24 KiB per block cut
+// occupancy from 8 to 6 waves/SIMD, and the walk is bound by the node and triangle loads, not by
+// the stack.
+struct ScratchStack {
+    int s[84];    // node index; 2 x (the builder's depth limit 40 + 2)
+    float t[84];  // its box's entry distance
+};
+
+template <class S>
+VX_D void stack_push(S &st, int &sp, int node, float te) {
+    st.s[sp] = node;
+    st.t[sp] = te;
+    ++sp;
+}
+
 // push the children of an inner node, the nearer one on top (visited first, so the closest hit
 // shrinks the interval early); a child whose box the ray misses is not pushed
 template <class S>
@@ -57,25 +79,14 @@ VX_D void push_children(const BvhNode *nodes, int base, int left, V3 o, V3 inv, 
     const bool hb = box_hit(nodes[base + left + 1], o, inv, d, tmin, tmax, tb);
     if (ha && hb) {
         const bool aFirst = ta <= tb;
-        stack[sp++] = base + (aFirst ? left + 1 : left);
-        stack[sp++] = base + (aFirst ? left : left + 1);
+        stack_push(stack, sp, base + (aFirst ? left + 1 : left), aFirst ? tb : ta);
+        stack_push(stack, sp, base + (aFirst ? left : left + 1), aFirst ? ta : tb);
     } else if (ha) {
-        stack[sp++] = base + left;
+        stack_push(stack, sp, base + left, ta);
     } else if (hb) {
-        stack[sp++] = base + left + 1;
+        stack_push(stack, sp, base + left + 1, tb);
     }
 }
-
-// The walk keeps ONE per-thread stack for both levels: a BLAS walk runs on the entries above the
-// TLAS's pending ones and is done before the TLAS walk pops again (live entries <= tlasDepth +
-// blasDepth + 1).  It lives in scratch: a 24-entry LDS stack (entry k of lane t at
-// lds[k * 256 + t], conflict-free) was measured 4 % slower on tools/mesh_probe_bench.py (16.0 vs
-// 15.4 ms) -- 24 KiB per block cut occupancy from 8 to 6 waves/SIMD, and the walk is bound by
-// the node and triangle loads, not by the stack.
-struct ScratchStack {
-    int s[84];  // 2 x (the builder's depth limit 40 + 2)
-    VX_D int &operator[](int k) { return s[k]; }
-};
 
 struct Best {
     float t, u, v;
@@ -91,12 +102,14 @@ VX_D bool blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, fl
                     S &stack, const int sp0) {
     const int2 r = m.root[block];
     if (r.x < 0) return false;
+    float te0;
+    if (!box_hit(m.blas[r.x], o, inv, d, tmin, b.t, te0)) return false;
     int sp = sp0;
-    stack[sp++] = r.x;
+    stack_push(stack, sp, r.x, te0);
     while (sp > sp0) {
-        const BvhNode n = m.blas[stack[--sp]];
-        float te;
-        if (!box_hit(n, o, inv, d, tmin, b.t, te)) continue;
+        --sp;
+        if (stack.t[sp] > b.t) continue;
+        const BvhNode n = m.blas[stack.s[sp]];
         if (n.count == 0) {
             push_children(m.blas, r.x, n.left, o, inv, d, tmin, b.t, stack, sp);
             continue;
@@ -116,12 +129,15 @@ VX_D bool blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, fl
 
 template <bool kAny, class S>
 VX_D void mesh_walk(const MeshDev &m, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b, S &stack) {
+    if (m.nInst <= 0) return;
+    float te0;
+    if (!box_hit(m.tlas[0], o, inv, d, tmin, b.t, te0)) return;
     int sp = 0;
-    stack[sp++] = 0;
+    stack_push(stack, sp, 0, te0);
     while (sp > 0) {
-        const BvhNode nd = m.tlas[stack[--sp]];
-        float te;
-        if (!box_hit(nd, o, inv, d, tmin, b.t, te)) continue;
+        --sp;
+        if (stack.t[sp] > b.t) continue;
+        const BvhNode nd = m.tlas[stack.s[sp]];
         if (nd.count == 0) {
             push_children(m.tlas, 0, nd.left, o, inv, d, tmin, b.t, stack, sp);
             continue;

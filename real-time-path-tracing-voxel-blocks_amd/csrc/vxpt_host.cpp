@@ -1717,7 +1717,9 @@ int build_lights(vxpt_ctx *c) {
 // inner node adjacent, leaves of at most leafMax primitives (order = primitive order in the
 // leaves).  Node boxes are widened by 1e-4 (1 + |coordinate|), far above the slab test's
 // rounding, so box culling is conservative.  Fails past a depth of 40 (the walk's one stack holds
-// 84 entries, TLAS and BLAS together); *maxDepth = the deepest leaf.
+// 84 entries, TLAS and BLAS together) -- only for more than leafMax * 2^40 primitives, see the
+// split rule below; *maxDepth = the deepest leaf.
+constexpr int kBvhMaxDepth = 40;
 bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> &nodes, std::vector<int> &order,
                int *maxDepth) {
     const int n = (int)(box.size() / 6);
@@ -1731,7 +1733,7 @@ bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> 
     while (!jobs.empty()) {
         const Job j = jobs.back();
         jobs.pop_back();
-        if (j.depth > 40) return false;
+        if (j.depth > kBvhMaxDepth) return false;
         *maxDepth = std::max(*maxDepth, j.depth);
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
         float clo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, chi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -1755,27 +1757,40 @@ bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> 
             nd.count = j.e - j.b;
             continue;
         }
-        // binned SAH split (16 centroid bins per axis, cost = area x count on either side); the
-        // median of the widest axis when no bin boundary separates the primitives, and from depth
-        // 24 on, so the depth limit holds for any primitive count the median builder accepted
+        // binned SAH split (16 centroid bins per axis, cost = area x count on either side) while the
+        // depth budget allows it: an SAH split may leave all but one primitive on one side, so it
+        // is taken only if a child of n - 1 primitives still reaches its leaves within the limit
+        // by median splits (levels(c) = ceil(log2(ceil(c / leafMax)))); otherwise -- and when no
+        // bin boundary separates the primitives -- the median of the widest axis.  Any input of
+        // at most leafMax * 2^40 primitives then stays within the depth limit.
         int axis = 0;
         for (int k = 1; k < 3; ++k)
             if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
         int mid = -1;
-        if (j.depth < 24) {
+        const auto levels = [&](long long c) {
+            int l = 0;
+            for (long long cap = leafMax; cap < c; cap *= 2) ++l;
+            return l;
+        };
+        if (j.depth + 1 + levels((long long)(j.e - j.b) - 1) <= kBvhMaxDepth) {
             constexpr int kBins = 16;
+            // centroid bin, clamped (also for non-finite coordinates)
+            const auto bin_of = [&](float cc, float c0, float ext) {
+                const float f = (cc - c0) / ext * (float)kBins;
+                return f >= 0.0f ? (f < (float)(kBins - 1) ? (int)f : kBins - 1) : 0;
+            };
             float bestCost = FLT_MAX;
             int bestAxis = -1, bestBin = 0;
             for (int k = 0; k < 3; ++k) {
                 const float ext = chi[k] - clo[k];
-                if (!(ext > 0.0f)) continue;
+                if (!(ext > 0.0f) || !std::isfinite(ext)) continue;
                 float blo[kBins][3], bhi[kBins][3];
                 int cnt[kBins] = {};
                 for (int q = 0; q < kBins; ++q)
                     for (int a = 0; a < 3; ++a) { blo[q][a] = FLT_MAX; bhi[q][a] = -FLT_MAX; }
                 for (int i = j.b; i < j.e; ++i) {
                     const float *bx = &box[(size_t)order[i] * 6];
-                    const int q = std::min(kBins - 1, (int)((0.5f * (bx[k] + bx[k + 3]) - clo[k]) / ext * kBins));
+                    const int q = bin_of(0.5f * (bx[k] + bx[k + 3]), clo[k], ext);
                     cnt[q]++;
                     for (int a = 0; a < 3; ++a) {
                         blo[q][a] = std::min(blo[q][a], bx[a]);
@@ -1808,8 +1823,7 @@ bool build_bvh(const std::vector<float> &box, int leafMax, std::vector<BvhNode> 
                 const float ext = chi[bestAxis] - clo[bestAxis], c0 = clo[bestAxis];
                 auto it = std::stable_partition(order.begin() + j.b, order.begin() + j.e, [&](int x) {
                     const float *bx = &box[(size_t)x * 6];
-                    const int q = std::min(kBins - 1, (int)((0.5f * (bx[bestAxis] + bx[bestAxis + 3]) - c0) / ext * kBins));
-                    return q <= bestBin;
+                    return bin_of(0.5f * (bx[bestAxis] + bx[bestAxis + 3]), c0, ext) <= bestBin;
                 });
                 mid = (int)(it - order.begin());
             }
@@ -2733,6 +2747,16 @@ int vxpt_band_gather_linked(vxpt_ctx **cs, int n, int which, int root) {
     HIPCHK(cs[0], hipSetDevice(cs[0]->dev));
     std::vector<vxpt_ctx *> v(cs, cs + n);
     return band_gather(v, which, root);
+}
+
+int vxpt_bvh_depth(const float *boxes, int n, int leaf_max, int *max_depth, int *n_nodes) {
+    if (!boxes || n < 0 || leaf_max < 1 || !max_depth) return VXPT_ERR_ARG;
+    std::vector<float> box(boxes, boxes + (size_t)n * 6);
+    std::vector<BvhNode> nodes;
+    std::vector<int> order;
+    const bool ok = build_bvh(box, leaf_max, nodes, order, max_depth);
+    if (n_nodes) *n_nodes = (int)nodes.size();
+    return ok ? VXPT_OK : VXPT_ERR_STATE;
 }
 
 int vxpt_band_rows(int height, int nranks, int rank, int *row_begin, int *row_end) {

@@ -169,6 +169,7 @@ def load_library(path=LIB_PATH):
         "vxpt_render_frame_linked": (I, [ctypes.POINTER(P), I, ctypes.POINTER(DenoiseParams), ctypes.c_int32,
                                          ctypes.c_int32]),
         "vxpt_band_rows": (I, [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
+        "vxpt_bvh_depth": (I, [P, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
         "vxpt_halo_plan": (I, [I, I, I, I, P, ctypes.POINTER(I)]),
         "vxpt_band_halo_rows": (I, [ctypes.POINTER(Camera), ctypes.POINTER(Camera), I, I, I, ctypes.POINTER(I),
                                     ctypes.POINTER(I)]),
@@ -583,6 +584,15 @@ def band_comm_id():
     if lib.vxpt_band_comm_id(buf, 128) != 0:
         raise VxptError("vxpt_band_comm_id failed")
     return buf.raw
+
+
+def bvh_depth(boxes, leaf_max):
+    """vxpt_bvh_depth: (deepest leaf, node count) of the mesh BVH builder over [N, 6] boxes
+    (pure host function); None if it cannot keep the depth limit."""
+    b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+    d, n = ctypes.c_int(0), ctypes.c_int(0)
+    r = load_library().vxpt_bvh_depth(b.ctypes.data, len(b), leaf_max, ctypes.byref(d), ctypes.byref(n))
+    return None if r != 0 else (d.value, n.value)
 
 
 def band_rows(height, nranks, rank):

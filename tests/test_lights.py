@@ -57,6 +57,26 @@ def _random_mesh_obj(path, n=600, seed=4):
             f.write("f %d %d %d\n" % (3 * t + 1, 3 * t + 2, 3 * t + 3))
 
 
+def _deep_mesh_triangles(n=3000, ratio=1.012, size=0.3):
+    """n triangles in the y-z plane at geometrically spaced x in (0, 1] (x_i = ratio^(i - n + 1)):
+    binned SAH peels a few per level, so the BLAS builds to the depth limit (40)."""
+    x = ratio ** np.arange(n, dtype=np.float64)
+    x /= x[-1]
+    s = size * x
+    return np.stack([np.stack([x, 0.5 - s, 0.5 - s], 1), np.stack([x, 0.5 + s, 0.5 - s], 1),
+                     np.stack([x, 0.5 + 0 * s, 0.5 + s], 1)], 1).astype(np.float32)
+
+
+def _deep_mesh_obj(path):
+    t = _deep_mesh_triangles()
+    with open(path, "w") as f:
+        for tri in t:
+            for v in tri:
+                f.write("v %.9g %.9g %.9g\n" % tuple(v))
+        for k in range(len(t)):
+            f.write("f %d %d %d\n" % (3 * k + 1, 3 * k + 2, 3 * k + 3))
+
+
 def _base_obj(path):
     """A flat quad (2 triangles) with `v//n` corners."""
     with open(path, "w") as f:
@@ -69,6 +89,16 @@ def model_root(tmp_path):
     _prism_obj(str(tmp_path / "models" / "lanternLight.obj"))
     _base_obj(str(tmp_path / "models" / "lanternBase.obj"))
     _random_mesh_obj(str(tmp_path / "models" / "leavesCube4.obj"))
+    return tmp_path
+
+
+@pytest.fixture
+def deep_model_root(tmp_path):
+    """The leaves' mesh replaced by _deep_mesh_triangles: a BLAS at the builder's depth limit."""
+    os.makedirs(tmp_path / "models")
+    _prism_obj(str(tmp_path / "models" / "lanternLight.obj"))
+    _base_obj(str(tmp_path / "models" / "lanternBase.obj"))
+    _deep_mesh_obj(str(tmp_path / "models" / "leavesCube4.obj"))
     return tmp_path
 
 
@@ -197,6 +227,10 @@ def test_mesh_probe_matches_brute_force(model_root, cull):
     instance and triangle bit for bit: t, barycentrics, instance row and triangle.  The any-hit
     walk of visibility rays (vxpt_mesh_occluded) reports exactly the rays the brute-force loop
     finds any triangle for, both faces (closesthit.cu:616-625 traces them without culling)."""
+    _probe_vs_brute_force(model_root, cull, 0.2)
+
+
+def _probe_vs_brute_force(model_root, cull, min_hit):
     r = vxpt.Renderer(64, 64)
     r.load_settings()
     r.generate_terrain(CH, height_scale=32.0)
@@ -223,7 +257,7 @@ def test_mesh_probe_matches_brute_force(model_root, cull):
     rays[:, 7] = np.where(np.arange(n) % 7 == 0, 20.0, 1e27)
     got, gid = r.mesh_probe(rays, cull)
     want, wid = oracle.mesh_probe(models, rows, rays, cull)
-    assert 0.2 < want[:, 3].mean() < 0.95
+    assert min_hit < want[:, 3].mean() < 0.95
     np.testing.assert_array_equal(gid, wid)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
     if not cull:
@@ -258,3 +292,36 @@ def test_light_id_remap_known_answers():
     o.light_edit(C, removed=False)
     o._light_update({C: (0, 4)}, 4, False)
     assert o._remap_keep.tolist() == [-1] * 4
+
+
+def test_bvh_builder_keeps_the_depth_limit():
+    """The mesh BVH builder (vxpt_bvh_depth, no GPU) on degenerate inputs: SAH splits only while a
+    child of n - 1 primitives could still reach its leaves by median splits, so the deepest leaf
+    stays <= 40 (the walk's 84-entry stack holds a TLAS and a BLAS path) -- geometrically spaced
+    boxes reach exactly the limit; identical, huge-range and non-finite boxes build too."""
+    t = _deep_mesh_triangles()
+    boxes = np.concatenate([t.min(1), t.max(1)], 1)
+    for leaf in (1, 2, 4):
+        d, nodes = vxpt.bvh_depth(boxes, leaf)
+        assert d <= 40 and nodes >= 2 * (len(boxes) // leaf) - 1
+    assert vxpt.bvh_depth(boxes, 4)[0] == 40  # the budget rule is what bounds it
+    same = np.tile(np.array([[0.4, 0.4, 0.4, 0.6, 0.6, 0.6]], np.float32), (5000, 1))
+    assert vxpt.bvh_depth(same, 4)[0] == 11  # identical centroids: balanced median splits
+    x = (2.0 ** np.arange(120)).astype(np.float32)
+    huge = np.stack([x - 0.01, 0 * x, 0 * x, x + 0.01, 0 * x + 1, 0 * x + 1], 1)
+    assert vxpt.bvh_depth(huge, 2)[0] <= 40
+    bad = huge.copy()
+    bad[::7, 0] = np.inf
+    bad[3::7, 3] = np.nan
+    assert vxpt.bvh_depth(bad, 2) is not None
+    rng = np.random.default_rng(1)
+    c = rng.random((20000, 3)).astype(np.float32)
+    assert vxpt.bvh_depth(np.concatenate([c - 0.01, c + 0.01], 1), 4)[0] <= 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cull", [0, 1])
+def test_deep_bvh_walk_matches_brute_force(deep_model_root, cull):
+    """A BLAS at the depth limit (40) under a TLAS of 90 instances: the walk's shared stack holds
+    both levels and the closest / any hits still equal the brute-force loop bit for bit."""
+    _probe_vs_brute_force(deep_model_root, cull, 0.05)
