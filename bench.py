@@ -69,7 +69,7 @@ def cpu_baseline(a, target_s):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     chunks, hs, fd, pos = scene_args(a)
-    o = oracle.Oracle(a.width, a.height)
+    o = oracle.Oracle(a.width, a.height, bounces=a.bounce_limits)
     o.terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
     o.set_camera(pos, C1_DIR, 90.0)
     o.set_camera(pos, C1_DIR, 90.0, which=1)
@@ -123,9 +123,14 @@ def main():
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--world", type=int, default=256, help="world edge in voxels (multiple of 64)")
     ap.add_argument("--primary-only", action="store_true", help="C2: primary rays + sky + G-buffer, no denoiser")
+    ap.add_argument("--bounces", default="3/1",
+                    help="total/diffuse bounce limits: 3/1 = the reference's (RayGen.cu:146-147); 4/4 = the "
+                         "'4 bounces' of BASELINE.json's config line, labelled as such")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
+    a.bounce_limits = tuple(int(v) for v in a.bounces.split("/"))
+    assert len(a.bounce_limits) == 2 and a.bounce_limits[0] >= a.bounce_limits[1] >= 1, a.bounces
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -142,7 +147,7 @@ def main():
     import bands
 
     chunks, hs, fd, pos = scene_args(a)
-    r = vxpt.Renderer(a.width, a.height, device=local)
+    r = vxpt.Renderer(a.width, a.height, device=local, bounces=a.bounce_limits)
     r.load_settings()
     r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
     r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
@@ -242,7 +247,10 @@ def main():
             "config": {"workload": "C2: %dx%d primary-only DDA + sky + G-buffer" % (a.width, a.height) if
                        a.primary_only else "C3: %dx%d, %d spp full path + ReLAX denoiser" % (a.width, a.height, a.spp),
                        "width": a.width, "height": a.height, "spp": spp, "world": "%d^3 voxels, Perlin seed 124" % a.world,
-                       "bounces": "3 total / 1 diffuse",
+                       "bounces": "%d total / %d diffuse%s" % (
+                           a.bounce_limits + ((" (the reference's RayGen.cu:146-147 limits)",) if a.bounce_limits == (3, 1)
+                                              else (" (BASELINE.json's '4 bounces' reading; the reference renders 3/1)",)
+                                              if a.bounce_limits == (4, 4) else ("",))),
                        "parallelism": ("replicas%d (band exchange unavailable: %s)" % (world, replicas[:120]) if replicas
                                        else ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

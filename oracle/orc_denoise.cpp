@@ -415,6 +415,18 @@ void pass_temporal(const Scene &s, Frame &f, const DenoiseParams &p) {
                                 "prevI %.9g %.9g %.9g illum %.9g %.9g %.9g pnr.n %.9g\n", x, y, ox, oy, estDepth, t0, bicValid,
                                 tapsValid[0], tapsValid[1], tapsValid[2], tapsValid[3], found, quality, hist, prevI.x, prevI.y,
                                 prevI.z, illum.x, illum.y, illum.z, dot(nIn, pnr));
+                if (std::sscanf(dbg, "%d,%d", &dx, &dy) == 2 && dx == x && dy == y) {
+                    for (int a = 0; a < 4; ++a)
+                        for (int b = 0; b < 2; ++b) {
+                            float pz = ld1(f.prevDepth, f, ox + bc[a][b][0], oy + bc[a][b][1]);
+                            std::printf("  bc %d %d pz %.9g diff %.9g thr %.9g\n", a, b, pz, std::fabs(pz - estDepth), thr4[a]);
+                        }
+                    for (int a = 0; a < 4; ++a) {
+                        float pz = ld1(f.prevDepth, f, ox + bl[a][0], oy + bl[a][1]);
+                        std::printf("  bl %d pz %.9g diff %.9g thr %.9g\n", a, pz, std::fabs(pz - estDepth), thr4[a]);
+                    }
+                    std::printf("  prevUV %.9g %.9g NoV %.9g parMax %.9g z %.9g\n", prevUV.x, prevUV.y, NoV, parMax, z);
+                }
             }
         }
 }

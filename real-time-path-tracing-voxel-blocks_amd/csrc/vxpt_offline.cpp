@@ -46,6 +46,7 @@ struct Options {
     int chunks[3] = {2, 1, 2};
     int device = 0;
     std::string dataDir = "data";
+    std::string assetsDir;  // root of the instanced meshes' OBJ files (empty: the data directory)
     std::string perfReport;
     bool testSequence = false, removal20 = false, removalCircle = false;
     bool textures = true;
@@ -71,6 +72,7 @@ void usage(const char *argv0) {
               << "  --chunks <x> <y> <z>   World size in 32^3 chunks (default: 2 1 2)\n"
               << "  --device <int>         HIP device (default: 0)\n"
               << "  --data <dir>           Data directory: settings/, assets/, tables/ (default: data)\n"
+              << "  --models <dir>         Root of the instanced meshes' OBJ files (<dir>/models/*.obj; default: the data directory)\n"
               << "  --perf-report <file>   Performance report path (default: <output>_performance_report.txt)\n"
               << "  --no-textures          Untextured materials (textures load from <data>/textures when present)\n"
               << "  --help, -h             Show this help message\n";
@@ -114,6 +116,7 @@ int parse(int argc, char **argv, Options &o) {
         }
         else if (a == "--device") { if ((v = next("--device"))) { o.device = std::atoi(v); } }
         else if (a == "--data") { if ((v = next("--data"))) { o.dataDir = v; } }
+        else if (a == "--models") { if ((v = next("--models"))) { o.assetsDir = v; } }
         else if (a == "--perf-report") { if ((v = next("--perf-report"))) { o.perfReport = v; } }
         else if (a == "--no-textures") o.textures = false;
         else if (a == "--test-sequence") o.testSequence = true;
@@ -207,6 +210,14 @@ int main(int argc, char **argv) {
     }
     if (vxpt_generate_terrain(ctx, o.chunks[0], o.chunks[1], o.chunks[2], 32.0f, 32.0f * o.chunks[0], 0) != VXPT_OK)
         return fail("generating terrain");
+    // VoxelEngine::init (VoxelEngine.cu:809-816): the instanced meshes, their instances in the world and
+    // the light table (a full light update); block types whose OBJ file is missing stay empty
+    {
+        int nModels = 0;
+        if (vxpt_load_models(ctx, o.assetsDir.empty() ? nullptr : o.assetsDir.c_str(), &nModels) != VXPT_OK)
+            return fail("loading the instanced meshes");
+        std::cout << "Instanced meshes loaded: " << nModels << std::endl;
+    }
 
     // :200-251: camera from the scene file (defaults when it is absent), history camera = camera
     vxpt_camera cam{};

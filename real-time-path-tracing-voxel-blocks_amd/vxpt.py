@@ -569,6 +569,7 @@ def render_offline(width, height, frames, spp=1, chunks=(2, 1, 2), height_scale=
     r = Renderer(width, height, device=device)
     r.load_settings()
     r.generate_terrain(chunks, height_scale=height_scale)
+    r.load_models()  # VoxelEngine::init: the instanced meshes present under the data directory
     cam = r.scene_camera()
     r.set_camera(list(cam.pos), list(cam.dir), cam.fov_deg)
     r.set_sky()

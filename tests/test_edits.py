@@ -214,12 +214,13 @@ def test_cli_accepts_the_edit_sequence_flags():
         assert flag in r.stdout
 
 
-def _mirror(mode, w, h, frames, dts, angles):
+def _mirror(mode, w, h, frames, dts, angles, models=None):
     """mainOffline.cpp's frame loop with scripted clicks, through the Python mirror
     (the circular test's camera angles are the CLI's own, printed exactly)."""
     r = vxpt.Renderer(w, h)
     r.load_settings()
     r.generate_terrain(CH)
+    r.load_models(models)
     cam = r.scene_camera(os.path.join(REPO, "data", "scene", "scene_export.yaml"))
     c = (list(cam.pos), list(cam.dir), cam.fov_deg)
     r.set_camera(*c[:2], fov=c[2], prev=c)
@@ -274,9 +275,24 @@ def _mirror(mode, w, h, frames, dts, angles):
                                               ("circle", "--test-remove-circle", 44),
                                               ("sequence", "--test-sequence", 10)])
 def test_cli_edit_sequences_match_mirror(mode, flag, frames, tmp_path):
+    """The CLI's scripted edit runs equal the Python mirror bit for bit.  The sequence places
+    lanterns (block 16): with synthetic lantern / leaves meshes (test_lights' OBJ files under
+    --models) they render as emissive meshes with their triangle lights, and each placement or
+    removal is an incremental light update with the light-id remap (tests/test_gpu_meshes.py
+    pins those frames against the oracle)."""
     w, h = 64, 64
     prefix = str(tmp_path / "e")
-    res = _run_cli("--width", str(w), "--height", str(h), "--frames", str(frames), "--output", prefix, flag)
+    models = None
+    extra = []
+    if mode == "sequence":
+        from test_lights import _base_obj, _prism_obj, _random_mesh_obj
+        os.makedirs(tmp_path / "assets" / "models")
+        _prism_obj(str(tmp_path / "assets" / "models" / "lanternLight.obj"))
+        _base_obj(str(tmp_path / "assets" / "models" / "lanternBase.obj"))
+        _random_mesh_obj(str(tmp_path / "assets" / "models" / "leavesCube4.obj"), n=60)
+        models = str(tmp_path / "assets")
+        extra = ["--models", models]
+    res = _run_cli("--width", str(w), "--height", str(h), "--frames", str(frames), "--output", prefix, flag, *extra)
     assert res.returncode == 0, (res.stdout[-2000:], res.stderr[-2000:])
     assert res.stdout.count("EDIT: frame") >= (3 if mode == "sequence" else 10)
     rows = [ln.split(",") for ln in open(prefix + "_performance_report.txt") if ln[0].isdigit()]
@@ -289,7 +305,9 @@ def test_cli_edit_sequences_match_mirror(mode, flag, frames, tmp_path):
     assert mode != "circle" or len(angles) == frames
     # the last saved frame (1-indexed 1/4/16/64) through the Python mirror, bit for bit
     last_saved = max(k for k in (1, 4, 16, 64) if k <= frames)
-    out, vox = _mirror(mode, w, h, last_saved, dts, angles)
+    out, vox = _mirror(mode, w, h, last_saved, dts, angles, models)
+    if mode == "sequence":
+        assert "Instanced meshes loaded: 3" in res.stdout
     mine = str(tmp_path / "m.png")
     vxpt.write_png(mine, out)
     np.testing.assert_array_equal(vxpt.read_png(mine), vxpt.read_png("%s_%04d.png" % (prefix, last_saved - 1)))

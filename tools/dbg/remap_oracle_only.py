@@ -1,0 +1,40 @@
+"""Debug: the lantern-edit scenario on the oracle alone (CPU), printing one pixel's temporal taps."""
+import os, sys, tempfile
+sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "..", d) for d in ("tests", "oracle", "real-time-path-tracing-voxel-blocks_amd")]
+import numpy as np
+import oracle
+import test_gpu_meshes as T
+from test_lights import _base_obj, _prism_obj, _random_mesh_obj
+from golden.make_golden import C1_CAMERA
+
+d = tempfile.mkdtemp(); os.makedirs(d + "/models")
+_prism_obj(d + "/models/lanternLight.obj"); _base_obj(d + "/models/lanternBase.obj")
+_random_mesh_obj(d + "/models/leavesCube4.obj", n=120)
+w, h = 128, 96
+o = oracle.Oracle(w, h)
+o.terrain(T.CH)
+ids = o.voxels()
+placed = T.place_meshes(ids)
+o.set_voxels(ids, T.CH)
+cam = (C1_CAMERA[0], C1_CAMERA[1], C1_CAMERA[2])
+o.set_camera(*cam[:2], fov=cam[2]); o.set_camera(*cam[:2], fov=cam[2], which=1)
+o.set_sky(0.25, 45.0, 0.0, 1.0)
+o.set_denoise_params(T.DN_FLOATS, T.DN_INTS)
+defs, params = T.asset_tables()
+for b, p in params.items():
+    o.set_material(b, **p)
+models = {b: oracle.parse_obj(d + "/models/" + f) for b, f in ((T.LIGHT, "lanternLight.obj"), (T.BASE, "lanternBase.obj"), (T.LEAVES, "leavesCube4.obj"))}
+o.set_meshes(models, defs)
+first, width = min(defs), T.CH[0] * 32
+lanterns = sorted((p for p in placed if p[3] == T.LIGHT), key=lambda p: oracle.instance_id(first, width, T.LIGHT - 1, *p[:3]))
+edits = {2: (lanterns[-1], 0), 4: (lanterns[0], 0)}
+for f in range(6):
+    if f in edits:
+        (x, y, z, _), b = edits[f]
+        ids[T._idx(x, y, z)] = b
+        o.set_voxels(ids, T.CH)
+        o.set_prev_scene_empty(True)
+        o.light_edit(oracle.instance_id(first, width, T.LIGHT - 1, x, y, z), removed=b == 0)
+        o.set_meshes(models, defs, light_update="update")
+    o.trace(f); o.set_prev_scene_empty(False); o.post_trace(); o.denoise(f, f + 1)
+    print("frame", f, flush=True)
