@@ -1,0 +1,40 @@
+#!/bin/bash
+# One GPU call's worth of round-2 checks, each step under its own time limit; stops at the first
+# GPU fault / timeout.  Usage (on the box): tools/gpu_batch.sh STEP...   steps:
+#   dbg      the lantern-edit pixel debug (libvxpt_dbg.so)
+#   tests    pytest -m gpu on the files in $TESTS (default: all)
+#   bench    bench.py --steps 20 --warmup 6 --no-cpu-baseline  -> gpurun_out/b_default.json
+#   caps     trace iteration-cap sweep (VXPT_ITER_CAP / VXPT_ITER_CAP2)   -> gpurun_out/b_cap*.json
+#   full     bench.py (defaults, CPU baseline on)                          -> gpurun_out/b_full.json
+#   c2       bench.py --primary-only                                       -> gpurun_out/b_c2.json
+#   b44      bench.py --bounces 4/4 --no-cpu-baseline                      -> gpurun_out/b_44.json
+#   counters rocprofv3 -L                                                  -> gpurun_out/counters.txt
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+run() {  # name seconds cmd...
+    local name=$1 secs=$2; shift 2
+    echo "== $name $(date +%T)"
+    timeout -k 10 "$secs" "$@"
+    local rc=$?
+    echo "== $name rc=$rc $(date +%T)"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+}
+for step in "$@"; do
+    case $step in
+    dbg) ORC_DBG_PX=40,12 VXPT_LIB=real-time-path-tracing-voxel-blocks_amd/libvxpt_dbg.so run dbg 120 \
+             python -u tools/dbg/remap_dbg.py > gpurun_out/remap_dbg.log 2>&1 || exit $? ;;
+    tests) run tests 900 python -u -m pytest -v --timeout 240 --timeout-method thread -m gpu ${TESTS:-tests} \
+               > gpurun_out/tests.log 2>&1 || exit $? ;;
+    bench) run bench 200 python -u bench.py --steps 20 --warmup 6 --no-cpu-baseline > gpurun_out/b_default.json 2> gpurun_out/b_default.err || exit $? ;;
+    caps) for c in 4:0 6:0 8:0 6:16 12:0; do
+              VXPT_ITER_CAP=${c%%:*} VXPT_ITER_CAP2=${c##*:} run cap$c 200 python -u bench.py --steps 20 --warmup 6 \
+                  --no-cpu-baseline > gpurun_out/b_cap${c/:/_}.json 2>/dev/null || exit $?
+          done ;;
+    full) run full 400 python -u bench.py > gpurun_out/b_full.json 2> gpurun_out/b_full.err || exit $? ;;
+    c2) run c2 300 python -u bench.py --primary-only --cpu-seconds 8 > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || exit $? ;;
+    b44) run b44 200 python -u bench.py --bounces 4/4 --steps 10 --warmup 4 --no-cpu-baseline > gpurun_out/b_44.json 2> gpurun_out/b_44.err || exit $? ;;
+    counters) (cd /tmp && TMPDIR=/tmp timeout -k 5 60 rocprofv3 -L > "$GRAFT_REPO_ROOT/gpurun_out/counters.txt" 2>&1); true ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
