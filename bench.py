@@ -232,6 +232,14 @@ def main():
         with open(pmc[-1]) as f:
             traffic = json.load(f)["traffic_bytes_per_frame"] * band_px / (a.width * a.height)
         traffic_src = os.path.relpath(pmc[-1], REPO)
+    # VALU issue utilisation of the trace kernels from the committed PMC pass (tools/valu_util.py ->
+    # profiles/*_valu_util.json): how much of the chip's VALU issue the traversal / shading keeps busy
+    valu, valu_src = None, None
+    vu = sorted(glob.glob(os.path.join(REPO, "profiles", "*_valu_util.json")))
+    if vu and not a.primary_only and a.width == 1920 and a.height == 1080:
+        with open(vu[-1]) as f:
+            valu = json.load(f)["trace_valu_util"]
+        valu_src = os.path.relpath(vu[-1], REPO)
     depth = r.read("DEPTH")
     hit_frac = float((depth < 1e26).mean())  # scene sanity: fraction of primary rays that hit voxels
     cpu = None
@@ -260,6 +268,7 @@ def main():
             "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4), "primary_hit_frac": round(hit_frac, 4),
             # the trace passes over this rank's rows (bands: with their halo exchanges)
             "trace_mpaths_s": round(band_px * spp / (avg_trace * 1e-3) / 1e6, 3),
+            "trace_valu_util": valu, "trace_valu_util_source": valu_src,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

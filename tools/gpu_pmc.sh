@@ -21,3 +21,11 @@ echo sq ok
 python tools/pmc_traffic.py gpurun_out/${TAG}_fetch/run_results.db gpurun_out/${TAG}_write/run_results.db gpurun_out/${TAG}_kt/run_results.db 4 gpurun_out/${TAG}_pmc_denoise.json gpurun_out/${TAG}_pmc_calib.json
 python tools/pmcsum.py gpurun_out/${TAG}_sq/run_results.db gpurun_out/${TAG}_fetch/run_results.db gpurun_out/${TAG}_write/run_results.db > gpurun_out/${TAG}_pmc.txt
 python tools/profsum.py gpurun_out/${TAG}_kt/run_results.db > gpurun_out/${TAG}_kernel_stats.txt
+# VALU lane activity (divergence) when the device exposes the counters (rocprofv3 -L); the issue
+# utilisation needs only the SQ pass above
+if grep -q "SQ_THREAD_CYCLES_VALU" gpurun_out/counters.txt 2>/dev/null && grep -q "SQ_ACTIVE_INST_VALU" gpurun_out/counters.txt; then
+    timeout -k 10 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU -f csv rocpd -d gpurun_out/${TAG}_valu -o run -- python bench.py $ARGS > gpurun_out/${TAG}_valu.log 2>&1 || { echo "valu pass failed"; exit 1; }
+    python tools/valu_util.py gpurun_out/${TAG}_valu/run_results.db gpurun_out/${TAG}_kt/run_results.db gpurun_out/${TAG}_valu_util.json
+else
+    python tools/valu_util.py gpurun_out/${TAG}_sq/run_results.db gpurun_out/${TAG}_kt/run_results.db gpurun_out/${TAG}_valu_util.json
+fi
