@@ -626,8 +626,9 @@ VX_D void history_fix_px(const DenoiseArgs &a, int W, int H, int x, int y, size_
 
 // One pixel per 32-lane half-wave: lane t < 25 of the half takes tap t of the 5x5 pattern (t = 12
 // is the centre, weight 1), so all 24 sparse taps are fetched at once instead of one dependent
-// round trip after another; the sums are combined across the half's lanes (the V4 operators keep
-// the reference's w-from-z behaviour).
+// round trip after another.  The taps' products are then added in the reference's order (centre
+// first, then j-major, k-minor: HistoryFix.h's loop) by every lane of the half from shuffles, so
+// the sums round exactly as history_fix_px's -- a tree reduction rounds differently.
 VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, size_t i, int lane, bool store) {
     const float z = a.depth[i], hist = a.histLen[i];
     const float cMat = ld_ushort(a.material, W, H, x, y);
@@ -635,13 +636,13 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
     const V3 cWP = wp(a, x, y);
     const float dthr = 0.003f * z;
     const float r = exp2f(4.0f - hist) + 1.0f;
-    V4 sum;
-    float wsum = 0.0f;
+    V4 c;            // this lane's tap: ping x weight (the centre: ping, weight 1)
+    float cw = 0.0f;  // its weight, 0 when the tap is not taken (w <= 1e-4)
     if (lane < 25) {
         const int j = lane / 5 - 2, k = lane % 5 - 2;
         if (j == 0 && k == 0) {
-            sum = f4(a.ping[i]);
-            wsum = 1.0f;
+            c = f4(a.ping[i]);
+            cw = 1.0f;
         } else {
             const int sx = x + (int)(k * r), sy = y + (int)(j * r);
             const bool inside = sx >= 0 && sy >= 0 && sx < W && sy < H;
@@ -653,17 +654,23 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
             w = inside ? w : 0;
             w *= (float)(sMat == cMat);
             if (w > 1e-4f) {
-                sum = ld4(a.ping, W, H, sx, sy) * w;
-                wsum = w;
+                c = ld4(a.ping, W, H, sx, sy) * w;
+                cw = w;
             }
         }
     }
-    for (int o = 16; o > 0; o >>= 1) {  // the half's 32 lanes hold every tap
-        sum.x += __shfl_xor(sum.x, o);
-        sum.y += __shfl_xor(sum.y, o);
-        sum.z += __shfl_xor(sum.z, o);
-        sum.w += __shfl_xor(sum.w, o);
-        wsum += __shfl_xor(wsum, o);
+    const int base = (int)(threadIdx.x & 32u);  // the half's first lane in the wave
+    V4 sum(__shfl(c.x, base + 12), __shfl(c.y, base + 12), __shfl(c.z, base + 12), __shfl(c.w, base + 12));
+    float wsum = 1.0f;
+#pragma unroll 1
+    for (int t = 0; t < 25; ++t) {
+        if (t == 12) continue;
+        const float tw = __shfl(cw, base + t);
+        const V4 tc(__shfl(c.x, base + t), __shfl(c.y, base + t), __shfl(c.z, base + t), __shfl(c.w, base + t));
+        if (tw > 0.0f) {
+            sum += tc;
+            wsum += tw;
+        }
     }
     if (lane == 0 && store) a.pong[i] = tf(sum / wsum);
 }
