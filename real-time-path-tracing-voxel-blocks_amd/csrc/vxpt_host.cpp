@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/vxpt.h"
+#include "light_map.hpp"
 #include "vx_internal.hpp"
 
 using namespace vx;
@@ -204,9 +205,7 @@ struct vxpt_ctx {
     float localLightLum = 0.0f;
     // light-update state (Scene.h:91-115): the update type, the edits' instance sets, the instance ->
     // (first light, count) table of the last incremental update, and the remap the next pass applies
-    bool lightIncremental = false;
-    std::set<uint32_t> lightChanged, lightRemoved;
-    std::map<uint32_t, std::pair<uint32_t, uint32_t>> instLightRange;
+    LightUpdateState lightState;
     unsigned prevNumLights = 0;
     int lightsDirty = 0;
     DBuf<int> lightRemap;
@@ -1912,38 +1911,11 @@ int build_tlas(vxpt_ctx *c) {
 }
 
 // VoxelEngine::updateLight (VoxelEngine.cu:658-709) after the light table was rebuilt from
-// prevN lights: buildLightIdMapping (:503-539) -- every previous light unmapped, and for an
-// incremental update buildIncrementalLightMapping (:541-633): a light keeps its position within
-// its instance's run unless the instance was removed or changed; the instance -> range table is
-// only refreshed by an incremental update, so the first one after a full build maps nothing.
-// The edit sets are cleared only when there were previous lights.  The next trace pass applies
-// the table (Restir.h:48-79).
+// prevN lights: the remap table (light_map.hpp), uploaded for the next trace pass, which applies
+// it to the previous reservoirs (Restir.h:48-79).
 int light_update(vxpt_ctx *c, unsigned prevN) {
-    std::vector<int> remap(prevN, -1);
+    const std::vector<int> remap = light_id_map(c->lightState, c->lightMap, prevN, c->nLights);
     if (prevN > 0) {
-        if (c->lightIncremental) {
-            std::map<uint32_t, std::pair<uint32_t, uint32_t>> cur;
-            for (size_t k = 0; k < c->lightMap.size(); k += 3)
-                cur[c->lightMap[k]] = {c->lightMap[k + 1], c->lightMap[k + 2]};
-            std::vector<int64_t> owner(prevN, -1);
-            for (const auto &e : c->instLightRange)
-                for (uint32_t i = 0; i < e.second.second; ++i)
-                    if (e.second.first + i < prevN) owner[e.second.first + i] = e.first;
-            for (unsigned p = 0; p < prevN; ++p) {
-                if (owner[p] < 0) continue;
-                const uint32_t id = (uint32_t)owner[p];
-                if (c->lightRemoved.count(id) || c->lightChanged.count(id)) continue;
-                const auto it = cur.find(id);
-                if (it == cur.end()) continue;
-                const auto &pr = c->instLightRange[id];
-                const uint32_t rel = p - pr.first;
-                if (rel < pr.second && rel < it->second.second && it->second.first + rel < c->nLights)
-                    remap[p] = (int)(it->second.first + rel);
-            }
-            c->instLightRange = cur;
-        }
-        c->lightChanged.clear();
-        c->lightRemoved.clear();
         if (int r = upload_vec(c, c->lightRemap, remap.data(), remap.size())) return r;
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
@@ -1959,7 +1931,7 @@ int refresh_instances(vxpt_ctx *c, bool lights, bool full) {
     collect_instances(c);
     if (int r = build_tlas(c)) return r;
     if (lights) {
-        if (full) c->lightIncremental = false;
+        if (full) c->lightState.incremental = false;
         const unsigned prevN = c->nLights;
         if (int r = build_lights(c)) return r;
         if (int r = light_update(c, prevN)) return r;
@@ -2254,9 +2226,9 @@ int vxpt_set_block(vxpt_ctx *c, int x, int y, int z, int block_id) {
         return -1;
     };
     const int lo = old != block_id ? light_obj(old) : -1, ln = old != block_id ? light_obj(block_id) : -1;
-    if (lo >= 0) c->lightRemoved.insert(instance_id(c, lo, x, y, z));
-    if (ln >= 0) c->lightChanged.insert(instance_id(c, ln, x, y, z));
-    if (lo >= 0 || ln >= 0) c->lightIncremental = true;
+    if (lo >= 0) c->lightState.removed.insert(instance_id(c, lo, x, y, z));
+    if (ln >= 0) c->lightState.changed.insert(instance_id(c, ln, x, y, z));
+    if (lo >= 0 || ln >= 0) c->lightState.incremental = true;
     return refresh_instances(c, lo >= 0 || ln >= 0, false);
 }
 

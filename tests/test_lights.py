@@ -325,3 +325,59 @@ def test_deep_bvh_walk_matches_brute_force(deep_model_root, cull):
     """A BLAS at the depth limit (40) under a TLAS of 90 instances: the walk's shared stack holds
     both levels and the closest / any hits still equal the brute-force loop bit for bit."""
     _probe_vs_brute_force(deep_model_root, cull, 0.05)
+
+
+def test_library_light_remap_matches_oracle_on_random_edits(tmp_path):
+    """The library's light-id remap (csrc/light_map.hpp, compiled here into a CPU driver) equals the
+    oracle's restatement of buildLightIdMapping / buildIncrementalLightMapping over random sequences
+    of lantern placements / removals and occasional full reloads (incl. emptying the light table)."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "light_map_driver")
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-I", os.path.join(repo, "real-time-path-tracing-voxel-blocks_amd", "csrc"),
+                           os.path.join(repo, "tests", "native", "light_map_driver.cpp"), "-o", exe])
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        o = oracle.Oracle(8, 8)
+        live = {}  # instance id -> light count
+        script, expect = [], []
+
+        def update(full):
+            m = sorted(live.items())
+            ranges, first = {}, 0
+            for iid, cnt in m:
+                ranges[iid] = (first, cnt)
+                first += cnt
+            prev = o._lights["num"]
+            o._light_update(ranges, first, full)
+            expect.append(o._remap_keep[:prev].tolist())
+            trip = " ".join("%d %d %d" % (iid, f, c) for iid, (f, c) in sorted(ranges.items()))
+            script.append("update %d %d %d %d %s" % (int(full), prev, first, len(m), trip))
+
+        update(True)
+        for step in range(40):
+            r = rng.random()
+            if r < 0.08:
+                update(True)  # reload
+                continue
+            for _ in range(int(rng.integers(1, 4))):
+                if live and rng.random() < 0.5:
+                    iid = int(rng.choice(sorted(live)))
+                    del live[iid]
+                    o.light_edit(iid, removed=True)
+                    script.append("edit %d 1" % iid)
+                else:
+                    iid = int(rng.integers(13, 13 + 300))
+                    live[iid] = 8 if trial % 2 == 0 else int(rng.integers(1, 9))
+                    o.light_edit(iid, removed=False)
+                    script.append("edit %d 0" % iid)
+            if rng.random() < 0.1:
+                for iid in list(live):
+                    del live[iid]
+                    o.light_edit(iid, removed=True)
+                    script.append("edit %d 1" % iid)
+            update(False)
+        out = subprocess.run([exe], input="\n".join(script) + "\n", capture_output=True, text=True, check=True).stdout
+        got = [[int(v) for v in ln.split()[1:]] for ln in out.splitlines()]
+        assert got == expect, trial
+        assert any(any(v >= 0 for v in e) for e in expect)  # some lights were carried over
