@@ -1183,7 +1183,9 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBefor
     // secondary / visibility rays go through the compacted queues; their
     // counters (4 per segment) are zeroed once per pass
     hipMemsetAsync(a.wb.qCount, 0, (64 + 3 * 16 * kShards * 16) * sizeof(unsigned), st);
-    const dim3 gr(a.numCU * 16);
+    // the stragglers' grid: a fixed number of workgroups per CU (their count is on the device; each
+    // wave reads it and strides over its shard), VXPT_RESUME_WG per CU for the sweep in DESIGN.md
+    const dim3 gr(a.numCU * (a.resumeWgPerCU > 0 ? a.resumeWgPerCU : 16));
     auto trav = [&](bool occ, int q, int cap) {
         const dim3 gq((cap + 255) / 256);
         const int shardCap = (int)((gq.x + kShards - 1) / kShards) * 256;

@@ -208,6 +208,7 @@ struct TraceArgs {
     const int *lightRemap;
     int prevNumLights;
     int lightsDirty;
+    int resumeWgPerCU;  // k_resume workgroups per CU (0: 16)
 };
 
 // kernel launchers (defined in the .hip translation units)

@@ -742,6 +742,7 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.numCU = c->numCU;
     a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
     a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
+    a.resumeWgPerCU = getenv("VXPT_RESUME_WG") ? atoi(getenv("VXPT_RESUME_WG")) : 16;
     a.prevSceneEmpty = c->prevSceneEmpty;
     // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
     a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;

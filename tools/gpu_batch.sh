@@ -30,6 +30,10 @@ for step in "$@"; do
     caps) for c in 4:0 6:0 8:0 6:16 12:0; do
               VXPT_ITER_CAP=${c%%:*} VXPT_ITER_CAP2=${c##*:} run cap$c 200 python -u bench.py --steps 20 --warmup 6 \
                   --no-cpu-baseline > gpurun_out/b_cap${c/:/_}.json 2>/dev/null || exit $?
+          done
+          for g in 4 8 32; do
+              VXPT_RESUME_WG=$g run wg$g 200 python -u bench.py --steps 20 --warmup 6 --no-cpu-baseline \
+                  > gpurun_out/b_wg$g.json 2>/dev/null || exit $?
           done ;;
     full) run full 400 python -u bench.py > gpurun_out/b_full.json 2> gpurun_out/b_full.err || exit $? ;;
     c2) run c2 300 python -u bench.py --primary-only --cpu-seconds 8 > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || exit $? ;;
