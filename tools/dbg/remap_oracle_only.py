@@ -38,3 +38,11 @@ for f in range(6):
         o.set_meshes(models, defs, light_update="update")
     o.trace(f); o.set_prev_scene_empty(False); o.post_trace(); o.denoise(f, f + 1)
     print("frame", f, flush=True)
+h = o.read(19)
+dep = o.read(1)
+mat = o.read(5)
+for (x, y) in [(40, 12), (51, 15), (35, 17), (38, 27), (76, 30), (50, 71)]:
+    win = h[max(0, y - 2):y + 3, max(0, x - 2):x + 3]
+    print("px", x, y, "hist", h[y, x], "min hist 5x5", win.min(), "n<=4", int((win <= 4).sum()),
+          "depth", dep[y, x], "mat", mat[y, x], "sky in 5x5", int((dep[max(0, y - 2):y + 3, max(0, x - 2):x + 3] > 5e5).sum()))
+print("listed (hist<=4, non-sky) pixels:", int(((h <= 4) & (dep < 5e5)).sum()))
