@@ -240,6 +240,25 @@ def main():
         with open(vu[-1]) as f:
             valu = json.load(f)["trace_valu_util"]
         valu_src = os.path.relpath(vu[-1], REPO)
+    # the box's practical HBM ceiling ("record the measured copy-kernel bandwidth"): a
+    # 1 GiB device-to-device copy, read + write bytes / time, best of 5
+    copy_gbs = None
+    try:
+        src = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:%d" % local)
+        dst = torch.empty_like(src)
+        best = None
+        for _ in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dst.copy_(src)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        copy_gbs = round(2 * src.numel() / (best * 1e-3) / 1e9, 1)
+        del src, dst
+    except Exception as e:  # measurement extra only
+        print("copy bandwidth not measured: %s" % e, file=sys.stderr)
     depth = r.read("DEPTH")
     hit_frac = float((depth < 1e26).mean())  # scene sanity: fraction of primary rays that hit voxels
     cpu = None
@@ -269,6 +288,7 @@ def main():
             # the trace passes over this rank's rows (bands: with their halo exchanges)
             "trace_mpaths_s": round(band_px * spp / (avg_trace * 1e-3) / 1e6, 3),
             "trace_valu_util": valu, "trace_valu_util_source": valu_src,
+            "hbm_copy_gbs": copy_gbs,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
