@@ -20,10 +20,10 @@ with the exchanges inserted:
 
 The rows are moved by a transport: DistExchange (torch.distributed: RCCL over
 xGMI on GPUs, gloo on CPU) or LocalExchange (bands of one process; tests).
-Bands must be at least TRACE_HALO rows tall.  This host-driven schedule assumes a
-static camera (reprojection offsets <= 8 rows); the library's own schedule
-(vxpt_render_frame with a communicator, vxpt_render_frame_linked) deepens its halos
-for a camera that turns between frames (vxpt_band_halo_rows).
+Bands must be at least TRACE_HALO rows tall.  A camera that turns between
+frames needs deeper halos: pass run_frame the depths vxpt.band_halo_rows gives
+for the frame's camera pair (and the previous frame's), as the library's own
+schedule (vxpt_render_frame with a communicator, vxpt_render_frame_linked) does.
 """
 import numpy as np
 
@@ -47,15 +47,26 @@ def atrous_rows(step):
     return step + (step // 4 if step > 4 else 0)
 
 
-def frame_ops(frame, spp, p):
+# the previous pass's G-buffer as the next trace reads it ("PREV:<name>"): the library's last slot
+# (the same buffer as <name>), the oracle's Prev* copies
+PREV_GBUF = ["PREV:" + n for n in GBUF]
+
+
+def frame_ops(frame, spp, p, halo=(TRACE_HALO, 2), prev_halo=(TRACE_HALO, 2)):
     """Operations of one banded frame.  p: dict with the denoiser switches
-    (ta, hf, hc, spatial, firefly, iters).  Yields ("trace", it, flags),
+    (ta, hf, hc, spatial, firefly, iters).  halo: (trace rows, history rows) for this frame's
+    camera motion (vxpt.band_halo_rows); prev_halo: the depths the previous frame exchanged --
+    deeper halos are topped up before the first pass.  Yields ("trace", it, flags),
     ("post_trace",), ("pass", id, arg, arg2), ("exchange", [buffers], rows)."""
     it0 = frame * spp
+    trace_rows, hist_rows = halo
+    if frame > 0 and (trace_rows > prev_halo[0] or hist_rows > prev_halo[1]):
+        yield ("exchange", PREV_GBUF + [RES[(it0 - 1) & 1]], trace_rows)
+        yield ("exchange", HISTORY, hist_rows)
     for s in range(spp):
         flags = 0 if spp == 1 else (ACCUMULATE | (ACCUM_FIRST if s == 0 else 0) | (spp << 8))
         yield ("trace", it0 + s, flags)
-        yield ("exchange", GBUF + [RES[(it0 + s) & 1]], TRACE_HALO)
+        yield ("exchange", GBUF + [RES[(it0 + s) & 1]], trace_rows)
         yield ("post_trace",)
     yield ("exchange", ["ILLUM"], 2)
     it = it0 + spp
@@ -63,13 +74,13 @@ def frame_ops(frame, spp, p):
     if p["firefly"]:
         # the firefly pass writes the world-position plane too (pass 11 alone otherwise)
         yield ("pass", 0, used & 1, 0)
-        yield ("exchange", [RES[used & 1]], TRACE_HALO)
+        yield ("exchange", [RES[used & 1]], trace_rows)
         yield ("exchange", ["ILLUM"], 2)
     else:
         yield ("pass", 11, 0, 0)
     if frame == 0:
         yield ("pass", 12, 0, 0)
-        yield ("exchange", HISTORY, 2)
+        yield ("exchange", HISTORY, hist_rows)
     fin = 0
     if p["ta"] and frame > 0:
         yield ("pass", 2, 0, 0)
@@ -82,7 +93,7 @@ def frame_ops(frame, spp, p):
             fin = 2
         if p["hc"]:
             yield ("pass", 4, 0, 0)
-            yield ("exchange", HISTORY, 2)
+            yield ("exchange", HISTORY, hist_rows)
             fin = 3
     out_done = False
     if p["spatial"]:
@@ -176,9 +187,9 @@ class DistExchange:
                     self.b.put_rows(name, ry, rn, recv)
 
 
-def run_frame(backends, exchange, frame, spp, p):
+def run_frame(backends, exchange, frame, spp, p, halo=(TRACE_HALO, 2), prev_halo=(TRACE_HALO, 2)):
     """Apply one frame's operations to every band backend of this process."""
-    for op in frame_ops(frame, spp, p):
+    for op in frame_ops(frame, spp, p, halo, prev_halo):
         kind = op[0]
         if kind == "exchange":
             exchange(op[1], op[2])
@@ -208,14 +219,19 @@ class GpuBand:
     def dpass(self, which, arg, arg2):
         self.r.denoise_pass(which, arg, arg2, self.params)
 
+    @staticmethod
+    def _name(name):  # the library's last G-buffer slot is the next trace's previous one
+        return name[5:] if name.startswith("PREV:") else name
+
     def read_full(self, name):
-        return self.r.read(name)
+        return self.r.read(self._name(name))
 
     def write_full(self, name, data):
-        self.r.write(name, data)
+        self.r.write(self._name(name), data)
 
     def rows_tensor(self, name, y, n, device):
         import torch
+        name = self._name(name)
         rb = self.r.row_bytes(name)
         t = torch.empty(max(1, n * rb), dtype=torch.uint8, device=device)
         if n:
@@ -224,6 +240,7 @@ class GpuBand:
         return t
 
     def put_rows(self, name, y, n, t):
+        name = self._name(name)
         if n:
             self.r.copy_rows(name, y, n, t.data_ptr(), to_buffer=True)
             self.r.sync()

@@ -4,6 +4,9 @@ import numpy as np
 
 IDS = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERIAL=5, MAT_PARAM=6, PING=15,
            PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19, PREV_HIST_LEN=20, OUTPUT=21)
+# the previous pass's G-buffer the oracle's next trace reads: its Prev* copies
+IDS.update({"PREV:NORMAL_ROUGH": 8, "PREV:GEO_NORMAL_THIN": 9, "PREV:ALBEDO": 10, "PREV:MAT_PARAM": 11,
+            "PREV:DEPTH": 12, "PREV:MATERIAL": 13})
 COPY_SRC = {0: 0, 1: 15, 2: 16, 3: 17}
 
 

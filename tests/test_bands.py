@@ -299,3 +299,45 @@ def test_gpu_linked_bands_follow_a_turning_camera(n, w, h, turns):
         r.set_camera(*far[:2], fov=far[2], prev=prev)
     with pytest.raises(vxpt.VxptError):
         linked.render_frame(len(turns), spp, p)
+
+
+def _oracle_turning(turns, halos_from_library):
+    """Banded (2 oracle bands, LocalExchange) and single-band oracle renders of a camera turning
+    between frames; the banded schedule's halo depths come from the library's vxpt_band_halo_rows
+    (or stay static).  Returns the per-frame outputs of both."""
+    import vxpt
+    bands_ = [bands.band_rows(H, 2, r) for r in range(2)]
+    single = _oracle()
+    backs = [OracleBand(_oracle(), *b) for b in bands_]
+    ex = bands.LocalExchange(backs, bands_)
+    d, prev, prev_halo = C1_CAMERA[1], C1_CAMERA, (bands.TRACE_HALO, 2)
+    outs = []
+    for f, (dy, dp) in enumerate(turns):
+        d = _turn(d, dy, dp)
+        cur = (C1_CAMERA[0], d, C1_CAMERA[2])
+        for o in [single] + [b.o for b in backs]:
+            o.set_camera(*cur[:2], fov=cur[2])
+            o.set_camera(*prev[:2], fov=prev[2], which=1)
+        halo = vxpt.band_halo_rows(cur, prev, W, H, 2) if halos_from_library else (bands.TRACE_HALO, 2)
+        assert halo is not None
+        single.trace(f)
+        single.post_trace()
+        single.denoise(f, f + 1)
+        bands.run_frame(backs, ex, f, 1, P, halo, prev_halo)
+        out = np.concatenate([b.o.read(21)[y0:y1] for b, (y0, y1) in zip(backs, bands_)])
+        outs.append((single.read(21), out, halo))
+        prev, prev_halo = cur, halo
+    return outs
+
+
+def test_oracle_bands_follow_a_turning_camera():
+    """The band schedule with the library's camera-aware halo depths (vxpt_band_halo_rows, topped
+    up at the start of a frame) renders a pitching camera bit for bit like one band; the static
+    depths do not -- so the computed depths are what makes it exact."""
+    turns = [(0, 0), (0, 3), (1, -3), (0, 0)]
+    good = _oracle_turning(turns, True)
+    assert any(h != (bands.TRACE_HALO, 2) for _, _, h in good)
+    for f, (ref, out, _) in enumerate(good):
+        np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32), err_msg="frame %d" % f)
+    static = _oracle_turning(turns, False)
+    assert any(not np.array_equal(out.view(np.uint32), ref.view(np.uint32)) for ref, out, _ in static)
