@@ -214,9 +214,13 @@ int main(int argc, char **argv) {
     // the light table (a full light update); block types whose OBJ file is missing stay empty
     {
         int nModels = 0;
-        if (vxpt_load_models(ctx, o.assetsDir.empty() ? nullptr : o.assetsDir.c_str(), &nModels) != VXPT_OK)
+        const int rc = vxpt_load_models(ctx, o.assetsDir.empty() ? nullptr : o.assetsDir.c_str(), &nModels);
+        if (rc == VXPT_ERR_IO)  // a data directory without the asset yaml files: no instanced blocks
+            std::cout << "Instanced meshes not loaded: " << vxpt_last_error(ctx) << std::endl;
+        else if (rc != VXPT_OK)
             return fail("loading the instanced meshes");
-        std::cout << "Instanced meshes loaded: " << nModels << std::endl;
+        else
+            std::cout << "Instanced meshes loaded: " << nModels << std::endl;
     }
 
     // :200-251: camera from the scene file (defaults when it is absent), history camera = camera
