@@ -92,6 +92,7 @@ VX_D void stat_wave(int kind, bool active, const int *it) {
 #endif
 // mode 2: camera rays (RayGen.cu:102-126; initialises the path state);
 // mode 0: continuing path rays; mode 1: BRDF-candidate queue.
+template <bool BOX>
 __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     int px, py;
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
     }
     int iters[5] = {0, 0, 0, 0, 0};
     if (active) {
-        const Hit h = dda_closest(a.world, o, d, tmax VX_IT);
+        const Hit h = dda_closest<BOX>(a.world, o, d, tmax VX_IT);
         w.cHit[s] = pack_hit(h);
         w.cT[s] = h.t;
     }
@@ -216,7 +217,7 @@ VX_D unsigned *straggler_count(const WaveBufs &w, int level, int q, int k) {
     return w.qCount + 64 + (((level - 1) * 16 + q) * kShards + k) * 16;
 }
 
-template <bool OCC>
+template <bool OCC, bool BOX>
 __global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int shardCap) {
     __shared__ unsigned sTot[4], sBase[4];
     const WaveBufs &w = a.wb;
@@ -236,8 +237,8 @@ __global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int 
     if (live) {
         const float4 ro = w.qO[i], rd = w.qD[i];
         id = w.qId[i];
-        rc = dda_begin<OCC>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
-        for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC>(a.world, st, h, itp);
+        rc = dda_begin<OCC, BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
+        for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC, BOX>(a.world, st, h, itp);
     }
 #ifdef VX_STATS
     stat_wave((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), live, iters);
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int 
 // grid normally covers every straggler in one round).  With cap > 0 the walks
 // stop after cap more iterations and the unfinished ones move on to the next
 // level, same shard, one atomic per wave.
-template <bool OCC>
+template <bool OCC, bool BOX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
     const WaveBufs &w = a.wb;
     const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
@@ -297,9 +298,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             e = sv.cell.w;
             const float4 ro = w.qO[e], rd = w.qD[e];
             id = w.qId[e];
-            dda_resume(a.world, xyz(ro), xyz(rd), ro.w, rd.w, sv, st);
+            dda_resume<BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, sv, st);
             rc = DdaRun;
-            for (int it = 0; rc == DdaRun && (cap <= 0 || it < cap); ++it) rc = dda_iter<OCC>(a.world, st, h, itp);
+            for (int it = 0; rc == DdaRun && (cap <= 0 || it < cap); ++it) rc = dda_iter<OCC, BOX>(a.world, st, h, itp);
         }
 #ifdef VX_STATS
         stat_wave(5, live, iters);
@@ -1102,6 +1103,7 @@ __global__ __launch_bounds__(256) void k_primary_gbuffer(TraceArgs a) {
     a.illum[pi] = make_float4(0.0f, 0.0f, 0.0f, h.t);
 }
 
+template <bool BOX>
 __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *rays, int *out, float *t, int mode) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
@@ -1115,11 +1117,11 @@ __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *r
         Dda st;
         const bool occ = (mode & 2) != 0;
         const float tmin = occ ? r[6] : 0.0f;
-        int rc = occ ? dda_begin<true>(w, o, d, tmin, r[7], st, h) : dda_begin<false>(w, o, d, 0.0f, r[7], st, h);
+        int rc = occ ? dda_begin<true, BOX>(w, o, d, tmin, r[7], st, h) : dda_begin<false, BOX>(w, o, d, 0.0f, r[7], st, h);
         while (rc == DdaRun) {
             const DdaSaved sv = dda_save(st, i);
-            dda_resume(w, o, d, tmin, r[7], sv, st);
-            rc = occ ? dda_iter<true>(w, st, h) : dda_iter<false>(w, st, h);
+            dda_resume<BOX>(w, o, d, tmin, r[7], sv, st);
+            rc = occ ? dda_iter<true, BOX>(w, st, h) : dda_iter<false, BOX>(w, st, h);
         }
         if (occ) {
             q[0] = rc == DdaEvent ? 1 : 0;
@@ -1133,12 +1135,12 @@ __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *r
         return;
     }
     if (mode == 2) {
-        q[0] = dda_occluded(w, o, d, r[6], r[7]) ? 1 : 0;
+        q[0] = dda_occluded<BOX>(w, o, d, r[6], r[7]) ? 1 : 0;
         q[1] = q[2] = q[3] = q[4] = q[5] = 0;
         t[i] = 0.0f;
         return;
     }
-    const Hit h = dda_closest(w, o, d, r[7]);
+    const Hit h = dda_closest<BOX>(w, o, d, r[7]);
     q[0] = h.hit; q[1] = h.x; q[2] = h.y; q[3] = h.z; q[4] = h.face; q[5] = h.id;
     t[i] = h.t;
 }
@@ -1168,14 +1170,21 @@ hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *
 }
 
 hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, float *t, int mode, hipStream_t st) {
-    hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, st, w, n, rays, out, t, mode);
+    if (w.bbox) hipLaunchKernelGGL(k_probe<true>, dim3((n + 255) / 256), dim3(256), 0, st, w, n, rays, out, t, mode);
+    else hipLaunchKernelGGL(k_probe<false>, dim3((n + 255) / 256), dim3(256), 0, st, w, n, rays, out, t, mode);
     return hipGetLastError();
 }
 
 hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir) {
     const dim3 g((a.nSlots + 255) / 256), g4((4 * a.nSlots + 255) / 256), b(256);
     const bool mesh = a.mesh.nInst > 0;
-    hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 2);
+    // the walks use the empty-box tables when the world has them (VXPT_DDA_BOXES), else the cubes
+    const bool box = a.world.bbox != nullptr;
+    auto closest = [&](int mode) {
+        if (box) hipLaunchKernelGGL(k_closest<true>, g, b, 0, st, a, mode);
+        else hipLaunchKernelGGL(k_closest<false>, g, b, 0, st, a, mode);
+    };
+    closest(2);
     if (a.primaryOnly) {  // C2 bring-up: the voxel G-buffer only
         hipLaunchKernelGGL(k_primary_gbuffer, g, b, 0, st, a);
         return hipGetLastError();
@@ -1189,22 +1198,32 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBefor
     auto trav = [&](bool occ, int q, int cap) {
         const dim3 gq((cap + 255) / 256);
         const int shardCap = (int)((gq.x + kShards - 1) / kShards) * 256;
-        if (occ) {
-            hipLaunchKernelGGL(k_queue<true>, gq, b, 0, st, a, q, a.iterCap, shardCap);
-            hipLaunchKernelGGL(k_resume<true>, gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
-            if (a.iterCap2 > 0) hipLaunchKernelGGL(k_resume<true>, gr, b, 0, st, a, q, 2, shardCap, 0);
-            if (mesh) hipLaunchKernelGGL(k_mesh_queue<true>, gq, b, 0, st, a, q);
+        if (occ && box) {
+            hipLaunchKernelGGL((k_queue<true, true>), gq, b, 0, st, a, q, a.iterCap, shardCap);
+            hipLaunchKernelGGL((k_resume<true, true>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
+            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<true, true>), gr, b, 0, st, a, q, 2, shardCap, 0);
+        } else if (occ) {
+            hipLaunchKernelGGL((k_queue<true, false>), gq, b, 0, st, a, q, a.iterCap, shardCap);
+            hipLaunchKernelGGL((k_resume<true, false>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
+            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<true, false>), gr, b, 0, st, a, q, 2, shardCap, 0);
+        } else if (box) {
+            hipLaunchKernelGGL((k_queue<false, true>), gq, b, 0, st, a, q, a.iterCap, shardCap);
+            hipLaunchKernelGGL((k_resume<false, true>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
+            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<false, true>), gr, b, 0, st, a, q, 2, shardCap, 0);
         } else {
-            hipLaunchKernelGGL(k_queue<false>, gq, b, 0, st, a, q, a.iterCap, shardCap);
-            hipLaunchKernelGGL(k_resume<false>, gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
-            if (a.iterCap2 > 0) hipLaunchKernelGGL(k_resume<false>, gr, b, 0, st, a, q, 2, shardCap, 0);
-            if (mesh) hipLaunchKernelGGL(k_mesh_queue<false>, gq, b, 0, st, a, q);
+            hipLaunchKernelGGL((k_queue<false, false>), gq, b, 0, st, a, q, a.iterCap, shardCap);
+            hipLaunchKernelGGL((k_resume<false, false>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
+            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<false, false>), gr, b, 0, st, a, q, 2, shardCap, 0);
+        }
+        if (mesh) {
+            if (occ) hipLaunchKernelGGL(k_mesh_queue<true>, gq, b, 0, st, a, q);
+            else hipLaunchKernelGGL(k_mesh_queue<false>, gq, b, 0, st, a, q);
         }
     };
     if (mesh) hipLaunchKernelGGL(k_mesh_slots, g, b, 0, st, a, 2);
     for (int seg = 0; seg < a.segments; ++seg) {
         if (seg > 0) {
-            hipLaunchKernelGGL(k_closest, g, b, 0, st, a, 0);
+            closest(0);
             if (mesh) hipLaunchKernelGGL(k_mesh_slots, g, b, 0, st, a, 0);
         }
         // the shading kernels' mesh variants (mesh hits, thin films, local lights) run only with meshes

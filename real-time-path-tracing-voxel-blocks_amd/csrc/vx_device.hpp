@@ -14,11 +14,14 @@ constexpr float kRoughThresh = 0.00001f, kTranslThresh = 0.001f;
 constexpr float kMinPdf = 1e-5f, kMaxThroughput = 32.0f, kMinLobe = 0.05f;
 
 // ----------------------------------------------------------------- voxel DDA
-VX_D bool is_cube(int id) { return id >= 1 && id <= 12; }
+// host + device bit casts (the walk also runs on the host in the CPU tests)
+VX_HD float bits_as_float(int v) { return __builtin_bit_cast(float, v); }
+VX_HD int float_as_bits(float v) { return __builtin_bit_cast(int, v); }
+VX_HD bool is_cube(int id) { return id >= 1 && id <= 12; }
 
 struct Hit { int hit, x, y, z, face, id; float t; };
 
-VX_D int entry_face(int a, int s) {
+VX_HD int entry_face(int a, int s) {
     return a == 0 ? (s > 0 ? 2 : 3) : (a == 1 ? (s > 0 ? 1 : 0) : (s > 0 ? 5 : 4));
 }
 
@@ -36,29 +39,29 @@ struct Cell {
 
 // t of the next plane after cell c along one axis; the only formula for plane t,
 // so skipped and stepped walks produce identical values.
-VX_D float next_t(int c, int s, float o, float inv, bool mv) {
+VX_HD float next_t(int c, int s, float o, float inv, bool mv) {
     if (!mv) return INFINITY;
     return ((float)(s > 0 ? c + 1 : c) - o) * inv;
 }
 // axis order of the reference tie rule (VoxelEngine.cu:1040-1166 strict '<'):
 // smallest t first, ties to Z, then Y, then X
-VX_D int pick3(float tx, float ty, float tz) {
+VX_HD int pick3(float tx, float ty, float tz) {
     if (tx < ty) return tx < tz ? 0 : 2;
     return ty < tz ? 1 : 2;
 }
-VX_D bool before(float t1, int a1, float t2, int a2) { return t1 < t2 || (t1 == t2 && a1 > a2); }
+VX_HD bool before(float t1, int a1, float t2, int a2) { return t1 < t2 || (t1 == t2 && a1 > a2); }
 
 // brick index shared by bdist / cellMask / bricks (macro-major: a 16^3 macro
 // cell's 64 bricks are contiguous) and the cell inside the brick
-VX_D int brick_index(const WorldDev &w, int x, int y, int z) {
+VX_HD int brick_index(const WorldDev &w, int x, int y, int z) {
     const int m = (x >> 4) + w.mx * ((z >> 4) + w.mz * (y >> 4));
     return m * 64 + (((x >> 2) & 3) + 4 * (((z >> 2) & 3) + 4 * ((y >> 2) & 3)));
 }
-VX_D int cell_of(int x, int y, int z) { return (x & 3) + 4 * ((z & 3) + 4 * (y & 3)); }
+VX_HD int cell_of(int x, int y, int z) { return (x & 3) + 4 * ((z & 3) + 4 * (y & 3)); }
 
 // Advance one axis to the cell it occupies when the walk leaves the box through
 // the crossing (Te, ea): exactly the planes the cell-by-cell walk would cross first.
-VX_D void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int lo, int hi, int ab, float Te, int ea) {
+VX_HD void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int lo, int hi, int ab, float Te, int ea) {
     int est = clampi((int)floorf(o + Te * d), lo, hi);
     est = s > 0 ? max(est, cb) : min(est, cb);
     while (est != cb) {
@@ -74,15 +77,16 @@ VX_D void skip_axis(int &cb, float &tb, int s, float o, float d, float inv, int 
     cb = est;
     tb = tn;
 }
-// Jump from the current cell to the last cell, inside the empty cube of S
+// Jump from the current cell to the last cell, inside the empty box of Sx x Sy x Sz
 // bricks that starts at the current brick and extends in the ray's octant
-// (clamped to the world), that the ray visits; the cube's exit crossing is
-// then the walk's next step.
-VX_D void skip_cube(const WorldDev &w, const Ray3 &r, Cell &c, int S) {
-    const int e = 4 * (S - 1);
-    const int lx = r.sx > 0 ? (c.x & ~3) : max((c.x & ~3) - e, 0), hx = r.sx > 0 ? min((c.x | 3) + e, w.wx - 1) : (c.x | 3);
-    const int ly = r.sy > 0 ? (c.y & ~3) : max((c.y & ~3) - e, 0), hy = r.sy > 0 ? min((c.y | 3) + e, w.wy - 1) : (c.y | 3);
-    const int lz = r.sz > 0 ? (c.z & ~3) : max((c.z & ~3) - e, 0), hz = r.sz > 0 ? min((c.z | 3) + e, w.wz - 1) : (c.z | 3);
+// (clamped to the world), that the ray visits; the box's exit crossing is
+// then the walk's next step.  The landing is exact per axis (skip_axis), so any
+// empty box gives the cell-by-cell walk's result.
+VX_HD void skip_box(const WorldDev &w, const Ray3 &r, Cell &c, int Sx, int Sy, int Sz) {
+    const int ex = 4 * (Sx - 1), ey = 4 * (Sy - 1), ez = 4 * (Sz - 1);
+    const int lx = r.sx > 0 ? (c.x & ~3) : max((c.x & ~3) - ex, 0), hx = r.sx > 0 ? min((c.x | 3) + ex, w.wx - 1) : (c.x | 3);
+    const int ly = r.sy > 0 ? (c.y & ~3) : max((c.y & ~3) - ey, 0), hy = r.sy > 0 ? min((c.y | 3) + ey, w.wy - 1) : (c.y | 3);
+    const int lz = r.sz > 0 ? (c.z & ~3) : max((c.z & ~3) - ez, 0), hz = r.sz > 0 ? min((c.z | 3) + ez, w.wz - 1) : (c.z | 3);
     const float Tx = r.mx ? ((float)(r.sx > 0 ? hx + 1 : lx) - r.ox) * r.ix : INFINITY;
     const float Ty = r.my ? ((float)(r.sy > 0 ? hy + 1 : ly) - r.oy) * r.iy : INFINITY;
     const float Tz = r.mz ? ((float)(r.sz > 0 ? hz + 1 : lz) - r.oz) * r.iz : INFINITY;
@@ -95,8 +99,10 @@ VX_D void skip_cube(const WorldDev &w, const Ray3 &r, Cell &c, int S) {
     if (ea == 2) { c.z = r.sz > 0 ? hz : lz; c.tz = Tz; }
     else if (r.mz) skip_axis(c.z, c.tz, r.sz, r.oz, r.dz, r.iz, lz, hz, 2, Te, ea);
 }
+// the empty cube of S bricks (the default tables)
+VX_HD void skip_cube(const WorldDev &w, const Ray3 &r, Cell &c, int S) { skip_box(w, r, c, S, S, S); }
 
-VX_D bool slab(float o, float d, float W, int a, float &t0, float &t1, int &ax) {
+VX_HD bool slab(float o, float d, float W, int a, float &t0, float &t1, int &ax) {
     if (d == 0.0f) return !(o < 0.0f || o >= W);
     const float inv = 1.0f / d;
     const float ta = (0.0f - o) * inv, tb = (W - o) * inv;
@@ -109,14 +115,14 @@ VX_D bool slab(float o, float d, float W, int a, float &t0, float &t1, int &ax) 
 // Start a walk; returns false if the ray never meets the world box.  For an
 // origin outside the box, `outside` is set and the entry crossing (axis `ax`,
 // t `tEnter`) is already taken.
-VX_D void ray_setup(V3 o, V3 d, Ray3 &r) {
+VX_HD void ray_setup(V3 o, V3 d, Ray3 &r) {
     r.ox = o.x; r.oy = o.y; r.oz = o.z;
     r.dx = d.x; r.dy = d.y; r.dz = d.z;
     r.mx = d.x != 0.0f; r.my = d.y != 0.0f; r.mz = d.z != 0.0f;
     r.sx = d.x > 0.0f ? 1 : -1; r.sy = d.y > 0.0f ? 1 : -1; r.sz = d.z > 0.0f ? 1 : -1;
     r.ix = r.mx ? 1.0f / d.x : 0.0f; r.iy = r.my ? 1.0f / d.y : 0.0f; r.iz = r.mz ? 1.0f / d.z : 0.0f;
 }
-VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outside, int &ax, float &tEnter) {
+VX_HD bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outside, int &ax, float &tEnter) {
     ray_setup(o, d, r);
     c.x = (int)floorf(o.x); c.y = (int)floorf(o.y); c.z = (int)floorf(o.z);
     outside = !(c.x >= 0 && c.x < w.wx && c.y >= 0 && c.y < w.wy && c.z >= 0 && c.z < w.wz);
@@ -141,7 +147,7 @@ VX_D bool walk_begin(const WorldDev &w, V3 o, V3 d, Ray3 &r, Cell &c, bool &outs
 
 // One step of the walk: cross the nearest plane.  Returns the crossed plane's
 // t and coordinate and the face of the entered cell the crossing goes through.
-VX_D void walk_step(const Ray3 &r, Cell &c, float &t, int &planeCoord, int &face) {
+VX_HD void walk_step(const Ray3 &r, Cell &c, float &t, int &planeCoord, int &face) {
     const int a = pick3(c.tx, c.ty, c.tz);
     if (a == 0) {
         t = c.tx; planeCoord = r.sx > 0 ? c.x + 1 : c.x; face = r.sx > 0 ? 2 : 3;
@@ -154,11 +160,11 @@ VX_D void walk_step(const Ray3 &r, Cell &c, float &t, int &planeCoord, int &face
         c.z += r.sz; c.tz = next_t(c.z, r.sz, r.oz, r.iz, true);
     }
 }
-VX_D bool in_world(const WorldDev &w, const Cell &c) {
+VX_HD bool in_world(const WorldDev &w, const Cell &c) {
     return (unsigned)c.x < (unsigned)w.wx && (unsigned)c.y < (unsigned)w.wy && (unsigned)c.z < (unsigned)w.wz;
 }
 // face through which a ray entering the world box along axis ax enters the cell
-VX_D int entry_face_of(int ax, V3 d) {
+VX_HD int entry_face_of(int ax, V3 d) {
     return ax == 0 ? (d.x > 0.0f ? 2 : 3) : (ax == 1 ? (d.y > 0.0f ? 1 : 0) : (d.z > 0.0f ? 5 : 4));
 }
 
@@ -170,8 +176,10 @@ struct Dda {
     Ray3 r;
     Cell c;
     const uint8_t *od;  // the ray octant's empty-cube table
+    const uint32_t *ob; // the ray octant's empty-box table (BOX walks only)
     int nb;        // brick of the current cell
-    int dist;      // its empty-cube edge in bricks (0 = occupied: walk its cells)
+    int dist;      // its empty-cube edge in bricks (0 = occupied: walk its cells); BOX: the box's x extent
+    uint32_t box;  // BOX walks: the box's packed extents
     uint64_t cm;   // its cube-cell mask (dist == 0)
     int prevId, prevLoc, steps;
     float tmin, tmax;
@@ -179,16 +187,23 @@ struct Dda {
 enum { DdaRun = 0, DdaEvent = 1, DdaNone = 2 };
 
 // brick data of the walk's current cell (cached per brick); returns the cube bit
-VX_D bool locate(const WorldDev &w, Dda &s) {
+template <bool BOX = false>
+VX_HD bool locate(const WorldDev &w, Dda &s) {
     const int nb = brick_index(w, s.c.x, s.c.y, s.c.z);
     if (nb != s.nb) {
         s.nb = nb;
-        s.dist = s.od[nb];
+        if constexpr (BOX) {
+            s.box = s.ob[nb];
+            s.dist = (int)(s.box & 0xFFu);
+        } else {
+            s.dist = s.od[nb];
+        }
         s.cm = s.dist ? 0ull : w.cellMask[nb];
     }
     return (s.cm >> cell_of(s.c.x, s.c.y, s.c.z)) & 1ull;
 }
-VX_D int prev_id(const WorldDev &w, const Dda &s) { return s.prevId > 0 ? s.prevId : (int)w.bricks[s.prevLoc]; }
+VX_HD int octant_of(const Ray3 &r) { return (r.sx > 0 ? 1 : 0) | (r.sy > 0 ? 2 : 0) | (r.sz > 0 ? 4 : 0); }
+VX_HD int prev_id(const WorldDev &w, const Dda &s) { return s.prevId > 0 ? s.prevId : (int)w.bricks[s.prevLoc]; }
 
 // The face rule at one crossing into a cell with cube bit `solid` (byte index
 // `loc`).  Radiance rays (OCC = false): entering cube b from cell a hits iff
@@ -196,7 +211,7 @@ VX_D int prev_id(const WorldDev &w, const Dda &s) { return s.prevId > 0 ? s.prev
 // (OCC = true, t >= tmin): any crossing that enters or leaves a cube face
 // (no culling).  Returns true on an event; otherwise updates prevId/prevLoc.
 template <bool OCC>
-VX_D bool cross(const WorldDev &w, Dda &s, bool solid, int loc, bool chunkPlane, float t, int face, Hit &h) {
+VX_HD bool cross(const WorldDev &w, Dda &s, bool solid, int loc, bool chunkPlane, float t, int face, Hit &h) {
     if (OCC) {
         if (t >= s.tmin) {
             if (solid != (s.prevId != 0)) return true;
@@ -227,7 +242,7 @@ VX_D bool cross(const WorldDev &w, Dda &s, bool solid, int loc, bool chunkPlane,
 // world.  Returns 0 when the next crossing leaves the brick (state = last cell
 // inside), 1 on an event (h filled for radiance rays), 2 when t exceeds tmax.
 template <bool OCC>
-VX_D int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
+VX_HD int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     const Ray3 &r = s.r;
     Cell &c = s.c;
     int lc = cell_of(c.x, c.y, c.z);
@@ -243,17 +258,17 @@ VX_D int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
         const int sa = (r.sx & mx) | (r.sy & my) | (r.sz & mz);
         const int la = ((c.x & mx) | (c.y & my) | (c.z & mz)) & 3;
         if (sa > 0 ? la == 3 : la == 0) return 0;
-        const float t = __int_as_float((__float_as_int(c.tx) & mx) | (__float_as_int(c.ty) & my) |
-                                       (__float_as_int(c.tz) & mz));
+        const float t = bits_as_float((float_as_bits(c.tx) & mx) | (float_as_bits(c.ty) & my) |
+                                       (float_as_bits(c.tz) & mz));
         if (!(t <= s.tmax)) return 2;
         c.x += sa & mx;
         c.y += sa & my;
         c.z += sa & mz;
         const int ca = (c.x & mx) | (c.y & my) | (c.z & mz);
-        const float oa = __int_as_float((__float_as_int(r.ox) & mx) | (__float_as_int(r.oy) & my) |
-                                        (__float_as_int(r.oz) & mz));
-        const float ia = __int_as_float((__float_as_int(r.ix) & mx) | (__float_as_int(r.iy) & my) |
-                                        (__float_as_int(r.iz) & mz));
+        const float oa = bits_as_float((float_as_bits(r.ox) & mx) | (float_as_bits(r.oy) & my) |
+                                        (float_as_bits(r.oz) & mz));
+        const float ia = bits_as_float((float_as_bits(r.ix) & mx) | (float_as_bits(r.iy) & my) |
+                                        (float_as_bits(r.iz) & mz));
         const float nt = ((float)(sa > 0 ? ca + 1 : ca) - oa) * ia;
         c.tx = mx ? nt : c.tx;
         c.ty = my ? nt : c.ty;
@@ -273,8 +288,8 @@ VX_D int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
 // plane is a chunk boundary, or a is outside the world.
 // Visibility rays (OCC = true): any face crossing with tmin <= t <= tmax (no
 // culling, so leaving a cube cell counts too).
-template <bool OCC>
-VX_D int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s, Hit &h) {
+template <bool OCC, bool BOX = false>
+VX_HD int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s, Hit &h) {
     bool outside;
     int ax = -1;
     float tEnter = 0;
@@ -282,9 +297,10 @@ VX_D int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s
     s.tmax = tmax;
     s.steps = 0;
     if (!walk_begin(w, o, d, s.r, s.c, outside, ax, tEnter)) return DdaNone;
-    s.od = w.bdist + (size_t)w.nBricks * ((s.r.sx > 0 ? 1 : 0) | (s.r.sy > 0 ? 2 : 0) | (s.r.sz > 0 ? 4 : 0));
+    if constexpr (BOX) s.ob = w.bbox + (size_t)w.nBricks * octant_of(s.r);
+    else s.od = w.bdist + (size_t)w.nBricks * octant_of(s.r);
     s.nb = -1;
-    const bool solid = locate(w, s);
+    const bool solid = locate<BOX>(w, s);
     s.prevId = solid ? -1 : 0;
     s.prevLoc = s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z);
     if (outside) {
@@ -301,32 +317,36 @@ VX_D int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s
 // and its plane crossings, the face-rule state and the step count; the rest
 // is rebuilt from the ray exactly as dda_begin builds it.
 struct DdaSaved { int4 cell; float4 t; int2 face; };
-VX_D DdaSaved dda_save(const Dda &s, int entry) {
+VX_HD DdaSaved dda_save(const Dda &s, int entry) {
     return DdaSaved{make_int4(s.c.x, s.c.y, s.c.z, entry), make_float4(s.c.tx, s.c.ty, s.c.tz, 0.0f),
                     make_int2(s.prevLoc, (s.prevId + 1) | (s.steps << 16))};
 }
-VX_D void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, const DdaSaved &v, Dda &s) {
+template <bool BOX = false>
+VX_HD void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, const DdaSaved &v, Dda &s) {
     ray_setup(o, d, s.r);
     s.c.x = v.cell.x; s.c.y = v.cell.y; s.c.z = v.cell.z;
     s.c.tx = v.t.x; s.c.ty = v.t.y; s.c.tz = v.t.z;
     s.tmin = tmin;
     s.tmax = tmax;
-    s.od = w.bdist + (size_t)w.nBricks * ((s.r.sx > 0 ? 1 : 0) | (s.r.sy > 0 ? 2 : 0) | (s.r.sz > 0 ? 4 : 0));
+    if constexpr (BOX) s.ob = w.bbox + (size_t)w.nBricks * octant_of(s.r);
+    else s.od = w.bdist + (size_t)w.nBricks * octant_of(s.r);
     s.nb = -1;
-    locate(w, s);
+    locate<BOX>(w, s);
     s.prevLoc = v.face.x;
     s.prevId = (v.face.y & 0xFFFF) - 1;
     s.steps = v.face.y >> 16;
 }
 
-template <bool OCC>
-VX_D int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
+template <bool OCC, bool BOX = false>
+VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;
     if (cnt) ++cnt[s.dist == 0 ? 3 : (s.dist == 1 ? 2 : 1)];
     if (s.dist == 0) {
         const int rc = brick_walk<OCC>(w, s, h, cnt ? cnt + 4 : nullptr);
         if (rc == 1) return DdaEvent;
         if (rc == 2) return DdaNone;
+    } else if constexpr (BOX) {
+        skip_box(w, s.r, s.c, (int)(s.box & 0xFFu), (int)((s.box >> 8) & 0xFFu), (int)((s.box >> 16) & 0xFFu));
     } else {
         skip_cube(w, s.r, s.c, s.dist);
     }
@@ -341,7 +361,7 @@ VX_D int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
         // leaving the world: only a visibility ray leaving a cube cell sees a face
         return (OCC && t >= s.tmin && s.prevId != 0) ? DdaEvent : DdaNone;
     }
-    const bool solid = locate(w, s);
+    const bool solid = locate<BOX>(w, s);
     if (solid || s.prevId != 0) {
         if (cross<OCC>(w, s, solid, s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z), chunkPlane, t, face, h))
             return DdaEvent;
@@ -349,20 +369,22 @@ VX_D int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     return DdaRun;
 }
 
-VX_D Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax, int *iters = nullptr) {
+template <bool BOX = false>
+VX_HD Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax, int *iters = nullptr) {
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
     Dda s;
-    int rc = dda_begin<false>(w, o, d, 0.0f, tmax, s, h);
-    while (rc == DdaRun) rc = dda_iter<false>(w, s, h, iters);
+    int rc = dda_begin<false, BOX>(w, o, d, 0.0f, tmax, s, h);
+    while (rc == DdaRun) rc = dda_iter<false, BOX>(w, s, h, iters);
     if (rc != DdaEvent) h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
     return h;
 }
 
-VX_D bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int *iters = nullptr) {
+template <bool BOX = false>
+VX_HD bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int *iters = nullptr) {
     Hit h;
     Dda s;
-    int rc = dda_begin<true>(w, o, d, tmin, tmax, s, h);
-    while (rc == DdaRun) rc = dda_iter<true>(w, s, h, iters);
+    int rc = dda_begin<true, BOX>(w, o, d, tmin, tmax, s, h);
+    while (rc == DdaRun) rc = dda_iter<true, BOX>(w, s, h, iters);
     return rc == DdaEvent;
 }
 

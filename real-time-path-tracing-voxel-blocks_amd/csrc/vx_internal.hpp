@@ -61,6 +61,9 @@ struct WorldDev {
     const uint8_t *bdist;     // 8 octant tables of nBricks bytes (brick index as cellMask): edge in bricks
                               // of the largest empty brick cube cornered at the brick and extending into
                               // the octant (0 = occupied, capped at 255); octant = (dx>0) | (dy>0)<<1 | (dz>0)<<2
+    const uint32_t *bbox;     // optional (VXPT_DDA_BOXES): 8 octant tables of nBricks words, an empty brick
+                              // BOX's extents in bricks (x | y << 8 | z << 16; 0 = occupied) grown from the
+                              // cube; null: the cube tables alone
     int nBricks;
     uint64_t top;
     int topValid;

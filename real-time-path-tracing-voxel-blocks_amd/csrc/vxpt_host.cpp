@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/vxpt.h"
+#include "box_tables.hpp"
 #include "light_map.hpp"
 #include "vx_internal.hpp"
 
@@ -152,6 +153,11 @@ struct vxpt_ctx {
     DBuf<uint8_t> bricks;
     DBuf<uint64_t> macro, cellMask;
     DBuf<uint8_t> bdist;
+    // optional empty-box skip tables (VXPT_DDA_BOXES=1 at vxpt_create; box_tables.hpp)
+    bool useBoxes = false;
+    BrickPrefix brickPrefix;
+    std::vector<uint32_t> hBox;
+    DBuf<uint32_t> bbox;
     int nBricks = 0;
     uint64_t top = 0;
     int topValid = 0;
@@ -421,6 +427,7 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.macro = c->macro.p;
     w.cellMask = c->cellMask.p;
     w.bdist = c->bdist.p;
+    w.bbox = c->useBoxes ? c->bbox.p : nullptr;
     w.nBricks = c->nBricks;
     w.top = c->top;
     w.topValid = c->topValid;
@@ -589,6 +596,22 @@ void octant_fill(vxpt_ctx *c, int oct, int x0, int x1, int y0, int y1, int z0, i
             }
 }
 
+// the box tables over brick box [x0,x1] x [y0,y1] x [z0,z1] of octant oct, from the cube tables and
+// the occupancy prefix counts (both current)
+void box_fill(vxpt_ctx *c, int oct, int x0, int x1, int y0, int y1, int z0, int z1) {
+    const size_t nB = (size_t)c->cx * 8 * c->cy * 8 * c->cz * 8;
+    for (int y = y0; y <= y1; ++y)
+        for (int z = z0; z <= z1; ++z)
+            for (int x = x0; x <= x1; ++x) {
+                const size_t b = brick_lin(c, x, y, z);
+                c->hBox[oct * nB + b] = grow_box(c->brickPrefix, x, y, z, oct, c->hOd[oct * nB + b]);
+            }
+}
+void brick_prefix(vxpt_ctx *c) {
+    c->brickPrefix.build(c->cx * 8, c->cy * 8, c->cz * 8,
+                         [&](int x, int y, int z) { return c->hCell[brick_lin(c, x, y, z)] != 0; });
+}
+
 inline int top_block(const vxpt_ctx *c, int x, int y, int z) {
     const int tx = (c->cx * 32 + 63) / 64, tz = (c->cz * 32 + 63) / 64;
     return (x >> 6) + tx * ((z >> 6) + tz * (y >> 6));
@@ -632,6 +655,12 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     for (int oct = 0; oct < 8; ++oct) octant_fill(c, oct, 0, BX - 1, 0, BY - 1, 0, BZ - 1);
     c->nBricks = (int)nB;
     if (int r = upload_vec(c, c->bdist, c->hOd.data(), c->hOd.size())) return r;
+    if (c->useBoxes) {
+        brick_prefix(c);
+        c->hBox.assign(8 * nB, 0u);
+        for (int oct = 0; oct < 8; ++oct) box_fill(c, oct, 0, BX - 1, 0, BY - 1, 0, BZ - 1);
+        if (int r = upload_vec(c, c->bbox, c->hBox.data(), c->hBox.size())) return r;
+    }
     if (int r = upload_vec(c, c->bricks, c->hBricks.data(), c->hBricks.size())) return r;
     if (int r = upload_vec(c, c->macro, c->hMacro.data(), c->hMacro.size())) return r;
     if (int r = upload_vec(c, c->cellMask, c->hCell.data(), c->hCell.size())) return r;
@@ -673,6 +702,13 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
                 octant_fill(c, oct, (oct & 1) ? 0 : bx, (oct & 1) ? bx : BX - 1, (oct & 2) ? 0 : by,
                             (oct & 2) ? by : BY - 1, (oct & 4) ? 0 : bz, (oct & 4) ? bz : BZ - 1);
             HIPCHK(c, hipMemcpyAsync(c->bdist.p, c->hOd.data(), c->hOd.size(), hipMemcpyHostToDevice, st));
+            if (c->useBoxes) {  // the boxes that could reach the brick: the same bricks behind it
+                brick_prefix(c);
+                for (int oct = 0; oct < 8; ++oct)
+                    box_fill(c, oct, (oct & 1) ? 0 : bx, (oct & 1) ? bx : BX - 1, (oct & 2) ? 0 : by,
+                             (oct & 2) ? by : BY - 1, (oct & 4) ? 0 : bz, (oct & 4) ? bz : BZ - 1);
+                HIPCHK(c, hipMemcpyAsync(c->bbox.p, c->hBox.data(), c->hBox.size() * 4, hipMemcpyHostToDevice, st));
+            }
         }
     }
     // the mirrors are the copies' sources: let them land before the host edits them again
@@ -1163,6 +1199,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (cfg->total_bounce_limit > 0) c->totalBounce = cfg->total_bounce_limit;
     if (cfg->diffuse_bounce_limit > 0) c->diffuseBounce = cfg->diffuse_bounce_limit;
     c->dataDir = cfg->data_dir ? cfg->data_dir : "data";
+    // the DDA's empty-box skip tables (an experiment, off by default: box_tables.hpp)
+    c->useBoxes = getenv("VXPT_DDA_BOXES") && atoi(getenv("VXPT_DDA_BOXES")) != 0;
     c->yamlPost = default_post();
     c->yamlDenoise = default_denoise();
     *out = c;

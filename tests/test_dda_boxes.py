@@ -1,0 +1,92 @@
+"""The voxel walk's optional empty-box skip tables (VXPT_DDA_BOXES; csrc/box_tables.hpp).
+
+CPU: the library's own walk (vx_device.hpp is host + device code) runs on the host in a driver
+compiled with hipcc (no kernel launch), once with the default empty-cube tables and once with the
+box tables, over the C1 world, the C3 (256^3) world and a random sparse world: every ray's closest
+hit (cell, face, block id, t bits) and occlusion answer must be identical, also through the
+straggler save / resume hand-over, with fewer outer iterations for the boxes.
+GPU: the probe kernels with the box tables against the oracle's DDA, bit for bit.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "real-time-path-tracing-voxel-blocks_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def driver(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("dda") / "dda_box_driver")
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+                           "-I", CSRC, "-x", "hip", os.path.join(REPO, "tests", "native", "dda_box_driver.hip"),
+                           "-o", exe])
+    return exe
+
+
+def _random_world(chunks, seed):
+    cx, cy, cz = chunks
+    W, H, D = cx * 32, cy * 32, cz * 32
+    rng = np.random.default_rng(seed)
+    g = np.zeros((H, D, W), np.uint8)  # [y, z, x]
+    for _ in range(120):
+        x, y, z = rng.integers(0, W), rng.integers(0, H), rng.integers(0, D)
+        s = rng.integers(1, 12, 3)
+        g[y:y + s[1], z:z + s[2], x:x + s[0]] = rng.integers(1, 16)  # ids past 12 are not cubes
+    g[rng.random(g.shape) < 0.002] = 5
+    # chunk-major (the library's upload layout)
+    return g.reshape(cy, 32, cz, 32, cx, 32).transpose(0, 2, 4, 1, 3, 5).reshape(-1).copy()
+
+
+@pytest.mark.parametrize("world", ["c1", "c3", "random"])
+def test_box_tables_walk_equals_cube_walk(driver, world, tmp_path):
+    if world == "random":
+        chunks = (4, 2, 4)
+        ids = _random_world(chunks, 3)
+    else:
+        o = oracle.Oracle(8, 8)
+        if world == "c1":
+            chunks = (2, 1, 2)
+            o.terrain(chunks)
+        else:
+            chunks = (8, 8, 8)
+            o.terrain(chunks, height_scale=128.0, freq_den=256.0, global_y=True)
+        ids = o.voxels()
+    path = str(tmp_path / "ids.bin")
+    ids.astype(np.uint8).tofile(path)
+    n = 60000 if world == "c3" else 120000
+    out = subprocess.run([driver, path, *map(str, chunks), str(n), "7"], capture_output=True, text=True, check=True,
+                         timeout=600).stdout
+    import re
+    vals = dict(re.findall(r"([a-z-]+) ([0-9.]+)", out.strip().splitlines()[-1]))
+    assert int(vals["diff"]) == 0, out
+    assert int(vals["hits"]) > n // 10
+    assert float(vals["box"]) < float(vals["cube"]), out  # the iterations the boxes save
+
+
+@pytest.mark.gpu
+@pytest.mark.xfail(strict=False, reason="the opt-in box tables have not run on a GPU yet (this round's GPU access "
+                                        "ended before they were written); the CPU test runs the same walk code")
+@pytest.mark.parametrize("outside", [False, True])
+def test_dda_probe_with_box_tables_bit_exact(outside, monkeypatch):
+    import vxpt
+    from test_gpu_parity import _random_rays, _setup
+    monkeypatch.setenv("VXPT_DDA_BOXES", "1")
+    r, o = _setup()
+    try:
+        rays = _random_rays(20000, 31 + outside, outside=outside)
+        g, tg = r.probe_rays(rays, 0)
+        c, tc = o.rays(rays, 0)
+        np.testing.assert_array_equal(g, c)
+        np.testing.assert_array_equal(tg.view(np.uint32), tc.view(np.uint32))
+        rays[:, 6] = 1e-3
+        rays[:, 7] = np.random.default_rng(4).uniform(0.5, 60.0, len(rays)).astype(np.float32)
+        g, _ = r.probe_rays(rays, 2)
+        c, _ = o.rays(rays, 2)
+        np.testing.assert_array_equal(g[:, 0], c[:, 0])
+    finally:
+        r.close()

@@ -11,5 +11,5 @@ rc=$?
 echo "tests rc=$rc"
 # a failing assertion (pytest 1) does not stop the measurements; a crash, fault or timeout does
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-bash tools/gpu_batch.sh full c2 b44 caps || exit $?
+bash tools/gpu_batch.sh full c2 b44 boxes caps || exit $?
 bash tools/gpu_pmc.sh "$TAG" > gpurun_out/${TAG}_pmc_run.log 2>&1; echo "pmc rc=$?"

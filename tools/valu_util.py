@@ -20,7 +20,9 @@ TRACE = ["k_closest", "k_shade", "k_nee", "k_restir", "k_finish", "k_queue<true>
 
 
 def short(n):
-    return n.replace("vx::(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
+    n = n.replace("vx::(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
+    # the default (cube-table) walks: k_queue<true, false> -> k_queue<true>, k_closest<false> -> k_closest
+    return n.replace(", false>", ">").replace("k_closest<false>", "k_closest")
 
 
 def main():
