@@ -3,8 +3,12 @@
 // tables and once with the empty-box tables of box_tables.hpp.  Prints the number of rays whose
 // results differ (hit, cell, face, id, t bits; occlusion) and the mean outer iterations of both.
 // Usage: dda_box_driver ids.bin CX CY CZ nrays seed
+//        dda_box_driver ids.bin CX CY CZ --rays rays.bin out.bin   (rays: 8 f32 each, o d tmin tmax;
+//        out per ray: 16 i32 = cube closest (hit x y z face id, t bits), box closest (same, through
+//        save / resume), cube occluded, box occluded -- the probe kernels' modes 0 and 2)
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <random>
 #include <vector>
 
@@ -89,6 +93,42 @@ int main(int argc, char **argv) {
     w.cx = CX; w.cy = CY; w.cz = CZ;
     w.wx = wx; w.wy = wy; w.wz = wz;
     w.mx = wx / 16; w.my = wy / 16; w.mz = wz / 16;
+    if (std::string(argv[5]) == "--rays") {
+        FILE *fr = fopen(argv[6], "rb");
+        if (!fr) return 1;
+        std::vector<float> rays;
+        float buf[8];
+        while (fread(buf, 4, 8, fr) == 8) rays.insert(rays.end(), buf, buf + 8);
+        fclose(fr);
+        const size_t n = rays.size() / 8;
+        std::vector<int32_t> out(n * 16, 0);
+        for (size_t i = 0; i < n; ++i) {
+            const float *r = &rays[i * 8];
+            const V3 o(r[0], r[1], r[2]), d(r[3], r[4], r[5]);
+            int32_t *q = &out[i * 16];
+            const Hit hc = dda_closest<false>(w, o, d, r[7]);
+            Hit hb{0, 0, 0, 0, -1, 0, kRayMax};
+            Dda sb;
+            int rb = dda_begin<false, true>(w, o, d, 0.0f, r[7], sb, hb);
+            while (rb == DdaRun) {
+                const DdaSaved sv = dda_save(sb, 0);
+                dda_resume<true>(w, o, d, 0.0f, r[7], sv, sb);
+                rb = dda_iter<false, true>(w, sb, hb);
+            }
+            if (rb != DdaEvent) hb = Hit{0, 0, 0, 0, -1, 0, kRayMax};
+            const Hit hs[2] = {hc, hb};
+            for (int k = 0; k < 2; ++k) {
+                q[7 * k + 0] = hs[k].hit; q[7 * k + 1] = hs[k].x; q[7 * k + 2] = hs[k].y; q[7 * k + 3] = hs[k].z;
+                q[7 * k + 4] = hs[k].face; q[7 * k + 5] = hs[k].id; q[7 * k + 6] = float_as_bits(hs[k].t);
+            }
+            q[14] = dda_occluded<false>(w, o, d, r[6], r[7]) ? 1 : 0;
+            q[15] = dda_occluded<true>(w, o, d, r[6], r[7]) ? 1 : 0;
+        }
+        FILE *fo = fopen(argv[7], "wb");
+        if (!fo || fwrite(out.data(), 4, out.size(), fo) != out.size()) return 1;
+        fclose(fo);
+        return 0;
+    }
     std::mt19937 rng(seed);
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
     long diff = 0, hits = 0, itCube = 0, itBox = 0;

@@ -90,3 +90,30 @@ def test_dda_probe_with_box_tables_bit_exact(outside, monkeypatch):
         np.testing.assert_array_equal(g[:, 0], c[:, 0])
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("outside", [False, True])
+def test_library_walk_on_host_equals_oracle_dda(driver, outside, tmp_path):
+    """The library's voxel walk itself (vx_device.hpp, run on the host by the driver) against the
+    oracle's DDA on the C1 world: closest hits (cell, face, block id, t bits) and occlusion answers
+    bit for bit, with the cube tables and with the box tables -- the GPU probe tests' comparison,
+    runnable without a GPU."""
+    from test_oracle import _random_rays
+    o = oracle.Oracle(8, 8)
+    o.terrain((2, 1, 2))
+    ids_path, rays_path, out_path = (str(tmp_path / f) for f in ("ids.bin", "rays.bin", "out.bin"))
+    o.voxels().astype(np.uint8).tofile(ids_path)
+    rays = _random_rays(40000, 41 + outside, outside=outside)
+    rays[::3, 6] = 1e-3
+    rays[::2, 7] = np.random.default_rng(5).uniform(0.5, 60.0, len(rays[::2])).astype(np.float32)
+    rays.tofile(rays_path)
+    subprocess.run([driver, ids_path, "2", "1", "2", "--rays", rays_path, out_path], check=True, timeout=600)
+    got = np.fromfile(out_path, np.int32).reshape(-1, 16)
+    want, tw = o.rays(rays, 0)
+    for k in (0, 1):  # cube, box
+        np.testing.assert_array_equal(got[:, 7 * k:7 * k + 6], want)
+        np.testing.assert_array_equal(got[:, 7 * k + 6], tw.view(np.int32))
+    occ, _ = o.rays(rays, 2)
+    np.testing.assert_array_equal(got[:, 14], occ[:, 0])
+    np.testing.assert_array_equal(got[:, 15], occ[:, 0])
+    assert 0.05 < got[:, 0].mean() < 0.95
