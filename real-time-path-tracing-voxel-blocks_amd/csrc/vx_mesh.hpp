@@ -1,16 +1,17 @@
 // vxpt -- device-side instanced-mesh queries and hit geometry, shared by
 // meshes.hip (the probe kernels) and trace.hip (the path kernels).  See meshes.hip for the BVH
-// walk's design notes.
+// walk's design notes.  The walk is host + device code: the CPU tests run it on the host
+// (tests/native/mesh_walk_driver.hip).
 #pragma once
 #include "vx_internal.hpp"
 
 namespace vx {
 namespace {
 
-VX_D float dt3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-VX_D V3 cr3(V3 a, V3 b) { return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+VX_HD float dt3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+VX_HD V3 cr3(V3 a, V3 b) { return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 
-VX_D bool tri_hit(V3 o, V3 d, const float *t9, float tmin, float tmax, int cull, float &t, float &u, float &v) {
+VX_HD bool tri_hit(V3 o, V3 d, const float *t9, float tmin, float tmax, int cull, float &t, float &u, float &v) {
     const V3 v0(t9[0], t9[1], t9[2]), v1(t9[3], t9[4], t9[5]), v2(t9[6], t9[7], t9[8]);
     const V3 e1 = v1 - v0, e2 = v2 - v0;
     const V3 p = cr3(d, e2);
@@ -30,7 +31,7 @@ VX_D bool tri_hit(V3 o, V3 d, const float *t9, float tmin, float tmax, int cull,
 }
 
 // slab test against a widened box; an axis the ray does not move along only checks the origin
-VX_D bool box_hit(const BvhNode &n, V3 o, V3 inv, V3 d, float tmin, float tmax, float &tEnter) {
+VX_HD bool box_hit(const BvhNode &n, V3 o, V3 inv, V3 d, float tmin, float tmax, float &tEnter) {
     float t0 = tmin, t1 = tmax;
     const float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z}, dd[3] = {d.x, d.y, d.z};
 #pragma unroll
@@ -63,7 +64,7 @@ struct ScratchStack {
 };
 
 template <class S>
-VX_D void stack_push(S &st, int &sp, int node, float te) {
+VX_HD void stack_push(S &st, int &sp, int node, float te) {
     st.s[sp] = node;
     st.t[sp] = te;
     ++sp;
@@ -72,7 +73,7 @@ VX_D void stack_push(S &st, int &sp, int node, float te) {
 // push the children of an inner node, the nearer one on top (visited first, so the closest hit
 // shrinks the interval early); a child whose box the ray misses is not pushed
 template <class S>
-VX_D void push_children(const BvhNode *nodes, int base, int left, V3 o, V3 inv, V3 d, float tmin, float tmax,
+VX_HD void push_children(const BvhNode *nodes, int base, int left, V3 o, V3 inv, V3 d, float tmin, float tmax,
                         S &stack, int &sp) {
     float ta, tb;
     const bool ha = box_hit(nodes[base + left], o, inv, d, tmin, tmax, ta);
@@ -92,13 +93,13 @@ struct Best {
     float t, u, v;
     int inst, tri;
     int leaf;  // the triangle's index in BLAS leaf order (its vertices at MeshDev::tri + 9 * leaf)
-    VX_D bool better(float tt, int i, int k) const {
+    VX_HD bool better(float tt, int i, int k) const {
         return inst < 0 || tt < t || (tt == t && (i < inst || (i == inst && k < tri)));
     }
 };
 
 template <bool kAny, class S>
-VX_D bool blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b,
+VX_HD bool blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b,
                     S &stack, const int sp0) {
     const int2 r = m.root[block];
     if (r.x < 0) return false;
@@ -128,7 +129,7 @@ VX_D bool blas_walk(const MeshDev &m, int row, int block, V3 o, V3 d, V3 inv, fl
 }
 
 template <bool kAny, class S>
-VX_D void mesh_walk(const MeshDev &m, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b, S &stack) {
+VX_HD void mesh_walk(const MeshDev &m, V3 o, V3 d, V3 inv, float tmin, int cull, Best &b, S &stack) {
     if (m.nInst <= 0) return;
     float te0;
     if (!box_hit(m.tlas[0], o, inv, d, tmin, b.t, te0)) return;
