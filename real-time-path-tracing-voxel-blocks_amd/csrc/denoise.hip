@@ -29,28 +29,28 @@ namespace {
 
 constexpr float kRange = 500000.0f;
 
-VX_D int cl(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
-VX_D V4 f4(float4 v) { return V4(v.x, v.y, v.z, v.w); }
-VX_D float4 tf(V4 v) { return make_float4(v.x, v.y, v.z, v.w); }
-VX_D V4 ld4(const float4 *b, int W, int H, int x, int y) { return f4(b[(size_t)cl(y, H) * W + cl(x, W)]); }
-VX_D float ld1(const float *b, int W, int H, int x, int y) { return b[(size_t)cl(y, H) * W + cl(x, W)]; }
+VX_HD int cl(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
+VX_HD V4 f4(float4 v) { return V4(v.x, v.y, v.z, v.w); }
+VX_HD float4 tf(V4 v) { return make_float4(v.x, v.y, v.z, v.w); }
+VX_HD V4 ld4(const float4 *b, int W, int H, int x, int y) { return f4(b[(size_t)cl(y, H) * W + cl(x, W)]); }
+VX_HD float ld1(const float *b, int W, int H, int x, int y) { return b[(size_t)cl(y, H) * W + cl(x, W)]; }
 // 16-bit read of the R32F material plane at byte offset 2x (Load2DUshort1 semantics)
-VX_D float ld_ushort(const float *b, int W, int H, int x, int y) {
+VX_HD float ld_ushort(const float *b, int W, int H, int x, int y) {
     const int ux = clampi(x, 0, 2 * W - 1);
     const uint16_t *row = reinterpret_cast<const uint16_t *>(b + (size_t)cl(y, H) * W);
     return (float)row[ux];
 }
-VX_D V3 world_pos(const CamDev &c, int x, int y, float depth) {
+VX_HD V3 world_pos(const CamDev &c, int x, int y, float depth) {
     const V2 uv = (V2((float)x, (float)y) + 0.5f) * c.invRes;
     return c.pos + c.uv_to_dir(uv) * depth;
 }
-VX_D V3 xyz4(float4 v) { return V3(v.x, v.y, v.z); }
+VX_HD V3 xyz4(float4 v) { return V3(v.x, v.y, v.z); }
 // world position of the (edge-clamped) pixel's hit, from the per-frame plane
-VX_D V3 wp(const DenoiseArgs &a, int x, int y) { return xyz4(a.wpos[(size_t)cl(y, a.H) * a.W + cl(x, a.W)]); }
+VX_HD V3 wp(const DenoiseArgs &a, int x, int y) { return xyz4(a.wpos[(size_t)cl(y, a.H) * a.W + cl(x, a.W)]); }
 // the packed plane's value of a pixel: world position of its primary hit and, in w, its 16-bit
 // material read (Load2DUshort1 quirk, ld_ushort) for the a-trous / history-fix material tests,
 // -1 for sky (no tap weight)
-VX_D float4 wpos_px(const DenoiseArgs &a, int x, int y, float z) {
+VX_HD float4 wpos_px(const DenoiseArgs &a, int x, int y, float z) {
     const V3 p = world_pos(a.cam, x, y, z);
     return make_float4(p.x, p.y, p.z, z > kRange ? -1.0f : ld_ushort(a.material, a.W, a.H, x, y));
 }
@@ -95,8 +95,8 @@ struct Plane4 {
         return V4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
     }
 };
-VX_D V3 rgb_to_ycocg(V3 c) { return V3(0.25f * (c.x + 2.0f * c.y + c.z), c.x - c.z, c.y - 0.5f * (c.x + c.z)); }
-VX_D V3 ycocg_to_rgb(V3 c) { return V3(c.x + 0.5f * (c.y - c.z), c.x + 0.5f * c.z, c.x - 0.5f * (c.y + c.z)); }
+VX_HD V3 rgb_to_ycocg(V3 c) { return V3(0.25f * (c.x + 2.0f * c.y + c.z), c.x - c.z, c.y - 0.5f * (c.x + c.z)); }
+VX_HD V3 ycocg_to_rgb(V3 c) { return V3(c.x + 0.5f * (c.y - c.z), c.x + 0.5f * c.z, c.x - 0.5f * (c.y + c.z)); }
 VX_D uint32_t seq_hash(uint32_t x) {
     x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
     return x;
@@ -336,7 +336,7 @@ VX_D bool xcd_tile(const DenoiseArgs &a, int &tx, int &ty) {
 
 // ---------------------------------------------------------------- TA
 template <bool kQuirk>
-VX_D V4 bicubic12(const float4 *b, int W, int H, V2 uv) {
+VX_HD V4 bicubic12(const float4 *b, int W, int H, V2 uv) {
     const V2 UV(uv.x * (float)W, uv.y * (float)H);
     const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
     const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
@@ -363,7 +363,7 @@ VX_D V4 bicubic12(const float4 *b, int W, int H, V2 uv) {
     out3 /= sum;
     return V4(out3, 0.0f);
 }
-VX_D void bilinear_taps(int W, int H, V2 uv, int &x0, int &y0, float w[4]) {
+VX_HD void bilinear_taps(int W, int H, V2 uv, int &x0, int &y0, float w[4]) {
     const V2 UV(uv.x * (float)W, uv.y * (float)H);
     const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
     const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f);
@@ -372,7 +372,7 @@ VX_D void bilinear_taps(int W, int H, V2 uv, int &x0, int &y0, float w[4]) {
     y0 = (int)fy;
     w[0] = w0.x * w0.y; w[1] = w1.x * w0.y; w[2] = w0.x * w1.y; w[3] = w1.x * w1.y;
 }
-VX_D V4 bilinear_custom4(const float4 *b, int W, int H, V2 uv, const float cw[4]) {
+VX_HD V4 bilinear_custom4(const float4 *b, int W, int H, V2 uv, const float cw[4]) {
     int x0, y0;
     float w[4];
     bilinear_taps(W, H, uv, x0, y0, w);
@@ -389,7 +389,7 @@ VX_D V4 bilinear_custom4(const float4 *b, int W, int H, V2 uv, const float cw[4]
     return out;
 }
 // v[k]: the plane at the bilinear taps (x0 + (k & 1), y0 + (k >> 1)), edge-clamped
-VX_D float bilinear_custom1(const float v[4], int W, int H, V2 uv, const float cw[4]) {
+VX_HD float bilinear_custom1(const float v[4], int W, int H, V2 uv, const float cw[4]) {
     int x0, y0;
     float w[4];
     bilinear_taps(W, H, uv, x0, y0, w);
@@ -403,7 +403,7 @@ VX_D float bilinear_custom1(const float v[4], int W, int H, V2 uv, const float c
     }
     return out / sum;
 }
-VX_D V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
+VX_HD V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
     const V2 UV(uv.x * (float)W, uv.y * (float)H);
     const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
     const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
@@ -424,7 +424,7 @@ VX_D V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
 
 // Returns whether the history fix must filter the pixel (HistoryFix.h:20-22:
 // non-sky and history <= 4; pixels past the denoising range keep last frame's length).
-VX_D bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol) {
+VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol) {
     const int W = a.W, H = a.H;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
@@ -697,48 +697,9 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
     history_fix_px(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i);
 }
 
-// ---------------------------------------------------------------- HC
-// The 5x5 neighbourhood of the 16x16 tile (20x20 with edge clamp) is staged
-// once in LDS: YCoCg of the fast history and the noisy radiance.
-__global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
-    const int W = a.W, H = a.H;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
-    const int x0 = btx * 16, y0 = a.y0 + bty * 16;
-    const int x = x0 + tx, y = y0 + ty;
-    __shared__ float sY[3][400], sR[3][400];
-    for (int k = threadIdx.x; k < 400; k += 256) {
-        const int gx = cl(x0 + k % 20 - 2, W), gy = cl(y0 + k / 20 - 2, H);
-        const size_t j = (size_t)gy * W + gx;
-        const V3 yc = rgb_to_ycocg(f4(a.pong[j]).xyz());
-        const float4 n = a.illum[j];
-        sY[0][k] = yc.x; sY[1][k] = yc.y; sY[2][k] = yc.z;
-        sR[0][k] = n.x; sR[1][k] = n.y; sR[2][k] = n.z;
-    }
-    __syncthreads();
-    if (x >= W || y >= a.y1) return;
-    const size_t i = (size_t)y * W + x;
-    if (a.depth[i] > kRange) return;
-    const float hist = a.histLen[i];
-    V3 m1(0.0f), m2(0.0f), nm1(0.0f);
-    float nm2 = 0.0f;
-    // one column of taps per iteration: fully unrolled, the 25 taps' LDS values were all held in
-    // registers (118 VGPRs, 4 waves/SIMD); a column at a time runs at 65 (7 waves), 61 -> 50 us.
-    // Precomputing the per-pixel moment terms in the staging loop (3 float4 planes in LDS) was
-    // slower (59 us at 44 or 87 VGPRs).
-#pragma unroll 1
-    for (int dx = -2; dx <= 2; ++dx)
-#pragma unroll
-        for (int dy = -2; dy <= 2; ++dy) {
-            const int k = (ty + 2 + dy) * 20 + (tx + 2 + dx);
-            const V3 s(sY[0][k], sY[1][k], sY[2][k]);
-            m1 += s;
-            m2 += s * s;
-            const V3 nz(sR[0][k], sR[1][k], sR[2][k]);
-            const float nl = luminance_fast(nz);
-            nm1 += nz;
-            nm2 += nl * nl;
-        }
+// HistoryClamping's per-pixel step after the 5x5 moments (m1, m2: the fast history's YCoCg; nm1,
+// nm2: the radiance), shared by k_history_clamp (moments from its LDS tile) and the host tests
+VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V3 m2, V3 nm1, float nm2) {
     m1 /= 25.0f; m2 /= 25.0f; nm1 /= 25.0f; nm2 /= 25.0f;
     const V3 sigma(sqrtf(fmaxf(0.0f, m2.x - m1.x * m1.x)), sqrtf(fmaxf(0.0f, m2.y - m1.y * m1.y)),
                    sqrtf(fmaxf(0.0f, m2.z - m1.z * m1.z)));
@@ -784,6 +745,73 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
     a.prevIllum[i] = tf(outD);
     a.prevFast[i] = tf(outR);
     a.prevHistLen[i] = hist;
+}
+
+// ---------------------------------------------------------------- HC
+// The 5x5 neighbourhood of the 16x16 tile (20x20 with edge clamp) is staged
+// once in LDS: YCoCg of the fast history and the noisy radiance.
+__global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
+    const int W = a.W, H = a.H;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
+    const int x0 = btx * 16, y0 = a.y0 + bty * 16;
+    const int x = x0 + tx, y = y0 + ty;
+    __shared__ float sY[3][400], sR[3][400];
+    for (int k = threadIdx.x; k < 400; k += 256) {
+        const int gx = cl(x0 + k % 20 - 2, W), gy = cl(y0 + k / 20 - 2, H);
+        const size_t j = (size_t)gy * W + gx;
+        const V3 yc = rgb_to_ycocg(f4(a.pong[j]).xyz());
+        const float4 n = a.illum[j];
+        sY[0][k] = yc.x; sY[1][k] = yc.y; sY[2][k] = yc.z;
+        sR[0][k] = n.x; sR[1][k] = n.y; sR[2][k] = n.z;
+    }
+    __syncthreads();
+    if (x >= W || y >= a.y1) return;
+    const size_t i = (size_t)y * W + x;
+    if (a.depth[i] > kRange) return;
+    const float hist = a.histLen[i];
+    V3 m1(0.0f), m2(0.0f), nm1(0.0f);
+    float nm2 = 0.0f;
+    // one column of taps per iteration: fully unrolled, the 25 taps' LDS values were all held in
+    // registers (118 VGPRs, 4 waves/SIMD); a column at a time runs at 65 (7 waves), 61 -> 50 us.
+    // Precomputing the per-pixel moment terms in the staging loop (3 float4 planes in LDS) was
+    // slower (59 us at 44 or 87 VGPRs).
+#pragma unroll 1
+    for (int dx = -2; dx <= 2; ++dx)
+#pragma unroll
+        for (int dy = -2; dy <= 2; ++dy) {
+            const int k = (ty + 2 + dy) * 20 + (tx + 2 + dx);
+            const V3 s(sY[0][k], sY[1][k], sY[2][k]);
+            m1 += s;
+            m2 += s * s;
+            const V3 nz(sR[0][k], sR[1][k], sR[2][k]);
+            const float nl = luminance_fast(nz);
+            nm1 += nz;
+            nm2 += nl * nl;
+        }
+    history_clamp_px(a, i, hist, m1, m2, nm1, nm2);
+}
+
+// host restatement of the kernel's moments (the same taps in the same order, read from the planes
+// instead of the LDS tile) for the CPU tests (tests/native/denoise_driver.hip)
+VX_HD void history_clamp_host(const DenoiseArgs &a, int x, int y) {
+    const int W = a.W, H = a.H;
+    const size_t i = (size_t)y * W + x;
+    if (a.depth[i] > kRange) return;
+    const float hist = a.histLen[i];
+    V3 m1(0.0f), m2(0.0f), nm1(0.0f);
+    float nm2 = 0.0f;
+    for (int dx = -2; dx <= 2; ++dx)
+        for (int dy = -2; dy <= 2; ++dy) {
+            const V3 sv = rgb_to_ycocg(ld4(a.pong, W, H, x + dx, y + dy).xyz());
+            m1 += sv;
+            m2 += sv * sv;
+            const V3 nz = ld4(a.illum, W, H, x + dx, y + dy).xyz();
+            const float nl = luminance_fast(nz);
+            nm1 += nz;
+            nm2 += nl * nl;
+        }
+    history_clamp_px(a, i, hist, m1, m2, nm1, nm2);
 }
 
 // ---------------------------------------------------------------- A-trous (LDS variant)
