@@ -12,21 +12,11 @@
 //     float at x>>1 for even x, the high half for odd x; the byte coordinate
 //     clamps to [0, 4W-2], the row to [0, H-1].
 //   * surface reads clamp to the edge (Sampler.h:134-188).
-#include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include "orc_trace.h"
 
 namespace orc {
 namespace {
-
-struct int2_dbg { int x, y; };
-int2_dbg dbg_pixel() {  // ORC_DBG_PX=x,y (test infrastructure: one pixel's temporal taps on stdout)
-    int2_dbg p{-1, -1};
-    if (const char *e = std::getenv("ORC_DBG_PX"))
-        if (std::sscanf(e, "%d,%d", &p.x, &p.y) != 2) p = {-1, -1};
-    return p;
-}
 
 constexpr float kRange = 500000.0f;
 
@@ -416,24 +406,6 @@ void pass_temporal(const Scene &s, Frame &f, const DenoiseParams &p) {
             f.ping[i] = acc;
             f.pong[i] = F4(accR, 0.0f);
             f.histLen[i] = hist;
-            // debug hook: ORC_DBG_PX=x,y prints this pixel's temporal taps (read once per process)
-            static const int2_dbg dbgPx = dbg_pixel();
-            if (dbgPx.x == x && dbgPx.y == y) {
-                std::printf("ORC px %d %d ox %d oy %d est %.9g t0 %.9g bic %g taps %g %g %g %g found %g q %.9g hist %.9g "
-                            "prevI %.9g %.9g %.9g illum %.9g %.9g %.9g pnr.n %.9g\n", x, y, ox, oy, estDepth, t0, bicValid,
-                            tapsValid[0], tapsValid[1], tapsValid[2], tapsValid[3], found, quality, hist, prevI.x, prevI.y,
-                            prevI.z, illum.x, illum.y, illum.z, dot(nIn, pnr));
-                for (int a = 0; a < 4; ++a)
-                    for (int b = 0; b < 2; ++b) {
-                        const float pz = ld1(f.prevDepth, f, ox + bc[a][b][0], oy + bc[a][b][1]);
-                        std::printf("  bc %d %d pz %.9g diff %.9g thr %.9g\n", a, b, pz, std::fabs(pz - estDepth), thr4[a]);
-                    }
-                for (int a = 0; a < 4; ++a) {
-                    const float pz = ld1(f.prevDepth, f, ox + bl[a][0], oy + bl[a][1]);
-                    std::printf("  bl %d pz %.9g diff %.9g thr %.9g\n", a, pz, std::fabs(pz - estDepth), thr4[a]);
-                }
-                std::printf("  prevUV %.9g %.9g NoV %.9g parMax %.9g z %.9g\n", prevUV.x, prevUV.y, NoV, parMax, z);
-            }
         }
 }
 

@@ -539,12 +539,6 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
     a.ping[i] = tf(acc);
     a.pong[i] = make_float4(accR.x, accR.y, accR.z, 0.0f);
     a.histLen[i] = hist;
-#ifdef VX_DBG_PX
-    if (x == VX_DBG_X && y == VX_DBG_Y)
-        printf("HIP px %d %d ox %d oy %d est %.9g t0 %.9g bic %g taps %g %g %g %g found %g q %.9g hist %.9g prevI %.9g %.9g %.9g "
-               "illum %.9g %.9g %.9g pnr.n %.9g\n", x, y, ox, oy, estDepth, t0, bicValid, taps[0], taps[1], taps[2],
-               taps[3], found, quality, hist, prevI.x, prevI.y, prevI.z, illum.x, illum.y, illum.z, dot(nIn, pnr));
-#endif
     return hist <= 4.0f;
 }
 

@@ -1,7 +1,6 @@
 #!/bin/bash
 # One GPU call's worth of round-2 checks, each step under its own time limit; stops at the first
 # GPU fault / timeout.  Usage (on the box): tools/gpu_batch.sh STEP...   steps:
-#   dbg      the lantern-edit pixel debug (libvxpt_dbg.so)
 #   tests    pytest -m gpu on the files in $TESTS (default: all)
 #   bench    bench.py --steps 20 --warmup 6 --no-cpu-baseline  -> gpurun_out/b_default.json
 #   caps     trace iteration-cap sweep (VXPT_ITER_CAP / VXPT_ITER_CAP2)   -> gpurun_out/b_cap*.json
@@ -23,8 +22,6 @@ run() {  # name seconds cmd...
 }
 for step in "$@"; do
     case $step in
-    dbg) ORC_DBG_PX=40,12 VXPT_LIB=real-time-path-tracing-voxel-blocks_amd/libvxpt_dbg.so run dbg 120 \
-             python -u tools/dbg/remap_dbg.py > gpurun_out/remap_dbg.log 2>&1 || exit $? ;;
     tests) run tests 900 python -u -m pytest -v --timeout 240 --timeout-method thread -m gpu ${TESTS:-tests} \
                > gpurun_out/tests.log 2>&1 || exit $? ;;
     bench) run bench 200 python -u bench.py --steps 20 --warmup 6 --no-cpu-baseline > gpurun_out/b_default.json 2> gpurun_out/b_default.err || exit $? ;;

@@ -1,11 +1,11 @@
 #!/bin/bash
-# The round's GPU evidence in one call: the lantern-edit pixel debug, rocprofv3 -L, every GPU test,
+# The round's GPU evidence in one call: rocprofv3 -L, every GPU test,
 # the default bench line with the CPU baseline, the C2 primary-only and 4/4-bounce lines, the trace
 # iteration-cap sweep, and the profile passes (kernel trace + PMC) of tools/gpu_pmc.sh.
 # Usage (on the box): tools/gpu_round.sh TAG
 TAG=${1:-r02b}
 cd "$GRAFT_REPO_ROOT" || exit 1
-bash tools/gpu_batch.sh dbg counters || exit $?
+bash tools/gpu_batch.sh counters || exit $?
 bash tools/gpu_batch.sh tests
 rc=$?
 echo "tests rc=$rc"
