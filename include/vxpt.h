@@ -58,7 +58,10 @@ enum vxpt_buffer {
     /* emissive-triangle lights of the instanced meshes (vxpt_load_models / vxpt_get_lights) */
     VXPT_BUF_LIGHTS = 44,        /* nLights x 32 B LightInfo (Light.h:13-23)                     */
     VXPT_BUF_LIGHT_ALIAS = 45,   /* nLights x {f32 q, f32 p, i32 alias} (AliasTable.h bins)      */
-    VXPT_BUF_BLOOM = 46          /* post-process: the horizontally blurred bloom, Float4 per pixel */
+    VXPT_BUF_BLOOM = 46,         /* post-process: the horizontally blurred bloom, Float4 per pixel */
+    VXPT_BUF_TAP_RECORD = 47     /* read-only: the last pass's ReSTIR tap records, 32 B per pixel (normal xyz,
+                                  * roughness with the metallic flag in its sign bit; albedo xyz, depth) --
+                                  * the G-buffer planes GetPrevSurface reads (Restir.h:348-381), packed */
 };
 
 typedef struct vxpt_config {

@@ -325,6 +325,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 }
 
 // ----------------------------------------------------------------- shading
+// the pass's tap record (GBuf::rec) of pixel pi, written wherever the G-buffer planes are
+VX_D void store_rec(const TraceArgs &a, size_t pi, V3 n, float rough, bool metal, V3 alb, float depth) {
+    a.cur.rec[2 * pi] = make_float4(n.x, n.y, n.z, bits_as_float(float_as_bits(rough) | (metal ? (int)0x80000000u : 0)));
+    a.cur.rec[2 * pi + 1] = make_float4(alb.x, alb.y, alb.z, depth);
+}
+VX_D void store_rec_sky(const TraceArgs &a, size_t pi, float depth) {
+    store_rec(a, pi, V3(0.0f, -1.0f, 0.0f), 0.0f, false, V3(1.0f), depth);
+}
+
 VX_D void path_end(const TraceArgs &a, int px, int py, V3 radiance, float primaryDist) {
     if (isnan(radiance.x) || isnan(radiance.y) || isnan(radiance.z)) radiance = V3(0.5f);  // RayGen.cu:175-178
     const size_t pi = (size_t)py * a.W + px;
@@ -491,6 +500,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
             a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
             a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            store_rec_sky(a, pi, kRayMax);
             w.pPos[s].w = kRayMax;
         }
         seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false);
@@ -514,6 +524,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
                 a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
                 a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
                 a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                store_rec_sky(a, pi, h.t);
             }
         }
         if (seg == 0) w.pPos[s].w = h.t;  // the primary distance (no reservoir is stored)
@@ -568,6 +579,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     if (seg == 0) {
         meta.x |= F_HFD;
         a.cur.albedo[pi] = make_float4(sf.albedo.x, sf.albedo.y, sf.albedo.z, 1.0f);
+        store_rec(a, pi, sf.normal, sf.roughness, sf.metallic, sf.albedo, h.t);  // depth = the primary distance
         skipAlbedo = true;
         primaryDist = h.t;
     }
@@ -1085,6 +1097,7 @@ __global__ __launch_bounds__(256) void k_primary_gbuffer(TraceArgs a) {
         a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
         a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const V3 e = sky_emission(a.sky, d);
+        store_rec_sky(a, pi, kRayMax);
         a.cur.depth[pi] = kRayMax;
         a.illum[pi] = make_float4(e.x, e.y, e.z, kRayMax);
         return;
@@ -1098,6 +1111,7 @@ __global__ __launch_bounds__(256) void k_primary_gbuffer(TraceArgs a) {
     a.cur.geoNormalThin[pi] = make_float4(ng.x, ng.y, ng.z, 0.0f);
     a.cur.matParam[pi] = make_float4(m.metallic ? 1.0f : 0.0f, m.translucency, 0.0f, 0.0f);
     a.cur.albedo[pi] = make_float4(alb.x, alb.y, alb.z, 1.0f);
+    store_rec(a, pi, ng, m.roughness, m.metallic != 0, alb, h.t);
     a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     a.cur.depth[pi] = h.t;
     a.illum[pi] = make_float4(0.0f, 0.0f, 0.0f, h.t);
@@ -1151,6 +1165,15 @@ __global__ __launch_bounds__(256) void k_probe_rng(BlueNoiseDev bn, int n, const
     out[i] = bn_rand(bn, q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
 }
 
+// rebuilds a slot's tap records from its planes (after a host write to the planes)
+__global__ __launch_bounds__(256) void k_pack_rec(GBuf g, size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 nr = g.normalRough[i], al = g.albedo[i], mp = g.matParam[i];
+    g.rec[2 * i] = make_float4(nr.x, nr.y, nr.z, bits_as_float(float_as_bits(nr.w) | (mp.x == 1.0f ? (int)0x80000000u : 0)));
+    g.rec[2 * i + 1] = make_float4(al.x, al.y, al.z, g.depth[i]);
+}
+
 }  // namespace
 
 #ifdef VX_STATS
@@ -1163,6 +1186,11 @@ extern "C" int vxpt_debug_stats(unsigned long long *out64, int reset) {
     return 0;
 }
 #endif
+
+hipError_t launch_pack_rec(const GBuf &g, size_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_rec, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, n);
+    return hipGetLastError();
+}
 
 hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st) {
     hipLaunchKernelGGL(k_probe_rng, dim3((n + 255) / 256), dim3(256), 0, st, bn, n, q, out);

@@ -764,9 +764,12 @@ VX_D int reflect_view(int p, int n) {
 VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const V3 *vdIn, V3 *vdOut) {
     if (x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y) return false;
     const size_t i = (size_t)y * a.W + x;
-    sf.depth = a.prev.depth[i];
+    // the previous pass's tap record (GBuf::rec): the planes' depth, normal (normalRough and
+    // geoNormalThin hold the same one), roughness, metallic flag and albedo
+    const float4 b = a.prev.rec[2 * i + 1];
+    sf.depth = b.w;
     if (sf.depth == kRayMax) return false;
-    const float4 nr = a.prev.normalRough[i], gt = a.prev.geoNormalThin[i], mp = a.prev.matParam[i];
+    const float4 nr = a.prev.rec[2 * i];
     V3 vd;
     if (vdIn) {
         vd = *vdIn;
@@ -778,11 +781,12 @@ VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const 
     sf.pos = a.prevCam.pos + vd * sf.depth;
     sf.wo = -vd;
     sf.normal = V3(nr.x, nr.y, nr.z);
-    sf.geoNormal = V3(gt.x, gt.y, gt.z);
-    sf.albedo = ld3(a.prev.albedo, i);
-    sf.roughness = nr.w;
-    sf.metallic = (mp.x == 1.0f);
-    sf.translucency = mp.y;
+    sf.geoNormal = sf.normal;
+    sf.albedo = V3(b.x, b.y, b.z);
+    const int rb = float_as_bits(nr.w);
+    sf.roughness = bits_as_float(rb & 0x7FFFFFFF);
+    sf.metallic = rb < 0;
+    sf.translucency = 0.0f;  // not read by the taps' target pdf (disney_eval)
     return true;
 }
 

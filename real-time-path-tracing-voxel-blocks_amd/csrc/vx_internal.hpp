@@ -88,6 +88,11 @@ struct BlueNoiseDev { const uint8_t *sobol, *scramble, *rank; };
 struct GBuf {
     float4 *normalRough, *geoNormalThin, *albedo, *matParam;
     float *depth, *material;
+    // what a ReSTIR temporal tap reads of this pass's G-buffer (Restir.h:348-381 GetPrevSurface), one
+    // 32-byte record per pixel: [2i] = shading normal xyz (the geoNormalThin plane holds the same
+    // normal) + roughness with the metallic flag in its sign bit, [2i+1] = albedo xyz + depth.  Written
+    // beside the planes by the trace; a tap then reads one 32-byte record instead of five planes.
+    float4 *rec;
 };
 
 // Per-pixel state of the wavefront trace pass (trace.hip).  One slot per
@@ -221,6 +226,8 @@ hipError_t launch_sky(const float *cfg90, const float *rad10, const float *solar
 hipError_t launch_sky_lower(float4 *sky, float *skyPdf, int skyW, int skyH, float sumUpper, hipStream_t st);
 // waitBeforeRestir: event the pass's temporal-reuse kernel waits for (band halo exchange), or null
 hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir = nullptr);
+// GBuf::rec of the n pixels from the planes
+hipError_t launch_pack_rec(const GBuf &g, size_t n, hipStream_t st);
 hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st);
 
 struct DenoiseParamsDev {

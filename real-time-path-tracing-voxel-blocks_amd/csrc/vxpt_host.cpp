@@ -45,6 +45,8 @@ struct DBuf {
 struct GSlot {
     float4 *normalRough = nullptr, *geoNormalThin = nullptr, *albedo = nullptr, *matParam = nullptr;
     float *depth = nullptr, *material = nullptr;
+    float4 *rec = nullptr;  // ReSTIR tap records (GBuf::rec), 2 float4 per pixel
+    bool recStale = false;  // the planes were written from the host since the records were
 };
 
 // Perlin noise (siv::BasicPerlinNoise<float>, voxelengine/ext/PerlinNoise.hpp:229-494, 565-568)
@@ -551,6 +553,7 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_TEXELS: p = c->texels.p; bytes = c->nTexels * 4; return !forWrite && c->texels.p;
         case VXPT_BUF_BLOOM: p = c->bloomB; bytes = n * 16; return c->bloomB != nullptr;
         case VXPT_BUF_LIGHTS: p = c->lights.p; bytes = (size_t)c->nLights * sizeof(LightInfo); return !forWrite && c->nLights;
+        case VXPT_BUF_TAP_RECORD: p = g.rec; bytes = n * 32; return !forWrite;
         case VXPT_BUF_LIGHT_ALIAS:
             p = c->lightAlias.p; bytes = (size_t)c->nLights * sizeof(AliasBin); return !forWrite && c->nLights;
         default: return false;
@@ -748,8 +751,13 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     int next = 0;
     while (next == c->last || next == c->hist) ++next;
     const GSlot &cur = c->gb[next], &prev = c->gb[c->last];
-    a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material};
-    a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material};
+    a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material, cur.rec};
+    a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material, prev.rec};
+    if (prev.recStale) {  // planes uploaded or copied in from the host: rebuild the taps' records
+        HIPCHK(c, launch_pack_rec(a.prev, (size_t)c->W * c->H, c->stream));
+        c->gb[c->last].recStale = false;
+    }
+    c->gb[next].recStale = false;  // this pass writes both
     a.illum = c->illum;
     a.motion = c->motion;
     const size_t n = (size_t)c->W * c->H;
@@ -897,7 +905,15 @@ int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int a
 // host synchronisation.
 constexpr int kTraceHalo = 72;  // ReSTIR temporal taps: 64-pixel disk + reprojection (Restir.h:348-381)
 const int kGbufBufs[] = {VXPT_BUF_DEPTH, VXPT_BUF_NORMAL_ROUGH, VXPT_BUF_GEO_NORMAL_THIN,
-                         VXPT_BUF_ALBEDO, VXPT_BUF_MATERIAL, VXPT_BUF_MAT_PARAM};
+                         VXPT_BUF_ALBEDO, VXPT_BUF_MATERIAL, VXPT_BUF_MAT_PARAM, VXPT_BUF_TAP_RECORD};
+// a host-side write to a G-buffer plane leaves the slots' tap records stale (rebuilt before the next
+// trace reads them)
+bool is_gbuf_plane(int which) { return (which >= VXPT_BUF_DEPTH && which <= VXPT_BUF_MAT_PARAM) ||
+                                       (which >= VXPT_BUF_PREV_NORMAL_ROUGH && which <= VXPT_BUF_PREV_MATERIAL); }
+void gbuf_written(vxpt_ctx *c, int which) {
+    if (is_gbuf_plane(which))
+        for (GSlot &g : c->gb) g.recStale = true;
+}
 const int kHistoryBufs[] = {VXPT_BUF_PREV_ILLUM, VXPT_BUF_PREV_FAST, VXPT_BUF_PREV_HIST_LEN};
 
 void band_rows(int H, int world, int rank, int &y0, int &y1) {
@@ -1200,8 +1216,9 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (cfg->total_bounce_limit > 0) c->totalBounce = cfg->total_bounce_limit;
     if (cfg->diffuse_bounce_limit > 0) c->diffuseBounce = cfg->diffuse_bounce_limit;
     c->dataDir = cfg->data_dir ? cfg->data_dir : "data";
-    // the DDA's empty-box skip tables (an experiment, off by default: box_tables.hpp)
-    c->useBoxes = getenv("VXPT_DDA_BOXES") && atoi(getenv("VXPT_DDA_BOXES")) != 0;
+    // the DDA's empty-box skip tables (box_tables.hpp; measured 7.56 -> 7.06 ms of trace per
+    // C3 frame); VXPT_DDA_BOXES=0 walks with the empty-cube tables alone
+    c->useBoxes = !(getenv("VXPT_DDA_BOXES") && atoi(getenv("VXPT_DDA_BOXES")) == 0);
     c->yamlPost = default_post();
     c->yamlDenoise = default_denoise();
     *out = c;
@@ -1215,7 +1232,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     const size_t tiles16 = (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16);  // denoiser tiles
     for (auto &g : c->gb) {
         if (dalloc(c, g.normalRough, n) || dalloc(c, g.geoNormalThin, n) || dalloc(c, g.albedo, n) ||
-            dalloc(c, g.matParam, n) || dalloc(c, g.depth, n) || dalloc(c, g.material, n))
+            dalloc(c, g.matParam, n) || dalloc(c, g.depth, n) || dalloc(c, g.material, n) || dalloc(c, g.rec, 2 * n))
             return VXPT_ERR_HIP;
     }
     if (dalloc(c, c->illum, n) || dalloc(c, c->accum, n) || dalloc(c, c->motion, n) || dalloc(c, c->res, 2 * n) ||
@@ -2354,6 +2371,7 @@ int vxpt_copy_rows(vxpt_ctx *c, int which, int y, int rows, void *dev, int to_bu
     buffer_ptr(c, which, p, n, false, &mirror);
     HIPCHK(c, hipSetDevice(c->dev));
     char *row = static_cast<char *>(p) + (size_t)y * rb;
+    if (to_buffer) gbuf_written(c, which);
     if (to_buffer) HIPCHK(c, hipMemcpyAsync(row, dev, (size_t)rows * rb, hipMemcpyDeviceToDevice, c->stream));
     else HIPCHK(c, hipMemcpyAsync(dev, row, (size_t)rows * rb, hipMemcpyDeviceToDevice, c->stream));
     return VXPT_OK;
@@ -2372,6 +2390,7 @@ int vxpt_exchange_halo(vxpt_ctx *c, uint32_t mask, int rows) {
         size_t n;
         if (!buffer_ptr(c, b, ptr, n, false, &mirror) || b == VXPT_BUF_RESERVOIRS)
             return fail(c, VXPT_ERR_ARG, "buffer has no row layout");
+        gbuf_written(c, b);
         br.emplace_back(b, rows);
     }
     HIPCHK(c, hipSetDevice(c->dev));
@@ -2695,6 +2714,7 @@ int vxpt_upload(vxpt_ctx *c, int which, const void *host, size_t bytes) {
     if (!buffer_ptr(c, which, p, n, true, &mirror) || (which >= 32 && which <= 34))
         return fail(c, VXPT_ERR_ARG, "unknown or read-only buffer");
     if (bytes < n) return fail(c, VXPT_ERR_ARG, "host buffer too small");
+    gbuf_written(c, which);
     HIPCHK(c, hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
     if (mirror) HIPCHK(c, hipMemcpyAsync(mirror, host, n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

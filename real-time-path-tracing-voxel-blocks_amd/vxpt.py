@@ -24,7 +24,7 @@ BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERI
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
            PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38,
            OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42, TEXELS=43, LIGHTS=44,
-           LIGHT_ALIAS=45, BLOOM=46)
+           LIGHT_ALIAS=45, BLOOM=46, TAP_RECORD=47)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
@@ -510,6 +510,8 @@ class Renderer:
                     BUF["MACRO_MASKS"]: np.zeros(nb // 64, np.uint64)}[which]
         if which in FLOAT1_BUFS:
             return np.zeros((self.H, self.W), np.float32)
+        if which == BUF["TAP_RECORD"]:
+            return np.zeros((self.H, self.W, 8), np.float32)
         return np.zeros((self.H, self.W, 4), np.float32)
 
     def read(self, name):

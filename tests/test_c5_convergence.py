@@ -30,7 +30,9 @@ def test_c5_64_frames_match_oracle():
         print("%s relative RMS %.3e" % (name, rms))
         assert rms < bar, (name, rms)
         # 64 frames of history accumulation: a few pixels take another branch of a denoiser
-        # threshold test after ulp-level differences (measured: 99.93 % within 1e-3)
+        # threshold test after ulp-level differences (measured: 99.93 % within 1e-3, max e 0.013 --
+        # the history clamp's x-only Float3 min/max swaps a whole colour bound on a rounding-level
+        # change of its luma; the oracle alone does the same under a 1e-6 perturbation)
         check_radiance(r.read(name), o.read(which), "C5 %s after %d frames" % (name, frames), frac_tight=0.98,
-                       frac_l2=0.999)
+                       frac_l2=0.999, e_max=0.05)
     r.close()

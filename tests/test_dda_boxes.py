@@ -1,11 +1,12 @@
-"""The voxel walk's optional empty-box skip tables (VXPT_DDA_BOXES; csrc/box_tables.hpp).
+"""The voxel walk's empty-box skip tables (csrc/box_tables.hpp; the default walk since round 3,
+VXPT_DDA_BOXES=0 walks with the empty-cube tables alone).
 
 CPU: the library's own walk (vx_device.hpp is host + device code) runs on the host in a driver
 compiled with hipcc (no kernel launch), once with the default empty-cube tables and once with the
 box tables, over the C1 world, the C3 (256^3) world and a random sparse world: every ray's closest
 hit (cell, face, block id, t bits) and occlusion answer must be identical, also through the
 straggler save / resume hand-over, with fewer outer iterations for the boxes.
-GPU: the probe kernels with the box tables against the oracle's DDA, bit for bit.
+GPU: the probe kernels with either table against the oracle's DDA, bit for bit.
 """
 import os
 import subprocess
@@ -69,13 +70,11 @@ def test_box_tables_walk_equals_cube_walk(driver, world, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.xfail(strict=False, reason="the opt-in box tables have not run on a GPU yet (this round's GPU access "
-                                        "ended before they were written); the CPU test runs the same walk code")
+@pytest.mark.parametrize("boxes", ["1", "0"])
 @pytest.mark.parametrize("outside", [False, True])
-def test_dda_probe_with_box_tables_bit_exact(outside, monkeypatch):
-    import vxpt
+def test_dda_probe_with_box_tables_bit_exact(outside, boxes, monkeypatch):
     from test_gpu_parity import _random_rays, _setup
-    monkeypatch.setenv("VXPT_DDA_BOXES", "1")
+    monkeypatch.setenv("VXPT_DDA_BOXES", boxes)
     r, o = _setup()
     try:
         rays = _random_rays(20000, 31 + outside, outside=outside)

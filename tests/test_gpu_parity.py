@@ -135,12 +135,61 @@ def test_primary_gbuffer(pair):
     np.testing.assert_allclose(g, c, rtol=1e-5, atol=1e-6)
 
 
+def _expected_tap_record(r):
+    """GBuf::rec restated from the G-buffer planes: (normal xyz, roughness | metallic << 31),
+    (albedo xyz, depth), 32 bytes per pixel."""
+    nr, al, mp, d = r.read("NORMAL_ROUGH"), r.read("ALBEDO"), r.read("MAT_PARAM"), r.read("DEPTH")
+    exp = np.zeros(nr.shape[:2] + (8,), np.float32)
+    exp[..., :3], exp[..., 4:7], exp[..., 7] = nr[..., :3], al[..., :3], d
+    rb = nr[..., 3].view(np.uint32) | np.where(mp[..., 0] == 1.0, np.uint32(0x80000000), np.uint32(0))
+    exp[..., 3] = rb.view(np.float32)
+    return exp
+
+
+@pytest.mark.parametrize("primary_only", [False, True])
+def test_tap_record_matches_planes(primary_only):
+    """The trace writes each pixel's ReSTIR tap record beside its G-buffer planes; the record is
+    the planes' values bit for bit (and the geoNormalThin plane holds the normalRough normal, which
+    the record stores once)."""
+    r, o = _setup(100, 62)
+    try:
+        for it in range(2):
+            r.trace(it, primary_only=primary_only)
+            np.testing.assert_array_equal(r.read("TAP_RECORD").view(np.uint32), _expected_tap_record(r).view(np.uint32))
+            np.testing.assert_array_equal(r.read("GEO_NORMAL_THIN")[..., :3].view(np.uint32),
+                                          r.read("NORMAL_ROUGH")[..., :3].view(np.uint32))
+    finally:
+        r.close()
+
+
+def test_tap_records_rebuilt_after_a_plane_upload():
+    """A host write to a G-buffer plane marks the tap records stale; the next trace rebuilds them
+    from the planes (k_pack_rec) and renders exactly what an untouched context renders."""
+    a, _ = _setup(100, 62)
+    b, _ = _setup(100, 62)
+    try:
+        for r in (a, b):
+            r.trace(0)
+        b.write("NORMAL_ROUGH", b.read("NORMAL_ROUGH"))  # same values, through the upload path
+        for r in (a, b):
+            r.trace(1)
+        for name in ("ILLUM", "RES_ODD", "TAP_RECORD"):
+            np.testing.assert_array_equal(a.read(name).view(np.uint8), b.read(name).view(np.uint8))
+    finally:
+        a.close()
+        b.close()
+
+
 # Radiance bars (per pixel, RGB): relative L2 error e = |g - c|_2 / max(|c|_2, 1e-3).
 # North_star's per-pixel L2 tolerance is 1e-3; ocml vs glibc transcendentals can flip a
 # threshold test on a handful of pixels, so: >= 99.9 % of pixels with e < 1e-4, >= 99.95 %
-# with e < 1e-3, image mean within 1e-5 (measured: 100 %, max e ~1e-4, mean ~1e-7).
+# with e < 1e-3, image mean within 1e-5, and NO pixel above E_MAX.  Measured (round 3, every
+# GPU test): radiance max e 7.6e-5 except a 4-bounce chain's frame 3 (4.1e-4); denoised outputs
+# max e 1.0e-5, except 2.0e-3 on single pixels of the textured sequence (the denoiser amplifies
+# ulp-level input differences once history passes 4 frames, DESIGN.md §9) -- so E_MAX = 5e-3.  Only the 64-frame C5 gate passes a wider e_max (see its test).
 E_TIGHT, FRAC_TIGHT = 1e-4, 0.999
 E_L2, FRAC_L2 = 1e-3, 0.9995
+E_MAX = 5e-3
 MEAN_TOL_L2 = 1e-5
 
 
@@ -149,14 +198,16 @@ def pixel_l2(g, c):
     return np.linalg.norm(g - c, axis=-1) / np.maximum(np.linalg.norm(c, axis=-1), 1e-3)
 
 
-def check_radiance(g, c, what, frac_tight=FRAC_TIGHT, frac_l2=FRAC_L2):
+def check_radiance(g, c, what, frac_tight=FRAC_TIGHT, frac_l2=FRAC_L2, e_max=E_MAX):
     assert np.isfinite(g).all(), what
     e = pixel_l2(g, c)
     ft, fl = (e < E_TIGHT).mean(), (e < E_L2).mean()
     mean_rel = abs(g[..., :3].mean() - c[..., :3].mean()) / max(abs(c[..., :3].mean()), 1e-6)
-    msg = "%s: e<1e-4 %.5f, e<1e-3 %.5f, max e %.3g, mean rel %.2e" % (what, ft, fl, e.max(), mean_rel)
+    worst = np.unravel_index(e.argmax(), e.shape)
+    msg = "%s: e<1e-4 %.5f, e<1e-3 %.5f, max e %.3g at %s, mean rel %.2e" % (what, ft, fl, e.max(), worst, mean_rel)
     print(msg)
     assert ft >= frac_tight and fl >= frac_l2, msg
+    assert e.max() < e_max, msg
     assert mean_rel < MEAN_TOL_L2, msg
     return e
 
