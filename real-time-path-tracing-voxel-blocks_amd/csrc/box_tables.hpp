@@ -45,12 +45,15 @@ constexpr int kBoxCap = 8;  // growth limit in bricks per axis (past the cube)
 
 // the box of brick (x, y, z) in octant oct (bit a set: the ray moves + along axis a), grown from its
 // cube edge S (0 = occupied)
-inline uint32_t grow_box(const BrickPrefix &P, int x, int y, int z, int oct, int S, int cap = kBoxCap) {
+// capUp: the growth limit along y in the upward octants (the empty space above a terrain is tall)
+inline uint32_t grow_box(const BrickPrefix &P, int x, int y, int z, int oct, int S, int cap = kBoxCap,
+                         int capUp = kBoxCap) {
     if (S <= 0) return 0u;
     const int b[3] = {x, y, z}, n[3] = {P.BX, P.BY, P.BZ};
     const int sg[3] = {(oct & 1) ? 1 : -1, (oct & 2) ? 1 : -1, (oct & 4) ? 1 : -1};
     int e[3] = {S, S, S};
     const int lim = std::min(255, std::max(S, cap));
+    const int limUp = std::min(255, std::max(S, capUp));
     auto empty = [&](const int *ext) {
         int lo[3], hi[3];
         for (int a = 0; a < 3; ++a) {
@@ -61,7 +64,7 @@ inline uint32_t grow_box(const BrickPrefix &P, int x, int y, int z, int oct, int
     };
     static const int order[3] = {0, 2, 1};
     for (int a : order)
-        while (e[a] < lim) {
+        while (e[a] < (a == 1 && sg[1] > 0 ? limUp : lim)) {
             // the box already reaches the world's edge on this axis: growing adds nothing
             if (sg[a] > 0 ? b[a] + e[a] >= n[a] : b[a] - e[a] + 1 <= 0) break;
             int t[3] = {e[0], e[1], e[2]};

@@ -29,7 +29,9 @@
 namespace vx {
 namespace {
 
-constexpr int F_ALIVE = 1, F_HFD = 2, F_NEE = 4, F_RESTIR = 8;
+// F_EMPTY: the pixel's reservoir is the empty one (a seg-0 miss or specular hit); k_finish stores it, so
+// a pass's first half never writes reservoirs (the previous pass's temporal reuse may still read them)
+constexpr int F_ALIVE = 1, F_HFD = 2, F_NEE = 4, F_RESTIR = 8, F_EMPTY = 16;
 constexpr float kFltMax = 3.402823466e+38f;
 
 VX_D bool slot_pixel(const TraceArgs &a, int s, int &px, int &py) {
@@ -85,6 +87,25 @@ VX_D void stat_wave(int kind, bool active, const int *it) {
         atomicAdd(&g[2], (unsigned long long)mx);
         for (int k = 0; k < 5; ++k) atomicAdd(&g[3 + k], (unsigned long long)v[k]);
     }
+}
+// per kind: per-ray outer iterations in this launch, histogram bins [0,2) [2,4) [4,8) ... [128,inf)
+// (8 bins), rays going up (d.y > 0), rays ending on an event (hit / occluded), max iterations
+__device__ unsigned long long g_hist[8 * 16];
+VX_D void stat_ray(int kind, bool active, int its, float dy, bool event) {
+    int b = 0;
+    while (b < 7 && its >= (2 << b)) ++b;
+    unsigned long long *g = g_hist + kind * 16;
+    const bool lead = (threadIdx.x & 63) == 0;
+    for (int k = 0; k < 8; ++k) {
+        const unsigned long long m = __ballot(active && b == k);
+        if (lead && m) atomicAdd(&g[k], (unsigned long long)__popcll(m));
+    }
+    const unsigned long long up = __ballot(active && dy > 0.0f), ev = __ballot(active && event);
+    if (lead && up) atomicAdd(&g[8], (unsigned long long)__popcll(up));
+    if (lead && ev) atomicAdd(&g[9], (unsigned long long)__popcll(ev));
+    int mx = active ? its : 0;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    if (lead && mx) atomicMax(&g[10], (unsigned long long)mx);
 }
 #define VX_IT , iters
 #else
@@ -155,13 +176,64 @@ struct QRays {  // up to 4 rays of one slot (a local light is seen in a differen
     float t0, t1, t2, t3;  // tmin
 };
 
+// direction class of a queued ray (sortMode 1: its octant; 2: octant x dominant axis), the key of
+// the per-workgroup counting sort in block_enqueue
+VX_D int ray_key(int mode, V3 d) {
+    const int oct = (d.x > 0.0f ? 1 : 0) | (d.y > 0.0f ? 2 : 0) | (d.z > 0.0f ? 4 : 0);
+    if (mode == 1) return oct;
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const int dom = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+    return oct * 3 + dom;
+}
+
 // Appends every lane's rays (bits of r.mask) to queue q.  Every thread of the
-// 256-thread workgroup must call it.
+// 256-thread workgroup must call it.  With a.sortMode the workgroup's rays are
+// grouped by direction class (ray_key) inside its segment of the queue, so a
+// traversal wave holds rays of one class (coherent walks and table lines); the
+// order of rays within a queue never changes a result.
 VX_D void block_enqueue(const TraceArgs &a, int q, const QRays &r) {
     __shared__ unsigned sTot[4], sBase[4];
+    __shared__ unsigned sHist[32], sOff[32];
     const WaveBufs &w = a.wb;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int n = __popc(r.mask);
+    if (a.sortMode) {
+        if (threadIdx.x < 32) sHist[threadIdx.x] = 0u;
+        __syncthreads();
+        int key[4], rank[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            key[i] = 0;
+            rank[i] = 0;
+            if (!(r.mask & (1u << i))) continue;
+            key[i] = ray_key(a.sortMode, i == 0 ? r.d0 : (i == 1 ? r.d1 : (i == 2 ? r.d2 : r.d3)));
+            rank[i] = (int)atomicAdd(&sHist[key[i]], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned t = 0;
+            for (int k = 0; k < 32; ++k) {
+                sOff[k] = t;
+                t += sHist[k];
+            }
+            sBase[0] = t ? atomicAdd(&w.qCount[q], t) : 0u;
+        }
+        __syncthreads();
+        const unsigned base = sBase[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (!(r.mask & (1u << i))) continue;
+            const int k = (int)(base + sOff[key[i]]) + rank[i];
+            const V3 o = i == 0 ? r.o0 : (i == 1 ? r.o1 : (i == 2 ? r.o2 : r.o3));
+            const float tmin = i == 0 ? r.t0 : (i == 1 ? r.t1 : (i == 2 ? r.t2 : r.t3));
+            const V3 d = i == 0 ? r.d0 : (i == 1 ? r.d1 : (i == 2 ? r.d2 : r.d3));
+            const float tmax = i == 0 ? r.x0 : (i == 1 ? r.x1 : (i == 2 ? r.x2 : r.x3));
+            w.qO[k] = f4(o, tmin);
+            w.qD[k] = f4(d, tmax);
+            w.qId[k] = r.id0 + i;
+        }
+        return;
+    }
     int incl = n;
     for (int o = 1; o < 64; o <<= 1) {
         const int v = __shfl_up(incl, o);
@@ -242,6 +314,8 @@ __global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int 
     }
 #ifdef VX_STATS
     stat_wave((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), live, iters);
+    stat_ray((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), live, iters[0] + iters[1] + iters[2] + iters[3],
+             live ? st.r.dy : 0.0f, rc == DdaEvent);
 #endif
     if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h);
     // unfinished walks -> straggler queue
@@ -304,6 +378,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         }
 #ifdef VX_STATS
         stat_wave(5, live, iters);
+        stat_ray(5, live, iters[0] + iters[1] + iters[2] + iters[3], live ? st.r.dy : 0.0f, rc == DdaEvent);
 #endif
         if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h);
         const bool defer = live && rc == DdaRun;
@@ -338,16 +413,22 @@ VX_D void path_end(const TraceArgs &a, int px, int py, V3 radiance, float primar
     if (isnan(radiance.x) || isnan(radiance.y) || isnan(radiance.z)) radiance = V3(0.5f);  // RayGen.cu:175-178
     const size_t pi = (size_t)py * a.W + px;
     a.cur.depth[pi] = primaryDist;
-    if (a.accum) {
-        // spp > 1: average the passes' radiance, depth from the last pass
-        float4 acc = a.accumFirst ? make_float4(0.f, 0.f, 0.f, 0.f) : a.accum[pi];
-        acc.x += radiance.x * a.accumScale;
-        acc.y += radiance.y * a.accumScale;
-        acc.z += radiance.z * a.accumScale;
-        acc.w = primaryDist;
-        a.accum[pi] = acc;
-    }
     a.illum[pi] = make_float4(radiance.x, radiance.y, radiance.z, primaryDist);
+}
+
+// spp > 1: average the passes' radiance, depth from the last pass -- after the pass,
+// in pass order (a pass's paths end in both of its halves)
+__global__ __launch_bounds__(256) void k_accum(TraceArgs a) {
+    int px, py;
+    if (!slot_pixel(a, blockIdx.x * 256 + threadIdx.x, px, py)) return;
+    const size_t pi = (size_t)py * a.W + px;
+    const float4 r = a.illum[pi];
+    float4 acc = a.accumFirst ? make_float4(0.f, 0.f, 0.f, 0.f) : a.accum[pi];
+    acc.x += r.x * a.accumScale;
+    acc.y += r.y * a.accumScale;
+    acc.z += r.z * a.accumScale;
+    acc.w = r.w;
+    a.accum[pi] = acc;
 }
 
 // End of one TraceNextPath segment (RayGen.cu:146-173): accumulate, apply the
@@ -494,7 +575,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
 
     if (!h.hit) {  // __miss__radiance (miss.cu:9-82)
         if (seg == 0) {
-            a.resCur[pi] = empty_res();
+            meta.x |= F_EMPTY;
             a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
             a.cur.material[pi] = (float)0xFFFF;
             a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
@@ -587,7 +668,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.pPos[s] = f4(spawnPos, primaryDist);
     w.pDir[s] = f4(swi, spdf);
     if (!isDiffuse) {
-        if (seg == 0) a.resCur[pi] = empty_res();
+        if (seg == 0) meta.x |= F_EMPTY;
         seg_end(a, s, px, py, meta, V3(0.0f), sbop, spdf, terminate, false);
         meta.y = rng.idx;
         w.pMeta[s] = meta;
@@ -987,8 +1068,12 @@ __global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
     int4 meta = w.pMeta[s];
-    if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
     const size_t pi = (size_t)py * a.W + px;
+    if (meta.x & F_EMPTY) {
+        a.resCur[pi] = empty_res();
+        return;
+    }
+    if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
     bool skipAlbedo;
     SurfX sp;
     const SurfS sf = load_surf(w, s, skipAlbedo, &sp);
@@ -1179,9 +1264,11 @@ __global__ __launch_bounds__(256) void k_pack_rec(GBuf g, size_t n) {
 #ifdef VX_STATS
 extern "C" int vxpt_debug_stats(unsigned long long *out64, int reset) {
     hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_stats), sizeof(g_stats), 0, hipMemcpyDeviceToHost);
+    hipMemcpyFromSymbol(out64 + 64, HIP_SYMBOL(g_hist), sizeof(g_hist), 0, hipMemcpyDeviceToHost);
     if (reset) {
-        static const unsigned long long z[64] = {};
-        hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof(z), 0, hipMemcpyHostToDevice);
+        static const unsigned long long z[128] = {};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof(g_stats), 0, hipMemcpyHostToDevice);
+        hipMemcpyToSymbol(HIP_SYMBOL(g_hist), z, sizeof(g_hist), 0, hipMemcpyHostToDevice);
     }
     return 0;
 }
@@ -1203,27 +1290,24 @@ hipError_t launch_probe(const WorldDev &w, int n, const float *rays, int *out, f
     return hipGetLastError();
 }
 
-hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir) {
-    const dim3 g((a.nSlots + 255) / 256), g4((4 * a.nSlots + 255) / 256), b(256);
-    const bool mesh = a.mesh.nInst > 0;
-    // the walks use the empty-box tables when the world has them (VXPT_DDA_BOXES), else the cubes
-    const bool box = a.world.bbox != nullptr;
-    auto closest = [&](int mode) {
+namespace {
+struct Launcher {
+    const TraceArgs &a;
+    hipStream_t st;
+    dim3 g, b;
+    bool mesh, box;
+    Launcher(const TraceArgs &a_, hipStream_t st_)
+        : a(a_), st(st_), g((a_.nSlots + 255) / 256), b(256), mesh(a_.mesh.nInst > 0), box(a_.world.bbox != nullptr) {}
+    // the walks use the empty-box tables when the world has them, else the cubes
+    void closest(int mode) {
         if (box) hipLaunchKernelGGL(k_closest<true>, g, b, 0, st, a, mode);
         else hipLaunchKernelGGL(k_closest<false>, g, b, 0, st, a, mode);
-    };
-    closest(2);
-    if (a.primaryOnly) {  // C2 bring-up: the voxel G-buffer only
-        hipLaunchKernelGGL(k_primary_gbuffer, g, b, 0, st, a);
-        return hipGetLastError();
     }
-    // secondary / visibility rays go through the compacted queues; their
-    // counters (4 per segment) are zeroed once per pass
-    hipMemsetAsync(a.wb.qCount, 0, (64 + 3 * 16 * kShards * 16) * sizeof(unsigned), st);
-    // the stragglers' grid: a fixed number of workgroups per CU (their count is on the device; each
-    // wave reads it and strides over its shard), VXPT_RESUME_WG per CU for the sweep in DESIGN.md
-    const dim3 gr(a.numCU * (a.resumeWgPerCU > 0 ? a.resumeWgPerCU : 16));
-    auto trav = [&](bool occ, int q, int cap) {
+    // a ray queue's traversal: iteration-capped pass + straggler continuation (+ the mesh pass).  The
+    // stragglers' grid: a fixed number of workgroups per CU (their count is on the device; each wave
+    // reads it and strides over its shard), VXPT_RESUME_WG per CU for the sweep in DESIGN.md
+    void trav(bool occ, int q, int cap) {
+        const dim3 gr(a.numCU * (a.resumeWgPerCU > 0 ? a.resumeWgPerCU : 16));
         const dim3 gq((cap + 255) / 256);
         const int shardCap = (int)((gq.x + kShards - 1) / kShards) * 256;
         if (occ && box) {
@@ -1247,30 +1331,58 @@ hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBefor
             if (occ) hipLaunchKernelGGL(k_mesh_queue<true>, gq, b, 0, st, a, q);
             else hipLaunchKernelGGL(k_mesh_queue<false>, gq, b, 0, st, a, q);
         }
-    };
-    if (mesh) hipLaunchKernelGGL(k_mesh_slots, g, b, 0, st, a, 2);
-    for (int seg = 0; seg < a.segments; ++seg) {
-        if (seg > 0) {
-            closest(0);
-            if (mesh) hipLaunchKernelGGL(k_mesh_slots, g, b, 0, st, a, 0);
-        }
-        // the shading kernels' mesh variants (mesh hits, thin films, local lights) run only with meshes
+    }
+    // a segment's shading up to its NEE visibility rays (the shading kernels' mesh variants -- mesh hits,
+    // thin films, local lights -- run only with meshes)
+    void first_half(int seg) {
         if (mesh) hipLaunchKernelGGL(k_shade<true>, g, b, 0, st, a, seg);
         else hipLaunchKernelGGL(k_shade<false>, g, b, 0, st, a, seg);
         trav(false, 4 * seg + 1, a.nSlots);
         if (mesh) hipLaunchKernelGGL(k_nee<true>, g, b, 0, st, a, seg);
         else hipLaunchKernelGGL(k_nee<false>, g, b, 0, st, a, seg);
         trav(true, 4 * seg + 2, a.nSlots);
-        // the first reader of the previous pass's G-buffer and reservoirs (temporal taps):
-        // a band's halo rows of them may still be in flight on the exchange stream
-        if (seg == 0 && waitBeforeRestir) hipStreamWaitEvent(st, waitBeforeRestir, 0);
+    }
+    void restir(int seg) {
         if (mesh) hipLaunchKernelGGL(k_restir<true>, g, b, 0, st, a, seg);
         else hipLaunchKernelGGL(k_restir<false>, g, b, 0, st, a, seg);
-        if (seg == 0) {
-            trav(true, 4 * seg + 3, 4 * a.nSlots);
-            hipLaunchKernelGGL(k_finish, g, b, 0, st, a);
-        }
     }
+};
+}  // namespace
+
+// A pass's first half: camera rays, segment 0's shading, BRDF-candidate and RIS visibility rays.
+// It reads nothing of the previous pass (G-buffer slot, reservoirs): it writes its own slot, its
+// state set, and its own radiance plane.
+hipError_t launch_trace_front(const TraceArgs &a, hipStream_t st) {
+    Launcher L(a, st);
+    L.closest(2);
+    if (a.primaryOnly) {  // C2 bring-up: the voxel G-buffer only
+        hipLaunchKernelGGL(k_primary_gbuffer, L.g, L.b, 0, st, a);
+        return hipGetLastError();
+    }
+    // secondary / visibility rays go through the compacted queues; their counters (4 per segment)
+    // are zeroed once per pass
+    hipMemsetAsync(a.wb.qCount, 0, (64 + 3 * 16 * kShards * 16) * sizeof(unsigned), st);
+    if (L.mesh) hipLaunchKernelGGL(k_mesh_slots, L.g, L.b, 0, st, a, 2);
+    L.first_half(0);
+    return hipGetLastError();
+}
+
+// The second half: segment 0's temporal reuse (the first reader of the previous pass's G-buffer and
+// reservoirs -- a band's halo rows of them may still be in flight on the exchange stream), its rays,
+// k_finish (reservoir store), the later segments, and the spp accumulation.
+hipError_t launch_trace_back(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir) {
+    Launcher L(a, st);
+    if (waitBeforeRestir) hipStreamWaitEvent(st, waitBeforeRestir, 0);
+    L.restir(0);
+    L.trav(true, 3, 4 * a.nSlots);
+    hipLaunchKernelGGL(k_finish, L.g, L.b, 0, st, a);
+    for (int seg = 1; seg < a.segments; ++seg) {
+        L.closest(0);
+        if (L.mesh) hipLaunchKernelGGL(k_mesh_slots, L.g, L.b, 0, st, a, 0);
+        L.first_half(seg);
+        L.restir(seg);
+    }
+    if (a.accum) hipLaunchKernelGGL(k_accum, L.g, L.b, 0, st, a);
     return hipGetLastError();
 }
 

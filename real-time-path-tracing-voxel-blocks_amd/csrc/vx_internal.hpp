@@ -217,6 +217,7 @@ struct TraceArgs {
     int prevNumLights;
     int lightsDirty;
     int resumeWgPerCU;  // k_resume workgroups per CU (0: 16)
+    int sortMode;       // ray queues grouped by direction class per workgroup (0 off, 1 octant, 2 octant x axis)
 };
 
 // kernel launchers (defined in the .hip translation units)
@@ -224,8 +225,11 @@ hipError_t launch_sky(const float *cfg90, const float *rad10, const float *solar
                       float brightness, float4 *sky, float4 *sun, float *skyPdf, float *sunPdf, int skyW, int skyH,
                       int sunW, int sunH, hipStream_t st);
 hipError_t launch_sky_lower(float4 *sky, float *skyPdf, int skyW, int skyH, float sumUpper, hipStream_t st);
-// waitBeforeRestir: event the pass's temporal-reuse kernel waits for (band halo exchange), or null
-hipError_t launch_trace(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir = nullptr);
+// a trace pass in two halves (trace.hip): the first reads nothing of the previous pass; the second
+// starts with the temporal reuse.  waitBeforeRestir: event the temporal-reuse kernel waits for (band
+// halo exchange), or null
+hipError_t launch_trace_front(const TraceArgs &a, hipStream_t st);
+hipError_t launch_trace_back(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir);
 // GBuf::rec of the n pixels from the planes
 hipError_t launch_pack_rec(const GBuf &g, size_t n, hipStream_t st);
 hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st);

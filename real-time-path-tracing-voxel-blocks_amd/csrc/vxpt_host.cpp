@@ -159,6 +159,7 @@ struct vxpt_ctx {
     // optional empty-box skip tables (VXPT_DDA_BOXES=1 at vxpt_create; box_tables.hpp)
     bool useBoxes = false;
     BrickPrefix brickPrefix;
+    int boxCap = kBoxCap, boxCapUp = kBoxCap;  // box growth limits (box_tables.hpp)
     std::vector<uint32_t> hBox;
     DBuf<uint32_t> bbox;
     int nBricks = 0;
@@ -236,6 +237,7 @@ struct vxpt_ctx {
     DBuf<int4> meshRow;
     DBuf<int> meshRowLight;
     DBuf<MatDev> meshMats;
+    MatDev meshMatsUp[32] = {};  // what meshMats holds (uploaded when the materials change)
     // vxpt_mesh_probe / vxpt_mesh_occluded scratch (grown to the largest call)
     DBuf<float> probeRays, probeOut;
     DBuf<int> probeIds;
@@ -249,11 +251,15 @@ struct vxpt_ctx {
     // the previous pass's (its ReSTIR history) nor the denoiser's history slot
     // (the previous frame's final G-buffer, Denoiser.cu:394-407), so the frame
     // end hands the last slot to the denoiser by index instead of copying planes.
-    GSlot gb[3];
+    // A 4th slot lets a pass's first half (camera rays .. NEE visibility, which read no previous
+    // pass) run while the previous pass's temporal reuse still reads its own previous slot.
+    GSlot gb[4];
     int last = 0;              // slot of the most recent trace output
     int tracePrev = 0;         // slot the most recent trace read as its previous pass
     int hist = 2;              // denoiser history slot (zero at frame 0)
-    float4 *illum = nullptr, *accum = nullptr, *motion = nullptr;
+    float4 *illum = nullptr;   // the most recent pass's radiance (one of illumSet)
+    float4 *illumSet[2] = {nullptr, nullptr};  // per wavefront state set
+    float4 *accum = nullptr, *motion = nullptr;
     Reservoir *res = nullptr;  // 2*W*H
     float4 *ping = nullptr, *pong = nullptr, *prevIllum = nullptr, *prevFast = nullptr, *output = nullptr;
     float *histLen = nullptr, *prevHistLen = nullptr;
@@ -263,7 +269,15 @@ struct vxpt_ctx {
     float4 *ffColor = nullptr;
     Reservoir *ffRes = nullptr;
     bool denoiseInputIsAccum = false;
-    WaveBufs wb{};
+    // Two wavefront state sets, alternating by pass: pass k's first half (k_closest .. the RIS
+    // visibility rays) runs on frontStream while pass k-1's second half (temporal reuse, its rays,
+    // k_finish, later segments, the spp accumulation) runs on the context stream.
+    WaveBufs wb[2]{};
+    size_t wbSlots[2] = {0, 0};
+    int passCount = 0;         // trace passes so far (set = passCount % 2)
+    int lastSet = 0;           // the set of the most recent pass
+    hipStream_t frontStream = nullptr;
+    hipEvent_t frontDone[2] = {nullptr, nullptr}, backDone[2] = {nullptr, nullptr}, frontGate = nullptr;
     int numCU = 256;
     std::vector<void *> allocs;
 
@@ -603,12 +617,13 @@ void octant_fill(vxpt_ctx *c, int oct, int x0, int x1, int y0, int y1, int z0, i
 // the box tables over brick box [x0,x1] x [y0,y1] x [z0,z1] of octant oct, from the cube tables and
 // the occupancy prefix counts (both current)
 void box_fill(vxpt_ctx *c, int oct, int x0, int x1, int y0, int y1, int z0, int z1) {
+    const int boxCap = c->boxCap, boxCapUp = c->boxCapUp;
     const size_t nB = (size_t)c->cx * 8 * c->cy * 8 * c->cz * 8;
     for (int y = y0; y <= y1; ++y)
         for (int z = z0; z <= z1; ++z)
             for (int x = x0; x <= x1; ++x) {
                 const size_t b = brick_lin(c, x, y, z);
-                c->hBox[oct * nB + b] = grow_box(c->brickPrefix, x, y, z, oct, c->hOd[oct * nB + b]);
+                c->hBox[oct * nB + b] = grow_box(c->brickPrefix, x, y, z, oct, c->hOd[oct * nB + b], boxCap, boxCapUp);
             }
 }
 void brick_prefix(vxpt_ctx *c) {
@@ -727,7 +742,38 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
 static MeshDev mesh_dev(const vxpt_ctx *c);
 namespace {
 
-int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale) {
+// wavefront trace state of one set for ns slots (8x8 tiles of the band), 4 visibility rays per slot;
+// allocated at the first pass that needs it (a band context holds its band's slots only).  The
+// allocation's zero fill is enqueued on the context stream: `fresh` tells the caller
+int ensure_wave(vxpt_ctx *c, int set, size_t ns, bool &fresh) {
+    fresh = false;
+    if (c->wbSlots[set] >= ns) return 0;
+    fresh = true;
+    WaveBufs &w = c->wb[set];
+    w = WaveBufs{};  // a smaller earlier set stays allocated (freed with the context)
+    if (dalloc(c, w.pPos, ns) || dalloc(c, w.pDir, ns) || dalloc(c, w.pThr, ns) || dalloc(c, w.pRad, ns) ||
+        dalloc(c, w.pMeta, ns) || dalloc(c, w.pBop, ns) || dalloc(c, w.cRayO, ns) || dalloc(c, w.cRayD, ns) ||
+        dalloc(c, w.cHit, ns) || dalloc(c, w.cT, ns) || dalloc(c, w.sPos, ns) || dalloc(c, w.sNrm, ns) ||
+        dalloc(c, w.sGeo, ns) || dalloc(c, w.sAlb, ns) || dalloc(c, w.sWo, ns) || dalloc(c, w.rSun, ns) ||
+        dalloc(c, w.rSky, ns) || dalloc(c, w.rRis, ns) || dalloc(c, w.rRR, ns) || dalloc(c, w.nIdx, ns) ||
+        dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
+        dalloc(c, w.oHit, 4 * ns) ||
+        dalloc(c, w.qO, 4 * ns) || dalloc(c, w.qD, 4 * ns) ||
+        dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, 64 + 3 * 16 * 8 * 16) ||
+        dalloc(c, w.sCell[0], 4 * ns + 2048) || dalloc(c, w.sT[0], 4 * ns + 2048) ||
+        dalloc(c, w.sFace[0], 4 * ns + 2048) || dalloc(c, w.sCell[1], 4 * ns + 2048) ||
+        dalloc(c, w.sT[1], 4 * ns + 2048) || dalloc(c, w.sFace[1], 4 * ns + 2048) ||
+        dalloc(c, w.sBack, ns) || dalloc(c, w.rLoc, ns) || dalloc(c, w.lLoc0, ns) || dalloc(c, w.lLoc1, ns))
+        return VXPT_ERR_HIP;
+    c->wbSlots[set] = ns;
+    return 0;
+}
+
+// One 1-spp pass.  overlap: the pass's first half may run beside the previous pass's second half
+// (passes of one frame; the first half then waits only for the pass before that to release its
+// state set).  Otherwise the first half starts after everything enqueued on the context stream.
+int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
+             bool overlap = false) {
     if (!c->voxels.p) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
     if (!c->skyReady) return fail(c, VXPT_ERR_STATE, "sky not set");
     TraceArgs a{};
@@ -736,7 +782,11 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.bn = {c->bnSobol.p, c->bnScramble.p, c->bnRank.p};
     for (int i = 0; i < 13; ++i) a.mats[i] = c->mats[i];
     if (c->nMeshInst > 0) {
-        if (int r = upload_vec(c, c->meshMats, c->mats, 32)) return r;
+        if (!c->meshMats.p || std::memcmp(c->meshMatsUp, c->mats, sizeof(c->mats)) != 0) {
+            if (int r = upload_vec(c, c->meshMats, c->mats, 32)) return r;
+            std::memcpy(c->meshMatsUp, c->mats, sizeof(c->mats));
+            overlap = false;  // the first half reads them: after the upload
+        }
         a.mesh = mesh_dev(c);
         a.meshUV = c->blasUV.p;
         a.meshRow = c->meshRow.p;
@@ -748,8 +798,10 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     }
     a.cam = c->cam;
     a.prevCam = c->prevCam;
+    // the slot this pass writes: not the previous pass's (its temporal taps), not the denoiser's
+    // history, and not the one the previous pass's second half may still be reading
     int next = 0;
-    while (next == c->last || next == c->hist) ++next;
+    while (next == c->last || next == c->hist || next == c->tracePrev) ++next;
     const GSlot &cur = c->gb[next], &prev = c->gb[c->last];
     a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material, cur.rec};
     a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material, prev.rec};
@@ -758,7 +810,8 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
         c->gb[c->last].recStale = false;
     }
     c->gb[next].recStale = false;  // this pass writes both
-    a.illum = c->illum;
+    const int set = c->passCount & 1;
+    a.illum = c->illumSet[set];
     a.motion = c->motion;
     const size_t n = (size_t)c->W * c->H;
     a.resCur = c->res + (size_t)(((it % 2) + 2) % 2) * n;
@@ -781,29 +834,53 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
             anySpecular |= c->blocks[b].triangles > 0 && !c->mats[b].emissive && !(c->mats[b].roughness > 0.00001f);
     a.segments = (c->diffuseBounce == 1 && !anySpecular) ? 1 : c->totalBounce;
     a.primaryOnly = (flags & VXPT_TRACE_PRIMARY_ONLY) ? 1 : 0;
-    a.wb = c->wb;
     a.tilesX = (c->W + 7) / 8;
     a.nSlots = a.tilesX * ((a.y1 - a.y0 + 7) / 8) * 64;
+    bool fresh;
+    if (int r = ensure_wave(c, set, (size_t)a.nSlots, fresh)) return r;
+    if (fresh) overlap = false;  // the first half must follow the new buffers' zero fill
+    a.wb = c->wb[set];
     a.numCU = c->numCU;
     a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
     a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
     a.resumeWgPerCU = getenv("VXPT_RESUME_WG") ? atoi(getenv("VXPT_RESUME_WG")) : 16;
+    a.sortMode = getenv("VXPT_SORT") ? atoi(getenv("VXPT_SORT")) : 0;
     a.prevSceneEmpty = c->prevSceneEmpty;
     // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
     a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;
     a.prevNumLights = (int)c->prevNumLights;
     a.lightRemap = c->lightRemap.p;
-    c->lightsDirty = 0;
+    // a primary-only pass runs no temporal reuse: the remap waits for the next full pass
+    if (!(flags & VXPT_TRACE_PRIMARY_ONLY)) c->lightsDirty = 0;
     a.tex = c->texTable.p;
     a.texels = c->texels.p;
     a.texEnabled = (c->texEnabled && c->texTable.p) ? 1 : 0;
     c->prevSceneEmpty = 0;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(c, launch_trace(a, c->stream, c->haloPending ? c->haloDone : nullptr));
+    if (a.primaryOnly) {
+        HIPCHK(c, launch_trace_front(a, c->stream));
+    } else {
+        // first half on frontStream: after the pass that last used this state set (overlap), or
+        // after everything on the context stream
+        if (overlap) {
+            HIPCHK(c, hipStreamWaitEvent(c->frontStream, c->backDone[set], 0));
+        } else {
+            HIPCHK(c, hipEventRecord(c->frontGate, c->stream));
+            HIPCHK(c, hipStreamWaitEvent(c->frontStream, c->frontGate, 0));
+        }
+        HIPCHK(c, launch_trace_front(a, c->frontStream));
+        HIPCHK(c, hipEventRecord(c->frontDone[set], c->frontStream));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[set], 0));
+        HIPCHK(c, launch_trace_back(a, c->stream, c->haloPending ? c->haloDone : nullptr));
+        HIPCHK(c, hipEventRecord(c->backDone[set], c->stream));
+    }
     c->haloPending = false;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     c->tracePrev = c->last;
     c->last = next;
+    c->illum = c->illumSet[set];
+    c->lastSet = set;
+    ++c->passCount;
     return 0;
 }
 
@@ -1108,7 +1185,7 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     }
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
-        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp));
+        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0));
         std::vector<std::pair<int, int>> br;
         for (int b : kGbufBufs) br.emplace_back(b, traceRows);
         br.emplace_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows);
@@ -1219,11 +1296,16 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     // the DDA's empty-box skip tables (box_tables.hpp; measured 7.56 -> 7.06 ms of trace per
     // C3 frame); VXPT_DDA_BOXES=0 walks with the empty-cube tables alone
     c->useBoxes = !(getenv("VXPT_DDA_BOXES") && atoi(getenv("VXPT_DDA_BOXES")) == 0);
+    if (getenv("VXPT_BOX_CAP")) c->boxCap = std::max(1, std::min(255, atoi(getenv("VXPT_BOX_CAP"))));
+    if (getenv("VXPT_BOX_CAP_UP")) c->boxCapUp = std::max(1, std::min(255, atoi(getenv("VXPT_BOX_CAP_UP"))));
     c->yamlPost = default_post();
     c->yamlDenoise = default_denoise();
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->frontStream, hipStreamNonBlocking));
+    for (hipEvent_t *e : {&c->frontDone[0], &c->frontDone[1], &c->backDone[0], &c->backDone[1], &c->frontGate})
+        HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(c, hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->dev));
     // timing markers only (every read of them follows a stream synchronisation): no system-scope
     // fence, so a marker neither writes back / invalidates the L2 nor delays the next kernel
@@ -1243,24 +1325,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         dalloc(c, c->ffCand, tiles16 * 256) || dalloc(c, c->ffCandCount, 1) ||
         dalloc(c, c->hfList, tiles16 * 256) || dalloc(c, c->hfCount, tiles16))
         return VXPT_ERR_HIP;
-    {   // wavefront trace state: one slot per pixel (8x8 tiles), 4 visibility rays per slot
-        const size_t ns = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64;
-        WaveBufs &w = c->wb;
-        if (dalloc(c, w.pPos, ns) || dalloc(c, w.pDir, ns) || dalloc(c, w.pThr, ns) || dalloc(c, w.pRad, ns) ||
-            dalloc(c, w.pMeta, ns) || dalloc(c, w.pBop, ns) || dalloc(c, w.cRayO, ns) || dalloc(c, w.cRayD, ns) ||
-            dalloc(c, w.cHit, ns) || dalloc(c, w.cT, ns) || dalloc(c, w.sPos, ns) || dalloc(c, w.sNrm, ns) ||
-            dalloc(c, w.sGeo, ns) || dalloc(c, w.sAlb, ns) || dalloc(c, w.sWo, ns) || dalloc(c, w.rSun, ns) ||
-            dalloc(c, w.rSky, ns) || dalloc(c, w.rRis, ns) || dalloc(c, w.rRR, ns) || dalloc(c, w.nIdx, ns) ||
-            dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
-            dalloc(c, w.oHit, 4 * ns) ||
-            dalloc(c, w.qO, 4 * ns) || dalloc(c, w.qD, 4 * ns) ||
-            dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, 64 + 3 * 16 * 8 * 16) ||
-            dalloc(c, w.sCell[0], 4 * ns + 2048) || dalloc(c, w.sT[0], 4 * ns + 2048) ||
-            dalloc(c, w.sFace[0], 4 * ns + 2048) || dalloc(c, w.sCell[1], 4 * ns + 2048) ||
-            dalloc(c, w.sT[1], 4 * ns + 2048) || dalloc(c, w.sFace[1], 4 * ns + 2048) ||
-            dalloc(c, w.sBack, ns) || dalloc(c, w.rLoc, ns) || dalloc(c, w.lLoc0, ns) || dalloc(c, w.lLoc1, ns))
-            return VXPT_ERR_HIP;
-    }
+    if (dalloc(c, c->illumSet[1], n)) return VXPT_ERR_HIP;
+    c->illumSet[0] = c->illum;
     // tables
     const std::string t = c->dataDir + "/tables/";
     std::vector<uint8_t> so, sc, rk, f0, f1, f2, f3;
@@ -1286,8 +1352,12 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
 void vxpt_destroy(vxpt_ctx *c) {
     if (!c) return;
     hipSetDevice(c->dev);
+    if (c->frontStream) hipStreamSynchronize(c->frontStream);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void *p : c->allocs) hipFree(p);
+    for (hipEvent_t e : {c->frontDone[0], c->frontDone[1], c->backDone[0], c->backDone[1], c->frontGate})
+        if (e) hipEventDestroy(e);
+    if (c->frontStream) hipStreamDestroy(c->frontStream);
     for (auto &e : c->ev)
         if (e) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -2322,7 +2392,7 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
     const int it0 = frameNum * spp;
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
-        int r = do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp);
+        int r = do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0);
         if (r) return r;
         if (s == 0) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     }
@@ -2778,10 +2848,10 @@ extern "C" int vxpt_probe_rays(vxpt_ctx *c, int n, const float *rays, int32_t *o
 
 extern "C" int vxpt_trace_counters(vxpt_ctx *c, uint32_t *out, int cap) {
     if (!c || !out || cap < 48) return VXPT_ERR_ARG;
-    if (!c->wb.qCount) return fail(c, VXPT_ERR_STATE, "no trace buffers");
+    if (!c->wb[c->lastSet].qCount) return fail(c, VXPT_ERR_STATE, "no trace buffers");
     HIPCHK(c, hipSetDevice(c->dev));
     std::vector<uint32_t> q(64 + 3 * 16 * 8 * 16);
-    HIPCHK(c, hipMemcpyAsync(q.data(), c->wb.qCount, q.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(q.data(), c->wb[c->lastSet].qCount, q.size() * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < 16; ++k) {
         out[3 * k] = q[k];

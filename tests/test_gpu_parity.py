@@ -328,6 +328,28 @@ def test_denoiser_history_fix_after_camera_move():
     r.close()
 
 
+@pytest.mark.parametrize("w,h", [(64, 160), (100, 62)])
+def test_overlapped_passes_equal_sequential_passes(w, h):
+    """vxpt_render_frame runs a pass's first half (camera rays .. RIS visibility) beside the previous
+    pass's second half (temporal reuse .. reservoir store) on a second stream; the frame equals the
+    same passes as separate vxpt_trace calls (no overlap) + vxpt_denoise, every buffer bit for bit."""
+    a, _ = _setup(w, h)
+    b, _ = _setup(w, h)
+    p, spp = _dn_params(), 4
+    try:
+        for f in range(3):
+            a.render_frame(f, spp, p)
+            for s in range(spp):
+                b.trace_flags(f * spp + s, 2 | (4 if s == 0 else 0) | (spp << 8))  # ACCUMULATE | ACCUM_FIRST
+            b.denoise(f, f * spp + spp, p)
+            for name in ("ILLUM", "DEPTH", "NORMAL_ROUGH", "TAP_RECORD", "RES_EVEN", "RES_ODD", "OUTPUT"):
+                np.testing.assert_array_equal(a.read(name).view(np.uint8), b.read(name).view(np.uint8),
+                                              err_msg="frame %d %s" % (f, name))
+    finally:
+        a.close()
+        b.close()
+
+
 def test_render_frame_spp4_properties(pair):
     r, _ = pair
     r.render_frame(0, 1, _dn_params())

@@ -35,7 +35,7 @@ def main():
     r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
     r.set_sky()
     p = vxpt.DenoiseParams.defaults()
-    buf = np.zeros(64, np.uint64)
+    buf = np.zeros(192, np.uint64)
     for f in range(4):
         r.render_frame(f, 4, p)
     r.sync()
@@ -55,6 +55,14 @@ def main():
               "per ray: skip64 %.2f skip16 %.2f skip4 %.2f brick %.2f cellsteps %.2f" % (
                   name, rays / 16.0, rays / waves, its / rays, mx / waves, its / (64.0 * mx),
                   lv[0] / rays, lv[1] / rays, lv[2] / rays, lv[3] / rays, g[7] / rays))
+    print("per-ray iterations in the launch (bins [0,2) [2,4) [4,8) .. [128,inf)), up = d.y > 0, event = hit/occluded")
+    for k, name in KINDS.items():
+        g = [int(v) for v in buf[64 + 16 * k:64 + 16 * k + 16]]
+        n = sum(g[:8])
+        if n == 0:
+            continue
+        print("%-24s %s up %.3f event %.3f max %d" % (name, " ".join("%.4f" % (v / n) for v in g[:8]), g[8] / n,
+                                                       g[9] / n, g[10]))
     print("timings", r.timings())
 
 

@@ -4,13 +4,15 @@ Usage: python tools/valu_util.py SQ_DB KT_DB [OUT_JSON]
   SQ_DB: a --pmc run with SQ_INSTS_VALU (and, where the device has it, SQ_THREAD_CYCLES_VALU /
   SQ_ACTIVE_INST_VALU) of `bench.py --warmup W --steps S --no-cpu-baseline`; KT_DB: a --kernel-trace
   run of the same command (kernel durations).
-issue util = SQ_INSTS_VALU x 4 cycles (a wave64 VALU op occupies a 16-lane SIMD for 4 cycles)
-             / (kernel duration x 2.4 GHz x 1024 SIMDs)   -- the share of the chip's VALU issue slots used
-lane util  = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU x 4)  -- active lanes per issued op
-             (divergence), when both counters were collected.
+issue util = SQ_INSTS_VALU x 2 cycles (gfx950: a wave64 VALU op issues over 2 cycles on a SIMD-32;
+             MI355X_MICROARCH.md constants table) / (kernel duration x 2.4 GHz x 1024 SIMDs)
+             -- the share of the chip's VALU issue slots used
+lane util  = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)  -- active lanes per issued op
+             (divergence), when both counters were collected (both count in the same unit).
 """
 import collections
 import json
+import re
 import sqlite3
 import sys
 
@@ -20,9 +22,17 @@ TRACE = ["k_closest", "k_shade", "k_nee", "k_restir", "k_finish", "k_queue<true>
 
 
 def short(n):
+    """Kernel name without namespace and walk-table template argument: k_queue<true, true> and
+    k_queue<true, false> -> k_queue<true>, k_closest<true> -> k_closest, k_shade<false> -> k_shade
+    (k_shade<true>, the instanced-mesh variant -> k_shade<mesh>)."""
     n = n.replace("vx::(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
-    # the default (cube-table) walks: k_queue<true, false> -> k_queue<true>, k_closest<false> -> k_closest
-    return n.replace(", false>", ">").replace("k_closest<false>", "k_closest")
+    m = re.match(r"(k_queue|k_resume)<(true|false), (true|false)>", n)
+    if m:
+        return "%s<%s>" % (m.group(1), m.group(2))
+    m = re.match(r"(k_closest|k_shade|k_nee|k_restir)<(true|false)>", n)
+    if m:
+        return m.group(1) if (m.group(1) == "k_closest" or m.group(2) == "false") else m.group(1) + "<mesh>"
+    return n
 
 
 def main():
@@ -42,14 +52,17 @@ def main():
         t = sum(dur[k]) / len(dur[k]) * 1e-9
         row = {"avg_us": round(t * 1e6, 2), "valu_insts": c.get("SQ_INSTS_VALU")}
         if c.get("SQ_INSTS_VALU"):
-            row["issue_util"] = round(c["SQ_INSTS_VALU"] * 4 / (t * CLOCK_HZ * SIMDS), 4)
+            row["issue_util"] = round(c["SQ_INSTS_VALU"] * 2 / (t * CLOCK_HZ * SIMDS), 4)
         if c.get("SQ_THREAD_CYCLES_VALU") and c.get("SQ_ACTIVE_INST_VALU"):
-            row["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64 * 4 * c["SQ_ACTIVE_INST_VALU"]), 4)
+            row["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"]), 4)
         out[k] = row
     tot_t = sum(r["avg_us"] for r in out.values())
+    lanes = [r for r in out.values() if "lane_util" in r]
+    lane_agg = (sum(r["lane_util"] * r["avg_us"] for r in lanes) / sum(r["avg_us"] for r in lanes)) if lanes else None
     agg = sum(r.get("issue_util", 0) * r["avg_us"] for r in out.values()) / max(tot_t, 1e-9)
-    res = {"trace_valu_util": round(agg, 4), "kernels": out,
-           "note": "issue util = SQ_INSTS_VALU x 4 / (duration x 2.4 GHz x 1024 SIMDs), time-weighted over the trace kernels"}
+    res = {"trace_valu_util": round(agg, 4), "trace_valu_lane_util": round(lane_agg, 4) if lane_agg else None,
+           "kernels": out,
+           "note": "issue util = SQ_INSTS_VALU x 2 cycles / (duration x 2.4 GHz x 1024 SIMDs), time-weighted over the trace kernels; lane util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)"}
     print(json.dumps(res, indent=1))
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as f:
