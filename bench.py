@@ -154,7 +154,6 @@ def main():
     r.set_sky()
     params = vxpt.DenoiseParams.defaults()
     band = None
-    replicas = None
     if world > 1:
         # the library renders this rank's band and enqueues the halo exchanges itself
         # (RCCL over xGMI on the context stream); the host only hands out the unique id
@@ -168,11 +167,14 @@ def main():
         errs = [None] * world
         dist.all_gather_object(errs, err)
         if any(errs):
-            # no band communicator on some rank: every rank renders whole frames (labelled replicas)
-            replicas = next(e for e in errs if e)
-            print("band exchange unavailable, running replicas: %s" % replicas, file=sys.stderr, flush=True)
-        else:
-            band = bands.band_rows(a.height, world, rank)
+            # no band communicator on some rank: no banded frame can be rendered, and N independent
+            # whole frames would not be the banded workload -- fail instead of reporting them
+            bad = next(e for e in errs if e)
+            print("band exchange unavailable (vxpt_band_comm_init): %s" % bad, file=sys.stderr, flush=True)
+            r.close()
+            dist.destroy_process_group()
+            sys.exit(3)
+        band = bands.band_rows(a.height, world, rank)
 
     def step(frame):
         if a.primary_only:
@@ -213,8 +215,8 @@ def main():
         band_px = a.width * (band[1] - band[0])
     spp = 1 if a.primary_only else a.spp
     paths = a.width * a.height * spp
-    # single GPU / bands: the whole frame's paths per step; replicas: one frame per rank
-    value = paths * (world if replicas else 1) * a.steps / elapsed / 1e6
+    # single GPU / bands: the whole frame's paths per step
+    value = paths * a.steps / elapsed / 1e6
     avg_trace = sum(trace_ms) / len(trace_ms)
     avg_dn = sum(denoise_ms) / len(denoise_ms)
     if a.primary_only:
@@ -269,7 +271,7 @@ def main():
             "metric": "Mpaths/s @1080p 4spp (+ms/frame, denoiser HBM GB/s vs roofline)",
             "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "strong" if (world > 1 and not replicas) else "weak",
+            "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C2: %dx%d primary-only DDA + sky + G-buffer" % (a.width, a.height) if
                        a.primary_only else "C3: %dx%d, %d spp full path + ReLAX denoiser" % (a.width, a.height, a.spp),
@@ -278,8 +280,7 @@ def main():
                            a.bounce_limits + ((" (the reference's RayGen.cu:146-147 limits)",) if a.bounce_limits == (3, 1)
                                               else (" (BASELINE.json's '4 bounces' reading; the reference renders 3/1)",)
                                               if a.bounce_limits == (4, 4) else ("",))),
-                       "parallelism": ("replicas%d (band exchange unavailable: %s)" % (world, replicas[:120]) if replicas
-                                       else ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU")},
+                       "parallelism": ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,

@@ -341,3 +341,54 @@ def test_oracle_bands_follow_a_turning_camera():
         np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32), err_msg="frame %d" % f)
     static = _oracle_turning(turns, False)
     assert any(not np.array_equal(out.view(np.uint32), ref.view(np.uint32)) for ref, out, _ in static)
+
+
+@pytest.mark.gpu
+def test_gpu_c4_eight_bands_4k_c3_world():
+    """BASELINE config C4's workload on one device: 3840x2160, 4 spp, the C3 256^3 world and camera
+    (bench.py's scene), split into 8 linked bands of 272 rows (8-row aligned; the last 256) -- the
+    schedule vxpt_band_comm_init runs over RCCL, with device copies as the transport.  After each
+    of 3 frames the gathered denoiser output and post-processed frame (vxpt_band_gather_linked into
+    band 0) equal one context's render bit for bit.  Footprint: 9 contexts with full-frame 4K planes
+    (~6 GB each) + wavefront state for their rows (two sets) -- ~75 GB of the device's 288."""
+    import vxpt
+    from bench import C1_DIR, scene_args
+
+    class A:
+        world = 256
+
+    chunks, hs, fd, pos = scene_args(A)
+    w, h, spp, n = 3840, 2160, 4, 8
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
+        r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    single = make()
+    rs = [make() for _ in range(n)]
+    try:
+        linked = vxpt.LinkedBands(rs)
+        rows = [bands.band_rows(h, n, k) for k in range(n)]
+        assert rows[0] == (0, 272) and rows[-1] == (1904, 2160)
+        pp = single.post_params()
+        for f in range(3):
+            single.render_frame(f, spp, p)
+            linked.render_frame(f, spp, p)
+            single.postprocess(pp, 16.0)
+            linked.postprocess(pp, 16.0)
+            for name in ("OUTPUT", "FRAME"):
+                linked.gather(name, 0)
+                got, ref = rs[0].read(name), single.read(name)
+                assert np.isfinite(ref).all()
+                np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32), err_msg="frame %d %s" % (f, name))
+        hit = (single.read("DEPTH") < 1e26).mean()
+        assert 0.5 < hit < 0.9, hit  # the C3 camera sees terrain and sky
+    finally:
+        single.close()
+        for r in rs:
+            r.close()
