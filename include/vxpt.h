@@ -59,9 +59,11 @@ enum vxpt_buffer {
     VXPT_BUF_LIGHTS = 44,        /* nLights x 32 B LightInfo (Light.h:13-23)                     */
     VXPT_BUF_LIGHT_ALIAS = 45,   /* nLights x {f32 q, f32 p, i32 alias} (AliasTable.h bins)      */
     VXPT_BUF_BLOOM = 46,         /* post-process: the horizontally blurred bloom, Float4 per pixel */
-    VXPT_BUF_TAP_RECORD = 47     /* read-only: the last pass's ReSTIR tap records, 32 B per pixel (normal xyz,
+    VXPT_BUF_TAP_RECORD = 47,    /* read-only: the last pass's ReSTIR tap records, 32 B per pixel (normal xyz,
                                   * roughness with the metallic flag in its sign bit; albedo xyz, depth) --
                                   * the G-buffer planes GetPrevSurface reads (Restir.h:348-381), packed */
+    VXPT_BUF_BOX_TABLES = 48     /* read-only: 8 x nBricks u32, the walk's empty-box extents per brick and ray
+                                  * octant (x | y << 8 | z << 16 bricks; 0 = occupied), box_tables.hpp */
 };
 
 typedef struct vxpt_config {

@@ -568,6 +568,7 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_BLOOM: p = c->bloomB; bytes = n * 16; return c->bloomB != nullptr;
         case VXPT_BUF_LIGHTS: p = c->lights.p; bytes = (size_t)c->nLights * sizeof(LightInfo); return !forWrite && c->nLights;
         case VXPT_BUF_TAP_RECORD: p = g.rec; bytes = n * 32; return !forWrite;
+        case VXPT_BUF_BOX_TABLES: p = c->bbox.p; bytes = (size_t)8 * c->nBricks * 4; return !forWrite && c->bbox.p;
         case VXPT_BUF_LIGHT_ALIAS:
             p = c->lightAlias.p; bytes = (size_t)c->nLights * sizeof(AliasBin); return !forWrite && c->nLights;
         default: return false;

@@ -24,7 +24,7 @@ BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERI
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
            PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38,
            OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42, TEXELS=43, LIGHTS=44,
-           LIGHT_ALIAS=45, BLOOM=46, TAP_RECORD=47)
+           LIGHT_ALIAS=45, BLOOM=46, TAP_RECORD=47, BOX_TABLES=48)
 FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
@@ -503,9 +503,10 @@ class Renderer:
             return np.zeros(cx * cy * cz * 32768, np.uint8)
         if which == BUF["TEXELS"]:
             return np.zeros((self.texture_table()[1], 4), np.uint8)
-        if which in (BUF["OCTANT_TABLES"], BUF["CELL_MASKS"], BUF["BRICK_IDS"], BUF["MACRO_MASKS"]):
+        if which in (BUF["OCTANT_TABLES"], BUF["CELL_MASKS"], BUF["BRICK_IDS"], BUF["MACRO_MASKS"], BUF["BOX_TABLES"]):
             nb = int(np.prod(self.chunks)) * 512
             return {BUF["OCTANT_TABLES"]: np.zeros(8 * nb, np.uint8), BUF["CELL_MASKS"]: np.zeros(nb, np.uint64),
+                    BUF["BOX_TABLES"]: np.zeros(8 * nb, np.uint32),
                     BUF["BRICK_IDS"]: np.zeros(nb * 64, np.uint8),
                     BUF["MACRO_MASKS"]: np.zeros(nb // 64, np.uint64)}[which]
         if which in FLOAT1_BUFS:

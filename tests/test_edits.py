@@ -88,7 +88,9 @@ def _random_edits(r, ids, n, seed):
     ids[_idx(40, 30, 9)] = 5
 
 
-STRUCTS = ("VOXELS", "OCTANT_TABLES", "CELL_MASKS", "BRICK_IDS", "MACRO_MASKS")
+# BOX_TABLES: set_block recomputes the empty boxes behind an edited brick (vxpt_host.cpp set_block ->
+# box_fill over the bricks whose octant box could reach it); a stale box would skip a placed block
+STRUCTS = ("VOXELS", "OCTANT_TABLES", "CELL_MASKS", "BRICK_IDS", "MACRO_MASKS", "BOX_TABLES")
 
 
 @pytest.mark.gpu

@@ -1,10 +1,12 @@
 """Instanced meshes in the path tracer (the rendering half), GPU vs oracle.
 
 The C1 world with lanterns (emissive light mesh + its base, blocks 16 / 15) and leaves (thin-film
-mesh, block 14) placed on the terrain in front of the C1 camera.  The meshes are the synthetic OBJ
-files of test_lights (the reference's assets are not shipped); the materials are the repo's
-data/assets materials.yaml entries, read here independently of the library (MaterialManager.cpp:
-150-190: materialId = the material's index, an emissive material's albedo is its radiance).
+mesh, block 14) placed on the terrain in front of the C1 camera.  Two mesh sets: the reference's own
+meshes (data/models/lanternLight.obj 8 faces, lanternBase.obj 100, leavesCube4.obj 1,960 with
+bounds -0.05..1.07 overhanging its cell; committed as data fixtures under tests/golden/models) and
+the synthetic OBJ files of test_lights.  The materials are the repo's data/assets materials.yaml
+entries, read here independently of the library (MaterialManager.cpp:150-190: materialId = the
+material's index, an emissive material's albedo is its radiance).
 
 Covered against oracle/orc_mesh.cpp + orc_trace.cpp over 4 frames of trace + denoise:
   closest hit = min(voxel DDA, mesh BVH walk) with back faces culled, ties to the voxel face;
@@ -18,6 +20,7 @@ Covered against oracle/orc_mesh.cpp + orc_trace.cpp over 4 frames of trace + den
   the light-id remap across lantern edits (VoxelEngine.cu:503-633, 1192-1284; Restir.h:48-79).
 """
 import os
+import shutil
 
 import numpy as np
 import pytest
@@ -83,12 +86,19 @@ def place_meshes(ids):
     return placed
 
 
-@pytest.fixture
-def mesh_scene(tmp_path):
+GOLDEN_MODELS = os.path.join(REPO, "tests", "golden", "models")
+
+
+@pytest.fixture(params=["reference", "synthetic"])
+def mesh_scene(tmp_path, request):
     os.makedirs(tmp_path / "models")
-    _prism_obj(str(tmp_path / "models" / "lanternLight.obj"))
-    _base_obj(str(tmp_path / "models" / "lanternBase.obj"))
-    _random_mesh_obj(str(tmp_path / "models" / "leavesCube4.obj"), n=120)
+    if request.param == "reference":  # ModelManager.cpp:172-226 loads these from data/models
+        for f in ("lanternLight.obj", "lanternBase.obj", "leavesCube4.obj"):
+            shutil.copy(os.path.join(GOLDEN_MODELS, f), tmp_path / "models" / f)
+    else:
+        _prism_obj(str(tmp_path / "models" / "lanternLight.obj"))
+        _base_obj(str(tmp_path / "models" / "lanternBase.obj"))
+        _random_mesh_obj(str(tmp_path / "models" / "leavesCube4.obj"), n=120)
     w, h = 128, 96
     r = vxpt.Renderer(w, h)
     r.load_settings()

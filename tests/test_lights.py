@@ -12,6 +12,7 @@ known answers (IEEE f16 rounding against numpy, octahedral encodings of the axes
 Bit-exact: instance rows, light records, weights and alias bins.
 """
 import os
+import shutil
 
 import numpy as np
 import pytest
@@ -394,13 +395,16 @@ def mesh_walk_driver(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("deep", [False, True])
-def test_library_mesh_walk_on_host_equals_brute_force(mesh_walk_driver, tmp_path, deep):
+@pytest.mark.parametrize("meshes", ["synthetic", "deep", "reference"])
+def test_library_mesh_walk_on_host_equals_brute_force(mesh_walk_driver, tmp_path, meshes):
     """The library's two-level BVH (bvh_build.hpp) and its walk (vx_mesh.hpp: (node, entry distance)
     stack entries, one stack for both levels), run on the host by a driver, equal the oracle's
     brute-force loop over every instance and triangle bit for bit: closest hits with and without
     back-face culling (t, barycentrics, instance row, triangle) and the any-hit answer -- with the
-    regular meshes and with a BLAS at the builder's depth limit."""
+    synthetic meshes, with a BLAS at the builder's depth limit, and with the reference's own meshes
+    (tests/golden/models: lanternLight 8, lanternBase 100, leavesCube4 1,960 triangles overhanging
+    the cell)."""
+    deep = meshes == "deep"
     import subprocess
     o = oracle.Oracle(8, 8)
     o.terrain(CH, 32.0)
@@ -413,11 +417,18 @@ def test_library_mesh_walk_on_host_equals_brute_force(mesh_walk_driver, tmp_path
         ids[_idx(*c)] = (14, 14, 14, 14, 16, 15)[k % 6]
     rows = oracle.collect_instances(ids, CH, BLOCKS)
     leaves = _deep_mesh_triangles() if deep else None
-    if not deep:
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "models")
+    if meshes == "reference":
+        for src, dst in (("leavesCube4.obj", "leaves.obj"), ("lanternLight.obj", "light.obj"),
+                         ("lanternBase.obj", "base.obj")):
+            shutil.copy(os.path.join(golden, src), tmp_path / dst)
+        leaves = oracle.parse_obj(str(tmp_path / "leaves.obj"))[0]
+    elif not deep:
         _random_mesh_obj(str(tmp_path / "leaves.obj"))
         leaves = oracle.parse_obj(str(tmp_path / "leaves.obj"))[0]
-    _prism_obj(str(tmp_path / "light.obj"))
-    _base_obj(str(tmp_path / "base.obj"))
+    if meshes != "reference":
+        _prism_obj(str(tmp_path / "light.obj"))
+        _base_obj(str(tmp_path / "base.obj"))
     models = {14: np.asarray(leaves, np.float32).reshape(-1, 3, 3),
               15: oracle.parse_obj(str(tmp_path / "base.obj"))[0], 16: oracle.parse_obj(str(tmp_path / "light.obj"))[0]}
     with open(tmp_path / "meshes.bin", "wb") as f:
