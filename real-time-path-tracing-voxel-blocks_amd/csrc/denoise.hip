@@ -744,15 +744,17 @@ VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V
 // ---------------------------------------------------------------- HC
 // The 5x5 neighbourhood of the 16x16 tile (20x20 with edge clamp) is staged
 // once in LDS: YCoCg of the fast history and the noisy radiance.
-__global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
+template <int TS>
+__global__ __launch_bounds__(TS * TS) void k_history_clamp(DenoiseArgs a) {
+    constexpr int T = TS + 4, N = T * T;
     const int W = a.W, H = a.H;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int tx = threadIdx.x % TS, ty = threadIdx.x / TS;
     const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
-    const int x0 = btx * 16, y0 = a.y0 + bty * 16;
+    const int x0 = btx * TS, y0 = a.y0 + bty * TS;
     const int x = x0 + tx, y = y0 + ty;
-    __shared__ float sY[3][400], sR[3][400];
-    for (int k = threadIdx.x; k < 400; k += 256) {
-        const int gx = cl(x0 + k % 20 - 2, W), gy = cl(y0 + k / 20 - 2, H);
+    __shared__ float sY[3][N], sR[3][N];
+    for (int k = threadIdx.x; k < N; k += TS * TS) {
+        const int gx = cl(x0 + k % T - 2, W), gy = cl(y0 + k / T - 2, H);
         const size_t j = (size_t)gy * W + gx;
         const V3 yc = rgb_to_ycocg(f4(a.pong[j]).xyz());
         const float4 n = a.illum[j];
@@ -774,7 +776,7 @@ __global__ __launch_bounds__(256) void k_history_clamp(DenoiseArgs a) {
     for (int dx = -2; dx <= 2; ++dx)
 #pragma unroll
         for (int dy = -2; dy <= 2; ++dy) {
-            const int k = (ty + 2 + dy) * 20 + (tx + 2 + dx);
+            const int k = (ty + 2 + dy) * T + (tx + 2 + dx);
             const V3 s(sY[0][k], sY[1][k], sY[2][k]);
             m1 += s;
             m2 += s * s;
@@ -812,16 +814,18 @@ VX_HD void history_clamp_host(const DenoiseArgs &a, int x, int y) {
 // The 16x16 tile's 5x5 neighbourhood (20x20, edge-clamped) of the history,
 // normals, material ids and world positions is staged in LDS (AtrousSmem.h
 // stages the same tile in shared memory).
-__global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
+template <int TS>
+__global__ __launch_bounds__(TS * TS) void k_atrous_smem(DenoiseArgs a) {
+    constexpr int T = TS + 4, N = T * T;
     const int W = a.W, H = a.H;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int tx = threadIdx.x % TS, ty = threadIdx.x / TS;
     const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
-    const int x0 = btx * 16, y0 = a.y0 + bty * 16;
+    const int x0 = btx * TS, y0 = a.y0 + bty * TS;
     const int x = x0 + tx, y = y0 + ty;
-    __shared__ float4 sI[400];
-    __shared__ float sNx[400], sNy[400], sNz[400], sM[400], sPx[400], sPy[400], sPz[400];
-    for (int k = threadIdx.x; k < 400; k += 256) {
-        const int gx = cl(x0 + k % 20 - 2, W), gy = cl(y0 + k / 20 - 2, H);
+    __shared__ float4 sI[N];
+    __shared__ float sNx[N], sNy[N], sNz[N], sM[N], sPx[N], sPy[N], sPz[N];
+    for (int k = threadIdx.x; k < N; k += TS * TS) {
+        const int gx = cl(x0 + k % T - 2, W), gy = cl(y0 + k / T - 2, H);
         const size_t j = (size_t)gy * W + gx;
         sI[k] = a.prevIllum[j];
         const float4 n = a.normalRough[j], p = a.wpos[j];
@@ -835,7 +839,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
     const float z = a.depth[i];
     if (z > 500000.0f) return;
     // the centre's normal, position and material come from the staged tile
-    const int kc = (ty + 2) * 20 + tx + 2;
+    const int kc = (ty + 2) * T + tx + 2;
     const V3 cN(sNx[kc], sNy[kc], sNz[kc]);
     const V3 cWP(sPx[kc], sPy[kc], sPz[kc]);
     const float cMat = sM[kc];
@@ -846,7 +850,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
         const float kern[4] = {1.0f / 4.0f, 1.0f / 8.0f, 1.0f / 8.0f, 1.0f / 16.0f};
         for (int dx = -1; dx <= 1; ++dx)
             for (int dy = -1; dy <= 1; ++dy)
-                vs += f4(sI[(ty + 2 + dy) * 20 + tx + 2 + dx]) * kern[abs(dx) * 2 + abs(dy)];
+                vs += f4(sI[(ty + 2 + dy) * T + tx + 2 + dx]) * kern[abs(dx) * 2 + abs(dy)];
         const float vm1 = luminance(vs.xyz());
         const float var = fmaxf(0.0f, vs.w - vm1 * vm1);
         const float cLum = luminance_fast(f4(sI[kc]).xyz());
@@ -863,7 +867,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
                 const bool isC = cx == 0 && cy == 0;
                 const bool inside = px >= 0 && py >= 0 && px < W && py < H;
                 const float kernel = inside ? k3[abs(cx)] * k3[abs(cy)] : 0.0f;
-                const int k = (ty + 2 + cy) * 20 + tx + 2 + cx;  // = edge-clamped (px, py)
+                const int k = (ty + 2 + cy) * T + tx + 2 + cx;  // = edge-clamped (px, py)
                 const V3 sN(sNx[k], sNy[k], sNz[k]);
                 const V3 sWP(sPx[k], sPy[k], sPz[k]);
                 const float sMat = sM[k];
@@ -888,7 +892,7 @@ __global__ __launch_bounds__(256) void k_atrous_smem(DenoiseArgs a) {
 #pragma unroll 1
         for (int cx = -2; cx <= 2; ++cx)
             for (int cy = -2; cy <= 2; ++cy) {
-                const int k = (ty + 2 + cy) * 20 + tx + 2 + cx;
+                const int k = (ty + 2 + cy) * T + tx + 2 + cx;
                 const V3 sN(sNx[k], sNy[k], sNz[k]);
                 const float nw = nonexp_w(acos_approx_fast(dot_fast(cN, sN)), nwp);
                 const V4 smp = f4(sI[k]);
@@ -1114,12 +1118,22 @@ hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_history_fix, grid16(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
+// tile edge of the LDS-staged 5x5 stencils (history clamping, the first a-trous): 32 stages the
+// 2-pixel apron at 1.27x the tile's pixels instead of 1.56x (both kernels run at the HBM's rate on
+// their fetched bytes)
+inline int stencil_tile() {
+    static const int ts = getenv("VXPT_STENCIL_TILE") ? atoi(getenv("VXPT_STENCIL_TILE")) : 16;
+    return ts;
+}
+inline dim3 grid_ts(const DenoiseArgs &a, int ts) { return dim3((a.W + ts - 1) / ts, (a.y1 - a.y0 + ts - 1) / ts); }
 hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_history_clamp, grid16(a), dim3(256), 0, st, a);
+    if (stencil_tile() == 32) hipLaunchKernelGGL(k_history_clamp<32>, grid_ts(a, 32), dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL(k_history_clamp<16>, grid16(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_atrous_smem, grid16(a), dim3(256), 0, st, a);
+    if (stencil_tile() == 32) hipLaunchKernelGGL(k_atrous_smem<32>, grid_ts(a, 32), dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL(k_atrous_smem<16>, grid16(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex,

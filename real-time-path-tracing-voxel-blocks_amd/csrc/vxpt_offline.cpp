@@ -8,7 +8,9 @@
 // as <prefix>_%04d.png with the 0-indexed frame number, the canonical gate compares frame
 // totalFrames-1 and writes <prefix>_diff.png.  Additions: --spp (samples per pixel per frame,
 // the reference traces 1), --chunks X Y Z (world size, default the reference's 2 1 2), --device,
-// --data (the data directory), --perf-report (the reference writes ../../data/perf/...).
+// --data (the data directory), --perf-report (the run summary file; default <data>/perf/
+// performance_report.txt, the reference's data/perf/performance_report.txt), and a per-frame CSV
+// <prefix>_frames.csv of the library's timings.
 // The scripted voxel-edit sequences (--test-sequence, --test-remove20, --test-remove-circle) follow
 // the reference's timing: a click set after frame N is picked at frame N+1 against the world as
 // edited so far (VoxelEngine::update, VoxelEngine.cu:906-975) and the geometry changes at frame
@@ -22,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <filesystem>
 #include <fstream>
 #include <future>
@@ -73,7 +76,8 @@ void usage(const char *argv0) {
               << "  --device <int>         HIP device (default: 0)\n"
               << "  --data <dir>           Data directory: settings/, assets/, tables/ (default: data)\n"
               << "  --models <dir>         Root of the instanced meshes' OBJ files (<dir>/models/*.obj; default: the data directory)\n"
-              << "  --perf-report <file>   Performance report path (default: <output>_performance_report.txt)\n"
+              << "  --perf-report <file>   Performance report the run summary is appended to\n"
+              << "                         (default: <data>/perf/performance_report.txt)\n"
               << "  --no-textures          Untextured materials (textures load from <data>/textures when present)\n"
               << "  --help, -h             Show this help message\n";
 }
@@ -133,7 +137,7 @@ int parse(int argc, char **argv, Options &o) {
         std::cerr << "frames, spp and chunks must be positive\n";
         return -1;
     }
-    if (o.perfReport.empty()) o.perfReport = o.outputPrefix + "_performance_report.txt";
+    if (o.perfReport.empty()) o.perfReport = o.dataDir + "/perf/performance_report.txt";
     return 1;
 }
 
@@ -154,7 +158,64 @@ struct FrameRecord {  // PerformanceTracker's per-frame row, from the library's 
     vxpt_timing t;
     double postMs, wallMs;
     float dtMs;
+    double updateMs;  // the frame's voxel-engine update on the host (clicks, picks, block edits)
 };
+
+// PerformanceTracker's timestamp format (PerformanceTracker.h: "%Y-%m-%d %H:%M:%S.mmm", local time)
+std::string timestamp_now() {
+    const auto now = std::chrono::system_clock::now();
+    const std::time_t tt = std::chrono::system_clock::to_time_t(now);
+    const long ms = (long)(std::chrono::duration_cast<std::chrono::milliseconds>(now.time_since_epoch()).count() % 1000);
+    std::tm tmv{};
+    localtime_r(&tt, &tmv);
+    std::ostringstream ss;
+    ss << std::put_time(&tmv, "%Y-%m-%d %H:%M:%S") << '.' << std::setfill('0') << std::setw(3) << ms;
+    return ss.str();
+}
+
+// PerformanceTracker::saveReport (PerformanceTracker.h:98-183): one run-summary line appended to the
+// report, the header first when the file is new; columns are per-frame averages in ms.  Here
+// PathTrace and Denoiser are the library's HIP-event times (the reference's are CPU launch times),
+// ScenePrep is 0 (the sky is built once by vxpt_set_sky, before the loop), RendererUpd the host's
+// voxel-engine update.
+bool append_run_summary(const std::string &path, const std::string &stamp, int w, int h,
+                        const std::vector<FrameRecord> &perf, const std::string &comment) {
+    if (perf.empty()) return true;
+    const std::filesystem::path fp(path);
+    std::error_code ec;
+    if (fp.has_parent_path()) std::filesystem::create_directories(fp.parent_path(), ec);
+    std::ofstream f(path, std::ios::app);
+    if (!f) return false;
+    f.seekp(0, std::ios::end);
+    if (f.tellp() == 0)
+        f << "# Performance Report - Real-time Path Tracing Voxel Renderer (Run Summary)\n"
+          << "# Format: Timestamp         | Frames | Resolution | WholeFrame | StdDev | ScenePrep | RendererUpd | "
+             "PathTrace | Denoiser | PostProc | Comment\n"
+          << "# ==========================================================================================="
+             "====================================\n";
+    double whole = 0, upd = 0, trace = 0, den = 0, post = 0;
+    for (const auto &r : perf) {
+        whole += r.wallMs; upd += r.updateMs; trace += r.t.trace_ms; den += r.t.denoise_ms; post += r.postMs;
+    }
+    const double n = (double)perf.size();
+    whole /= n; upd /= n; trace /= n; den /= n; post /= n;
+    double var = 0;
+    for (const auto &r : perf) var += (r.wallMs - whole) * (r.wallMs - whole);
+    const double sd = std::sqrt(var / n);
+    f << std::fixed << std::setprecision(2);
+    f << std::setw(19) << std::left << stamp << " | ";
+    f << std::setw(6) << std::right << perf.size() << " | ";
+    f << std::setw(10) << std::left << (std::to_string(w) + "x" + std::to_string(h)) << " | ";
+    f << std::setw(10) << std::right << whole << " | ";
+    f << std::setw(6) << std::right << sd << " | ";
+    f << std::setw(9) << std::right << 0.0 << " | ";
+    f << std::setw(11) << std::right << upd << " | ";
+    f << std::setw(9) << std::right << trace << " | ";
+    f << std::setw(8) << std::right << den << " | ";
+    f << std::setw(8) << std::right << post << " | ";
+    f << comment << std::endl;
+    return (bool)f;
+}
 
 void print_diff(const vxpt_image_diff_result &r) {  // ImageDiffResult::print (ImageDiff.cpp)
     std::cout << "=== Image Comparison Results ===\n"
@@ -261,6 +322,7 @@ int main(int argc, char **argv) {
 
     std::vector<BatchedFrame> batch;
     std::vector<FrameRecord> perf;
+    std::string runStamp;
     const size_t frameBytes = (size_t)o.width * o.height * 4 * sizeof(float);
 
     for (int frame = 0; frame < o.totalFrames; frame++) {  // mainOffline.cpp:273-408
@@ -270,6 +332,7 @@ int main(int argc, char **argv) {
         last = t0;
         const bool shouldSave =
             std::find(o.savedFrames.begin(), o.savedFrames.end(), frameNumber) != o.savedFrames.end();
+        if (frame == 0) runStamp = timestamp_now();  // PerformanceTracker::beginFrame of the first frame
 
         // the edit picked last frame reaches the geometry now
         if (editPending) {
@@ -324,6 +387,7 @@ int main(int argc, char **argv) {
                           << edit[1] << "," << edit[2] << ")" << std::endl;
         }
 
+        const double updateMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (vxpt_render_frame(ctx, &dp, frame, o.spp) != VXPT_OK) return fail("rendering");
         const auto tp = std::chrono::steady_clock::now();
         if (vxpt_postprocess(ctx, &pp, dtMs) != VXPT_OK) return fail("post-processing");
@@ -341,7 +405,7 @@ int main(int argc, char **argv) {
                         (shouldSave ? "Saved frame " : "Convergence frame ") + std::to_string(frameNumber) + "/" +
                             std::to_string(o.totalFrames),
                         {}, std::chrono::duration<double, std::milli>(t1 - tp).count(),
-                        std::chrono::duration<double, std::milli>(t1 - t0).count(), dtMs};
+                        std::chrono::duration<double, std::milli>(t1 - t0).count(), dtMs, updateMs};
         vxpt_timings(ctx, &rec.t);
         perf.push_back(rec);
         // the clicks the reference scripts after a frame (mainOffline.cpp:346-395)
@@ -381,8 +445,9 @@ int main(int argc, char **argv) {
     }
     std::cout << "Output files saved with prefix: " << o.outputPrefix << std::endl;
 
-    {  // PerformanceTracker::saveReport
-        std::ofstream rep(o.perfReport);
+    {  // PerformanceTracker::saveReport: the run summary, and the per-frame rows as a CSV
+        const std::string csv = o.outputPrefix + "_frames.csv";
+        std::ofstream rep(csv);
         rep << "# " << o.runComment << "\n# " << o.width << "x" << o.height << ", " << o.spp << " spp\n"
             << "frame,trace_ms,denoise_ms,sky_ms,frame_ms,post_ms,wall_ms,dt_ms,comment\n";
         double sumTrace = 0, sumDen = 0, sumWall = 0;
@@ -395,9 +460,12 @@ int main(int argc, char **argv) {
             sumWall += r.wallMs;
         }
         const double n = (double)perf.size();
+        if (!append_run_summary(o.perfReport, runStamp, o.width, o.height, perf, o.runComment))
+            std::cerr << "Warning: cannot write the performance report " << o.perfReport << std::endl;
         std::cout << "\n=== Performance Report ===\n"
                   << "avg path tracing " << sumTrace / n << " ms, denoiser " << sumDen / n << " ms, wall "
-                  << sumWall / n << " ms per frame\nPerformance data saved to: " << o.perfReport << std::endl;
+                  << sumWall / n << " ms per frame\nPerformance data saved to: " << o.perfReport
+                  << " (per frame: " << csv << ")" << std::endl;
     }
 
     int rc = 0;

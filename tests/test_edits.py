@@ -294,10 +294,11 @@ def test_cli_edit_sequences_match_mirror(mode, flag, frames, tmp_path):
         _random_mesh_obj(str(tmp_path / "assets" / "models" / "leavesCube4.obj"), n=60)
         models = str(tmp_path / "assets")
         extra = ["--models", models]
-    res = _run_cli("--width", str(w), "--height", str(h), "--frames", str(frames), "--output", prefix, flag, *extra)
+    res = _run_cli("--width", str(w), "--height", str(h), "--frames", str(frames), "--output", prefix, flag, *extra,
+                   "--perf-report", str(tmp_path / "perf.txt"))
     assert res.returncode == 0, (res.stdout[-2000:], res.stderr[-2000:])
     assert res.stdout.count("EDIT: frame") >= (3 if mode == "sequence" else 10)
-    rows = [ln.split(",") for ln in open(prefix + "_performance_report.txt") if ln[0].isdigit()]
+    rows = [ln.split(",") for ln in open(prefix + "_frames.csv") if ln[0].isdigit()]
     dts = [float(x[7]) for x in rows]
     angles = {}
     for ln in res.stdout.splitlines():

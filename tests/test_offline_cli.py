@@ -54,14 +54,20 @@ def test_cli_offline_run_and_canonical_gate(tmp_path):
     canon = str(tmp_path / "canon.png")
     r = run("--width", str(w), "--height", str(h), "--frames", str(frames), "--output", prefix,
             "--update-canonical", "--test-canonical", "--canonical-image", canon, "--comment", "cli test",
-            timeout=120)
+            "--perf-report", str(tmp_path / "perf" / "performance_report.txt"), timeout=120)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
     # frames 1 and 4 (1-indexed) are saved under their 0-indexed numbers
     for f in (0, 3):
         assert os.path.exists("%s_%04d.png" % (prefix, f))
     assert not os.path.exists("%s_%04d.png" % (prefix, 1))
     assert "Assessment: IDENTICAL" in r.stdout and os.path.exists(prefix + "_diff.png")
-    assert os.path.exists(prefix + "_performance_report.txt")
+    assert os.path.exists(prefix + "_frames.csv")
+    # PerformanceTracker::saveReport's run summary (PerformanceTracker.h:98-183), header included
+    rep = open(tmp_path / "perf" / "performance_report.txt").read().splitlines()
+    assert rep[0].startswith("# Performance Report") and rep[1].startswith("# Format: Timestamp") and len(rep) == 4
+    cols = [c.strip() for c in rep[3].split("|")]
+    assert len(cols) == 11 and cols[1] == str(frames) and cols[2] == "%dx%d" % (w, h) and cols[10] == "cli test"
+    assert float(cols[7]) > 0.0 and float(cols[8]) > 0.0  # path tracing, denoiser ms
 
     # the same frames through the Python mirror of the same entry points
     rr = vxpt.Renderer(w, h)
@@ -73,7 +79,7 @@ def test_cli_offline_run_and_canonical_gate(tmp_path):
     rr.set_sky()
     dp, pp = rr.denoise_params(), rr.post_params()
     # the CLI's frame times (Timer::getDeltaTime) drive the exposure adaptation: replay them
-    rows = [ln.split(",") for ln in open(prefix + "_performance_report.txt") if ln[0].isdigit()]
+    rows = [ln.split(",") for ln in open(prefix + "_frames.csv") if ln[0].isdigit()]
     dts = [float(x[7]) for x in rows]
     assert len(dts) == frames
     for f in range(frames):

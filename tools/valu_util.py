@@ -56,13 +56,31 @@ def main():
         if c.get("SQ_THREAD_CYCLES_VALU") and c.get("SQ_ACTIVE_INST_VALU"):
             row["lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"]), 4)
         out[k] = row
+    # chip level: the trace kernels' VALU instructions over the time any of them runs (the union of
+    # their dispatch intervals: with two streams a pass's halves overlap, so per-kernel durations
+    # double-count the wall time)
+    ivs = sorted((s0, e0) for n, s0, e0 in sqlite3.connect(kt_db).cursor().execute(
+        "select name, start, end from kernels") if short(n) in TRACE for _ in [0])
+    busy, cs, ce = 0, None, None
+    for s0, e0 in ivs:
+        if cs is None or s0 > ce:
+            busy += (ce - cs) if cs is not None else 0
+            cs, ce = s0, e0
+        else:
+            ce = max(ce, e0)
+    busy += (ce - cs) if cs is not None else 0
+    ndisp = collections.Counter(short(n) for (n,) in sqlite3.connect(kt_db).cursor().execute("select name from kernels"))
+    insts = sum(r["valu_insts"] * ndisp[k] for k, r in out.items() if r.get("valu_insts"))
+    chip = insts * 2 / (busy * 1e-9 * CLOCK_HZ * SIMDS) if busy else None
     tot_t = sum(r["avg_us"] for r in out.values())
     lanes = [r for r in out.values() if "lane_util" in r]
     lane_agg = (sum(r["lane_util"] * r["avg_us"] for r in lanes) / sum(r["avg_us"] for r in lanes)) if lanes else None
     agg = sum(r.get("issue_util", 0) * r["avg_us"] for r in out.values()) / max(tot_t, 1e-9)
-    res = {"trace_valu_util": round(agg, 4), "trace_valu_lane_util": round(lane_agg, 4) if lane_agg else None,
+    res = {"trace_valu_util": round(chip, 4) if chip else round(agg, 4),
+           "trace_valu_lane_util": round(lane_agg, 4) if lane_agg else None,
+           "kernel_time_weighted_issue_util": round(agg, 4),
            "kernels": out,
-           "note": "issue util = SQ_INSTS_VALU x 2 cycles / (duration x 2.4 GHz x 1024 SIMDs), time-weighted over the trace kernels; lane util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)"}
+           "note": "trace_valu_util = the trace kernels' SQ_INSTS_VALU x 2 cycles / (the time any trace kernel runs x 2.4 GHz x 1024 SIMDs); per kernel issue util = SQ_INSTS_VALU x 2 / (its duration x 2.4 GHz x 1024) -- with the pass halves on two streams a kernel's duration includes the other stream's work; lane util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU), time-weighted"}
     print(json.dumps(res, indent=1))
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as f:
