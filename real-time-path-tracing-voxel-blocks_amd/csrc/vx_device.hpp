@@ -240,7 +240,8 @@ VX_HD bool cross(const WorldDev &w, Dda &s, bool solid, int loc, bool chunkPlane
 // Walk the crossings that stay inside the current occupied 4^3 brick (cube
 // bits in s.cm).  Inside a brick no crossing is a chunk plane or leaves the
 // world.  Returns 0 when the next crossing leaves the brick (state = last cell
-// inside), 1 on an event (h filled for radiance rays), 2 when t exceeds tmax.
+// inside), 1 on an event (h filled for radiance rays), 2 when t exceeds tmax,
+// 3 after w.brickSteps crossings inside the brick (the walk continues there).
 template <bool OCC>
 VX_HD int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     const Ray3 &r = s.r;
@@ -248,7 +249,9 @@ VX_HD int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     int lc = cell_of(c.x, c.y, c.z);
     const uint64_t cm = s.cm;
     const int base = s.nb * 64;
+    const int lim = w.brickSteps > 0 ? w.brickSteps : 10;
     for (int k = 0; k < 10; ++k) {  // at most 9 crossings stay inside a 4^3 brick
+        if (k == lim) return 3;
         const int a = pick3(c.tx, c.ty, c.tz);
         if (cnt) ++*cnt;
         // per-axis choices as bit blends, not selects between struct fields (a
@@ -345,6 +348,10 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
         const int rc = brick_walk<OCC>(w, s, h, cnt ? cnt + 4 : nullptr);
         if (rc == 1) return DdaEvent;
         if (rc == 2) return DdaNone;
+        if (rc == 3) {  // a continuation of the same brick: not a new step of the step bound
+            --s.steps;
+            return DdaRun;
+        }
     } else if constexpr (BOX) {
         skip_box(w, s.r, s.c, (int)(s.box & 0xFFu), (int)((s.box >> 8) & 0xFFu), (int)((s.box >> 16) & 0xFFu));
     } else {

@@ -65,6 +65,8 @@ struct WorldDev {
                               // BOX's extents in bricks (x | y << 8 | z << 16; 0 = occupied) grown from the
                               // cube; null: the cube tables alone
     int nBricks;
+    int brickSteps;           // cell crossings per brick walk before the walk yields an outer iteration
+                              // (0 = 10: a whole brick); VXPT_BRICK_STEPS
     uint64_t top;
     int topValid;
     int cx, cy, cz;       // chunks

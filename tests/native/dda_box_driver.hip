@@ -93,6 +93,10 @@ int main(int argc, char **argv) {
     w.cx = CX; w.cy = CY; w.cz = CZ;
     w.wx = wx; w.wy = wy; w.wz = wz;
     w.mx = wx / 16; w.my = wy / 16; w.mz = wz / 16;
+    // the box-table walks also yield every 3 cell crossings inside a brick (WorldDev::brickSteps; the
+    // cube-table walks take whole bricks): the same hits prove the yield and its save / resume exact
+    WorldDev wb = w;
+    wb.brickSteps = 3;
     if (std::string(argv[5]) == "--rays") {
         FILE *fr = fopen(argv[6], "rb");
         if (!fr) return 1;
@@ -109,11 +113,11 @@ int main(int argc, char **argv) {
             const Hit hc = dda_closest<false>(w, o, d, r[7]);
             Hit hb{0, 0, 0, 0, -1, 0, kRayMax};
             Dda sb;
-            int rb = dda_begin<false, true>(w, o, d, 0.0f, r[7], sb, hb);
+            int rb = dda_begin<false, true>(wb, o, d, 0.0f, r[7], sb, hb);
             while (rb == DdaRun) {
                 const DdaSaved sv = dda_save(sb, 0);
-                dda_resume<true>(w, o, d, 0.0f, r[7], sv, sb);
-                rb = dda_iter<false, true>(w, sb, hb);
+                dda_resume<true>(wb, o, d, 0.0f, r[7], sv, sb);
+                rb = dda_iter<false, true>(wb, sb, hb);
             }
             if (rb != DdaEvent) hb = Hit{0, 0, 0, 0, -1, 0, kRayMax};
             const Hit hs[2] = {hc, hb};
@@ -122,7 +126,7 @@ int main(int argc, char **argv) {
                 q[7 * k + 4] = hs[k].face; q[7 * k + 5] = hs[k].id; q[7 * k + 6] = float_as_bits(hs[k].t);
             }
             q[14] = dda_occluded<false>(w, o, d, r[6], r[7]) ? 1 : 0;
-            q[15] = dda_occluded<true>(w, o, d, r[6], r[7]) ? 1 : 0;
+            q[15] = dda_occluded<true>(wb, o, d, r[6], r[7]) ? 1 : 0;
         }
         FILE *fo = fopen(argv[7], "wb");
         if (!fo || fwrite(out.data(), 4, out.size(), fo) != out.size()) return 1;
@@ -149,11 +153,11 @@ int main(int argc, char **argv) {
         int rc = dda_begin<false, false>(w, o, d, 0.0f, tmax, sc, hc), n1 = 0;
         while (rc == DdaRun) { rc = dda_iter<false, false>(w, sc, hc); ++n1; }
         if (rc != DdaEvent) hc = Hit{0, 0, 0, 0, -1, 0, kRayMax};
-        int rb = dda_begin<false, true>(w, o, d, 0.0f, tmax, sb, hb), n2 = 0;
+        int rb = dda_begin<false, true>(wb, o, d, 0.0f, tmax, sb, hb), n2 = 0;
         while (rb == DdaRun) {
             // every other ray through the straggler hand-over (dda_save / dda_resume)
-            if (i & 1) { const DdaSaved sv = dda_save(sb, 0); dda_resume<true>(w, o, d, 0.0f, tmax, sv, sb); }
-            rb = dda_iter<false, true>(w, sb, hb);
+            if (i & 1) { const DdaSaved sv = dda_save(sb, 0); dda_resume<true>(wb, o, d, 0.0f, tmax, sv, sb); }
+            rb = dda_iter<false, true>(wb, sb, hb);
             ++n2;
         }
         if (rb != DdaEvent) hb = Hit{0, 0, 0, 0, -1, 0, kRayMax};
@@ -161,7 +165,7 @@ int main(int argc, char **argv) {
         hits += hc.hit;
         const bool same = hc.hit == hb.hit && hc.x == hb.x && hc.y == hb.y && hc.z == hb.z && hc.face == hb.face &&
                           hc.id == hb.id && float_as_bits(hc.t) == float_as_bits(hb.t);
-        const bool oc = dda_occluded<false>(w, o, d, tmin, tmax), ob = dda_occluded<true>(w, o, d, tmin, tmax);
+        const bool oc = dda_occluded<false>(w, o, d, tmin, tmax), ob = dda_occluded<true>(wb, o, d, tmin, tmax);
         if (!same || oc != ob) {
             if (diff < 5)
                 printf("diff ray %d: cube hit %d (%d %d %d) f%d t %.9g | box hit %d (%d %d %d) f%d t %.9g | occ %d %d\n", i,

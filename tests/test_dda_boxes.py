@@ -5,7 +5,8 @@ CPU: the library's own walk (vx_device.hpp is host + device code) runs on the ho
 compiled with hipcc (no kernel launch), once with the default empty-cube tables and once with the
 box tables, over the C1 world, the C3 (256^3) world and a random sparse world: every ray's closest
 hit (cell, face, block id, t bits) and occlusion answer must be identical, also through the
-straggler save / resume hand-over, with fewer outer iterations for the boxes.
+straggler save / resume hand-over; the box walks also yield to the outer loop every 3 in-brick
+crossings (WorldDev::brickSteps), which must not change a result either.
 GPU: the probe kernels with either table against the oracle's DDA, bit for bit.
 """
 import os
@@ -66,7 +67,8 @@ def test_box_tables_walk_equals_cube_walk(driver, world, tmp_path):
     vals = dict(re.findall(r"([a-z-]+) ([0-9.]+)", out.strip().splitlines()[-1]))
     assert int(vals["diff"]) == 0, out
     assert int(vals["hits"]) > n // 10
-    assert float(vals["box"]) < float(vals["cube"]), out  # the iterations the boxes save
+    # the box walk also yields every 3 in-brick crossings (more outer iterations), so its count is
+    # not compared with the cube walk's; the hits are (above)
 
 
 @pytest.mark.gpu
