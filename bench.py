@@ -128,6 +128,8 @@ def main():
                          "'4 bounces' of BASELINE.json's config line, labelled as such")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--frame-calls", action="store_true",
+                    help="time K vxpt_render_frame calls instead of one pipelined vxpt_render_frames(K)")
     a = ap.parse_args()
     a.bounce_limits = tuple(int(v) for v in a.bounces.split("/"))
     assert len(a.bounce_limits) == 2 and a.bounce_limits[0] >= a.bounce_limits[1] >= 1, a.bounces
@@ -195,14 +197,24 @@ def main():
         r.sync()
 
     trace_ms, denoise_ms = [], []
+    pipelined = not a.primary_only and not a.frame_calls
     barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(frame)
-        frame += 1
+    if pipelined:
+        # the K frames as one vxpt_render_frames call: same work and buffers as K render_frame
+        # calls, each frame's first trace pass overlapping the previous frame's last
+        r.render_frames(frame, a.steps, a.spp, params)
+        frame += a.steps
         t = r.timings()
         trace_ms.append(t["trace_ms"])
         denoise_ms.append(t["denoise_ms"])
+    else:
+        for _ in range(a.steps):
+            step(frame)
+            frame += 1
+            t = r.timings()
+            trace_ms.append(t["trace_ms"])
+            denoise_ms.append(t["denoise_ms"])
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -280,7 +292,8 @@ def main():
                            a.bounce_limits + ((" (the reference's RayGen.cu:146-147 limits)",) if a.bounce_limits == (3, 1)
                                               else (" (BASELINE.json's '4 bounces' reading; the reference renders 3/1)",)
                                               if a.bounce_limits == (4, 4) else ("",))),
-                       "parallelism": ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU"},
+                       "parallelism": ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU",
+                       "frame_loop": "vxpt_render_frames (pipelined)" if pipelined else "vxpt_render_frame per step"},
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,

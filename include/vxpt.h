@@ -257,6 +257,13 @@ int vxpt_denoise_pass(vxpt_ctx *ctx, const vxpt_denoise_params *p, int pass, int
 /* OfflineBackend::renderFrame: spp trace passes (radiance averaged) + denoise.  frame_num as
  * OfflineBackend::m_frameNum; iteration indices frame_num*spp .. +spp-1. */
 int vxpt_render_frame(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame_num, int32_t spp);
+/* n_frames consecutive vxpt_render_frame calls (frames frame0 .. frame0+n_frames-1) with the
+ * camera, world and lights left as they are: mainOffline's frame loop for a static camera.  The
+ * buffers afterwards equal those calls' bit for bit; each frame's first trace pass is enqueued
+ * beside the previous frame's last one, so the sequence takes less time.  Timing: frame_ms is the
+ * mean per frame, denoise_ms the last frame's, trace_ms the mean per frame without the denoiser. */
+int vxpt_render_frames(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame0, int32_t n_frames,
+                       int32_t spp);
 /* the denoiser parameters of global_settings.yaml's `denoising` section (GlobalSettings.h:82-141),
  * the ones every call above uses when p = NULL */
 int vxpt_get_denoise_params(vxpt_ctx *ctx, vxpt_denoise_params *out);

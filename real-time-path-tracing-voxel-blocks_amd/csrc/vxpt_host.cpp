@@ -774,11 +774,18 @@ int ensure_wave(vxpt_ctx *c, int set, size_t ns, bool &fresh) {
     return 0;
 }
 
-// One 1-spp pass.  overlap: the pass's first half may run beside the previous pass's second half
-// (passes of one frame; the first half then waits only for the pass before that to release its
-// state set).  Otherwise the first half starts after everything enqueued on the context stream.
-int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
-             bool overlap = false) {
+// A pass whose first half is enqueued (trace_front) and whose second half is not yet (trace_back).
+struct PassPlan {
+    TraceArgs a;
+    int next = 0, set = 0;
+};
+
+// One 1-spp pass, first half.  overlap: the first half may run beside the previous pass's second
+// half (it then waits only for the pass before that to release its state set).  Otherwise it starts
+// after everything enqueued on the context stream.  A primary-only pass runs whole on the context
+// stream here.
+int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
+                bool overlap, PassPlan &pl) {
     if (!c->voxels.p) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
     if (!c->skyReady) return fail(c, VXPT_ERR_STATE, "sky not set");
     TraceArgs a{};
@@ -861,7 +868,6 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
     a.texels = c->texels.p;
     a.texEnabled = (c->texEnabled && c->texTable.p) ? 1 : 0;
     c->prevSceneEmpty = 0;
-    HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     if (a.primaryOnly) {
         HIPCHK(c, launch_trace_front(a, c->stream));
     } else {
@@ -875,18 +881,37 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
         }
         HIPCHK(c, launch_trace_front(a, c->frontStream));
         HIPCHK(c, hipEventRecord(c->frontDone[set], c->frontStream));
+    }
+    pl.a = a;
+    pl.next = next;
+    pl.set = set;
+    return 0;
+}
+
+// The second half of the planned pass, on the context stream, and the ring bookkeeping.
+int trace_back(vxpt_ctx *c, const PassPlan &pl) {
+    const int set = pl.set;
+    if (!pl.a.primaryOnly) {
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[set], 0));
-        HIPCHK(c, launch_trace_back(a, c->stream, c->haloPending ? c->haloDone : nullptr));
+        HIPCHK(c, launch_trace_back(pl.a, c->stream, c->haloPending ? c->haloDone : nullptr));
         HIPCHK(c, hipEventRecord(c->backDone[set], c->stream));
     }
     c->haloPending = false;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     c->tracePrev = c->last;
-    c->last = next;
+    c->last = pl.next;
     c->illum = c->illumSet[set];
     c->lastSet = set;
     ++c->passCount;
     return 0;
+}
+
+int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
+             bool overlap = false) {
+    HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    PassPlan pl;
+    if (int r = trace_front(c, it, flags, accumulate, accumFirst, accumScale, overlap, pl)) return r;
+    return trace_back(c, pl);
 }
 
 // history hand-over NormalRough/Depth/Material -> Prev (Denoiser.cu:394-407):
@@ -2414,6 +2439,60 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
     c->timing.trace_ms = t;
     c->timing.denoise_ms = d;
     c->timing.frame_ms = f;
+    return VXPT_OK;
+}
+
+int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0, int32_t nFrames, int32_t spp) {
+    if (!c || spp < 1 || nFrames < 1 || frame0 < 0) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    if (c->comm) {  // banded: frame by frame (the halo exchange orders the passes)
+        for (int f = 0; f < nFrames; ++f)
+            if (int r = vxpt_render_frame(c, p, frame0 + f, spp)) return r;
+        return VXPT_OK;
+    }
+    const float scale = 1.0f / (float)spp;
+    HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+    PassPlan pend;
+    bool havePend = false;
+    for (int f = 0; f < nFrames; ++f) {
+        const int it0 = (frame0 + f) * spp;
+        HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+        for (int s = 0; s < spp; ++s) {
+            PassPlan pl;
+            if (s == 0 && havePend) {
+                pl = pend;
+                havePend = false;
+            } else if (int r = trace_front(c, it0 + s, 0, spp > 1, s == 0, scale, s > 0, pl)) {
+                return r;
+            }
+            if (int r = trace_back(c, pl)) return r;
+        }
+        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+        if (f + 1 < nFrames) {
+            // The next frame's first pass-half runs beside this frame's last second half.  It writes
+            // a G-buffer slot that is neither this frame's (the denoiser's input) nor the history
+            // the denoiser compares against, the other radiance set, and its own state set; the
+            // motion plane it stores is all zeros (static world) like the one the denoiser reads.
+            if (int r = trace_front(c, it0 + spp, 0, spp > 1, true, scale, true, pend)) return r;
+            havePend = true;
+            // the denoiser starts after it, so it runs alone and its timing stays its own
+            if (!pend.a.primaryOnly) HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
+        }
+        c->denoiseInputIsAccum = spp > 1;
+        if (int r = do_denoise(c, p, frame0 + f, it0 + spp)) return r;
+        if (havePend) {  // later first halves wait for the denoiser (it reads the old history slot)
+            HIPCHK(c, hipEventRecord(c->frontGate, c->stream));
+            HIPCHK(c, hipStreamWaitEvent(c->frontStream, c->frontGate, 0));
+        }
+    }
+    HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float d = 0, f = 0;
+    hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
+    c->timing.trace_ms = (f - d * nFrames) / (float)nFrames;  // per frame, denoiser runs excluded
+    c->timing.denoise_ms = d;
+    c->timing.frame_ms = f / (float)nFrames;
     return VXPT_OK;
 }
 

@@ -140,6 +140,7 @@ def load_library(path=LIB_PATH):
         "vxpt_denoise": (I, [P, ctypes.POINTER(DenoiseParams), ctypes.c_int32, ctypes.c_int32]),
         "vxpt_denoise_pass": (I, [P, ctypes.POINTER(DenoiseParams), I, I, I]),
         "vxpt_render_frame": (I, [P, ctypes.POINTER(DenoiseParams), ctypes.c_int32, ctypes.c_int32]),
+        "vxpt_render_frames": (I, [P, ctypes.POINTER(DenoiseParams), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
         "vxpt_exchange_halo": (I, [P, U32, I]),
         "vxpt_readback": (I, [P, I, P, ctypes.c_size_t]),
         "vxpt_upload": (I, [P, I, P, ctypes.c_size_t]),
@@ -478,6 +479,12 @@ class Renderer:
     def render_frame(self, frame_num, spp=1, params=None):
         p = params or DenoiseParams.defaults()
         self._chk(self.lib.vxpt_render_frame(self.ctx, ctypes.byref(p), frame_num, spp), "vxpt_render_frame")
+
+    def render_frames(self, frame0, n_frames, spp=1, params=None):
+        """vxpt_render_frames: frames frame0 .. frame0+n_frames-1 with the camera held, each frame's
+        first trace pass overlapping the previous frame's last (same buffers as render_frame calls)."""
+        p = params or DenoiseParams.defaults()
+        self._chk(self.lib.vxpt_render_frames(self.ctx, ctypes.byref(p), frame0, n_frames, spp), "vxpt_render_frames")
 
     def timings(self):
         t = Timing()

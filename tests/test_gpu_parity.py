@@ -350,6 +350,30 @@ def test_overlapped_passes_equal_sequential_passes(w, h):
         b.close()
 
 
+@pytest.mark.parametrize("spp", [4, 1])
+def test_pipelined_frames_equal_frame_calls(spp):
+    """vxpt_render_frames enqueues each frame's first pass-half beside the previous frame's last
+    second half (the denoiser then runs alone); after 4 frames every trace and denoiser buffer equals
+    4 vxpt_render_frame calls bit for bit, and a frame rendered after it (fresh call) still does."""
+    a, _ = _setup(96, 72)
+    b, _ = _setup(96, 72)
+    p = _dn_params()
+    try:
+        a.render_frames(0, 4, spp, p)
+        for f in range(4):
+            b.render_frame(f, spp, p)
+        a.render_frame(4, spp, p)
+        b.render_frame(4, spp, p)
+        for name in ("ILLUM", "DEPTH", "NORMAL_ROUGH", "ALBEDO", "MATERIAL", "PREV_NORMAL_ROUGH", "PREV_DEPTH",
+                     "TAP_RECORD", "RES_EVEN", "RES_ODD", "PREV_ILLUM", "PREV_FAST", "HIST_LEN", "OUTPUT"):
+            np.testing.assert_array_equal(a.read(name).view(np.uint8), b.read(name).view(np.uint8), err_msg=name)
+        t = a.timings()
+        assert t["frame_ms"] > 0 and t["denoise_ms"] > 0
+    finally:
+        a.close()
+        b.close()
+
+
 def test_render_frame_spp4_properties(pair):
     r, _ = pair
     r.render_frame(0, 1, _dn_params())
