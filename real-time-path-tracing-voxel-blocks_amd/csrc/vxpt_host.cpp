@@ -848,6 +848,9 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.primaryOnly = (flags & VXPT_TRACE_PRIMARY_ONLY) ? 1 : 0;
     a.tilesX = (c->W + 7) / 8;
     a.nSlots = a.tilesX * ((a.y1 - a.y0 + 7) / 8) * 64;
+    // VXPT_OVERLAP=0 (diagnostics): every first half after the previous pass, kernels one at a time
+    static const bool overlapOk = !(getenv("VXPT_OVERLAP") && atoi(getenv("VXPT_OVERLAP")) == 0);
+    if (!overlapOk) overlap = false;
     bool fresh;
     if (int r = ensure_wave(c, set, (size_t)a.nSlots, fresh)) return r;
     if (fresh) overlap = false;  // the first half must follow the new buffers' zero fill
