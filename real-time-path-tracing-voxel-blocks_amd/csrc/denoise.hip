@@ -334,6 +334,29 @@ VX_D bool xcd_tile(const DenoiseArgs &a, int &tx, int &ty) {
     return true;
 }
 
+// 4x4-tile supertiles dealt round-robin to the 8 XCDs (workgroup g runs on XCD g % 8): a tile's
+// neighbours inside its supertile run on its own XCD, so their shared apron rows and columns stay in
+// that XCD's L2, and every XCD gets supertiles from the whole frame (the sky / ground mix stays even).
+// Launch grid: grid_st(a).  False = the grid's padding.
+template <int TS = 16>
+VX_D bool st_tile(const DenoiseArgs &a, int &tx, int &ty) {
+    const int tilesX = (a.W + TS - 1) / TS, tilesY = (a.y1 - a.y0 + TS - 1) / TS;
+    const int sX = (tilesX + 3) / 4;
+    const int g = blockIdx.x, k = g % 8, l = g / 8;
+    const int S = (l / 16) * 8 + k, t = l % 16;
+    tx = (S % sX) * 4 + (t & 3);
+    ty = (S / sX) * 4 + (t >> 2);
+    return tx < tilesX && ty < tilesY;
+}
+// the tile mapping of a stencil kernel: raster (blockIdx) or supertiles (st_tile)
+template <bool ST, int TS = 16>
+VX_D bool map_tile(const DenoiseArgs &a, int &tx, int &ty) {
+    if (ST) return st_tile<TS>(a, tx, ty);
+    tx = blockIdx.x;
+    ty = blockIdx.y;
+    return true;
+}
+
 // ---------------------------------------------------------------- TA
 template <bool kQuirk>
 VX_HD V4 bicubic12(const float4 *b, int W, int H, V2 uv) {
@@ -553,7 +576,7 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
 __global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
     __shared__ unsigned sTot[4], sFFn, sFFmask[8];
     __shared__ float4 sFF[256];
-    const int tx = blockIdx.x, ty = blockIdx.y;
+    const int tx = blockIdx.x, ty = blockIdx.y;  // raster (supertiles measured 94.2 -> 94.5 us)
     const unsigned tile = ty * ((a.W + 15) / 16) + tx;
     if (threadIdx.x == 0) {
         const unsigned n = a.ffCount[tile];
@@ -749,7 +772,8 @@ __global__ __launch_bounds__(TS * TS) void k_history_clamp(DenoiseArgs a) {
     constexpr int T = TS + 4, N = T * T;
     const int W = a.W, H = a.H;
     const int tx = threadIdx.x % TS, ty = threadIdx.x / TS;
-    const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
+    // raster tiles (XCD strips measured slower: 51 -> 57 us; supertiles 49.7 -> 49.3)
+    const int btx = blockIdx.x, bty = blockIdx.y;
     const int x0 = btx * TS, y0 = a.y0 + bty * TS;
     const int x = x0 + tx, y = y0 + ty;
     __shared__ float sY[3][N], sR[3][N];
@@ -814,12 +838,15 @@ VX_HD void history_clamp_host(const DenoiseArgs &a, int x, int y) {
 // The 16x16 tile's 5x5 neighbourhood (20x20, edge-clamped) of the history,
 // normals, material ids and world positions is staged in LDS (AtrousSmem.h
 // stages the same tile in shared memory).
-template <int TS>
+// Supertiles (st_tile): 50.4 -> 46.9 us against raster tiles (XCD strips were 51 -> 57); staging
+// the depth and recomputing world positions instead of the 16-byte plane was slower (57.8 us).
+template <int TS, bool ST>
 __global__ __launch_bounds__(TS * TS) void k_atrous_smem(DenoiseArgs a) {
     constexpr int T = TS + 4, N = T * T;
     const int W = a.W, H = a.H;
     const int tx = threadIdx.x % TS, ty = threadIdx.x / TS;
-    const int btx = blockIdx.x, bty = blockIdx.y;  // raster tiles (XCD strips measured slower: 51 -> 57 us)
+    int btx, bty;
+    if (!map_tile<ST, TS>(a, btx, bty)) return;
     const int x0 = btx * TS, y0 = a.y0 + bty * TS;
     const int x = x0 + tx, y = y0 + ty;
     __shared__ float4 sI[N];
@@ -1109,6 +1136,12 @@ hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_frame0, grid1d(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
+template <int TS = 16>
+inline dim3 grid_st(const DenoiseArgs &a) {
+    const int tilesX = (a.W + TS - 1) / TS, tilesY = (a.y1 - a.y0 + TS - 1) / TS;
+    const int nS = ((tilesX + 3) / 4) * ((tilesY + 3) / 4);
+    return dim3((unsigned)((nS + 7) / 8 * 8 * 16));
+}
 hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
     const Qt rot = q_rotation_between(a.prevCam.dir, a.cam.dir);
     hipLaunchKernelGGL(k_temporal, grid16(a), dim3(256), 0, st, a, rot);
@@ -1132,8 +1165,8 @@ hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st) {
-    if (stencil_tile() == 32) hipLaunchKernelGGL(k_atrous_smem<32>, grid_ts(a, 32), dim3(1024), 0, st, a);
-    else hipLaunchKernelGGL(k_atrous_smem<16>, grid16(a), dim3(256), 0, st, a);
+    if (stencil_tile() == 32) hipLaunchKernelGGL((k_atrous_smem<32, false>), grid_ts(a, 32), dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL((k_atrous_smem<16, true>), grid_st(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex,

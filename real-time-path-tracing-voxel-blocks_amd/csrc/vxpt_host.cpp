@@ -138,8 +138,9 @@ bool as_bool(const std::string &s) { return s == "true" || s == "1" || s == "Tru
 
 }  // namespace
 
-constexpr int kBlockTypes = 30;
-constexpr int kPostHist = 257;   // 256 luminance bins + the lens flare's sun flag  // BlockTypeNum (generated/voxelengine/BlockType.h:39)
+constexpr int kBlockTypes = 30;  // BlockTypeNum (generated/voxelengine/BlockType.h:39)
+constexpr int kPostHist = 257;   // 256 luminance bins + the lens flare's sun flag
+constexpr int kMaxSets = 3;      // wavefront state sets (vxpt_ctx::nSets)
 
 struct vxpt_ctx {
     int W = 0, H = 0, dev = 0, rowBegin = 0, rowEnd = 0;
@@ -251,14 +252,15 @@ struct vxpt_ctx {
     // the previous pass's (its ReSTIR history) nor the denoiser's history slot
     // (the previous frame's final G-buffer, Denoiser.cu:394-407), so the frame
     // end hands the last slot to the denoiser by index instead of copying planes.
-    // A 4th slot lets a pass's first half (camera rays .. NEE visibility, which read no previous
-    // pass) run while the previous pass's temporal reuse still reads its own previous slot.
-    GSlot gb[4];
+    // Two more slots let first halves (camera rays .. NEE visibility, which read no previous pass)
+    // run ahead while up to two second halves still read their previous passes' slots.
+    GSlot gb[5];
     int last = 0;              // slot of the most recent trace output
     int tracePrev = 0;         // slot the most recent trace read as its previous pass
+    int tracePrev2 = 0;        // the one before (read by the second half before that)
     int hist = 2;              // denoiser history slot (zero at frame 0)
     float4 *illum = nullptr;   // the most recent pass's radiance (one of illumSet)
-    float4 *illumSet[2] = {nullptr, nullptr};  // per wavefront state set
+    float4 *illumSet[kMaxSets] = {};  // per wavefront state set
     float4 *accum = nullptr, *motion = nullptr;
     Reservoir *res = nullptr;  // 2*W*H
     float4 *ping = nullptr, *pong = nullptr, *prevIllum = nullptr, *prevFast = nullptr, *output = nullptr;
@@ -269,15 +271,18 @@ struct vxpt_ctx {
     float4 *ffColor = nullptr;
     Reservoir *ffRes = nullptr;
     bool denoiseInputIsAccum = false;
-    // Two wavefront state sets, alternating by pass: pass k's first half (k_closest .. the RIS
-    // visibility rays) runs on frontStream while pass k-1's second half (temporal reuse, its rays,
-    // k_finish, later segments, the spp accumulation) runs on the context stream.
-    WaveBufs wb[2]{};
-    size_t wbSlots[2] = {0, 0};
-    int passCount = 0;         // trace passes so far (set = passCount % 2)
+    // Wavefront state sets, used round-robin by pass: first halves (k_closest .. the RIS
+    // visibility rays) run in order on frontStream, each after the pass that last used its set;
+    // second halves (temporal reuse, its rays, k_finish, later segments, the spp accumulation) run
+    // in order on the context stream, each after its first half.  With 3 sets a first half may
+    // start while the two previous second halves are still running.
+    int nSets = 2;
+    WaveBufs wb[kMaxSets]{};
+    size_t wbSlots[kMaxSets] = {};
+    int passCount = 0;         // trace passes so far (set = passCount % nSets)
     int lastSet = 0;           // the set of the most recent pass
     hipStream_t frontStream = nullptr;
-    hipEvent_t frontDone[2] = {nullptr, nullptr}, backDone[2] = {nullptr, nullptr}, frontGate = nullptr;
+    hipEvent_t frontDone[kMaxSets] = {}, backDone[kMaxSets] = {}, frontGate = nullptr;
     int numCU = 256;
     std::vector<void *> allocs;
 
@@ -813,7 +818,7 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     // the slot this pass writes: not the previous pass's (its temporal taps), not the denoiser's
     // history, and not the one the previous pass's second half may still be reading
     int next = 0;
-    while (next == c->last || next == c->hist || next == c->tracePrev) ++next;
+    while (next == c->last || next == c->hist || next == c->tracePrev || next == c->tracePrev2) ++next;
     const GSlot &cur = c->gb[next], &prev = c->gb[c->last];
     a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material, cur.rec};
     a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material, prev.rec};
@@ -822,7 +827,7 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
         c->gb[c->last].recStale = false;
     }
     c->gb[next].recStale = false;  // this pass writes both
-    const int set = c->passCount & 1;
+    const int set = c->passCount % c->nSets;
     a.illum = c->illumSet[set];
     a.motion = c->motion;
     const size_t n = (size_t)c->W * c->H;
@@ -901,6 +906,7 @@ int trace_back(vxpt_ctx *c, const PassPlan &pl) {
     }
     c->haloPending = false;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    c->tracePrev2 = c->tracePrev;
     c->tracePrev = c->last;
     c->last = pl.next;
     c->illum = c->illumSet[set];
@@ -1337,8 +1343,14 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(c, hipStreamCreateWithFlags(&c->frontStream, hipStreamNonBlocking));
-    for (hipEvent_t *e : {&c->frontDone[0], &c->frontDone[1], &c->backDone[0], &c->backDone[1], &c->frontGate})
-        HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
+    // VXPT_SETS=3: a third wavefront state set, so a first half may run beside the two previous
+    // second halves (C3: 6.40 -> 6.39 ms per frame, within noise: the overlapped halves already
+    // fill the chip; two sets are the default)
+    if (getenv("VXPT_SETS")) c->nSets = std::max(2, std::min(kMaxSets, atoi(getenv("VXPT_SETS"))));
+    for (int k = 0; k < kMaxSets; ++k)
+        for (hipEvent_t *e : {&c->frontDone[k], &c->backDone[k]})
+            HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(c, hipEventCreateWithFlags(&c->frontGate, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(c, hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->dev));
     // timing markers only (every read of them follows a stream synchronisation): no system-scope
     // fence, so a marker neither writes back / invalidates the L2 nor delays the next kernel
@@ -1358,8 +1370,9 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         dalloc(c, c->ffCand, tiles16 * 256) || dalloc(c, c->ffCandCount, 1) ||
         dalloc(c, c->hfList, tiles16 * 256) || dalloc(c, c->hfCount, tiles16))
         return VXPT_ERR_HIP;
-    if (dalloc(c, c->illumSet[1], n)) return VXPT_ERR_HIP;
     c->illumSet[0] = c->illum;
+    for (int k = 1; k < c->nSets; ++k)
+        if (dalloc(c, c->illumSet[k], n)) return VXPT_ERR_HIP;
     // tables
     const std::string t = c->dataDir + "/tables/";
     std::vector<uint8_t> so, sc, rk, f0, f1, f2, f3;
@@ -1388,8 +1401,10 @@ void vxpt_destroy(vxpt_ctx *c) {
     if (c->frontStream) hipStreamSynchronize(c->frontStream);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void *p : c->allocs) hipFree(p);
-    for (hipEvent_t e : {c->frontDone[0], c->frontDone[1], c->backDone[0], c->backDone[1], c->frontGate})
-        if (e) hipEventDestroy(e);
+    for (int k = 0; k < kMaxSets; ++k)
+        for (hipEvent_t e : {c->frontDone[k], c->backDone[k]})
+            if (e) hipEventDestroy(e);
+    if (c->frontGate) hipEventDestroy(c->frontGate);
     if (c->frontStream) hipStreamDestroy(c->frontStream);
     for (auto &e : c->ev)
         if (e) hipEventDestroy(e);
