@@ -284,9 +284,8 @@ VX_D void store_result(const WaveBufs &w, int id, int rc, const Hit &h) {
 // k_resume finishes densely packed.  The straggler queue has 8 shards
 // (workgroup b appends to shard b % 8, one atomic per workgroup on that
 // shard's counter word) so no single word serialises the appends.
-constexpr int kShards = 8;
 VX_D unsigned *straggler_count(const WaveBufs &w, int level, int q, int k) {
-    return w.qCount + 64 + (((level - 1) * 16 + q) * kShards + k) * 16;
+    return w.qCount + 2 * kQueues + (((level - 1) * kQueues + q) * kShards + k) * 16;
 }
 
 template <bool OCC, bool BOX>
@@ -339,6 +338,57 @@ __global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int 
         w.sCell[0][k] = sv.cell;
         w.sT[0][k] = sv.t;
         w.sFace[0][k] = sv.face;
+    }
+}
+
+// Persistent traversal of queue q: every wave keeps up to 64 walks in flight and refills the
+// lanes whose walk has ended from the queue's head (qCount[kQueues + q], one atomic per refill), once
+// at least `refill` lanes are idle; a wave leaves when the queue is drained and its last walk has
+// ended.  The lanes stay busy with live walks instead of waiting for the wave's longest one, so no
+// iteration cap and no straggler pass are needed.  Each walk is the same sequence of dda_iter
+// steps as in k_queue, so the results are identical.
+template <bool OCC, bool BOX>
+__global__ __launch_bounds__(256) void k_persist(TraceArgs a, int q, int refill) {
+    const WaveBufs &w = a.wb;
+    const unsigned n = w.qCount[q];
+    unsigned *head = w.qCount + kQueues + q;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+    Dda st;
+    int id = 0;
+    bool active = false, drained = false;
+    for (;;) {
+        const unsigned long long im = __ballot(!active);
+        const int nIdle = __popcll(im);
+        if (!drained && nIdle >= refill) {
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(head, (unsigned)nIdle);
+            base = __shfl(base, 0);
+            if (base + (unsigned)nIdle >= n) drained = true;
+            if (!active) {
+                const unsigned i = base + (unsigned)__popcll(im & below);
+                if (i < n) {
+                    const float4 ro = w.qO[i], rd = w.qD[i];
+                    id = w.qId[i];
+                    h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
+                    const int rc = dda_begin<OCC, BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
+                    if (rc == DdaRun) active = true;
+                    else store_result<OCC>(w, id, rc, h);
+                }
+            }
+        }
+        if (__ballot(active) == 0ull) {
+            if (drained) break;
+            continue;
+        }
+        if (active) {
+            const int rc = dda_iter<OCC, BOX>(a.world, st, h, nullptr);
+            if (rc != DdaRun) {
+                store_result<OCC>(w, id, rc, h);
+                active = false;
+            }
+        }
     }
 }
 
@@ -1309,6 +1359,18 @@ struct Launcher {
     void trav(bool occ, int q, int cap) {
         const dim3 gr(a.numCU * (a.resumeWgPerCU > 0 ? a.resumeWgPerCU : 16));
         const dim3 gq((cap + 255) / 256);
+        if (a.persistWg > 0) {
+            const dim3 gp(a.numCU * a.persistWg);
+            if (occ && box) hipLaunchKernelGGL((k_persist<true, true>), gp, b, 0, st, a, q, a.persistRefill);
+            else if (occ) hipLaunchKernelGGL((k_persist<true, false>), gp, b, 0, st, a, q, a.persistRefill);
+            else if (box) hipLaunchKernelGGL((k_persist<false, true>), gp, b, 0, st, a, q, a.persistRefill);
+            else hipLaunchKernelGGL((k_persist<false, false>), gp, b, 0, st, a, q, a.persistRefill);
+            if (mesh) {
+                if (occ) hipLaunchKernelGGL(k_mesh_queue<true>, gq, b, 0, st, a, q);
+                else hipLaunchKernelGGL(k_mesh_queue<false>, gq, b, 0, st, a, q);
+            }
+            return;
+        }
         const int shardCap = (int)((gq.x + kShards - 1) / kShards) * 256;
         if (occ && box) {
             hipLaunchKernelGGL((k_queue<true, true>), gq, b, 0, st, a, q, a.iterCap, shardCap);
@@ -1361,7 +1423,7 @@ hipError_t launch_trace_front(const TraceArgs &a, hipStream_t st) {
     }
     // secondary / visibility rays go through the compacted queues; their counters (4 per segment)
     // are zeroed once per pass
-    hipMemsetAsync(a.wb.qCount, 0, (64 + 3 * 16 * kShards * 16) * sizeof(unsigned), st);
+    hipMemsetAsync(a.wb.qCount, 0, kQueueWords * sizeof(unsigned), st);
     if (L.mesh) hipLaunchKernelGGL(k_mesh_slots, L.g, L.b, 0, st, a, 2);
     L.first_half(0);
     return hipGetLastError();

@@ -100,6 +100,12 @@ struct GBuf {
 // Per-pixel state of the wavefront trace pass (trace.hip).  One slot per
 // pixel in 8x8-tile order (slot = tile*64 + lane, tiles row-major over the
 // band), so each 64-lane wave owns one tile in every stage.
+// ray queues: 4 per path segment (1 BRDF candidates, 2 RIS visibility, 3 ReSTIR visibility), so at
+// most kQueues / 4 segments (vxpt_create bounds total_bounce_limit); straggler queues in kShards shards
+constexpr int kQueues = 64;
+constexpr int kShards = 8;
+constexpr size_t kQueueWords = 2 * kQueues + 3 * kQueues * kShards * 16;
+
 struct WaveBufs {
     // path state
     float4 *pPos;   // ray origin xyz, primary distance
@@ -136,7 +142,7 @@ struct WaveBufs {
     // result id; one storage reused by the pass's queues, counters 4 per segment
     float4 *qO, *qD;
     int *qId;
-    unsigned *qCount;  // 64 queue counters, then per straggler level (1-3) 16 queues x 8 shard counters 16 words apart
+    unsigned *qCount;  // kQueueWords: kQueues queue counters, kQueues queue heads (k_persist), then per straggler level (1-3) kQueues queues x kShards shard counters 16 words apart
     // straggler queues (ping-pong by level): walk state of rays stopped at an iteration cap (DdaSaved)
     int4 *sCell[2];
     float4 *sT[2];
@@ -220,6 +226,8 @@ struct TraceArgs {
     int lightsDirty;
     int resumeWgPerCU;  // k_resume workgroups per CU (0: 16)
     int sortMode;       // ray queues grouped by direction class per workgroup (0 off, 1 octant, 2 octant x axis)
+    int persistWg;      // > 0: queue traversal by a persistent grid of this many workgroups per CU (k_persist)
+    int persistRefill;  // k_persist: a wave refills its finished lanes once at least this many are idle
 };
 
 // kernel launchers (defined in the .hip translation units)

@@ -769,7 +769,7 @@ int ensure_wave(vxpt_ctx *c, int set, size_t ns, bool &fresh) {
         dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
         dalloc(c, w.oHit, 4 * ns) ||
         dalloc(c, w.qO, 4 * ns) || dalloc(c, w.qD, 4 * ns) ||
-        dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, 64 + 3 * 16 * 8 * 16) ||
+        dalloc(c, w.qId, 4 * ns) || dalloc(c, w.qCount, kQueueWords) ||
         dalloc(c, w.sCell[0], 4 * ns + 2048) || dalloc(c, w.sT[0], 4 * ns + 2048) ||
         dalloc(c, w.sFace[0], 4 * ns + 2048) || dalloc(c, w.sCell[1], 4 * ns + 2048) ||
         dalloc(c, w.sT[1], 4 * ns + 2048) || dalloc(c, w.sFace[1], 4 * ns + 2048) ||
@@ -865,6 +865,8 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
     a.resumeWgPerCU = getenv("VXPT_RESUME_WG") ? atoi(getenv("VXPT_RESUME_WG")) : 16;
     a.sortMode = getenv("VXPT_SORT") ? atoi(getenv("VXPT_SORT")) : 0;
+    a.persistWg = getenv("VXPT_PERSIST") ? atoi(getenv("VXPT_PERSIST")) : 0;
+    a.persistRefill = getenv("VXPT_REFILL") ? std::max(1, std::min(64, atoi(getenv("VXPT_REFILL")))) : 32;
     a.prevSceneEmpty = c->prevSceneEmpty;
     // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
     a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;
@@ -1321,8 +1323,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (!cfg || !out) return VXPT_ERR_ARG;
     *out = nullptr;
     if (cfg->width <= 0 || cfg->height <= 0) return VXPT_ERR_ARG;  // any size: partial 8x8 trace tiles and 16x16 denoise tiles are masked
-    // the trace pass keeps 4 ray-queue counters per path segment, 64 in all
-    if (cfg->total_bounce_limit > 16 || cfg->diffuse_bounce_limit > 16) return VXPT_ERR_ARG;
+    // the trace pass keeps 4 ray queues per path segment, kQueues in all (vx_internal.hpp)
+    if (cfg->total_bounce_limit > kQueues / 4 || cfg->diffuse_bounce_limit > 16) return VXPT_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return VXPT_ERR_NODEV;
     auto *c = new vxpt_ctx();
@@ -2952,14 +2954,14 @@ extern "C" int vxpt_trace_counters(vxpt_ctx *c, uint32_t *out, int cap) {
     if (!c || !out || cap < 48) return VXPT_ERR_ARG;
     if (!c->wb[c->lastSet].qCount) return fail(c, VXPT_ERR_STATE, "no trace buffers");
     HIPCHK(c, hipSetDevice(c->dev));
-    std::vector<uint32_t> q(64 + 3 * 16 * 8 * 16);
+    std::vector<uint32_t> q(kQueueWords);
     HIPCHK(c, hipMemcpyAsync(q.data(), c->wb[c->lastSet].qCount, q.size() * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < 16; ++k) {
         out[3 * k] = q[k];
         for (int level = 1; level <= 2; ++level) {
             uint32_t n = 0;
-            for (int sh = 0; sh < 8; ++sh) n += q[64 + (((level - 1) * 16 + k) * 8 + sh) * 16];
+            for (int sh = 0; sh < kShards; ++sh) n += q[2 * kQueues + (((level - 1) * kQueues + k) * kShards + sh) * 16];
             out[3 * k + level] = n;
         }
     }
