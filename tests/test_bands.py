@@ -392,3 +392,39 @@ def test_gpu_c4_eight_bands_4k_c3_world():
         single.close()
         for r in rs:
             r.close()
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_one_rank_communicator_matches_plain_context():
+    """vxpt_band_comm_init with a one-rank communicator: ncclCommInitRank, the banded frame over the
+    communicator (its halo groups have no peer), the post-process histogram ncclAllReduce and
+    vxpt_band_gather run on one device -- RCCL executing in the library -- and equal a plain
+    context bit for bit over 3 frames (OUTPUT, FRAME)."""
+    import vxpt
+    w, h, spp = 96, 80, 4
+    cam = C1_CAMERA
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    a, b = make(), make()
+    try:
+        b.band_comm_init(vxpt.band_comm_id(), 1, 0)
+        for f in range(3):
+            a.render_frame(f, spp, p)
+            b.render_frame(f, spp, p)
+            a.postprocess()
+            b.postprocess()
+            b.band_gather("OUTPUT")
+            for name in ("OUTPUT", "FRAME"):
+                np.testing.assert_array_equal(a.read(name).view(np.uint32), b.read(name).view(np.uint32),
+                                              err_msg="frame %d %s" % (f, name))
+    finally:
+        a.close()
+        b.close()
