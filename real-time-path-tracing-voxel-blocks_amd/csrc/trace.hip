@@ -128,10 +128,10 @@ __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
             const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
             o = a.cam.pos;
             d = a.cam.uv_to_dir(uv);
+            // the path's throughput (1) and radiance (0) are not stored: segment 0's seg_end starts
+            // from them (first = true)
             w.pPos[s] = f4(o, kRayMax);
             w.pDir[s] = f4(d, 0.0f);
-            w.pThr[s] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-            w.pRad[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             w.pMeta[s] = make_int4(F_ALIVE, rng.idx, 0, 0);
         } else if (mode == 0) {
             active = (w.pMeta[s].x & F_ALIVE) != 0;
@@ -467,11 +467,9 @@ VX_D void path_end(const TraceArgs &a, int px, int py, V3 radiance, float primar
 }
 
 // spp > 1: average the passes' radiance, depth from the last pass -- after the pass,
-// in pass order (a pass's paths end in both of its halves)
-__global__ __launch_bounds__(256) void k_accum(TraceArgs a) {
-    int px, py;
-    if (!slot_pixel(a, blockIdx.x * 256 + threadIdx.x, px, py)) return;
-    const size_t pi = (size_t)py * a.W + px;
+// in pass order (a pass's paths end in both of its halves).  One-segment passes do it at the end of
+// k_finish (the pass's last kernel), for the slot's own pixel.
+VX_D void accum_px(const TraceArgs &a, size_t pi) {
     const float4 r = a.illum[pi];
     float4 acc = a.accumFirst ? make_float4(0.f, 0.f, 0.f, 0.f) : a.accum[pi];
     acc.x += r.x * a.accumScale;
@@ -480,14 +478,20 @@ __global__ __launch_bounds__(256) void k_accum(TraceArgs a) {
     acc.w = r.w;
     a.accum[pi] = acc;
 }
+__global__ __launch_bounds__(256) void k_accum(TraceArgs a) {
+    int px, py;
+    if (!slot_pixel(a, blockIdx.x * 256 + threadIdx.x, px, py)) return;
+    accum_px(a, (size_t)py * a.W + px);
+}
 
 // End of one TraceNextPath segment (RayGen.cu:146-173): accumulate, apply the
-// BSDF weight, bounce limits; writes the pass outputs when the path ends.
+// BSDF weight, bounce limits; writes the pass outputs when the path ends.  first: segment 0,
+// whose throughput (1), radiance (0) and travelled distance (travelled0) are not in the path state.
 VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segRad, V3 bop, float pdf, bool terminate,
-                  bool curDiffuse) {
+                  bool curDiffuse, bool first, float travelled0 = 0.0f) {
     const WaveBufs &w = a.wb;
-    const float4 rad4 = w.pRad[s];
-    V3 thr = xyz(w.pThr[s]), rad = xyz(rad4);
+    const float4 rad4 = first ? make_float4(0.0f, 0.0f, 0.0f, travelled0) : w.pRad[s];
+    V3 thr = first ? V3(1.0f) : xyz(w.pThr[s]), rad = xyz(rad4);
     rad += thr * segRad;
     const bool cont = !(terminate || pdf <= 0.0f || is_null(bop));
     if (cont) thr *= bop;
@@ -634,7 +638,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             store_rec_sky(a, pi, kRayMax);
             w.pPos[s].w = kRayMax;
         }
-        seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false);
+        seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false, seg == 0);
         w.pMeta[s] = meta;
         return;
     }
@@ -659,7 +663,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             }
         }
         if (seg == 0) w.pPos[s].w = h.t;  // the primary distance (no reservoir is stored)
-        seg_end(a, s, px, py, meta, e, V3(1.0f), 0.0f, true, false);
+        seg_end(a, s, px, py, meta, e, V3(1.0f), 0.0f, true, false, seg == 0);
         w.pMeta[s] = meta;
         return;
     }
@@ -675,10 +679,11 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     sf.geoNormal = ng;
     sf.wo = wo;
     sf.metallic = m.metallic != 0;
+    float travelled = 0.0f;  // the path's travelled distance with textures (else unused: 0)
     if (a.texEnabled) {
         // ray cone (closesthit.cu:194-195): width = spread * the path's travelled distance
-        const float travelled = w.pRad[s].w + h.t;
-        w.pRad[s].w = travelled;
+        travelled = (seg == 0 ? 0.0f : w.pRad[s].w) + h.t;
+        if (seg > 0) w.pRad[s].w = travelled;
         sf.albedo = V3(m.albedo[0], m.albedo[1], m.albedo[2]);
         sf.roughness = m.roughness;
         apply_textures(a.texels, a.tex, m, texPos, ng, wo, ray_cone_spread(a.cam, px, py) * travelled, sf.albedo,
@@ -719,7 +724,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.pDir[s] = f4(swi, spdf);
     if (!isDiffuse) {
         if (seg == 0) meta.x |= F_EMPTY;
-        seg_end(a, s, px, py, meta, V3(0.0f), sbop, spdf, terminate, false);
+        seg_end(a, s, px, py, meta, V3(0.0f), sbop, spdf, terminate, false, seg == 0, travelled);
         meta.y = rng.idx;
         w.pMeta[s] = meta;
         return;
@@ -996,7 +1001,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         V3 segRad(0.0f);
         if (ls.type != LtInvalid && ris.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, ris);
         const float4 b = w.pBop[s];
-        seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true);
+        seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true, false);
         w.pMeta[s] = meta;
         return;
     }
@@ -1112,10 +1117,7 @@ __global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
 }
 
 // seg 0: bias-corrected ReSTIR weight, final visibility, shading, reservoir store
-__global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
-    int px, py;
-    if (!slot_pixel(a, s, px, py)) return;
+VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     const WaveBufs &w = a.wb;
     int4 meta = w.pMeta[s];
     const size_t pi = (size_t)py * a.W + px;
@@ -1154,8 +1156,18 @@ __global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
     if (ls.type != LtInvalid && rr.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, rr);
     a.resCur[pi] = rr;
     const float4 b = w.pBop[s];
-    seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true);
+    // segment 0 (the only one with temporal reuse); travelled: its primary hit distance (sPos.w)
+    seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true, true, a.texEnabled ? sf.depth : 0.0f);
     w.pMeta[s] = meta;
+}
+__global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    int px, py;
+    if (!slot_pixel(a, s, px, py)) return;
+    finish_slot(a, s, px, py);
+    // a one-segment pass ends here: every path of the slot's pixel has ended (in this kernel or in
+    // the first half), so its spp accumulation follows (the k_accum launch folded in)
+    if (a.accum && a.segments == 1) accum_px(a, (size_t)py * a.W + px);
 }
 
 // ----------------------------------------------------------------- instanced meshes
@@ -1444,7 +1456,7 @@ hipError_t launch_trace_back(const TraceArgs &a, hipStream_t st, hipEvent_t wait
         L.first_half(seg);
         L.restir(seg);
     }
-    if (a.accum) hipLaunchKernelGGL(k_accum, L.g, L.b, 0, st, a);
+    if (a.accum && a.segments > 1) hipLaunchKernelGGL(k_accum, L.g, L.b, 0, st, a);
     return hipGetLastError();
 }
 
