@@ -112,7 +112,7 @@ VX_D void stat_ray(int kind, bool active, int its, float dy, bool event) {
 #define VX_IT
 #endif
 // mode 2: camera rays (RayGen.cu:102-126; initialises the path state);
-// mode 0: continuing path rays; mode 1: BRDF-candidate queue.
+// mode 0: continuing path rays (BRDF-candidate rays go through the compacted queue).
 template <bool BOX>
 __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
     const int s = blockIdx.x * 256 + threadIdx.x;
@@ -133,20 +133,11 @@ __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
             w.pPos[s] = f4(o, kRayMax);
             w.pDir[s] = f4(d, 0.0f);
             w.pMeta[s] = make_int4(F_ALIVE, rng.idx, 0, 0);
-        } else if (mode == 0) {
+        } else {
             active = (w.pMeta[s].x & F_ALIVE) != 0;
             if (active) {
                 o = xyz(w.pPos[s]);
                 d = xyz(w.pDir[s]);
-            }
-        } else {
-            active = (w.pMeta[s].x & F_NEE) != 0;
-            if (active) {
-                const float4 ro = w.cRayO[s];
-                active = ro.w >= 0.0f;
-                o = xyz(ro);
-                d = xyz(w.cRayD[s]);
-                tmax = ro.w;
             }
         }
     }
@@ -647,7 +638,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     const V3 wo = -rayD;
     const HitGeo g = hit_geometry<MESH>(a, h, rayO, rayD);
     V3 frontPos = g.front, backPos = g.back, ng = g.ng;
-    if (seg == 0) a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (seg == 0 && a.writeMotion) a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const MatDev &m = (MESH && g.mesh) ? a.meshMats[h.id] : a.mats[h.id];
     if (MESH && m.emissive) {  // closesthit.cu:107-122: emits until the first diffuse bounce
         V3 e(0.0f);
@@ -799,8 +790,10 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         disney_sample(u0, u1, u2, u3, sf.normal, sf.geoNormal, wo, sf.albedo, sf.metallic, sf.translucency,
                       sf.roughness, sd, bop, bp);
         const V3 org = spawn_toward(thin, sd, sf.normal, frontPos, backPos);
-        w.cRayO[s] = f4(org, bp > 0.0f ? kFltMax : -1.0f);
-        w.cRayD[s] = f4(sd, 0.0f);
+        // the candidate's direction, w = traced (1) or not (-1); its origin only for the mesh
+        // kernels (an emissive triangle's hit point is recomputed from it)
+        if (MESH) w.cRayO[s] = f4(org, 0.0f);
+        w.cRayD[s] = f4(sd, bp > 0.0f ? 1.0f : -1.0f);
         if (bp > 0.0f) {
             qr.mask = 1u;
             qr.id0 = s;
@@ -873,9 +866,9 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
         uint32_t li = kInvalidLight;
         V2 uv(0.0f, 0.0f);
         LSample cand = invalid_ls();
-        const float4 co = w.cRayO[s];
-        if (co.w >= 0.0f) {
-            const V3 sd = xyz(w.cRayD[s]);
+        const float4 cd = w.cRayD[s];
+        if (cd.w >= 0.0f) {
+            const V3 sd = xyz(cd);
             const Hit bh = unpack_hit(w.cHit[s], w.cT[s]);
             if (MESH && bh.hit && bh.face == 15) {
                 // __closesthit__bsdf_light (closesthit.cu:854-900): an emissive instance's triangle is
@@ -887,7 +880,7 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
                         li = kInvalidLight;
                     } else {
                         const int4 r = a.meshRow[bh.x];
-                        const V3 org = xyz(co);
+                        const V3 org = xyz(w.cRayO[s]);
                         float t, bu, bv;
                         tri_hit(V3(org.x - (float)r.x, org.y - (float)r.y, org.z - (float)r.z), sd,
                                 a.mesh.tri + (size_t)bh.y * 9, 0.0f, INFINITY, 1, t, bu, bv);
@@ -1259,7 +1252,7 @@ __global__ __launch_bounds__(256) void k_primary_gbuffer(TraceArgs a) {
     a.cur.matParam[pi] = make_float4(m.metallic ? 1.0f : 0.0f, m.translucency, 0.0f, 0.0f);
     a.cur.albedo[pi] = make_float4(alb.x, alb.y, alb.z, 1.0f);
     store_rec(a, pi, ng, m.roughness, m.metallic != 0, alb, h.t);
-    a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (a.writeMotion) a.motion[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     a.cur.depth[pi] = h.t;
     a.illum[pi] = make_float4(0.0f, 0.0f, 0.0f, h.t);
 }

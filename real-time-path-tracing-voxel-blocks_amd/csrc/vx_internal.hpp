@@ -226,6 +226,7 @@ struct TraceArgs {
     int lightsDirty;
     int resumeWgPerCU;  // k_resume workgroups per CU (0: 16)
     int sortMode;       // ray queues grouped by direction class per workgroup (0 off, 1 octant, 2 octant x axis)
+    int writeMotion;    // store the (zero) motion vectors: the plane may hold a host upload
     int persistWg;      // > 0: queue traversal by a persistent grid of this many workgroups per CU (k_persist)
     int persistRefill;  // k_persist: a wave refills its finished lanes once at least this many are idle
 };

@@ -262,6 +262,9 @@ struct vxpt_ctx {
     float4 *illum = nullptr;   // the most recent pass's radiance (one of illumSet)
     float4 *illumSet[kMaxSets] = {};  // per wavefront state set
     float4 *accum = nullptr, *motion = nullptr;
+    // the motion plane holds only zeros (allocated zeroed; the trace stores zeros, the world is static)
+    // until a host write: the trace then skips its zero stores
+    bool motionZero = true;
     Reservoir *res = nullptr;  // 2*W*H
     float4 *ping = nullptr, *pong = nullptr, *prevIllum = nullptr, *prevFast = nullptr, *output = nullptr;
     float *histLen = nullptr, *prevHistLen = nullptr;
@@ -830,6 +833,7 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     const int set = c->passCount % c->nSets;
     a.illum = c->illumSet[set];
     a.motion = c->motion;
+    a.writeMotion = c->motionZero ? 0 : 1;
     const size_t n = (size_t)c->W * c->H;
     a.resCur = c->res + (size_t)(((it % 2) + 2) % 2) * n;
     a.resPrev = c->res + (size_t)((((it + 1) % 2) + 2) % 2) * n;
@@ -1029,6 +1033,7 @@ const int kGbufBufs[] = {VXPT_BUF_DEPTH, VXPT_BUF_NORMAL_ROUGH, VXPT_BUF_GEO_NOR
 bool is_gbuf_plane(int which) { return (which >= VXPT_BUF_DEPTH && which <= VXPT_BUF_MAT_PARAM) ||
                                        (which >= VXPT_BUF_PREV_NORMAL_ROUGH && which <= VXPT_BUF_PREV_MATERIAL); }
 void gbuf_written(vxpt_ctx *c, int which) {
+    if (which == VXPT_BUF_MOTION) c->motionZero = false;
     if (is_gbuf_plane(which))
         for (GSlot &g : c->gb) g.recStale = true;
 }
