@@ -143,7 +143,9 @@ __global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
     }
     int iters[5] = {0, 0, 0, 0, 0};
     if (active) {
-        const Hit h = dda_closest<BOX>(a.world, o, d, tmax VX_IT);
+        WorldDev wc = a.world;
+        wc.brickSteps = wc.brickStepsCam;
+        const Hit h = dda_closest<BOX>(wc, o, d, tmax VX_IT);
         w.cHit[s] = pack_hit(h);
         w.cT[s] = h.t;
     }

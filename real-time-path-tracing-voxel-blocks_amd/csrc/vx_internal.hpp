@@ -66,6 +66,7 @@ struct WorldDev {
                               // cube; null: the cube tables alone
     int nBricks;
     int brickSteps;           // cell crossings per brick walk before the walk yields an outer iteration
+    int brickStepsCam;        // the same for the camera rays (k_closest, which runs every walk to its end)
                               // (0 = 10: a whole brick); VXPT_BRICK_STEPS
     uint64_t top;
     int topValid;

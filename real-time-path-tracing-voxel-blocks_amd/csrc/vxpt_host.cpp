@@ -458,6 +458,8 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     // long in-brick walks; C3 trace 6.44 -> 6.27 ms per frame)
     static const int brickSteps = getenv("VXPT_BRICK_STEPS") ? atoi(getenv("VXPT_BRICK_STEPS")) : 4;
     w.brickSteps = brickSteps;
+    static const int camSteps = getenv("VXPT_CAM_STEPS") ? atoi(getenv("VXPT_CAM_STEPS")) : 10;
+    w.brickStepsCam = camSteps;
     w.top = c->top;
     w.topValid = c->topValid;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
