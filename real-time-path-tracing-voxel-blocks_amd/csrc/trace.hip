@@ -26,6 +26,24 @@
 // one-thread-per-pixel program bit for bit.
 #include "vx_device.hpp"
 
+// occupancy bounds (waves per SIMD) of the traversal and shading kernels; the defaults are the
+// measured best, the macros let experiment builds try others
+#ifndef VX_WPE_QUEUE
+#define VX_WPE_QUEUE 8
+#endif
+#ifndef VX_WPE_RESUME
+#define VX_WPE_RESUME 6
+#endif
+#ifndef VX_WPE_SHADE
+#define VX_WPE_SHADE 5
+#endif
+#ifndef VX_WPE_NEE
+#define VX_WPE_NEE 1
+#endif
+#ifndef VX_WPE_CLOSEST
+#define VX_WPE_CLOSEST 8
+#endif
+
 namespace vx {
 namespace {
 
@@ -114,7 +132,7 @@ VX_D void stat_ray(int kind, bool active, int its, float dy, bool event) {
 // mode 2: camera rays (RayGen.cu:102-126; initialises the path state);
 // mode 0: continuing path rays (BRDF-candidate rays go through the compacted queue).
 template <bool BOX>
-__global__ __launch_bounds__(256) void k_closest(TraceArgs a, int mode) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOSEST))) void k_closest(TraceArgs a, int mode) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     int px, py;
     bool active = slot_pixel(a, s, px, py);
@@ -282,7 +300,7 @@ VX_D unsigned *straggler_count(const WaveBufs &w, int level, int q, int k) {
 }
 
 template <bool OCC, bool BOX>
-__global__ __launch_bounds__(256) void k_queue(TraceArgs a, int q, int cap, int shardCap) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_QUEUE))) void k_queue(TraceArgs a, int q, int cap, int shardCap) {
     __shared__ unsigned sTot[4], sBase[4];
     const WaveBufs &w = a.wb;
     const unsigned n = w.qCount[q];
@@ -392,7 +410,7 @@ __global__ __launch_bounds__(256) void k_persist(TraceArgs a, int q, int refill)
 // stop after cap more iterations and the unfinished ones move on to the next
 // level, same shard, one atomic per wave.
 template <bool OCC, bool BOX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESUME))) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
     const WaveBufs &w = a.wb;
     const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
     const int shard = wv % kShards, step = gridDim.x * 256 / kShards;
@@ -821,7 +839,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
 }
 
 template <bool MESH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 3 : 5))) void k_shade(TraceArgs a, int seg) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 3 : VX_WPE_SHADE))) void k_shade(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
     shade_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
@@ -951,7 +969,7 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
 }
 
 template <bool MESH>
-__global__ __launch_bounds__(256) void k_nee(TraceArgs a, int seg) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 1 : VX_WPE_NEE))) void k_nee(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
     nee_slot<MESH>(a, blockIdx.x * 256 + threadIdx.x, qr);
