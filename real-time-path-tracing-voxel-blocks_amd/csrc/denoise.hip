@@ -588,10 +588,12 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
 // 123 VGPRs (4 waves/SIMD); bounding it to 5 waves spills 80-116 B/lane and was slower (89 -> 105 us),
 // and fetching the pixel's inputs before the depth test or the history taps with the depth taps
 // raised it to 130 (3 waves: 100-103 us)
+template <bool ST>
 __global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
     __shared__ unsigned sTot[4], sFFn, sFFmask[8];
     __shared__ float4 sFF[256];
-    const int tx = blockIdx.x, ty = blockIdx.y;  // raster (supertiles measured 94.2 -> 94.5 us)
+    int tx, ty;  // supertiles (default) or raster tiles (VXPT_TA_ST=0)
+    if (!map_tile<ST>(a, tx, ty)) return;
     const unsigned tile = ty * ((a.W + 15) / 16) + tx;
     if (threadIdx.x == 0) {
         const unsigned n = a.ffCount[tile];
@@ -782,13 +784,15 @@ VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V
 // ---------------------------------------------------------------- HC
 // The 5x5 neighbourhood of the 16x16 tile (20x20 with edge clamp) is staged
 // once in LDS: YCoCg of the fast history and the noisy radiance.
-template <int TS>
+// Supertiles (st_tile) keep the neighbouring tiles' shared apron in one XCD's L2 (274 -> 200 MB per
+// frame, time 49.7 -> 49.3 us against raster tiles; XCD strips were slower, 51 -> 57 us).
+template <int TS, bool ST>
 __global__ __launch_bounds__(TS * TS) void k_history_clamp(DenoiseArgs a) {
     constexpr int T = TS + 4, N = T * T;
     const int W = a.W, H = a.H;
     const int tx = threadIdx.x % TS, ty = threadIdx.x / TS;
-    // raster tiles (XCD strips measured slower: 51 -> 57 us; supertiles 49.7 -> 49.3)
-    const int btx = blockIdx.x, bty = blockIdx.y;
+    int btx, bty;
+    if (!map_tile<ST, TS>(a, btx, bty)) return;
     const int x0 = btx * TS, y0 = a.y0 + bty * TS;
     const int x = x0 + tx, y = y0 + ty;
     __shared__ float sY[3][N], sR[3][N];
@@ -1163,7 +1167,11 @@ inline dim3 grid_st(const DenoiseArgs &a) {
 }
 hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
     const Qt rot = q_rotation_between(a.prevCam.dir, a.cam.dir);
-    hipLaunchKernelGGL(k_temporal, grid16(a), dim3(256), 0, st, a, rot);
+    // supertiles: the taps' history rows stay in the XCD's L2 (351 -> 266 MB per frame, time even);
+    // VXPT_TA_ST=0: raster tiles
+    static const bool stT = !(getenv("VXPT_TA_ST") && atoi(getenv("VXPT_TA_ST")) == 0);
+    if (stT) hipLaunchKernelGGL(k_temporal<true>, grid_st(a), dim3(256), 0, st, a, rot);
+    else hipLaunchKernelGGL(k_temporal<false>, grid16(a), dim3(256), 0, st, a, rot);
     return hipGetLastError();
 }
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {
@@ -1179,8 +1187,8 @@ inline int stencil_tile() {
 }
 inline dim3 grid_ts(const DenoiseArgs &a, int ts) { return dim3((a.W + ts - 1) / ts, (a.y1 - a.y0 + ts - 1) / ts); }
 hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st) {
-    if (stencil_tile() == 32) hipLaunchKernelGGL(k_history_clamp<32>, grid_ts(a, 32), dim3(1024), 0, st, a);
-    else hipLaunchKernelGGL(k_history_clamp<16>, grid16(a), dim3(256), 0, st, a);
+    if (stencil_tile() == 32) hipLaunchKernelGGL((k_history_clamp<32, false>), grid_ts(a, 32), dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL((k_history_clamp<16, true>), grid_st(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st) {

@@ -33,7 +33,7 @@ LOAD_MIX = {"k_firefly": {4: 10 / 26, 16: 16 / 26}, "k_temporal": {4: 12 / 124, 
 def short(n):
     n = n.replace("vx::(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     # the tile-size / tile-order template arguments of the LDS stencils are not part of the pass
-    for base in ("k_history_clamp", "k_atrous_smem"):
+    for base in ("k_history_clamp", "k_atrous_smem", "k_temporal", "k_firefly"):
         if n.startswith(base + "<"):
             return base
     return n
