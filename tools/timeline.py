@@ -9,7 +9,9 @@ import sys
 def main():
     db = sqlite3.connect(sys.argv[1])
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-    rows = list(db.cursor().execute("select name, start, end, queue_id from kernels order by start"))[-n:]
+    # the runtime's own copy / fill kernels after the timed frames (readbacks) are left out
+    rows = [r for r in db.cursor().execute("select name, start, end, queue_id from kernels order by start")
+            if not r[0].startswith("__amd_rocclr_copyBuffer")][-n:]
     t0 = rows[0][1]
     queues = sorted({r[3] for r in rows})
     for name, s, e, q in rows:
