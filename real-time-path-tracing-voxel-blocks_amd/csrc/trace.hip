@@ -129,6 +129,13 @@ VX_D void stat_ray(int kind, bool active, int its, float dy, bool event) {
 #else
 #define VX_IT
 #endif
+// the pass's camera ray direction of pixel (px, py): jitter = sampler dimensions 0 and 1
+VX_D V3 camera_ray(const TraceArgs &a, int px, int py) {
+    const float j0 = bn_rand(a.bn, px, py, a.iterationIndex, 0), j1 = bn_rand(a.bn, px, py, a.iterationIndex, 1);
+    const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
+    return a.cam.uv_to_dir(uv);
+}
+
 // mode 2: camera rays (RayGen.cu:102-126; initialises the path state);
 // mode 0: continuing path rays (BRDF-candidate rays go through the compacted queue).
 template <bool BOX>
@@ -142,14 +149,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOS
     if (active) {
         if (mode == 2) {
             Rng rng{&a.bn, px, py, a.iterationIndex, 0};
-            const float j0 = rng.next(), j1 = rng.next();
-            const V2 uv = (V2((float)px, (float)py) + V2(j0, j1)) * a.cam.invRes;
             o = a.cam.pos;
-            d = a.cam.uv_to_dir(uv);
+            d = camera_ray(a, px, py);
+            rng.idx = 2;
             // the path's throughput (1) and radiance (0) are not stored: segment 0's seg_end starts
-            // from them (first = true)
-            w.pPos[s] = f4(o, kRayMax);
-            w.pDir[s] = f4(d, 0.0f);
+            // from them (first = true); the camera ray itself only for the kernels that read it
+            // (mesh slots, the primary-only G-buffer) -- k_shade<false> recomputes it (camera_ray)
+            if (a.mesh.nInst > 0 || a.primaryOnly) {
+                w.pPos[s] = f4(o, kRayMax);
+                w.pDir[s] = f4(d, 0.0f);
+            }
             w.pMeta[s] = make_int4(F_ALIVE, rng.idx, 0, 0);
         } else {
             active = (w.pMeta[s].x & F_ALIVE) != 0;
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(256) void k_accum(TraceArgs a) {
 // BSDF weight, bounce limits; writes the pass outputs when the path ends.  first: segment 0,
 // whose throughput (1), radiance (0) and travelled distance (travelled0) are not in the path state.
 VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segRad, V3 bop, float pdf, bool terminate,
-                  bool curDiffuse, bool first, float travelled0 = 0.0f) {
+                  bool curDiffuse, bool first, float travelled0 = 0.0f, float primaryDist = -1.0f) {
     const WaveBufs &w = a.wb;
     const float4 rad4 = first ? make_float4(0.0f, 0.0f, 0.0f, travelled0) : w.pRad[s];
     V3 thr = first ? V3(1.0f) : xyz(w.pThr[s]), rad = xyz(rad4);
@@ -511,7 +520,8 @@ VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segR
     if (curDiffuse) meta.w += 1;
     if (meta.z == a.totalBounceLimit || meta.w == a.diffuseBounceLimit) done = true;
     if (done) {
-        path_end(a, px, py, rad, w.pPos[s].w);
+        // the primary distance: given by the caller (>= 0), else the path state's
+        path_end(a, px, py, rad, primaryDist >= 0.0f ? primaryDist : w.pPos[s].w);
         meta.x &= ~(F_ALIVE | F_NEE | F_RESTIR);
     } else {
         w.pThr[s] = f4(thr, 0.0f);
@@ -633,9 +643,18 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     meta.x &= ~(F_NEE | F_RESTIR);
     const size_t pi = (size_t)py * a.W + px;
     const Hit h = unpack_hit(w.cHit[s], w.cT[s]);
-    const float4 p4 = w.pPos[s];
-    const V3 rayO = xyz(p4), rayD = xyz(w.pDir[s]);
-    float primaryDist = p4.w;
+    V3 rayO, rayD;
+    float primaryDist;
+    if (!MESH && seg == 0) {  // the camera ray, as k_closest traced it (it stores no ray state)
+        rayO = a.cam.pos;
+        rayD = camera_ray(a, px, py);
+        primaryDist = kRayMax;
+    } else {
+        const float4 p4 = w.pPos[s];
+        rayO = xyz(p4);
+        rayD = xyz(w.pDir[s]);
+        primaryDist = p4.w;
+    }
     Rng rng{&a.bn, px, py, a.iterationIndex, meta.y};
 
     if (!h.hit) {  // __miss__radiance (miss.cu:9-82)
@@ -647,9 +666,8 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
             a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             store_rec_sky(a, pi, kRayMax);
-            w.pPos[s].w = kRayMax;
         }
-        seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false, seg == 0);
+        seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false, seg == 0, 0.0f, primaryDist);
         w.pMeta[s] = meta;
         return;
     }
@@ -673,8 +691,8 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
                 store_rec_sky(a, pi, h.t);
             }
         }
-        if (seg == 0) w.pPos[s].w = h.t;  // the primary distance (no reservoir is stored)
-        seg_end(a, s, px, py, meta, e, V3(1.0f), 0.0f, true, false, seg == 0);
+        if (seg == 0) primaryDist = h.t;  // the primary distance (no reservoir is stored)
+        seg_end(a, s, px, py, meta, e, V3(1.0f), 0.0f, true, false, seg == 0, 0.0f, primaryDist);
         w.pMeta[s] = meta;
         return;
     }
@@ -731,8 +749,12 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         primaryDist = h.t;
     }
     const V3 spawnPos = spawn_toward(thin, swi, sf.normal, frontPos, backPos);
-    w.pPos[s] = f4(spawnPos, primaryDist);
-    w.pDir[s] = f4(swi, spdf);
+    // the continuation ray: a one-segment pass ends every path at its first diffuse surface
+    // (k_finish), so only specular hits and multi-segment passes keep it
+    if (!isDiffuse || a.segments > 1) {
+        w.pPos[s] = f4(spawnPos, primaryDist);
+        w.pDir[s] = f4(swi, spdf);
+    }
     if (!isDiffuse) {
         if (seg == 0) meta.x |= F_EMPTY;
         seg_end(a, s, px, py, meta, V3(0.0f), sbop, spdf, terminate, false, seg == 0, travelled);
@@ -829,9 +851,8 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.sGeo[s] = f4(sf.geoNormal, sf.translucency);
     w.sAlb[s] = f4(sf.albedo, sf.metallic ? 1.0f : 0.0f);
     w.sWo[s] = f4(wo, (skipAlbedo ? 1.0f : 0.0f) + (thin ? 2.0f : 0.0f));
-    w.pBop[s] = f4(sbop, terminate ? 1.0f : 0.0f);
-    w.rSun[s] = sunRes;
-    w.rSky[s] = skyRes;
+    if (a.segments > 1) w.pBop[s] = f4(sbop, terminate ? 1.0f : 0.0f);
+    w.cSunSky[s] = make_float4(sunRes.weightSum, sunRes.targetPdf, skyRes.weightSum, skyRes.targetPdf);
     w.nIdx[s] = make_int4(sunSel, skySel, -1, 0);
     meta.x |= F_NEE | (seg == 0 ? F_RESTIR : 0);
     meta.y = rng.idx;
@@ -844,6 +865,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 3 : 
     qr.mask = 0u;
     shade_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
     block_enqueue(a, 4 * seg + 1, qr);
+}
+
+// A sun / sky candidate's reservoir as k_shade left it (stream_sample of one candidate, finalize,
+// M = 1): selected (sample index >= 0) -> the light, its sample's uv (the texel centre, quantised as
+// stream_sample does), the final weight sum and target pdf; otherwise the empty reservoir with M = 1
+// (an unselected candidate keeps target pdf 0, so finalize leaves weight sum 0).
+VX_D Reservoir cand_res(uint32_t light, int idx, int mapW, int mapH, float weightSum, float targetPdf) {
+    if (idx < 0) return Reservoir{0u, 0u, weightSum, targetPdf, 1.0f};
+    const int sx = idx % mapW, sy = idx / mapW;
+    const V2 uv((sx + 0.5f) / float(mapW), (sy + 0.5f) / float(mapH));
+    return Reservoir{light | kValidBit,
+                     (uint32_t)(saturate(uv.x) * 0xffff) | ((uint32_t)(saturate(uv.y) * 0xffff) << 16), weightSum,
+                     targetPdf, 1.0f};
 }
 
 // BRDF candidate from its traced ray, RIS over {local, sun, sky, BRDF}, visibility ray
@@ -874,8 +908,10 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
         finalize(localRes, 1.0f, (float)nMis);
         localRes.M = 1;
     }
-    const Reservoir sunRes = w.rSun[s], skyRes = w.rSky[s];
     const int4 idx = w.nIdx[s];
+    const float4 css = w.cSunSky[s];
+    const Reservoir sunRes = cand_res(kSunLight, idx.x, k.sunW, k.sunH, css.x, css.y);
+    const Reservoir skyRes = cand_res(kSkyLight, idx.y, k.skyW, k.skyH, css.z, css.w);
     const LSample sunLs = idx.x >= 0 ? sun_ls(k, idx.x) : invalid_ls();
     const LSample skyLs = idx.y >= 0 ? sky_ls(k, idx.y) : invalid_ls();
 
@@ -1168,9 +1204,12 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     V3 segRad(0.0f);
     if (ls.type != LtInvalid && rr.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, rr);
     a.resCur[pi] = rr;
-    const float4 b = w.pBop[s];
-    // segment 0 (the only one with temporal reuse); travelled: its primary hit distance (sPos.w)
-    seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true, true, a.texEnabled ? sf.depth : 0.0f);
+    // segment 0 (the only one with temporal reuse); travelled and the primary distance: its hit
+    // distance (sPos.w).  A one-segment pass ends the path here (k_shade stored no continuation).
+    const bool one = a.segments == 1;
+    const float4 b = one ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : w.pBop[s];
+    seg_end(a, s, px, py, meta, segRad, xyz(b), one ? 1.0f : w.pDir[s].w, b.w != 0.0f, true, true,
+            a.texEnabled ? sf.depth : 0.0f, sf.depth);
     w.pMeta[s] = meta;
 }
 __global__ __launch_bounds__(256) void k_finish(TraceArgs a) {

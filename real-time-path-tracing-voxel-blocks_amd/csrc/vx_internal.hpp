@@ -125,7 +125,9 @@ struct WaveBufs {
     float4 *sGeo;   // geometric normal xyz, translucency
     float4 *sAlb;   // albedo xyz, metallic
     float4 *sWo;    // wo xyz, skip-albedo flag
-    Reservoir *rSun, *rSky, *rRis, *rRR;
+    float4 *cSunSky;  // the sun and sky candidates' final weight sum and target pdf (x, y: sun; z, w: sky); a
+                      // candidate is selected iff its sample index (nIdx.x / .y) is >= 0 (trace.hip cand_res)
+    Reservoir *rRis, *rRR;
     int4 *nIdx;     // sun light index, sky light index, selected temporal tap, cached-tap mask
     float4 *ls0;    // selected light sample: direction xyz, solid-angle pdf
     float4 *ls1;    // radiance xyz, light type

@@ -769,8 +769,8 @@ int ensure_wave(vxpt_ctx *c, int set, size_t ns, bool &fresh) {
     if (dalloc(c, w.pPos, ns) || dalloc(c, w.pDir, ns) || dalloc(c, w.pThr, ns) || dalloc(c, w.pRad, ns) ||
         dalloc(c, w.pMeta, ns) || dalloc(c, w.pBop, ns) || dalloc(c, w.cRayO, ns) || dalloc(c, w.cRayD, ns) ||
         dalloc(c, w.cHit, ns) || dalloc(c, w.cT, ns) || dalloc(c, w.sPos, ns) || dalloc(c, w.sNrm, ns) ||
-        dalloc(c, w.sGeo, ns) || dalloc(c, w.sAlb, ns) || dalloc(c, w.sWo, ns) || dalloc(c, w.rSun, ns) ||
-        dalloc(c, w.rSky, ns) || dalloc(c, w.rRis, ns) || dalloc(c, w.rRR, ns) || dalloc(c, w.nIdx, ns) ||
+        dalloc(c, w.sGeo, ns) || dalloc(c, w.sAlb, ns) || dalloc(c, w.sWo, ns) || dalloc(c, w.cSunSky, ns) ||
+        dalloc(c, w.rRis, ns) || dalloc(c, w.rRR, ns) || dalloc(c, w.nIdx, ns) ||
         dalloc(c, w.ls0, ns) || dalloc(c, w.ls1, ns) || dalloc(c, w.tapPsv, ns) || dalloc(c, w.tapM, ns) ||
         dalloc(c, w.oHit, 4 * ns) ||
         dalloc(c, w.qO, 4 * ns) || dalloc(c, w.qD, 4 * ns) ||
