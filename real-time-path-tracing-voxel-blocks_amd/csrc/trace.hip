@@ -529,24 +529,34 @@ VX_D void seg_end(const TraceArgs &a, int s, int px, int py, int4 &meta, V3 segR
     }
 }
 
-// sPos: front spawn point, hit t; sWo.w: skip-albedo flag (1) + thin-film flag (2).  A thin
-// surface's back spawn point is in sBack (w = 1: the surface position -- the path's spawn point
-// -- is the back one, closesthit.cu:288 + 321).  front / back: the spawn points of rays leaving it.
+// The shaded surface between the shading kernels: sPos = front spawn point + hit t, sNrm = shading
+// normal + roughness, sAlb = albedo + flags (SF_*), sGeo = the geometric normal only where it differs
+// from the shading normal (SF_GEO), sWo = the view direction (recomputing segment 0's from the camera
+// ray in the readers was slower: k_restir's registers).  A thin surface's back spawn point is in sBack (w = 1: the surface
+// position -- the path's spawn point -- is the back one, closesthit.cu:288 + 321).  front / back:
+// the spawn points of rays leaving it.  (The translucency is read only where the surface is hit.)
+constexpr int SF_METAL = 1, SF_SKIPALB = 2, SF_THIN = 4, SF_GEO = 8;
 struct SurfX { V3 front, back; bool thin; };
-VX_D SurfS load_surf(const WaveBufs &w, int s, bool &skipAlbedo, SurfX *x = nullptr) {
+VX_D bool same_bits(V3 a, V3 b) {
+    return float_as_bits(a.x) == float_as_bits(b.x) && float_as_bits(a.y) == float_as_bits(b.y) &&
+           float_as_bits(a.z) == float_as_bits(b.z);
+}
+VX_D SurfS load_surf(const TraceArgs &a, int s, int px, int py, int seg, bool &skipAlbedo, SurfX *x = nullptr) {
+    const WaveBufs &w = a.wb;
     SurfS sf;
-    const float4 p = w.sPos[s], n = w.sNrm[s], g = w.sGeo[s], al = w.sAlb[s], wo = w.sWo[s];
+    const float4 p = w.sPos[s], n = w.sNrm[s], al = w.sAlb[s];
     sf.pos = xyz(p); sf.depth = p.w;
     sf.normal = xyz(n); sf.roughness = n.w;
-    sf.geoNormal = xyz(g); sf.translucency = g.w;
-    sf.albedo = xyz(al); sf.metallic = al.w != 0.0f;
-    sf.wo = xyz(wo);
-    const int fl = (int)wo.w;
-    skipAlbedo = (fl & 1) != 0;
+    const int fl = float_as_bits(al.w);
+    sf.geoNormal = (fl & SF_GEO) ? xyz(w.sGeo[s]) : sf.normal;
+    sf.translucency = 0.0f;
+    sf.albedo = xyz(al); sf.metallic = (fl & SF_METAL) != 0;
+    sf.wo = xyz(w.sWo[s]);
+    skipAlbedo = (fl & SF_SKIPALB) != 0;
     if (x) {
         x->front = sf.pos;
         x->back = sf.pos;
-        x->thin = (fl & 2) != 0;
+        x->thin = (fl & SF_THIN) != 0;
         if (x->thin) {
             const float4 b = w.sBack[s];
             x->back = xyz(b);
@@ -848,9 +858,12 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.sPos[s] = f4(frontPos, h.t);
     if (thin) w.sBack[s] = f4(backPos, dot(swi, sf.normal) > 0.0f ? 0.0f : 1.0f);
     w.sNrm[s] = f4(sf.normal, sf.roughness);
-    w.sGeo[s] = f4(sf.geoNormal, sf.translucency);
-    w.sAlb[s] = f4(sf.albedo, sf.metallic ? 1.0f : 0.0f);
-    w.sWo[s] = f4(wo, (skipAlbedo ? 1.0f : 0.0f) + (thin ? 2.0f : 0.0f));
+    const bool geoDiff = !same_bits(sf.geoNormal, sf.normal);
+    if (geoDiff) w.sGeo[s] = f4(sf.geoNormal, 0.0f);
+    const int sfl = (sf.metallic ? SF_METAL : 0) | (skipAlbedo ? SF_SKIPALB : 0) | (thin ? SF_THIN : 0) |
+                    (geoDiff ? SF_GEO : 0);
+    w.sAlb[s] = f4(sf.albedo, bits_as_float(sfl));
+    w.sWo[s] = f4(wo, 0.0f);
     if (a.segments > 1) w.pBop[s] = f4(sbop, terminate ? 1.0f : 0.0f);
     w.cSunSky[s] = make_float4(sunRes.weightSum, sunRes.targetPdf, skyRes.weightSum, skyRes.targetPdf);
     w.nIdx[s] = make_int4(sunSel, skySel, -1, 0);
@@ -882,7 +895,7 @@ VX_D Reservoir cand_res(uint32_t light, int idx, int mapW, int mapH, float weigh
 
 // BRDF candidate from its traced ray, RIS over {local, sun, sky, BRDF}, visibility ray
 template <bool MESH>
-VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
+VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
@@ -890,7 +903,7 @@ VX_D void nee_slot(const TraceArgs &a, int s, QRays &qr) {
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(w, s, skipAlbedo, &sp);
+    const SurfS sf = load_surf(a, s, px, py, seg, skipAlbedo, &sp);
     const SkyDev &k = a.sky;
     Rng rng{&a.bn, px, py, a.iterationIndex, meta.y};
     const int nLocal = (MESH && a.numLights > 0) ? 8 : 0;
@@ -1008,7 +1021,7 @@ template <bool MESH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 1 : VX_WPE_NEE))) void k_nee(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
-    nee_slot<MESH>(a, blockIdx.x * 256 + threadIdx.x, qr);
+    nee_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
     block_enqueue(a, 4 * seg + 2, qr);
 }
 
@@ -1037,7 +1050,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(w, s, skipAlbedo, &sp);
+    const SurfS sf = load_surf(a, s, px, py, seg, skipAlbedo, &sp);
     const bool hasLocal = MESH && a.numLights > 0;
     Reservoir ris = w.rRis[s];
     LSample ls = load_ls(w, s);
@@ -1177,7 +1190,7 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(w, s, skipAlbedo, &sp);
+    const SurfS sf = load_surf(a, s, px, py, 0, skipAlbedo, &sp);
     Reservoir rr = w.rRR[s];
     const LSample ls = load_ls(w, s);
     const int4 idx = w.nIdx[s];
