@@ -50,6 +50,13 @@ namespace {
 // F_EMPTY: the pixel's reservoir is the empty one (a seg-0 miss or specular hit); k_finish stores it, so
 // a pass's first half never writes reservoirs (the previous pass's temporal reuse may still read them)
 constexpr int F_ALIVE = 1, F_HFD = 2, F_NEE = 4, F_RESTIR = 8, F_EMPTY = 16;
+// the path's meta word, unpacked as (flags, sampler dimension, total segments, diffuse segments); stored
+// as 8 bytes (flags and the two counts share a word: every kernel reads and writes it)
+VX_D int4 load_meta(const WaveBufs &w, int s) {
+    const int2 m = w.pMeta[s];
+    return make_int4(m.x & 0xFF, m.y, (m.x >> 8) & 0xFF, (m.x >> 16) & 0xFF);
+}
+VX_D void store_meta(const WaveBufs &w, int s, int4 m) { w.pMeta[s] = make_int2(m.x | (m.z << 8) | (m.w << 16), m.y); }
 constexpr float kFltMax = 3.402823466e+38f;
 
 VX_D bool slot_pixel(const TraceArgs &a, int s, int &px, int &py) {
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOS
                 w.pPos[s] = f4(o, kRayMax);
                 w.pDir[s] = f4(d, 0.0f);
             }
-            w.pMeta[s] = make_int4(F_ALIVE, rng.idx, 0, 0);
+            store_meta(w, s, make_int4(F_ALIVE, rng.idx, 0, 0));
         } else {
             active = (w.pMeta[s].x & F_ALIVE) != 0;
             if (active) {
@@ -285,11 +292,13 @@ VX_D void block_enqueue(const TraceArgs &a, int q, const QRays &r) {
     }
 }
 
+// tOnly (closest-hit rays of voxel worlds, whose one reader needs hit / miss only): the distance
+// alone, kRayMax for a miss (a voxel hit is closer than the world's diagonal)
 template <bool OCC>
-VX_D void store_result(const WaveBufs &w, int id, int rc, const Hit &h) {
+VX_D void store_result(const WaveBufs &w, int id, int rc, const Hit &h, bool tOnly = false) {
     if (!OCC) {
         const Hit r = rc == DdaEvent ? h : Hit{0, 0, 0, 0, -1, 0, kRayMax};
-        w.cHit[id] = pack_hit(r);
+        if (!tOnly) w.cHit[id] = pack_hit(r);
         w.cT[id] = r.t;
     } else {
         w.oHit[id] = rc == DdaEvent ? 1 : 0;
@@ -336,7 +345,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_QUEU
     stat_ray((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), live, iters[0] + iters[1] + iters[2] + iters[3],
              live ? st.r.dy : 0.0f, rc == DdaEvent);
 #endif
-    if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h);
+    if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h, a.mesh.nInst == 0);
     // unfinished walks -> straggler queue
     const bool defer = live && rc == DdaRun;
     const unsigned long long m = __ballot(defer);
@@ -394,7 +403,7 @@ __global__ __launch_bounds__(256) void k_persist(TraceArgs a, int q, int refill)
                     h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
                     const int rc = dda_begin<OCC, BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
                     if (rc == DdaRun) active = true;
-                    else store_result<OCC>(w, id, rc, h);
+                    else store_result<OCC>(w, id, rc, h, a.mesh.nInst == 0);
                 }
             }
         }
@@ -405,7 +414,7 @@ __global__ __launch_bounds__(256) void k_persist(TraceArgs a, int q, int refill)
         if (active) {
             const int rc = dda_iter<OCC, BOX>(a.world, st, h, nullptr);
             if (rc != DdaRun) {
-                store_result<OCC>(w, id, rc, h);
+                store_result<OCC>(w, id, rc, h, a.mesh.nInst == 0);
                 active = false;
             }
         }
@@ -450,7 +459,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESU
         stat_wave(5, live, iters);
         stat_ray(5, live, iters[0] + iters[1] + iters[2] + iters[3], live ? st.r.dy : 0.0f, rc == DdaEvent);
 #endif
-        if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h);
+        if (live && rc != DdaRun) store_result<OCC>(w, id, rc, h, a.mesh.nInst == 0);
         const bool defer = live && rc == DdaRun;
         const unsigned long long m = __ballot(defer);
         if (m) {
@@ -648,7 +657,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
-    int4 meta = w.pMeta[s];
+    int4 meta = load_meta(w, s);
     if (!(meta.x & F_ALIVE)) return;
     meta.x &= ~(F_NEE | F_RESTIR);
     const size_t pi = (size_t)py * a.W + px;
@@ -678,7 +687,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             store_rec_sky(a, pi, kRayMax);
         }
         seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false, seg == 0, 0.0f, primaryDist);
-        w.pMeta[s] = meta;
+        store_meta(w, s, meta);
         return;
     }
 
@@ -703,7 +712,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         }
         if (seg == 0) primaryDist = h.t;  // the primary distance (no reservoir is stored)
         seg_end(a, s, px, py, meta, e, V3(1.0f), 0.0f, true, false, seg == 0, 0.0f, primaryDist);
-        w.pMeta[s] = meta;
+        store_meta(w, s, meta);
         return;
     }
     const bool thin = m.thin != 0;
@@ -769,7 +778,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         if (seg == 0) meta.x |= F_EMPTY;
         seg_end(a, s, px, py, meta, V3(0.0f), sbop, spdf, terminate, false, seg == 0, travelled);
         meta.y = rng.idx;
-        w.pMeta[s] = meta;
+        store_meta(w, s, meta);
         return;
     }
 
@@ -869,7 +878,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.nIdx[s] = make_int4(sunSel, skySel, -1, 0);
     meta.x |= F_NEE | (seg == 0 ? F_RESTIR : 0);
     meta.y = rng.idx;
-    w.pMeta[s] = meta;
+    store_meta(w, s, meta);
 }
 
 template <bool MESH>
@@ -899,7 +908,7 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
-    int4 meta = w.pMeta[s];
+    int4 meta = load_meta(w, s);
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
     SurfX sp;
@@ -938,7 +947,8 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         const float4 cd = w.cRayD[s];
         if (cd.w >= 0.0f) {
             const V3 sd = xyz(cd);
-            const Hit bh = unpack_hit(w.cHit[s], w.cT[s]);
+            // voxel worlds: hit / miss from the distance alone (store_result's tOnly)
+            const Hit bh = MESH ? unpack_hit(w.cHit[s], w.cT[s]) : Hit{w.cT[s] != kRayMax ? 1 : 0, 0, 0, 0, 0, 0, 0.0f};
             if (MESH && bh.hit && bh.face == 15) {
                 // __closesthit__bsdf_light (closesthit.cu:854-900): an emissive instance's triangle is
                 // light (its first light + the mesh's triangle index)
@@ -1014,7 +1024,7 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     w.rRis[s] = ris;
     store_ls(w, s, ls);
     meta.y = rng.idx;
-    w.pMeta[s] = meta;
+    store_meta(w, s, meta);
 }
 
 template <bool MESH>
@@ -1046,7 +1056,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
-    int4 meta = w.pMeta[s];
+    int4 meta = load_meta(w, s);
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
     SurfX sp;
@@ -1064,7 +1074,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         if (ls.type != LtInvalid && ris.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, ris);
         const float4 b = w.pBop[s];
         seg_end(a, s, px, py, meta, segRad, xyz(b), w.pDir[s].w, b.w != 0.0f, true, false);
-        w.pMeta[s] = meta;
+        store_meta(w, s, meta);
         return;
     }
 
@@ -1162,12 +1172,13 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         qr.x0 = tmax;
     }
     w.rRR[s] = rr;
-    store_ls(w, s, ls);
-    w.nIdx[s] = make_int4(0, 0, selLoop, (int)cached);
-    w.tapPsv[s] = make_float4(psv0, psv1, psv2, 0.0f);
-    w.tapM[s] = make_float4(tapM0, tapM1, tapM2, 0.0f);
+    // for k_finish: the taps' target pdfs and M, the selected tap and the accepted-tap mask (the
+    // selected light sample is not stored: with a tap selected it is the combined reservoir's light,
+    // which k_finish rebuilds from the same operands; else the RIS sample k_nee stored stays)
+    w.tapPsv[s] = make_float4(psv0, psv1, psv2, tapM0);
+    w.tapM[s] = make_float4(tapM1, tapM2, bits_as_float(selLoop), bits_as_float((int)cached));
     meta.y = rng.idx;
-    w.pMeta[s] = meta;
+    store_meta(w, s, meta);
 }
 
 template <bool MESH>
@@ -1181,7 +1192,7 @@ __global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
 // seg 0: bias-corrected ReSTIR weight, final visibility, shading, reservoir store
 VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     const WaveBufs &w = a.wb;
-    int4 meta = w.pMeta[s];
+    int4 meta = load_meta(w, s);
     const size_t pi = (size_t)py * a.W + px;
     if (meta.x & F_EMPTY) {
         a.resCur[pi] = empty_res();
@@ -1192,17 +1203,18 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     SurfX sp;
     const SurfS sf = load_surf(a, s, px, py, 0, skipAlbedo, &sp);
     Reservoir rr = w.rRR[s];
-    const LSample ls = load_ls(w, s);
-    const int4 idx = w.nIdx[s];
-    const int selLoop = idx.z;
-    const unsigned cached = (unsigned)idx.w;
+    const float4 psv4 = w.tapPsv[s], m4 = w.tapM[s];
+    const int selLoop = float_as_bits(m4.z);
+    const unsigned cached = (unsigned)float_as_bits(m4.w);
+    LSample ls = invalid_ls();  // restir_slot's selection: a tap's light (from rr) or the RIS sample
+    if (selLoop >= 0) light_from_res(a, ls, rr, sf.pos, a.mesh.nInst > 0 && a.numLights > 0);
+    else ls = load_ls(w, s);
     if (rr.lightData != 0) {
-        const float4 psv4 = w.tapPsv[s], m4 = w.tapM[s];
         float piv = rr.targetPdf, piSum = rr.targetPdf * 1;
         for (int i = 0; i < 3; ++i) {
             if ((cached & (1u << i)) == 0) continue;
             float psv = i == 0 ? psv4.x : (i == 1 ? psv4.y : psv4.z);
-            const float M = i == 0 ? m4.x : (i == 1 ? m4.y : m4.z);
+            const float M = i == 0 ? psv4.w : (i == 1 ? m4.x : m4.y);
             if (w.oHit[4 * s + 1 + i]) psv = 0.0f;
             if (selLoop == i) piv = psv;
             piSum += psv * M;
@@ -1223,7 +1235,7 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     const float4 b = one ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : w.pBop[s];
     seg_end(a, s, px, py, meta, segRad, xyz(b), one ? 1.0f : w.pDir[s].w, b.w != 0.0f, true, true,
             a.texEnabled ? sf.depth : 0.0f, sf.depth);
-    w.pMeta[s] = meta;
+    store_meta(w, s, meta);
 }
 __global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
     const int s = blockIdx.x * 256 + threadIdx.x;

@@ -113,7 +113,7 @@ struct WaveBufs {
     float4 *pDir;   // ray direction xyz, BSDF pdf
     float4 *pThr;   // throughput xyz
     float4 *pRad;   // accumulated radiance xyz
-    int4 *pMeta;    // flags, sampler dimension, total segments, diffuse segments
+    int2 *pMeta;    // x: flags | total segments << 8 | diffuse segments << 16, y: sampler dimension (trace.hip load_meta)
     float4 *pBop;   // BSDF weight of the sampled continuation xyz, terminate flag
     // closest-hit queue (camera / path / BRDF-candidate rays) and its results
     float4 *cRayO, *cRayD;  // o xyz + tmax (< 0: inactive), d xyz
