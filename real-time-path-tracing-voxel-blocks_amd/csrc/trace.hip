@@ -50,13 +50,16 @@ namespace {
 // F_EMPTY: the pixel's reservoir is the empty one (a seg-0 miss or specular hit); k_finish stores it, so
 // a pass's first half never writes reservoirs (the previous pass's temporal reuse may still read them)
 constexpr int F_ALIVE = 1, F_HFD = 2, F_NEE = 4, F_RESTIR = 8, F_EMPTY = 16;
-// the path's meta word, unpacked as (flags, sampler dimension, total segments, diffuse segments); stored
-// as 8 bytes (flags and the two counts share a word: every kernel reads and writes it)
+// the path's meta word, unpacked as (flags F_* | surface flags SF_* << 8, sampler dimension, total
+// segments, diffuse segments); stored as 8 bytes (the flags and the two counts share a word: every
+// kernel reads and writes it)
 VX_D int4 load_meta(const WaveBufs &w, int s) {
     const int2 m = w.pMeta[s];
-    return make_int4(m.x & 0xFF, m.y, (m.x >> 8) & 0xFF, (m.x >> 16) & 0xFF);
+    return make_int4((m.x & 0xFF) | (((m.x >> 24) & 0xF) << 8), m.y, (m.x >> 8) & 0xFF, (m.x >> 16) & 0xFF);
 }
-VX_D void store_meta(const WaveBufs &w, int s, int4 m) { w.pMeta[s] = make_int2(m.x | (m.z << 8) | (m.w << 16), m.y); }
+VX_D void store_meta(const WaveBufs &w, int s, int4 m) {
+    w.pMeta[s] = make_int2((m.x & 0xFF) | (m.z << 8) | (m.w << 16) | (((m.x >> 8) & 0xF) << 24), m.y);
+}
 constexpr float kFltMax = 3.402823466e+38f;
 
 VX_D bool slot_pixel(const TraceArgs &a, int s, int &px, int &py) {
@@ -550,13 +553,18 @@ VX_D bool same_bits(V3 a, V3 b) {
     return float_as_bits(a.x) == float_as_bits(b.x) && float_as_bits(a.y) == float_as_bits(b.y) &&
            float_as_bits(a.z) == float_as_bits(b.z);
 }
-VX_D SurfS load_surf(const TraceArgs &a, int s, int px, int py, int seg, bool &skipAlbedo, SurfX *x = nullptr) {
+// seg 0: the shading normal, roughness and albedo are the G-buffer's (pixel order, the same values;
+// recomputing the view direction from the camera ray as well was slower); flags = the meta word's SF_*
+VX_D SurfS load_surf(const TraceArgs &a, int s, int px, int py, int seg, int meta, bool &skipAlbedo,
+                     SurfX *x = nullptr) {
     const WaveBufs &w = a.wb;
     SurfS sf;
-    const float4 p = w.sPos[s], n = w.sNrm[s], al = w.sAlb[s];
+    const size_t pi = (size_t)py * a.W + px;
+    const float4 p = w.sPos[s], n = seg == 0 ? a.cur.normalRough[pi] : w.sNrm[s];
+    const float4 al = seg == 0 ? a.cur.albedo[pi] : w.sAlb[s];
     sf.pos = xyz(p); sf.depth = p.w;
     sf.normal = xyz(n); sf.roughness = n.w;
-    const int fl = float_as_bits(al.w);
+    const int fl = (meta >> 8) & 0xF;
     sf.geoNormal = (fl & SF_GEO) ? xyz(w.sGeo[s]) : sf.normal;
     sf.translucency = 0.0f;
     sf.albedo = xyz(al); sf.metallic = (fl & SF_METAL) != 0;
@@ -866,12 +874,15 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     }
     w.sPos[s] = f4(frontPos, h.t);
     if (thin) w.sBack[s] = f4(backPos, dot(swi, sf.normal) > 0.0f ? 0.0f : 1.0f);
-    w.sNrm[s] = f4(sf.normal, sf.roughness);
+    if (seg > 0) {  // segment 0's are in the G-buffer planes just written
+        w.sNrm[s] = f4(sf.normal, sf.roughness);
+        w.sAlb[s] = f4(sf.albedo, 0.0f);
+    }
     const bool geoDiff = !same_bits(sf.geoNormal, sf.normal);
     if (geoDiff) w.sGeo[s] = f4(sf.geoNormal, 0.0f);
     const int sfl = (sf.metallic ? SF_METAL : 0) | (skipAlbedo ? SF_SKIPALB : 0) | (thin ? SF_THIN : 0) |
                     (geoDiff ? SF_GEO : 0);
-    w.sAlb[s] = f4(sf.albedo, bits_as_float(sfl));
+    meta.x = (meta.x & 0xFF) | (sfl << 8);
     w.sWo[s] = f4(wo, 0.0f);
     if (a.segments > 1) w.pBop[s] = f4(sbop, terminate ? 1.0f : 0.0f);
     w.cSunSky[s] = make_float4(sunRes.weightSum, sunRes.targetPdf, skyRes.weightSum, skyRes.targetPdf);
@@ -912,7 +923,7 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(a, s, px, py, seg, skipAlbedo, &sp);
+    const SurfS sf = load_surf(a, s, px, py, seg, meta.x, skipAlbedo, &sp);
     const SkyDev &k = a.sky;
     Rng rng{&a.bn, px, py, a.iterationIndex, meta.y};
     const int nLocal = (MESH && a.numLights > 0) ? 8 : 0;
@@ -1060,7 +1071,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     if (!(meta.x & F_NEE)) return;
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(a, s, px, py, seg, skipAlbedo, &sp);
+    const SurfS sf = load_surf(a, s, px, py, seg, meta.x, skipAlbedo, &sp);
     const bool hasLocal = MESH && a.numLights > 0;
     Reservoir ris = w.rRis[s];
     LSample ls = load_ls(w, s);
@@ -1201,7 +1212,7 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(a, s, px, py, 0, skipAlbedo, &sp);
+    const SurfS sf = load_surf(a, s, px, py, 0, meta.x, skipAlbedo, &sp);
     Reservoir rr = w.rRR[s];
     const float4 psv4 = w.tapPsv[s], m4 = w.tapM[s];
     const int selLoop = float_as_bits(m4.z);
