@@ -595,15 +595,25 @@ VX_D void mis_params(const SkyDev &k, const SurfS &sf, bool thin, int nLocal, in
     brdfMis = 1.0f / nMis;
 }
 
-VX_D void store_ls(const WaveBufs &w, int s, const LSample &ls) {
-    w.ls0[s] = f4(ls.position, ls.solidAnglePdf);
-    w.ls1[s] = f4(ls.radiance, (float)ls.type);
-}
-VX_D LSample load_ls(const WaveBufs &w, int s) {
-    const float4 a = w.ls0[s], b = w.ls1[s];
-    return LSample{xyz(a), xyz(b), a.w, (int)b.w};
-}
 VX_D LSample invalid_ls() { return LSample{V3(0.f), V3(0.f), 0.f, LtInvalid}; }
+// A light sample between kernels: its position / direction and, for the sun and the sky, the map
+// texel it was built from (tex: the index sun_ls / sky_ls took), from which its radiance and pdf
+// are rebuilt with the same arithmetic; a local light's radiance and pdf are stored (ls1).
+VX_D void store_ls(const WaveBufs &w, int s, const LSample &ls, int tex) {
+    w.ls0[s] = f4(ls.position, bits_as_float((ls.type << 24) | (tex & 0xFFFFFF)));
+    if (ls.type == LtLocal) w.ls1[s] = f4(ls.radiance, ls.solidAnglePdf);
+}
+VX_D LSample load_ls(const TraceArgs &a, int s) {
+    const WaveBufs &w = a.wb;
+    const float4 p = w.ls0[s];
+    const int tb = float_as_bits(p.w), type = (tb >> 24) & 0xFF, tex = tb & 0xFFFFFF;
+    if (type == LtLocal) {
+        const float4 b = w.ls1[s];
+        return LSample{xyz(p), xyz(b), b.w, LtLocal};
+    }
+    if (type == LtInvalid) return invalid_ls();
+    return type == LtSun ? sun_ls_at(a.sky, tex, xyz(p)) : sky_ls_at(a.sky, tex, xyz(p));
+}
 
 VX_D V3 shade_light(const SurfS &sf, bool skipAlbedo, const LSample &ls, const Reservoir &r) {
     const V3 alb = skipAlbedo ? V3(1.0f) : sf.albedo;  // closesthit.cu:829-841
@@ -950,11 +960,13 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
 
     Reservoir brdfRes = empty_res();
     LSample brdfLs = invalid_ls();
+    int brdfTex = 0;  // the BRDF candidate's sun / sky map texel
     {
         float lightSrcPdf = 0.0f;
         uint32_t li = kInvalidLight;
         V2 uv(0.0f, 0.0f);
         LSample cand = invalid_ls();
+        int candTex = 0;
         const float4 cd = w.cRayD[s];
         if (cd.w >= 0.0f) {
             const V3 sd = xyz(cd);
@@ -989,6 +1001,7 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
                     const int l = y * k.sunW + x;
                     cand = sun_ls(k, l);
                     cand.position = sd;
+                    candTex = l;
                     lightSrcPdf = k.sunAlias[l].p;
                 } else {
                     li = kSkyLight;
@@ -997,6 +1010,7 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
                     const int l = y * k.skyW + x;
                     cand = sky_ls(k, l);
                     cand.position = sd;
+                    candTex = l;
                     lightSrcPdf = k.skyAlias[l].p;
                 }
             }
@@ -1006,7 +1020,10 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             float blended, tp;
             mis_and_target(sf, cand, lightSrcPdf, misW, brdfMis, blended, tp);
             const float rr = rng.next();
-            if (stream_sample(brdfRes, li, uv, rr, tp, 1.0f / blended)) brdfLs = cand;
+            if (stream_sample(brdfRes, li, uv, rr, tp, 1.0f / blended)) {
+                brdfLs = cand;
+                brdfTex = candTex;
+            }
         }
     }
     finalize(brdfRes, 1.0f, (float)nMis);
@@ -1020,6 +1037,7 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     finalize(ris, 1.0f, 1.0f);
     ris.M = 1;
     const LSample ls = selBrdf ? brdfLs : (selSky ? skyLs : (selSun ? sunLs : localLs));
+    const int lsTex = selBrdf ? brdfTex : (selSky ? idx.y : (selSun ? idx.x : 0));
     const bool trace = ls.type != LtInvalid && ris.lightData != 0;
     if (trace) {
         V3 dir;
@@ -1032,8 +1050,9 @@ VX_D void nee_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         qr.d0 = dir;
         qr.x0 = tmax;
     }
-    w.rRis[s] = ris;
-    store_ls(w, s, ls);
+    w.rRis[s] = make_float4(bits_as_float((int)ris.lightData), bits_as_float((int)ris.uvData), ris.weightSum,
+                            ris.targetPdf);
+    store_ls(w, s, ls, lsTex);
     meta.y = rng.idx;
     store_meta(w, s, meta);
 }
@@ -1073,8 +1092,9 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     SurfX sp;
     const SurfS sf = load_surf(a, s, px, py, seg, meta.x, skipAlbedo, &sp);
     const bool hasLocal = MESH && a.numLights > 0;
-    Reservoir ris = w.rRis[s];
-    LSample ls = load_ls(w, s);
+    const float4 ris4 = w.rRis[s];
+    Reservoir ris{(uint32_t)float_as_bits(ris4.x), (uint32_t)float_as_bits(ris4.y), ris4.z, ris4.w, 1.0f};
+    LSample ls = load_ls(a, s);
     bool visible = false;
     if (ls.type != LtInvalid && ris.lightData != 0) {
         visible = !w.oHit[4 * s];
@@ -1219,7 +1239,7 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     const unsigned cached = (unsigned)float_as_bits(m4.w);
     LSample ls = invalid_ls();  // restir_slot's selection: a tap's light (from rr) or the RIS sample
     if (selLoop >= 0) light_from_res(a, ls, rr, sf.pos, a.mesh.nInst > 0 && a.numLights > 0);
-    else ls = load_ls(w, s);
+    else ls = load_ls(a, s);
     if (rr.lightData != 0) {
         float piv = rr.targetPdf, piSum = rr.targetPdf * 1;
         for (int i = 0; i < 3; ++i) {

@@ -649,6 +649,25 @@ VX_D LSample sky_ls(const SkyDev &k, int idx) {
     return s;
 }
 
+// the same samples with the position given (a stored light sample's direction, trace.hip load_ls)
+VX_D LSample sun_ls_at(const SkyDev &k, int idx, V3 dir) {
+    const int sx = idx % k.sunW, sy = idx / k.sunW;
+    LSample s;
+    s.solidAnglePdf = (k.sunW * k.sunH) / (kTwoPi * (1.0f - k.sunCosMax));
+    s.position = dir;
+    s.radiance = ld3(k.sun, (size_t)clampi(sy, 0, k.sunH - 1) * k.sunW + clampi(sx, 0, k.sunW - 1));
+    s.type = LtSun;
+    return s;
+}
+VX_D LSample sky_ls_at(const SkyDev &k, int idx, V3 dir) {
+    LSample s;
+    s.solidAnglePdf = (k.skyW * k.skyH) / (4.0f * kPi);
+    s.position = dir;
+    s.radiance = ld3(k.sky, (size_t)idx);
+    s.type = LtSky;
+    return s;
+}
+
 struct SurfS {
     V3 pos, normal, geoNormal, albedo, wo;
     float depth, roughness, translucency;

@@ -127,10 +127,11 @@ struct WaveBufs {
     float4 *sWo;    // wo xyz, skip-albedo flag
     float4 *cSunSky;  // the sun and sky candidates' final weight sum and target pdf (x, y: sun; z, w: sky); a
                       // candidate is selected iff its sample index (nIdx.x / .y) is >= 0 (trace.hip cand_res)
-    Reservoir *rRis, *rRR;
+    float4 *rRis;   // the RIS reservoir (lightData, uvData, weightSum, targetPdf; M = 1)
+    Reservoir *rRR;
     int4 *nIdx;     // sun light index, sky light index, selected temporal tap, cached-tap mask
-    float4 *ls0;    // selected light sample: direction xyz, solid-angle pdf
-    float4 *ls1;    // radiance xyz, light type
+    float4 *ls0;    // selected light sample: position / direction xyz, type << 24 | map texel (sun / sky)
+    float4 *ls1;    // local lights only: radiance xyz, solid-angle pdf (trace.hip store_ls)
     float4 *tapPsv; // target pdf of the selection at the three temporal taps, first-visibility flag
     float4 *tapM;   // the taps' clamped M
     // instanced meshes: back spawn point of a thin-film surface (xyz, w = thin
