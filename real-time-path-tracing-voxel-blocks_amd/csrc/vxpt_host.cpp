@@ -456,7 +456,7 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.nBricks = c->nBricks;
     // a brick walk yields its lanes back to the outer loop after 4 crossings (fewer lanes idle behind
     // long in-brick walks; C3 trace 6.44 -> 6.27 ms per frame)
-    static const int brickSteps = getenv("VXPT_BRICK_STEPS") ? atoi(getenv("VXPT_BRICK_STEPS")) : 4;
+    static const int brickSteps = getenv("VXPT_BRICK_STEPS") ? atoi(getenv("VXPT_BRICK_STEPS")) : 3;
     w.brickSteps = brickSteps;
     static const int camSteps = getenv("VXPT_CAM_STEPS") ? atoi(getenv("VXPT_CAM_STEPS")) : 10;
     w.brickStepsCam = camSteps;
