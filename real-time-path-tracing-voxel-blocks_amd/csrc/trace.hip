@@ -163,13 +163,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOS
             d = camera_ray(a, px, py);
             rng.idx = 2;
             // the path's throughput (1) and radiance (0) are not stored: segment 0's seg_end starts
-            // from them (first = true); the camera ray itself only for the kernels that read it
-            // (mesh slots, the primary-only G-buffer) -- k_shade<false> recomputes it (camera_ray)
-            if (a.mesh.nInst > 0 || a.primaryOnly) {
-                w.pPos[s] = f4(o, kRayMax);
-                w.pDir[s] = f4(d, 0.0f);
+            // from them (first = true); the camera ray itself only for the mesh kernels that read it
+            // -- k_shade<false> and the primary-only G-buffer recompute it (camera_ray)
+            if (!a.primaryOnly) {
+                if (a.mesh.nInst > 0) {
+                    w.pPos[s] = f4(o, kRayMax);
+                    w.pDir[s] = f4(d, 0.0f);
+                }
+                store_meta(w, s, make_int4(F_ALIVE, rng.idx, 0, 0));
             }
-            store_meta(w, s, make_int4(F_ALIVE, rng.idx, 0, 0));
         } else {
             active = (w.pMeta[s].x & F_ALIVE) != 0;
             if (active) {
@@ -1343,7 +1345,7 @@ __global__ __launch_bounds__(256) void k_primary_gbuffer(TraceArgs a) {
     const WaveBufs &w = a.wb;
     const size_t pi = (size_t)py * a.W + px;
     const Hit h = unpack_hit(w.cHit[s], w.cT[s]);
-    const V3 o = xyz(w.pPos[s]), d = xyz(w.pDir[s]);
+    const V3 o = a.cam.pos, d = camera_ray(a, px, py);  // the camera ray, as k_closest traced it
     if (!h.hit) {
         a.resCur[pi] = empty_res();
         a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
