@@ -43,6 +43,9 @@
 #ifndef VX_WPE_CLOSEST
 #define VX_WPE_CLOSEST 8
 #endif
+#ifndef VX_WPE_FINISH
+#define VX_WPE_FINISH 1
+#endif
 
 namespace vx {
 namespace {
@@ -1270,7 +1273,7 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
             a.texEnabled ? sf.depth : 0.0f, sf.depth);
     store_meta(w, s, meta);
 }
-__global__ __launch_bounds__(256) void k_finish(TraceArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_FINISH))) void k_finish(TraceArgs a) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
