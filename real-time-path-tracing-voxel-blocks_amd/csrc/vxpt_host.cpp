@@ -254,15 +254,18 @@ struct vxpt_ctx {
     // (the previous frame's final G-buffer, Denoiser.cu:394-407), so the frame
     // end hands the last slot to the denoiser by index instead of copying planes.
     // Two more slots let first halves (camera rays .. NEE visibility, which read no previous pass)
-    // run ahead while up to two second halves still read their previous passes' slots.
-    GSlot gb[5];
+    // run ahead while up to two second halves still read their previous passes' slots, and one more
+    // keeps the denoiser's previous history slot while a split denoiser chain may still read it.
+    GSlot gb[6];
     int last = 0;              // slot of the most recent trace output
     int tracePrev = 0;         // slot the most recent trace read as its previous pass
     int tracePrev2 = 0;        // the one before (read by the second half before that)
     int hist = 2;              // denoiser history slot (zero at frame 0)
+    int histOld = 2;           // the one before (the history of the most recently enqueued denoiser run)
     float4 *illum = nullptr;   // the most recent pass's radiance (one of illumSet)
     float4 *illumSet[kMaxSets] = {};  // per wavefront state set
     float4 *accum = nullptr, *motion = nullptr;
+    float4 *accumBuf[2] = {};  // accum alternates between these per accumulation (first pass picks the other)
     // the motion plane holds only zeros (allocated zeroed; the trace stores zeros, the world is static)
     // until a host write: the trace then skips its zero stores
     bool motionZero = true;
@@ -287,6 +290,12 @@ struct vxpt_ctx {
     int lastSet = 0;           // the set of the most recent pass
     hipStream_t frontStream = nullptr;
     hipEvent_t frontDone[kMaxSets] = {}, backDone[kMaxSets] = {}, frontGate = nullptr;
+    // split denoiser chains (vxpt_render_frames): the firefly stage on the context stream, the rest
+    // (temporal .. a-trous) on dnStream beside the next frame's first pass
+    hipStream_t dnStream = nullptr;
+    hipEvent_t dnStart = nullptr, dnDone = nullptr;
+    bool dnOutstanding = false;  // a split chain not yet waited for by the context stream
+    int dnBacks = 0;             // second halves enqueued since it
     int numCU = 256;
     std::vector<void *> allocs;
 
@@ -829,7 +838,8 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     // the slot this pass writes: not the previous pass's (its temporal taps), not the denoiser's
     // history, and not the one the previous pass's second half may still be reading
     int next = 0;
-    while (next == c->last || next == c->hist || next == c->tracePrev || next == c->tracePrev2) ++next;
+    while (next == c->last || next == c->hist || next == c->histOld || next == c->tracePrev || next == c->tracePrev2)
+        ++next;
     const GSlot &cur = c->gb[next], &prev = c->gb[c->last];
     a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material, cur.rec};
     a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material, prev.rec};
@@ -845,7 +855,10 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     const size_t n = (size_t)c->W * c->H;
     a.resCur = c->res + (size_t)(((it % 2) + 2) % 2) * n;
     a.resPrev = c->res + (size_t)((((it + 1) % 2) + 2) % 2) * n;
-    a.accum = accumulate ? c->accum : nullptr;
+    // the first pass of an accumulation writes the other buffer: a denoiser chain still reading the
+    // previous accumulation (split chains) keeps its input; trace_back makes it current
+    a.accum = accumulate ? (accumFirst ? (c->accum == c->accumBuf[0] ? c->accumBuf[1] : c->accumBuf[0]) : c->accum)
+                         : nullptr;
     a.accumScale = accumScale;
     a.accumFirst = accumFirst ? 1 : 0;
     a.W = c->W; a.H = c->H;
@@ -913,6 +926,14 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
 // The second half of the planned pass, on the context stream, and the ring bookkeeping.
 int trace_back(vxpt_ctx *c, const PassPlan &pl) {
     const int set = pl.set;
+    // the second half after a split denoiser chain's first overlapping one waits for it: everything
+    // behind it on this stream -- the next accumulation into the chain's input, the next firefly
+    // stage, and (through their backDone events) the first halves that may reuse its G-buffer
+    // slots -- then follows the chain
+    if (c->dnOutstanding && ++c->dnBacks == 2) {
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->dnDone, 0));
+        c->dnOutstanding = false;
+    }
     if (!pl.a.primaryOnly) {
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[set], 0));
         HIPCHK(c, launch_trace_back(pl.a, c->stream, c->haloPending ? c->haloDone : nullptr));
@@ -924,6 +945,7 @@ int trace_back(vxpt_ctx *c, const PassPlan &pl) {
     c->tracePrev = c->last;
     c->last = pl.next;
     c->illum = c->illumSet[set];
+    if (pl.a.accum) c->accum = pl.a.accum;
     c->lastSet = set;
     ++c->passCount;
     return 0;
@@ -941,6 +963,7 @@ int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accu
 // the slot the frame's last trace wrote becomes the denoiser's history slot
 // (whole planes, so the rows a band received from its neighbours come along)
 hipError_t history_copies(vxpt_ctx *c) {
+    c->histOld = c->hist;
     c->hist = c->last;
     return hipSuccess;
 }
@@ -954,48 +977,66 @@ hipError_t firefly_band(const DenoiseArgs &a, bool detect, bool apply, hipStream
     return launch_firefly(a, std::max(0, a.y0 - kWposHalo), std::min(a.H, a.y1 + kWposHalo), detect, apply, st);
 }
 
-int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) {
+// split (vxpt_render_frames): the firefly stage -- which writes the filtered reservoirs the next
+// pass's temporal reuse reads -- runs on the context stream, the rest of the chain on dnStream, where
+// it runs beside the next frame's first pass (which writes the other accumulation buffer and a
+// G-buffer slot that is neither this chain's input nor its history)
+int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it, bool split = false) {
     if (!p) p = &c->yamlDenoise;
     const int used = it > 0 ? it - 1 : 0;
     DenoiseArgs a{};
     fill_denoise(c, p, a, used & 1);
+    // the previous split chain reads the firefly lists and world positions this one rewrites
+    if (c->dnOutstanding) HIPCHK(c, hipStreamWaitEvent(c->stream, c->dnDone, 0));
+    c->dnOutstanding = false;
     HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
-    // the temporal pass applies the firefly lists when it runs
-    const bool ffFold = p->enable_temporal_accumulation && frameNum > 0;
+    // the temporal pass applies the firefly lists when it runs (split: the firefly launch does)
+    const bool ffFold = p->enable_temporal_accumulation && frameNum > 0 && !split;
     HIPCHK(c, firefly_band(a, p->enable_firefly_filter, !ffFold, c->stream));
-    if (frameNum == 0) HIPCHK(c, launch_frame0_init(a, c->stream));
+    hipStream_t st = c->stream;
+    if (split) {
+        HIPCHK(c, hipEventRecord(c->dnStart, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->dnStream, c->dnStart, 0));
+        st = c->dnStream;
+    }
+    if (frameNum == 0) HIPCHK(c, launch_frame0_init(a, st));
     int fin = 0;  // 0 illum, 1 ping, 2 pong, 3 prevIllum
     if (p->enable_temporal_accumulation && frameNum > 0) {
-        HIPCHK(c, launch_temporal(a, c->stream));
+        HIPCHK(c, launch_temporal(a, st));
         fin = 1;
-        if (p->enable_history_fix) { HIPCHK(c, launch_history_fix(a, c->stream)); fin = 2; }
-        if (p->enable_history_clamping) { HIPCHK(c, launch_history_clamp(a, c->stream)); fin = 3; }
+        if (p->enable_history_fix) { HIPCHK(c, launch_history_fix(a, st)); fin = 2; }
+        if (p->enable_history_clamping) { HIPCHK(c, launch_history_clamp(a, st)); fin = 3; }
     }
     bool outputDone = false;
     if (p->enable_spatial_filtering) {
-        HIPCHK(c, launch_atrous_smem(a, c->stream));
+        HIPCHK(c, launch_atrous_smem(a, st));
         fin = 1;
         if (p->atrous_iteration_num > 0) {
             int idx = 1;
             unsigned step = 1u << idx;
             const int maxIt = p->atrous_iteration_num * 2;
             while (idx < maxIt) {
-                HIPCHK(c, launch_atrous(a, a.ping, a.pong, step, (unsigned)it, false, c->stream));
+                HIPCHK(c, launch_atrous(a, a.ping, a.pong, step, (unsigned)it, false, st));
                 ++idx; step = 1u << idx;
-                HIPCHK(c, launch_atrous(a, a.pong, a.ping, step, (unsigned)it, false, c->stream));
+                HIPCHK(c, launch_atrous(a, a.pong, a.ping, step, (unsigned)it, false, st));
                 ++idx; step = 1u << idx;
             }
-            HIPCHK(c, launch_atrous(a, a.ping, a.pong, step, (unsigned)it, true, c->stream));
+            HIPCHK(c, launch_atrous(a, a.ping, a.pong, step, (unsigned)it, true, st));
             fin = 2;
             outputDone = true;
         }
     }
     if (!outputDone) {
         const float4 *src = fin == 1 ? a.ping : (fin == 2 ? a.pong : (fin == 3 ? a.prevIllum : a.illum));
-        HIPCHK(c, launch_copy_output(a, src, c->stream));
+        HIPCHK(c, launch_copy_output(a, src, st));
     }
     HIPCHK(c, history_copies(c));
-    HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[3], st));
+    if (split) {
+        HIPCHK(c, hipEventRecord(c->dnDone, st));
+        c->dnOutstanding = true;
+        c->dnBacks = 0;
+    }
     return 0;
 }
 
@@ -1366,6 +1407,17 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         for (hipEvent_t *e : {&c->frontDone[k], &c->backDone[k]})
             HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(c, hipEventCreateWithFlags(&c->frontGate, hipEventDisableTiming | hipEventDisableSystemFence));
+    {
+        // the split denoiser chains' stream at the lowest priority: beside the next frame's trace the
+        // dispatcher places their workgroups behind the trace's (C3 frame 6.02 -> 5.95 ms at equal
+        // priority, 5.92 at the lowest; VXPT_DN_PRIO=0 equal)
+        int least = 0, greatest = 0;
+        HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        const bool low = !(getenv("VXPT_DN_PRIO") && atoi(getenv("VXPT_DN_PRIO")) == 0);
+        HIPCHK(c, hipStreamCreateWithPriority(&c->dnStream, hipStreamNonBlocking, low ? least : 0));
+    }
+    HIPCHK(c, hipEventCreateWithFlags(&c->dnStart, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(c, hipEventCreateWithFlags(&c->dnDone, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(c, hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->dev));
     // timing markers only (every read of them follows a stream synchronisation): no system-scope
     // fence, so a marker neither writes back / invalidates the L2 nor delays the next kernel
@@ -1386,6 +1438,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         dalloc(c, c->hfList, tiles16 * 256) || dalloc(c, c->hfCount, tiles16))
         return VXPT_ERR_HIP;
     c->illumSet[0] = c->illum;
+    c->accumBuf[0] = c->accum;
+    if (dalloc(c, c->accumBuf[1], n)) return VXPT_ERR_HIP;
     for (int k = 1; k < c->nSets; ++k)
         if (dalloc(c, c->illumSet[k], n)) return VXPT_ERR_HIP;
     // tables
@@ -1414,6 +1468,7 @@ void vxpt_destroy(vxpt_ctx *c) {
     if (!c) return;
     hipSetDevice(c->dev);
     if (c->frontStream) hipStreamSynchronize(c->frontStream);
+    if (c->dnStream) hipStreamSynchronize(c->dnStream);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void *p : c->allocs) hipFree(p);
     for (int k = 0; k < kMaxSets; ++k)
@@ -1421,6 +1476,9 @@ void vxpt_destroy(vxpt_ctx *c) {
             if (e) hipEventDestroy(e);
     if (c->frontGate) hipEventDestroy(c->frontGate);
     if (c->frontStream) hipStreamDestroy(c->frontStream);
+    for (hipEvent_t e : {c->dnStart, c->dnDone})
+        if (e) hipEventDestroy(e);
+    if (c->dnStream) hipStreamDestroy(c->dnStream);
     for (auto &e : c->ev)
         if (e) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -2484,6 +2542,16 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         return VXPT_OK;
     }
     const float scale = 1.0f / (float)spp;
+    // Split denoiser chains (VXPT_DN_SPLIT=1; default: each chain after the next frame's first half,
+    // alone): an accumulated frame's chain reads its own accumulation buffer and G-buffer slots, which
+    // the next frame's passes leave alone, so all of it but the firefly stage can overlap the next
+    // frame's trace.  Measured: C3 frame 6.02 -> 5.92 ms, but the overlapped chains take ~3x as long
+    // and k_restir beside them +0.5 ms, and the chain's kernel timings stop being its
+    // own -- not the default.
+    const bool splitOk = getenv("VXPT_DN_SPLIT") && atoi(getenv("VXPT_DN_SPLIT")) == 1;  // read per call
+    // (the first halves not ordered behind the chain through the wait in trace_back are the nSets
+    // after it, all enqueued before the next chain moves the history: nSets <= spp)
+    const bool split = splitOk && spp > 1 && c->nSets <= spp;
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     PassPlan pend;
     bool havePend = false;
@@ -2508,22 +2576,29 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             // motion plane it stores is all zeros (static world) like the one the denoiser reads.
             if (int r = trace_front(c, it0 + spp, 0, spp > 1, true, scale, true, pend)) return r;
             havePend = true;
-            // the denoiser starts after it, so it runs alone and its timing stays its own
-            if (!pend.a.primaryOnly) HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
+            if (!split) {
+                // the denoiser starts after it, so it runs alone and its timing stays its own
+                if (!pend.a.primaryOnly) HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
+            }
         }
         c->denoiseInputIsAccum = spp > 1;
-        if (int r = do_denoise(c, p, frame0 + f, it0 + spp)) return r;
-        if (havePend) {  // later first halves wait for the denoiser (it reads the old history slot)
+        // split chains: every one but the last runs beside the next frame's first pass
+        if (int r = do_denoise(c, p, frame0 + f, it0 + spp, split && f + 1 < nFrames)) return r;
+        if (havePend && !split) {  // later first halves wait for the denoiser (it reads the old history slot)
             HIPCHK(c, hipEventRecord(c->frontGate, c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->frontStream, c->frontGate, 0));
         }
     }
+    if (c->dnOutstanding) HIPCHK(c, hipStreamWaitEvent(c->stream, c->dnDone, 0));
+    c->dnOutstanding = false;
     HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float d = 0, f = 0;
-    hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    hipEventElapsedTime(&d, c->ev[2], c->ev[3]);  // the last chain: alone, after every pass
     hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
-    c->timing.trace_ms = (f - d * nFrames) / (float)nFrames;  // per frame, denoiser runs excluded
+    // per frame, denoiser runs excluded (split: all but the last run beside the trace, which then
+    // carries whatever they cost it)
+    c->timing.trace_ms = (f - d * (split ? 1 : nFrames)) / (float)nFrames;
     c->timing.denoise_ms = d;
     c->timing.frame_ms = f / (float)nFrames;
     return VXPT_OK;

@@ -350,11 +350,14 @@ def test_overlapped_passes_equal_sequential_passes(w, h):
         b.close()
 
 
-@pytest.mark.parametrize("spp", [4, 1])
-def test_pipelined_frames_equal_frame_calls(spp):
+@pytest.mark.parametrize("spp,split", [(4, "0"), (1, "0"), (4, "1")])
+def test_pipelined_frames_equal_frame_calls(spp, split, monkeypatch):
     """vxpt_render_frames enqueues each frame's first pass-half beside the previous frame's last
-    second half (the denoiser then runs alone); after 4 frames every trace and denoiser buffer equals
-    4 vxpt_render_frame calls bit for bit, and a frame rendered after it (fresh call) still does."""
+    second half, and (spp > 1, VXPT_DN_SPLIT=1) every denoiser chain but the last after its firefly
+    stage on a stream of its own beside the next frame's first pass (the other accumulation buffer, a G-buffer slot
+    outside the chain's two); after 4 frames every trace and denoiser buffer equals 4
+    vxpt_render_frame calls bit for bit, and a frame rendered after it (fresh call) still does."""
+    monkeypatch.setenv("VXPT_DN_SPLIT", split)
     a, _ = _setup(96, 72)
     b, _ = _setup(96, 72)
     p = _dn_params()
