@@ -116,6 +116,53 @@ def test_incremental_edits_match_full_rebuild_and_oracle_dda():
     r2.close()
 
 
+def _rays_toward(origins, target, n, seed, spread=0.6):
+    rng = np.random.default_rng(seed)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3] = origins[rng.integers(0, len(origins), n)]
+    tgt = np.asarray(target, np.float32) + rng.uniform(-spread, spread, (n, 3)).astype(np.float32)
+    d = tgt - r[:, 0:3]
+    d[: n // 8, 1] = 0.0  # level rays too (the exit also takes d.y == 0)
+    r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    r[:, 6] = 0.0
+    r[:, 7] = 1e20
+    return r
+
+
+@pytest.mark.gpu
+def test_sky_exit_follows_edits():
+    """The walk ends once it is above the highest cube and not going down (WorldDev::skyY): a cube
+    placed above the terrain raises that height (rays up at it must hit it), and removing it again
+    leaves the height conservative (the same rays then miss, as the oracle's full walk says)."""
+    r = vxpt.Renderer(64, 64)
+    r.load_settings()
+    r.generate_terrain(CH)
+    ids = r.read("VOXELS").copy()
+    g = ids.reshape(-1, 32, 32, 32)  # chunk-major: [chunk][y][z][x] (one chunk layer in y)
+    ys = [y for y in range(32) if ((g[:, y] >= 1) & (g[:, y] <= 12)).any()]
+    top = max(ys)
+    assert top < 28, "terrain reaches the world's top: no air above it to test"
+    o = oracle.Oracle(64, 64)
+    rng = np.random.default_rng(4)
+    origins = np.stack([rng.uniform(2, 62, 64), np.full(64, top + 1.5), rng.uniform(2, 62, 64)], 1).astype(np.float32)
+    cube = (37, 30, 21)
+    rays = _rays_toward(origins, (cube[0] + 0.5, cube[1] + 0.5, cube[2] + 0.5), 4000, 6)
+    for b in (3, 0):
+        r.set_block(*cube, b)
+        ids[_idx(*cube)] = b
+        o.set_voxels(ids, CH)
+        got, tg = r.probe_rays(rays, 0)
+        want, tw = o.rays(rays, 0)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(tg.view(np.uint32), tw.view(np.uint32))
+        occ, _ = r.probe_rays(rays, 2)
+        occw, _ = o.rays(rays, 2)
+        np.testing.assert_array_equal(occ[:, 0], occw[:, 0])
+        hits = (got[:, 1] == cube[0]) & (got[:, 2] == cube[1]) & (got[:, 3] == cube[2])
+        assert hits.sum() > (1000 if b else -1) and (b or not hits.any())
+    r.close()
+
+
 @pytest.mark.gpu
 def test_pick_and_click_follow_the_reference_walk():
     r = vxpt.Renderer(64, 64)
