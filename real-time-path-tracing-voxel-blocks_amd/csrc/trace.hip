@@ -157,6 +157,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOS
     int px, py;
     bool active = slot_pixel(a, s, px, py);
     const WaveBufs &w = a.wb;
+    if (mode == 2)  // the pass's queue counters (4 per segment, straggler shards), zeroed here rather than by a fill launch
+        for (unsigned z = (unsigned)s; z < kQueueWords / 4; z += gridDim.x * 256u)
+            reinterpret_cast<uint4 *>(w.qCount)[z] = make_uint4(0u, 0u, 0u, 0u);
     V3 o, d;
     float tmax = kRayMax;
     if (active) {
@@ -1547,8 +1550,7 @@ hipError_t launch_trace_front(const TraceArgs &a, hipStream_t st) {
         return hipGetLastError();
     }
     // secondary / visibility rays go through the compacted queues; their counters (4 per segment)
-    // are zeroed once per pass
-    hipMemsetAsync(a.wb.qCount, 0, kQueueWords * sizeof(unsigned), st);
+    // are zeroed once per pass, by k_closest above
     if (L.mesh) hipLaunchKernelGGL(k_mesh_slots, L.g, L.b, 0, st, a, 2);
     L.first_half(0);
     return hipGetLastError();

@@ -108,6 +108,7 @@ struct GBuf {
 constexpr int kQueues = 64;
 constexpr int kShards = 8;
 constexpr size_t kQueueWords = 2 * kQueues + 3 * kQueues * kShards * 16;
+static_assert(kQueueWords % 4 == 0, "k_closest zeroes the counters as uint4");
 
 struct WaveBufs {
     // path state
