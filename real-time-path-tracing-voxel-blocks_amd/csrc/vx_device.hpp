@@ -346,9 +346,6 @@ VX_HD void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, con
 template <bool OCC, bool BOX = false>
 VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;
-    // above every cube and not going down: no cell ahead holds a cube, and the current one is empty,
-    // so no later crossing (leaving the world included) can be an event
-    if (w.skyY > 0 && s.c.y >= w.skyY && (s.r.sy > 0 || !s.r.my)) return DdaNone;
     if (cnt) ++cnt[s.dist == 0 ? 3 : (s.dist == 1 ? 2 : 1)];
     if (s.dist == 0) {
         const int rc = brick_walk<OCC>(w, s, h, cnt ? cnt + 4 : nullptr);

@@ -70,8 +70,6 @@ struct WorldDev {
                               // (0 = 10: a whole brick); VXPT_BRICK_STEPS
     uint64_t top;
     int topValid;
-    int skyY;             // 1 + the highest cell y holding a cube (conservative after removals; 0 = not
-                          // used): a walk at or above it going up can enter no cube and ends there
     int cx, cy, cz;       // chunks
     int wx, wy, wz;       // cells
     int mx, my, mz;       // 16^3 macro cells

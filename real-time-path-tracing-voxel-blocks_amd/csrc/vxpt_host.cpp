@@ -166,7 +166,6 @@ struct vxpt_ctx {
     int nBricks = 0;
     uint64_t top = 0;
     int topValid = 0;
-    int skyY = 0;  // WorldDev::skyY
     // host mirrors of the world: picking, incremental edits, chunk files (the device copies are
     // updated from them in place)
     std::vector<uint8_t> hIds, hBricks, hOd;
@@ -472,8 +471,6 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.brickStepsCam = camSteps;
     w.top = c->top;
     w.topValid = c->topValid;
-    static const bool skyExit = !getenv("VXPT_SKY_EXIT") || atoi(getenv("VXPT_SKY_EXIT")) != 0;
-    w.skyY = skyExit ? c->skyY : 0;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
     w.wx = c->cx * 32; w.wy = c->cy * 32; w.wz = c->cz * 32;
     w.mx = w.wx / 16; w.my = w.wy / 16; w.mz = w.wz / 16;
@@ -677,7 +674,6 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     c->hCell.assign((size_t)mx * my * mz * 64, 0ull);
     const int tx = (wx + 63) / 64, ty = (wy + 63) / 64, tz = (wz + 63) / 64;
     c->topCount.assign((size_t)tx * ty * tz, 0);
-    c->skyY = 0;
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -692,7 +688,6 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
                     c->hMacro[b / 64] |= 1ull << (b % 64);
                     c->hCell[b] |= 1ull << lc;
                     c->topCount[top_block(c, x, y, z)]++;
-                    c->skyY = std::max(c->skyY, y + 1);
                 }
             }
     c->topValid = (tx * ty * tz <= 64) ? 1 : 0;
@@ -740,7 +735,6 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
         c->hCell[b] = is_cube(id) ? (before | (1ull << lc)) : (before & ~(1ull << lc));
         HIPCHK(c, hipMemcpyAsync(c->cellMask.p + b, &c->hCell[b], 8, hipMemcpyHostToDevice, st));
         c->topCount[top_block(c, x, y, z)] += is_cube(id) ? 1 : -1;
-        if (is_cube(id)) c->skyY = std::max(c->skyY, y + 1);  // a removal keeps it (conservative)
         refresh_top(c);
         if ((before != 0) != (c->hCell[b] != 0)) {
             const size_t m = b / 64;

@@ -33,7 +33,6 @@ int main(int argc, char **argv) {
     };
     std::vector<uint8_t> bricks(nB * 64, 0);
     std::vector<uint64_t> cellMask(nB, 0);
-    int skyY = 0;
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -43,10 +42,7 @@ int main(int argc, char **argv) {
                 const size_t b = blin(x >> 2, y >> 2, z >> 2);
                 const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
                 bricks[b * 64 + lc] = id;
-                if (id >= 1 && id <= 12) {
-                    cellMask[b] |= 1ull << lc;
-                    skyY = std::max(skyY, y + 1);
-                }
+                if (id >= 1 && id <= 12) cellMask[b] |= 1ull << lc;
             }
     // the default cube tables (vxpt_host.cpp octant_fill's recurrence, whole grid)
     std::vector<uint8_t> od(8 * nB, 0);
@@ -101,8 +97,6 @@ int main(int argc, char **argv) {
     // cube-table walks take whole bricks): the same hits prove the yield and its save / resume exact
     WorldDev wb = w;
     wb.brickSteps = 3;
-    // and end above the highest cube (WorldDev::skyY); the cube-table walks run to the world's edge
-    wb.skyY = skyY;
     if (std::string(argv[5]) == "--rays") {
         FILE *fr = fopen(argv[6], "rb");
         if (!fr) return 1;

@@ -130,10 +130,10 @@ def _rays_toward(origins, target, n, seed, spread=0.6):
 
 
 @pytest.mark.gpu
-def test_sky_exit_follows_edits():
-    """The walk ends once it is above the highest cube and not going down (WorldDev::skyY): a cube
-    placed above the terrain raises that height (rays up at it must hit it), and removing it again
-    leaves the height conservative (the same rays then miss, as the oracle's full walk says)."""
+def test_edits_above_the_terrain():
+    """A cube placed in the open air above a low terrain and removed again: rays up at it from just
+    above the terrain (some level) hit it, then miss it, as the oracle's walk over the edited grid
+    says -- the traversal structures above the highest cube follow the edit both ways."""
     r = vxpt.Renderer(64, 64)
     r.load_settings()
     r.generate_terrain(CH, height_scale=12.0)  # low terrain: air above it
