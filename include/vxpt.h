@@ -319,10 +319,19 @@ int vxpt_halo_plan(int height, int nranks, int rank, int rows, int32_t out[10], 
 /* halo depths a banded frame exchanges for a camera that turned from prev to cur between passes:
  * trace_rows (ReSTIR temporal taps: 64 rows around the reprojected row, >= 72) and history_rows
  * (the temporal accumulation's bicubic history taps, >= 2).  VXPT_ERR_STATE when the camera
- * translated (depth-dependent parallax), part of a band falls behind the previous camera, or the
- * trace halo is deeper than a band: vxpt_render_frame / _linked refuse such a frame the same way. */
+ * translated (depth-dependent parallax: see vxpt_band_halo_rows_near), part of a band falls behind
+ * the previous camera, or the trace halo is deeper than a band: vxpt_render_frame / _linked refuse
+ * such a frame the same way. */
 int vxpt_band_halo_rows(const vxpt_camera *cur, const vxpt_camera *prev, int width, int height, int nranks,
                         int *trace_rows, int *history_rows);
+/* the same for a camera that may also translate: near_depth > 0 bounds every primary hit's distance
+ * from the camera (a pixel's reprojected row is monotone in its hit distance, so the rows at
+ * near_depth and at infinity bound it).  vxpt_render_frame / _linked use the world's own bound,
+ * vxpt_nearest_surface: the distance from pos to the nearest non-air cell grown by one cell (mesh
+ * overhang), searched up to 64 cells (host mirror of the world; no GPU work). */
+int vxpt_band_halo_rows_near(const vxpt_camera *cur, const vxpt_camera *prev, int width, int height, int nranks,
+                             float near_depth, int *trace_rows, int *history_rows);
+int vxpt_nearest_surface(vxpt_ctx *ctx, const float pos[3], float *dist);
 /* end-of-frame gather: every band's rows of a per-pixel buffer (e.g. VXPT_BUF_OUTPUT, or
  * VXPT_BUF_FRAME after vxpt_postprocess) into the root rank's buffer, which then holds the whole
  * frame (RCCL: ncclSend to the root, ncclRecv per band at the root; blocking) */

@@ -373,8 +373,10 @@ VX_D bool map_tile(const DenoiseArgs &a, int &tx, int &ty) {
 }
 
 // ---------------------------------------------------------------- TA
-template <bool kQuirk>
-VX_HD V4 bicubic12(const float4 *b, int W, int H, V2 uv) {
+// The tap functions read their plane through a loader ld(x, y) (the edge-clamped global plane, or
+// the k_temporal workgroup's LDS window)
+template <bool kQuirk, class L>
+VX_HD V4 bicubic12(const L &ld, int W, int H, V2 uv) {
     const V2 UV(uv.x * (float)W, uv.y * (float)H);
     const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
     const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
@@ -393,7 +395,7 @@ VX_HD V4 bicubic12(const float4 *b, int W, int H, V2 uv) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         sum += wt[k];
-        const V4 v = ld4(b, W, H, sx[k], sy[k]);
+        const V4 v = ld(sx[k], sy[k]);
         if (kQuirk) out += v * wt[k];
         else out3 += v.xyz() * wt[k];
     }
@@ -410,7 +412,8 @@ VX_HD void bilinear_taps(int W, int H, V2 uv, int &x0, int &y0, float w[4]) {
     y0 = (int)fy;
     w[0] = w0.x * w0.y; w[1] = w1.x * w0.y; w[2] = w0.x * w1.y; w[3] = w1.x * w1.y;
 }
-VX_HD V4 bilinear_custom4(const float4 *b, int W, int H, V2 uv, const float cw[4]) {
+template <class L>
+VX_HD V4 bilinear_custom4(const L &ld, int W, int H, V2 uv, const float cw[4]) {
     int x0, y0;
     float w[4];
     bilinear_taps(W, H, uv, x0, y0, w);
@@ -421,7 +424,7 @@ VX_HD V4 bilinear_custom4(const float4 *b, int W, int H, V2 uv, const float cw[4
         const float wt = w[k] * cw[k];
         const float weight = (wt < 1e-6f) ? 1e-6f : wt;
         sum += weight;
-        out += ld4(b, W, H, x0 + (k & 1), y0 + (k >> 1)) * weight;
+        out += ld(x0 + (k & 1), y0 + (k >> 1)) * weight;
     }
     out /= sum;
     return out;
@@ -441,7 +444,8 @@ VX_HD float bilinear_custom1(const float v[4], int W, int H, V2 uv, const float 
     }
     return out / sum;
 }
-VX_HD V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
+template <class L>
+VX_HD V3 bicubic_smoothstep3(const L &ld, int W, int H, V2 uv) {
     const V2 UV(uv.x * (float)W, uv.y * (float)H);
     const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
     const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
@@ -454,26 +458,113 @@ VX_HD V3 bicubic_smoothstep3(const float4 *b, int W, int H, V2 uv) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         sum += wt[k];
-        out += ld4(b, W, H, x0 + (k & 1), y0 + (k >> 1)).xyz() * wt[k];
+        out += ld(x0 + (k & 1), y0 + (k >> 1)).xyz() * wt[k];
     }
     out /= sum;
     return out;
 }
 
+// The planes temporal_px reads around a pixel: edge-clamped global loads (TaGlobal), or the
+// k_temporal workgroup's LDS window (TaLds: the previous frame's planes over the tile + a 2-pixel
+// apron, the current normals over the tile + 1).  A window entry holds the edge-clamped pixel's
+// value, so a tap inside the window reads exactly what ld4 / ld1 would.
+struct TaGlobal {
+    const DenoiseArgs *a;
+    VX_HD V4 n(int x, int y) const { return ld4(a->normalRough, a->W, a->H, x, y); }
+    VX_HD float pz(int x, int y) const { return ld1(a->prevDepth, a->W, a->H, x, y); }
+    VX_HD V4 pn(int x, int y) const { return ld4(a->prevNormalRough, a->W, a->H, x, y); }
+    VX_HD V4 pi(int x, int y) const { return ld4(a->prevIllum, a->W, a->H, x, y); }
+    VX_HD V4 pf(int x, int y) const { return ld4(a->prevFast, a->W, a->H, x, y); }
+    VX_HD float ph(int x, int y) const { return ld1(a->prevHistLen, a->W, a->H, x, y); }
+};
+constexpr int kTaWin = 20, kTaNWin = 18;  // window edges: the 16x16 tile + 2 (history taps) / + 1 (normals)
+struct TaLds {
+    const float4 *sN, *sPN, *sPI, *sPF;
+    const float *sPZ, *sPH;
+    int x0, y0;  // the window's first pixel (tile origin - 2)
+    VX_HD int w(int x, int y) const { return (y - y0) * kTaWin + (x - x0); }
+    VX_HD V4 n(int x, int y) const { return f4(sN[(y - y0 - 1) * kTaNWin + (x - x0 - 1)]); }
+    VX_HD float pz(int x, int y) const { return sPZ[w(x, y)]; }
+    VX_HD V4 pn(int x, int y) const { return f4(sPN[w(x, y)]); }
+    VX_HD V4 pi(int x, int y) const { return f4(sPI[w(x, y)]); }
+    VX_HD V4 pf(int x, int y) const { return f4(sPF[w(x, y)]); }
+    VX_HD float ph(int x, int y) const { return sPH[w(x, y)]; }
+};
+
+// The reprojected history of a pixel (TemporalAccumulation.h loadSurfaceMotionBasedPrevData):
+// the 12 depth taps' validity, the previous normal's test, the bicubic / custom-bilinear history
+// and fast history, and the bilinear history length.
+struct TaHist {
+    V4 prevI;
+    V3 prevF;
+    float bicValid, found, quality, hist;
+};
+template <class T>
+VX_HD TaHist ta_history(const T &t, int W, int H, const Qt &rot, V3 nIn, V2 prevUV, int ox, int oy, float estDepth,
+                        const float thrv[4]) {
+    const int bcx[8] = {0, -1, 1, 2, -1, 0, 2, 1}, bcy[8] = {-1, 0, -1, 0, 1, 2, 1, 2};
+    TaHist r;
+    float bicValid = 1.0f;
+    float taps[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float pz = t.pz(ox + bcx[k], oy + bcy[k]);
+        bicValid *= fabsf(pz - estDepth) > thrv[k >> 1] ? 0.0f : 1.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float pz = t.pz(ox + (k & 1), oy + (k >> 1));
+        const float v = fabsf(pz - estDepth) > thrv[k] ? 0.0f : 1.0f;
+        bicValid *= v;
+        taps[k] = v;
+    }
+    const V3 pnf = normalize(bicubic_smoothstep3([&](int x, int y) { return t.pn(x, y); }, W, H, prevUV));
+    const V3 pnr = normalize(q_rotate(rot, pnf));
+    if (dot(nIn, pnr) < 0.0f) {
+        taps[0] = taps[1] = taps[2] = taps[3] = 0.0f;
+        bicValid = 0.0f;
+    }
+    const bool useBic = bicValid > 0;
+    const auto li = [&](int x, int y) { return t.pi(x, y); };
+    const auto lf = [&](int x, int y) { return t.pf(x, y); };
+    V4 prevI = useBic ? bicubic12<true>(li, W, H, prevUV) : bilinear_custom4(li, W, H, prevUV, taps);
+    V3 prevF = useBic ? bicubic12<false>(lf, W, H, prevUV).xyz() : bilinear_custom4(lf, W, H, prevUV, taps).xyz();
+    r.prevI = V4(fmaxf(prevI.x, 0.0f), fmaxf(prevI.y, 0.0f), fmaxf(prevI.z, 0.0f), fmaxf(prevI.w, 0.0f));
+    r.prevF = max3(prevF, V3(0.0f));
+    r.found = (bicValid > 0.0f) ? 2.0f : 1.0f;
+    int bx0, by0;
+    float bw[4];
+    bilinear_taps(W, H, prevUV, bx0, by0, bw);
+    r.quality = (bicValid > 0) ? 1.0f : (bw[0] * 1.0f + bw[1] * 1.0f + bw[2] * 1.0f + bw[3] * 1.0f);
+    if ((taps[0] * 1.0f + taps[1] * 1.0f + taps[2] * 1.0f + taps[3] * 1.0f) == 0.0f) {
+        r.found = 0.0f; r.quality = 0.0f; r.hist = 0.0f;
+    } else {
+        float histTap[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) histTap[k] = t.ph(ox + (k & 1), oy + (k >> 1));
+        r.hist = bilinear_custom1(histTap, W, H, prevUV, taps);
+    }
+    r.bicValid = bicValid;
+    return r;
+}
+
 // Returns whether the history fix must filter the pixel (HistoryFix.h:20-22:
 // non-sky and history <= 4; pixels past the denoising range keep last frame's length).
-VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol) {
+// `lds`: the workgroup's window (k_temporal<.., true>); the history taps read it when their
+// 4x4 footprint lies inside it, the global planes otherwise.
+VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol, const TaLds *lds = nullptr) {
     const int W = a.W, H = a.H;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
     if (z > a.p.denoisingRange) return z <= kRange && a.histLen[i] <= 4.0f;
     const CamDev &cam = a.cam, &pc = a.prevCam;
-    const V3 cN = f4(a.normalRough[i]).xyz();
+    const TaGlobal g{&a};
+    const V3 cN = (lds ? lds->n(x, y) : f4(a.normalRough[i])).xyz();
     V3 avgN = cN;
     for (int ax = -1; ax <= 1; ++ax)
         for (int by = -1; by <= 1; ++by) {
             if (ax == 0 && by == 0) continue;
-            avgN += ld4(a.normalRough, W, H, x + ax, y + by).xyz();
+            avgN += (lds ? lds->n(x + ax, y + by) : g.n(x + ax, y + by)).xyz();
         }
     avgN /= 9.0f;
     const V2 pixelUv = (V2((float)x, (float)y) + 0.5f) * V2(a.invW, a.invH);
@@ -517,47 +608,15 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
     }
     thr4 -= 1e-6f;
     const float thrv[4] = {thr4.x, thr4.y, thr4.z, thr4.w};
-    const int bcx[8] = {0, -1, 1, 2, -1, 0, 2, 1}, bcy[8] = {-1, 0, -1, 0, 1, 2, 1, 2};
-    float bicValid = 1.0f;
-    float taps[4];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const float pz = ld1(a.prevDepth, W, H, ox + bcx[k], oy + bcy[k]);
-        bicValid *= fabsf(pz - estDepth) > thrv[k >> 1] ? 0.0f : 1.0f;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float pz = ld1(a.prevDepth, W, H, ox + (k & 1), oy + (k >> 1));
-        const float v = fabsf(pz - estDepth) > thrv[k] ? 0.0f : 1.0f;
-        bicValid *= v;
-        taps[k] = v;
-    }
-    const V3 pnf = normalize(bicubic_smoothstep3(a.prevNormalRough, W, H, prevUV));
-    const V3 pnr = normalize(q_rotate(rot, pnf));
-    if (dot(nIn, pnr) < 0.0f) {
-        taps[0] = taps[1] = taps[2] = taps[3] = 0.0f;
-        bicValid = 0.0f;
-    }
-    const bool useBic = bicValid > 0;
-    V4 prevI = useBic ? bicubic12<true>(a.prevIllum, W, H, prevUV) : bilinear_custom4(a.prevIllum, W, H, prevUV, taps);
-    V3 prevF = useBic ? bicubic12<false>(a.prevFast, W, H, prevUV).xyz()
-                      : bilinear_custom4(a.prevFast, W, H, prevUV, taps).xyz();
-    prevI = V4(fmaxf(prevI.x, 0.0f), fmaxf(prevI.y, 0.0f), fmaxf(prevI.z, 0.0f), fmaxf(prevI.w, 0.0f));
-    prevF = max3(prevF, V3(0.0f));
-    float found = (bicValid > 0.0f) ? 2.0f : 1.0f;
-    int bx0, by0;
-    float bw[4];
-    bilinear_taps(W, H, prevUV, bx0, by0, bw);
-    float quality = (bicValid > 0) ? 1.0f : (bw[0] * 1.0f + bw[1] * 1.0f + bw[2] * 1.0f + bw[3] * 1.0f);
-    float hist;
-    if ((taps[0] * 1.0f + taps[1] * 1.0f + taps[2] * 1.0f + taps[3] * 1.0f) == 0.0f) {
-        found = 0.0f; quality = 0.0f; hist = 0.0f;
-    } else {
-        float histTap[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) histTap[k] = ld1(a.prevHistLen, W, H, ox + (k & 1), oy + (k >> 1));
-        hist = bilinear_custom1(histTap, W, H, prevUV, taps);
-    }
+    // every tap of the history lies in [ox - 1, ox + 2] x [oy - 1, oy + 2]
+    const bool inWin = lds && ox - 1 >= lds->x0 && ox + 2 < lds->x0 + kTaWin && oy - 1 >= lds->y0 &&
+                       oy + 2 < lds->y0 + kTaWin;
+    const TaHist hh = inWin ? ta_history(*lds, W, H, rot, nIn, prevUV, ox, oy, estDepth, thrv)
+                            : ta_history(g, W, H, rot, nIn, prevUV, ox, oy, estDepth, thrv);
+    const V4 prevI = hh.prevI;
+    const V3 prevF = hh.prevF;
+    const float found = hh.found;
+    float quality = hh.quality, hist = hh.hist;
     hist = hist + 1.0f;
     const V3 Vp = normalize(prevWP - pc.pos);
     const float NoVp = fabsf(dot(cN, Vp));
@@ -588,10 +647,20 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
 // 123 VGPRs (4 waves/SIMD); bounding it to 5 waves spills 80-116 B/lane and was slower (89 -> 105 us),
 // and fetching the pixel's inputs before the depth test or the history taps with the depth taps
 // raised it to 130 (3 waves: 100-103 us)
-template <bool ST>
-__global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
+// LDS = true: the workgroup first stages its window of the previous frame's depth, normal, history,
+// fast history and history length (20x20) and of the current normals (18x18) -- one round of
+// independent loads -- and the pixels' history taps read LDS while they stay inside the window
+// (a static or slowly moving camera); tiles without a pixel in the denoising range stage nothing.
+#ifndef VX_WPE_TA
+#define VX_WPE_TA 1  // occupancy bound of k_temporal (waves per SIMD; 1 = the compiler's choice)
+#endif
+template <bool ST, bool LDS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_TA))) void k_temporal(DenoiseArgs a, Qt rot) {
     __shared__ unsigned sTot[4], sFFn, sFFmask[8];
     __shared__ float4 sFF[256];
+    __shared__ float4 sN[LDS ? kTaNWin * kTaNWin : 1], sPN[LDS ? kTaWin * kTaWin : 1], sPI[LDS ? kTaWin * kTaWin : 1],
+        sPF[LDS ? kTaWin * kTaWin : 1];
+    __shared__ float sPZ[LDS ? kTaWin * kTaWin : 1], sPH[LDS ? kTaWin * kTaWin : 1];
     int tx, ty;  // supertiles (default) or raster tiles (VXPT_TA_ST=0)
     if (!map_tile<ST>(a, tx, ty)) return;
     const unsigned tile = ty * ((a.W + 15) / 16) + tx;
@@ -616,7 +685,28 @@ __global__ __launch_bounds__(256) void k_temporal(DenoiseArgs a, Qt rot) {
     }
     const bool own = nff && ((sFFmask[threadIdx.x >> 5] >> (threadIdx.x & 31)) & 1u);
     const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);
-    const bool fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr);
+    bool fix;
+    if (LDS) {
+        const int W = a.W, H = a.H, x0 = tx * 16 - 2, y0 = a.y0 + ty * 16 - 2;
+        const bool act = x < W && y < a.y1 && a.depth[(size_t)y * W + x] <= a.p.denoisingRange;
+        if (__syncthreads_or(act)) {
+            for (int k = threadIdx.x; k < kTaWin * kTaWin; k += 256) {
+                const size_t j = (size_t)cl(y0 + k / kTaWin, H) * W + cl(x0 + k % kTaWin, W);
+                sPZ[k] = a.prevDepth[j];
+                sPN[k] = a.prevNormalRough[j];
+                sPI[k] = a.prevIllum[j];
+                sPF[k] = a.prevFast[j];
+                sPH[k] = a.prevHistLen[j];
+            }
+            for (int k = threadIdx.x; k < kTaNWin * kTaNWin; k += 256)
+                sN[k] = a.normalRough[(size_t)cl(y0 + 1 + k / kTaNWin, H) * W + cl(x0 + 1 + k % kTaNWin, W)];
+            __syncthreads();
+        }
+        const TaLds w{sN, sPN, sPI, sPF, sPZ, sPH, x0, y0};
+        fix = x < W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr, &w);
+    } else {
+        fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr);
+    }
     const unsigned long long m = __ballot(fix);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0) sTot[wv] = (unsigned)__popcll(m);
@@ -693,6 +783,28 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
             }
         }
     }
+#ifndef VX_HF_BPERMUTE
+    // the taps' values reach every lane of the half through v_readlane (constant lane indices, both
+    // halves read, each keeps its own): no LDS-crossbar round trip per tap
+    const bool hi = (threadIdx.x & 32u) != 0;
+    auto rl = [&](float v, int l) {
+        const float lo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+        const float up = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l + 32));
+        return hi ? up : lo;
+    };
+    V4 sum(rl(c.x, 12), rl(c.y, 12), rl(c.z, 12), rl(c.w, 12));
+    float wsum = 1.0f;
+#pragma unroll
+    for (int t = 0; t < 25; ++t) {
+        if (t == 12) continue;
+        const float tw = rl(cw, t);
+        const V4 tc(rl(c.x, t), rl(c.y, t), rl(c.z, t), rl(c.w, t));
+        if (tw > 0.0f) {
+            sum += tc;
+            wsum += tw;
+        }
+    }
+#else
     const int base = (int)(threadIdx.x & 32u);  // the half's first lane in the wave
     V4 sum(__shfl(c.x, base + 12), __shfl(c.y, base + 12), __shfl(c.z, base + 12), __shfl(c.w, base + 12));
     float wsum = 1.0f;
@@ -706,6 +818,7 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
             wsum += tw;
         }
     }
+#endif
     if (lane == 0 && store) a.pong[i] = tf(sum / wsum);
 }
 
@@ -1170,8 +1283,13 @@ hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
     // supertiles: the taps' history rows stay in the XCD's L2 (351 -> 266 MB per frame, time even);
     // VXPT_TA_ST=0: raster tiles
     static const bool stT = !(getenv("VXPT_TA_ST") && atoi(getenv("VXPT_TA_ST")) == 0);
-    if (stT) hipLaunchKernelGGL(k_temporal<true>, grid_st(a), dim3(256), 0, st, a, rot);
-    else hipLaunchKernelGGL(k_temporal<false>, grid16(a), dim3(256), 0, st, a, rot);
+    // VXPT_TA_LDS=1: the LDS window (measured slower: 95 -> 109 us at 137 VGPRs / 3 waves, 0.367 ->
+    // 0.382 ms chain; bounded to 4 waves it spills 48 B/lane, 0.378 ms)
+    static const bool lds = getenv("VXPT_TA_LDS") && atoi(getenv("VXPT_TA_LDS")) == 1;
+    if (stT && lds) hipLaunchKernelGGL((k_temporal<true, true>), grid_st(a), dim3(256), 0, st, a, rot);
+    else if (stT) hipLaunchKernelGGL((k_temporal<true, false>), grid_st(a), dim3(256), 0, st, a, rot);
+    else if (lds) hipLaunchKernelGGL((k_temporal<false, true>), grid16(a), dim3(256), 0, st, a, rot);
+    else hipLaunchKernelGGL((k_temporal<false, false>), grid16(a), dim3(256), 0, st, a, rot);
     return hipGetLastError();
 }
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {

@@ -1111,26 +1111,35 @@ std::vector<Halo> halo_plan(int H, int world, int rank, int rows) {
 }
 
 // Halo depths of a banded frame whose camera moved between passes (cur vs prev).  A band's
-// pixels reproject to rows prevCam.dir_to_uv(cam ray).y * H: the ReSTIR temporal taps read the
-// previous pass's G-buffer and reservoirs within 64 rows of that row (Restir.h:348-381, truncated
-// row), the temporal accumulation its histories within its bicubic footprint (-1..+2 around
-// floor(row - 0.5), TemporalAccumulation.h:29-215).  For a rotation the reprojection does not
-// depend on depth: the extreme rows over the band come from the pixel corners on the band's first
-// and last row boundaries (all columns) plus a 33-column grid over every row; 2 rows of margin
-// cover host/device rounding.  A translated camera makes it depth dependent (unbounded parallax
-// for near surfaces): refused, as is a point behind the previous camera or a halo deeper than a
-// neighbouring band (the plan only reaches ranks r +/- 1).  An unmoved camera keeps the static
-// depths (72 / 2).
+// pixels reproject to rows prevCam.dir_to_uv(hit - prevCam.pos).y * H: the ReSTIR temporal taps
+// read the previous pass's G-buffer and reservoirs within 64 rows of that row (Restir.h:348-381,
+// truncated row), the temporal accumulation its histories within its bicubic footprint (-1..+2
+// around floor(row - 0.5), TemporalAccumulation.h:29-215).  For a rotation the reprojection does
+// not depend on depth: the extreme rows over the band come from the pixel corners on the band's
+// first and last row boundaries (all columns) plus a 33-column grid over every row; 2 rows of
+// margin cover host/device rounding.  A translation t makes a pixel's row depend on its hit
+// distance d: row(d) = (d a.y + b.y) / (d a.z + b.z) with a = worldToUv dir, b = worldToUv t, a
+// Moebius map of d, monotone on [nearDepth, inf) while its denominator stays positive there -- so
+// with a lower bound nearDepth on every primary hit's distance the extremes are the rows at
+// nearDepth and at infinity (the rotation's), sampled on a 129-column grid.  Without such a bound
+// (nearDepth <= 0) a translated camera is refused; so is a point behind the previous camera or a
+// halo deeper than a neighbouring band (the plan only reaches ranks r +/- 1).  An unmoved camera
+// keeps the static depths (72 / 2).
 bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, int world, int &traceRows, int &histRows,
-                    std::string &err) {
+                    std::string &err, float nearDepth = 0.0f) {
     traceRows = kTraceHalo;
     histRows = 2;
     if (world <= 1) return true;
     if (std::memcmp(&cam, &pc, sizeof(CamDev)) == 0) return true;
-    if (cam.pos.x != pc.pos.x || cam.pos.y != pc.pos.y || cam.pos.z != pc.pos.z) {
-        err = "banded frames need a camera that does not translate between passes (depth-dependent reprojection)";
+    const V3 t = cam.pos - pc.pos;
+    const bool moved = t.x != 0.0f || t.y != 0.0f || t.z != 0.0f;
+    if (moved && !(nearDepth > 0.0f)) {
+        err = "banded frames need a camera that does not translate between passes, or a lower bound on the "
+              "primary hits' distance (depth-dependent reprojection)";
         return false;
     }
+    const V3 b = m3_apply(pc.worldToUv, t);
+    const int cols = moved ? 128 : 32;
     int minBand = H;
     float reach = 0.0f;  // rows beyond its band any band pixel reprojects to
     for (int r = 0; r < world; ++r) {
@@ -1147,15 +1156,22 @@ bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, int world
             const float py = n.y / n.z * (float)H;
             lo = std::min(lo, py);
             hi = std::max(hi, py);
+            if (moved) {  // the hit at the nearest distance
+                const V3 m = n * nearDepth + b;
+                if (!(m.z > 0.0f)) { behind = true; return; }
+                const float pm = m.y / m.z * (float)H;
+                lo = std::min(lo, pm);
+                hi = std::max(hi, pm);
+            }
         };
         for (int x = 0; x <= W; ++x) {
             sample((float)x / (float)W, (float)y0 / (float)H);
             sample((float)x / (float)W, (float)y1 / (float)H);
         }
         for (int y = y0; y <= y1; ++y)
-            for (int k = 0; k <= 32; ++k) sample((float)k / 32.0f, (float)y / (float)H);
+            for (int k = 0; k <= cols; ++k) sample((float)k / (float)cols, (float)y / (float)H);
         if (behind) {
-            err = "the camera turned so far that part of a band lies behind the previous camera";
+            err = "the camera moved so far that part of a band lies behind the previous camera";
             return false;
         }
         if (r > 0) reach = std::max(reach, (float)y0 - lo);
@@ -1170,6 +1186,46 @@ bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, int world
         return false;
     }
     return true;
+}
+
+// A lower bound on the distance from p to any primary hit: the nearest non-air cell's box, grown by
+// one cell on every side (instanced meshes may overhang their cell), over the host mirror of the
+// world, searched in Chebyshev rings around p's cell up to 64 cells (beyond that, 63 is the bound).
+// Empty space outside the world holds no geometry.
+float nearest_surface(const vxpt_ctx *c, V3 p) {
+    const int WX = c->cx * 32, WY = c->cy * 32, WZ = c->cz * 32;
+    if (c->hIds.empty() || WX == 0) return 1e30f;
+    const int px = (int)std::floor(p.x), py = (int)std::floor(p.y), pz = (int)std::floor(p.z);
+    constexpr int kRings = 64;
+    constexpr float kGrow = 1.0f;
+    float best = 1e30f;
+    auto cell = [&](int x, int y, int z) {
+        if (x < 0 || y < 0 || z < 0 || x >= WX || y >= WY || z >= WZ) return;
+        if (c->hIds[(size_t)((x >> 5) + c->cx * ((z >> 5) + c->cz * (y >> 5))) * 32768 + (x & 31) +
+                    32 * ((z & 31) + 32 * (y & 31))] == 0)
+            return;
+        auto ax = [&](float v, int lo) {
+            const float a = (float)lo - kGrow, b = (float)(lo + 1) + kGrow;
+            return v < a ? a - v : (v > b ? v - b : 0.0f);
+        };
+        const float dx = ax(p.x, x), dy = ax(p.y, y), dz = ax(p.z, z);
+        best = std::min(best, std::sqrt(dx * dx + dy * dy + dz * dz));
+    };
+    for (int r = 0; r <= kRings; ++r) {
+        // every cell of ring r is at least r - 1 - kGrow away along its farthest axis
+        if (best <= (float)(r - 1) - kGrow) break;
+        for (int dy = -r; dy <= r; ++dy)
+            for (int dz = -r; dz <= r; ++dz) {
+                const bool face = dy == -r || dy == r || dz == -r || dz == r;
+                if (face) {
+                    for (int dx = -r; dx <= r; ++dx) cell(px + dx, py + dy, pz + dz);
+                } else {
+                    cell(px - r, py + dy, pz + dz);
+                    if (r > 0) cell(px + r, py + dy, pz + dz);
+                }
+            }
+    }
+    return std::min(best, (float)(kRings - 1) - kGrow);
 }
 
 char *buffer_rows(vxpt_ctx *c, int which, int y, size_t &rowBytes) {
@@ -1258,7 +1314,11 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     {
         vxpt_ctx *c0 = cs[0];
         std::string err;
-        if (!band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err))
+        // a translated camera: the nearest surface bounds every primary hit's distance
+        const bool moved = c0->cam.pos.x != c0->prevCam.pos.x || c0->cam.pos.y != c0->prevCam.pos.y ||
+                           c0->cam.pos.z != c0->prevCam.pos.z;
+        const float nearDepth = moved ? nearest_surface(c0, c0->cam.pos) : 0.0f;
+        if (!band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err, nearDepth))
             return fail(c0, VXPT_ERR_STATE, err.c_str());
     }
     if (frame > 0 && (traceRows > cs[0]->haloTraceRows || histRows > cs[0]->haloHistRows)) {
@@ -2937,6 +2997,22 @@ int vxpt_band_halo_rows(const vxpt_camera *cur, const vxpt_camera *prev, int wid
     const CamDev pc = make_camera(width, height, prev ? *prev : *cur, nullptr, nullptr);
     std::string err;
     return band_halo_rows(c, pc, width, height, nranks, *trace_rows, *history_rows, err) ? VXPT_OK : VXPT_ERR_STATE;
+}
+
+int vxpt_band_halo_rows_near(const vxpt_camera *cur, const vxpt_camera *prev, int width, int height, int nranks,
+                             float near_depth, int *trace_rows, int *history_rows) {
+    if (!cur || width < 1 || height < 1 || nranks < 1 || !trace_rows || !history_rows) return VXPT_ERR_ARG;
+    const CamDev c = make_camera(width, height, *cur, nullptr, nullptr);
+    const CamDev pc = make_camera(width, height, prev ? *prev : *cur, nullptr, nullptr);
+    std::string err;
+    return band_halo_rows(c, pc, width, height, nranks, *trace_rows, *history_rows, err, near_depth) ? VXPT_OK
+                                                                                                     : VXPT_ERR_STATE;
+}
+
+int vxpt_nearest_surface(vxpt_ctx *c, const float pos[3], float *dist) {
+    if (!c || !pos || !dist) return VXPT_ERR_ARG;
+    *dist = nearest_surface(c, V3(pos[0], pos[1], pos[2]));
+    return VXPT_OK;
 }
 
 int vxpt_render_frame_linked(vxpt_ctx **cs, int n, const vxpt_denoise_params *p, int32_t frameNum, int32_t spp) {

@@ -174,6 +174,9 @@ def load_library(path=LIB_PATH):
         "vxpt_halo_plan": (I, [I, I, I, I, P, ctypes.POINTER(I)]),
         "vxpt_band_halo_rows": (I, [ctypes.POINTER(Camera), ctypes.POINTER(Camera), I, I, I, ctypes.POINTER(I),
                                     ctypes.POINTER(I)]),
+        "vxpt_band_halo_rows_near": (I, [ctypes.POINTER(Camera), ctypes.POINTER(Camera), I, I, I, ctypes.c_float,
+                                         ctypes.POINTER(I), ctypes.POINTER(I)]),
+        "vxpt_nearest_surface": (I, [P, P, ctypes.POINTER(ctypes.c_float)]),
         "vxpt_band_gather": (I, [P, I, I]),
         "vxpt_band_gather_linked": (I, [ctypes.POINTER(P), I, I, I]),
     }
@@ -224,6 +227,14 @@ class Renderer:
             pass
 
     # --- scene set-up (mainOffline.cpp:142-251) ---
+    def nearest_surface(self, pos):
+        """vxpt_nearest_surface: a lower bound on the distance from pos to any primary hit (the
+        nearest non-air cell grown by one cell, searched up to 64 cells)"""
+        d = ctypes.c_float(0.0)
+        p = (ctypes.c_float * 3)(*pos)
+        self._chk(self.lib.vxpt_nearest_surface(self.ctx, p, ctypes.byref(d)), "vxpt_nearest_surface")
+        return d.value
+
     def load_settings(self):
         self._chk(self.lib.vxpt_load_settings(self.ctx), "vxpt_load_settings")
 
@@ -623,14 +634,20 @@ def halo_plan(height, nranks, rank, rows):
     return {int(p): ((int(sy), int(sn)), (int(ry), int(rn))) for p, sy, sn, ry, rn in e}
 
 
-def band_halo_rows(cur, prev, width, height, nranks):
+def band_halo_rows(cur, prev, width, height, nranks, near=None):
     """vxpt_band_halo_rows: (trace rows, history rows) of a banded frame whose camera moved from
-    prev to cur ((pos, dir, fov) each); None when the library refuses the motion."""
+    prev to cur ((pos, dir, fov) each); None when the library refuses the motion.  With `near`
+    (vxpt_band_halo_rows_near) the camera may also translate: every primary hit lies at least
+    `near` from it."""
     def cam(c):
         return Camera((ctypes.c_float * 3)(*c[0]), (ctypes.c_float * 3)(*c[1]), c[2])
     t, h = ctypes.c_int(0), ctypes.c_int(0)
-    r = load_library().vxpt_band_halo_rows(ctypes.byref(cam(cur)), ctypes.byref(cam(prev)), width, height, nranks,
-                                           ctypes.byref(t), ctypes.byref(h))
+    if near is None:
+        r = load_library().vxpt_band_halo_rows(ctypes.byref(cam(cur)), ctypes.byref(cam(prev)), width, height,
+                                               nranks, ctypes.byref(t), ctypes.byref(h))
+    else:
+        r = load_library().vxpt_band_halo_rows_near(ctypes.byref(cam(cur)), ctypes.byref(cam(prev)), width, height,
+                                                    nranks, float(near), ctypes.byref(t), ctypes.byref(h))
     if r == -4:  # VXPT_ERR_STATE
         return None
     if r != 0:

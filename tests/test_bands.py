@@ -240,6 +240,7 @@ def test_band_halo_rows_follow_the_camera():
     assert vxpt.band_halo_rows(cam, cam, 640, 640, 1) == (72, 2)
     moved = ((cam[0][0] + 0.1, cam[0][1], cam[0][2]), cam[1], cam[2])
     assert vxpt.band_halo_rows(moved, cam, 640, 640, 2) is None
+    assert vxpt.band_halo_rows(moved, cam, 640, 640, 2, near=0.0) is None
     last = (72, 2)
     for pitch in (0.2, 0.5, 1.0, 1.5):
         got = vxpt.band_halo_rows((cam[0], _turn(cam[1], 0.0, pitch), cam[2]), cam, 640, 640, 2)
@@ -249,6 +250,107 @@ def test_band_halo_rows_follow_the_camera():
     # 8 bands of 80 rows: a 3-degree pitch needs more than a band
     assert vxpt.band_halo_rows((cam[0], _turn(cam[1], 0.0, 3.0), cam[2]), cam, 640, 640, 8) is None
     assert vxpt.band_halo_rows((cam[0], _turn(cam[1], 0.0, 3.0), cam[2]), cam, 640, 640, 2) is not None
+
+
+def test_band_halo_rows_bound_a_translation():
+    """vxpt_band_halo_rows_near: a translating camera gets halos from the hit-distance bound -- deeper
+    for nearer surfaces and longer moves, the rotation's depths as the bound goes to infinity, refused
+    when the bound is too small for the bands; every reprojected row of a hit at or beyond the bound
+    (sampled pixels, random distances) lies within the returned history depth."""
+    import vxpt
+    cam = C1_CAMERA
+    w, h = 640, 640
+    up = ((cam[0][0], cam[0][1] + 0.05, cam[0][2]), cam[1], cam[2])
+    far = vxpt.band_halo_rows(up, cam, w, h, 2, near=1e6)
+    # the rotation's computed depths (margins included) for an unturned camera
+    assert far[0] == 72 and far[1] <= 5
+    last = far
+    for near in (40.0, 10.0, 3.0, 1.0):
+        got = vxpt.band_halo_rows(up, cam, w, h, 2, near=near)
+        assert got is not None and got[0] >= last[0] and got[1] >= last[1], (near, got)
+        last = got
+    assert last[1] > 2
+    longer = ((cam[0][0], cam[0][1] + 0.5, cam[0][2]), cam[1], cam[2])
+    assert vxpt.band_halo_rows(longer, cam, w, h, 2, near=1.0)[1] > last[1]
+    assert vxpt.band_halo_rows(longer, cam, w, h, 8, near=0.2) is None
+    # the bound holds for sampled hits: project them with the camera model of band_halo_rows
+    near, (tr, hr) = 3.0, vxpt.band_halo_rows(up, cam, w, h, 2, near=3.0)
+    rng = np.random.default_rng(3)
+
+    def basis(c):
+        d = np.asarray(c[1], np.float64)
+        d /= np.linalg.norm(d)
+        right = np.cross(d, [0.0, 1.0, 0.0])
+        right /= np.linalg.norm(right)
+        upv = np.cross(right, d)
+        t = np.tan(np.radians(c[2]) / 2)
+        return d, right * t * w / h, upv * t
+
+    cd, cr, cu = basis(up)
+    pd, pr, pu = basis(cam)
+    y0, y1 = bands.band_rows(h, 2, 0)
+    for _ in range(4000):
+        px, py = rng.uniform(0, w), rng.uniform(y0, y1)
+        ray = cd + cr * (2 * px / w - 1) - cu * (2 * py / h - 1)
+        ray /= np.linalg.norm(ray)
+        hit = np.asarray(up[0]) + ray * near * (1 + rng.exponential(2.0))
+        v = hit - np.asarray(cam[0])
+        z = v @ pd
+        row = (1 - (v @ pu) / np.linalg.norm(pu) ** 2 / z) * h / 2
+        assert row < y1 + hr, (px, py, row)
+
+
+def _near_bound(o):
+    """nearest_surface restated over the oracle's voxels, brute force: the distance from the camera
+    to the nearest non-air cell grown by one cell"""
+    cx, cy, cz = o.chunks
+    ids = o.voxels().reshape(cz * cx * cy, 32, 32, 32)  # chunk, y, z, x
+    ch, yy, zz, xx = np.nonzero(ids)
+    x = (ch % cx) * 32 + xx
+    z = ((ch // cx) % cz) * 32 + zz
+    y = (ch // (cx * cz)) * 32 + yy
+
+    def gap(p, lo):
+        a, b = lo - 1.0, lo + 2.0
+        return np.where(p < a, a - p, np.where(p > b, p - b, 0.0))
+
+    def near(pos):
+        d = np.sqrt(gap(pos[0], x) ** 2 + gap(pos[1], y) ** 2 + gap(pos[2], z) ** 2)
+        return float(min(d.min(), 62.0))
+    return near
+
+
+def test_oracle_bands_follow_a_translating_camera():
+    """A camera that moves (and turns) between frames: halo depths from vxpt_band_halo_rows_near with
+    the world's nearest-surface bound (as vxpt_render_frame computes it) render the oracle's two bands
+    bit for bit like one band."""
+    import vxpt
+    bands_ = [bands.band_rows(H, 2, r) for r in range(2)]
+    single = _oracle()
+    backs = [OracleBand(_oracle(), *b) for b in bands_]
+    ex = bands.LocalExchange(backs, bands_)
+    near_of = _near_bound(single)
+    moves = [((0, 0, 0), 0), ((0, 0.15, 0), 0), ((0.1, -0.1, -0.1), 1.0), ((0, 0, 0), 0)]
+    pos, d = list(C1_CAMERA[0]), C1_CAMERA[1]
+    prev, prev_halo, deep = C1_CAMERA, (bands.TRACE_HALO, 2), 0
+    for f, (dp, pitch) in enumerate(moves):
+        pos = [pos[k] + dp[k] for k in range(3)]
+        d = _turn(d, 0.0, pitch)
+        cur = (tuple(pos), d, C1_CAMERA[2])
+        for o in [single] + [b.o for b in backs]:
+            o.set_camera(*cur[:2], fov=cur[2])
+            o.set_camera(*prev[:2], fov=prev[2], which=1)
+        halo = vxpt.band_halo_rows(cur, prev, W, H, 2, near=near_of(pos))
+        assert halo is not None, f
+        deep += halo[1] > 2
+        single.trace(f)
+        single.post_trace()
+        single.denoise(f, f + 1)
+        bands.run_frame(backs, ex, f, 1, P, halo, prev_halo)
+        out = np.concatenate([b.o.read(21)[y0:y1] for b, (y0, y1) in zip(backs, bands_)])
+        np.testing.assert_array_equal(out.view(np.uint32), single.read(21).view(np.uint32), err_msg="frame %d" % f)
+        prev, prev_halo = cur, halo
+    assert deep >= 2
 
 
 @pytest.mark.gpu
@@ -299,6 +401,58 @@ def test_gpu_linked_bands_follow_a_turning_camera(n, w, h, turns):
         r.set_camera(*far[:2], fov=far[2], prev=prev)
     with pytest.raises(vxpt.VxptError):
         linked.render_frame(len(turns), spp, p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,w,h", [(2, 96, 320), (8, 640, 640)])
+def test_gpu_linked_bands_follow_a_translating_camera(n, w, h):
+    """A camera that moves (and turns) between frames: the banded frame takes its halo depths from
+    the world's nearest-surface bound (vxpt_nearest_surface, equal to the restatement over the
+    oracle's voxels) and stays bit-exact against one context; a move too long for the bands is
+    refused."""
+    import vxpt
+    spp = 2
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_sky()
+        return r
+
+    o = oracle.Oracle(8, 8)
+    o.terrain((2, 1, 2))
+    near_of = _near_bound(o)
+    p = vxpt.DenoiseParams.defaults()
+    single = make()
+    rs = [make() for _ in range(n)]
+    linked = vxpt.LinkedBands(rs)
+    rows = [bands.band_rows(h, n, k) for k in range(n)]
+    moves = [((0, 0, 0), 0), ((0, 0.02, 0), 0), ((0.02, -0.02, -0.02), 0.3), ((0, 0, 0.03), 0), ((0, 0, 0), 0)]
+    pos, d = list(C1_CAMERA[0]), C1_CAMERA[1]
+    prev, deep = C1_CAMERA, 0
+    for f, (dp, pitch) in enumerate(moves):
+        pos = [pos[k] + dp[k] for k in range(3)]
+        d = _turn(d, 0.0, pitch)
+        cur = (tuple(pos), d, C1_CAMERA[2])
+        assert abs(single.nearest_surface(pos) - near_of(pos)) < 1e-4
+        halo = vxpt.band_halo_rows(cur, prev, w, h, n, near=single.nearest_surface(pos))
+        assert halo is not None, f
+        deep += halo[1] > 2
+        for r in [single] + rs:
+            r.set_camera(*cur[:2], fov=cur[2], prev=prev)
+        single.render_frame(f, spp, p)
+        linked.render_frame(f, spp, p)
+        ref = single.read("OUTPUT")
+        out = np.concatenate([r.read("OUTPUT")[y0:y1] for r, (y0, y1) in zip(rs, rows)])
+        np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32), err_msg="frame %d" % f)
+        prev = cur
+    assert deep >= 2
+    far = ((pos[0], pos[1] + 2.0, pos[2]), d, C1_CAMERA[2])
+    for r in rs:
+        r.set_camera(*far[:2], fov=far[2], prev=prev)
+    with pytest.raises(vxpt.VxptError):
+        linked.render_frame(len(moves), spp, p)
 
 
 def _oracle_turning(turns, halos_from_library):
