@@ -46,6 +46,9 @@
 #ifndef VX_WPE_FINISH
 #define VX_WPE_FINISH 1
 #endif
+#ifndef VX_WPE_RESTIR
+#define VX_WPE_RESTIR 1
+#endif
 
 namespace vx {
 namespace {
@@ -1221,7 +1224,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
 }
 
 template <bool MESH>
-__global__ __launch_bounds__(256) void k_restir(TraceArgs a, int seg) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESTIR))) void k_restir(TraceArgs a, int seg) {
     QRays qr;
     qr.mask = 0u;
     restir_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
