@@ -1285,7 +1285,9 @@ hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
     static const bool stT = !(getenv("VXPT_TA_ST") && atoi(getenv("VXPT_TA_ST")) == 0);
     // VXPT_TA_LDS=1: the LDS window (measured slower: 95 -> 109 us at 137 VGPRs / 3 waves, 0.367 ->
     // 0.382 ms chain; bounded to 4 waves it spills 48 B/lane, 0.378 ms)
-    static const bool lds = getenv("VXPT_TA_LDS") && atoi(getenv("VXPT_TA_LDS")) == 1;
+    // (read per launch: a test switches it between frames)
+    const char *ldsEnv = getenv("VXPT_TA_LDS");
+    const bool lds = ldsEnv && atoi(ldsEnv) == 1;
     if (stT && lds) hipLaunchKernelGGL((k_temporal<true, true>), grid_st(a), dim3(256), 0, st, a, rot);
     else if (stT) hipLaunchKernelGGL((k_temporal<true, false>), grid_st(a), dim3(256), 0, st, a, rot);
     else if (lds) hipLaunchKernelGGL((k_temporal<false, true>), grid16(a), dim3(256), 0, st, a, rot);

@@ -328,6 +328,30 @@ def test_denoiser_history_fix_after_camera_move():
     r.close()
 
 
+def test_temporal_lds_window_equals_global_taps(monkeypatch):
+    """The opt-in LDS window of the temporal accumulation (VXPT_TA_LDS=1, read per launch) gives the
+    global-tap kernel's results bit for bit: 8 frames with the camera held, turned and moved (taps
+    outside the window fall back to the global planes)."""
+    rs = [_setup(100, 70)[0] for _ in range(2)]
+    p = _dn_params()
+    pos, d, fov = C1_CAMERA[0], C1_CAMERA[1], C1_CAMERA[2]
+    cams = [(pos, d)] * 4 + [((pos[0] + 0.3, pos[1], pos[2] - 0.2), d)] + \
+        [((pos[0] + 0.3, pos[1], pos[2] - 0.2), (d[0] + 0.05, d[1] + 0.03, d[2]))] * 3
+    prev = (pos, d)
+    for f, cur in enumerate(cams):
+        outs = []
+        for k, r in enumerate(rs):
+            monkeypatch.setenv("VXPT_TA_LDS", str(k))
+            r.set_camera(*cur, fov=fov, prev=(prev[0], prev[1], fov))
+            r.render_frame(f, 1, p)
+            outs.append([r.read(n).view(np.uint32) for n in ("OUTPUT", "PREV_ILLUM", "PREV_FAST", "HIST_LEN")])
+        for a, b in zip(*outs):
+            np.testing.assert_array_equal(a, b, err_msg="frame %d" % f)
+        prev = cur
+    for r in rs:
+        r.close()
+
+
 @pytest.mark.parametrize("w,h", [(64, 160), (100, 62)])
 def test_overlapped_passes_equal_sequential_passes(w, h):
     """vxpt_render_frame runs a pass's first half (camera rays .. RIS visibility) beside the previous
