@@ -773,12 +773,20 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
             const float sMat = ld_ushort(a.material, W, H, sx, sy);
             const V3 sN = ld4(a.normalRough, W, H, sx, sy).xyz();
             const V3 sWP = wp(a, sx, sy);
+            // the tap's value is fetched beside its weight's inputs (edge-clamped, so always a valid
+            // read): one dependent round trip fewer; used only when the weight passes
+#ifndef VX_HF_LATE_VALUE
+            const V4 sv = ld4(a.ping, W, H, sx, sy);
+#endif
             float w = plane_w(cWP, cN, sWP, dthr);
             w *= powf(fmaxf(0.01f, dot(cN, sN)), 8.0f);
             w = inside ? w : 0;
             w *= (float)(sMat == cMat);
             if (w > 1e-4f) {
-                c = ld4(a.ping, W, H, sx, sy) * w;
+#ifdef VX_HF_LATE_VALUE
+                const V4 sv = ld4(a.ping, W, H, sx, sy);
+#endif
+                c = sv * w;
                 cw = w;
             }
         }
@@ -825,13 +833,16 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
 // One workgroup per 16x16 tile, over the tile's list from k_temporal: a
 // sparse list (<= 64 pixels, the steady state) is walked one pixel per wave at
 // a time, a dense one (history just reset) gets one lane per pixel.
+// blockIdx.z splits a sparse list over gridDim.z workgroups (rounds of 8 pixels dealt round-robin): a
+// round is the listed pixel's chain of dependent loads, so a tile's rounds run side by side.
 __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
     const unsigned tile = blockIdx.y * ((a.W + 15) / 16) + blockIdx.x;
     const unsigned n = a.hfCount[tile];
     const unsigned wv = threadIdx.x >> 6;
     if (n <= 64) {  // sparse (steady state): each half-wave takes every 8th listed pixel, its taps in parallel
         const unsigned half = wv * 2 + ((threadIdx.x >> 5) & 1);
-        for (unsigned k0 = wv * 2; k0 < n; k0 += 8) {  // wave-uniform trip count; the halves share the shuffles
+        // wave-uniform trip count; the halves share the readlanes
+        for (unsigned k0 = blockIdx.z * 8 + wv * 2; k0 < n; k0 += 8 * gridDim.z) {
             const unsigned k = k0 + (half & 1);
             const bool has = k < n;
             const size_t i = a.hfList[tile * 256 + (has ? k : k0)];
@@ -839,7 +850,7 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
         }
         return;
     }
-    if (threadIdx.x >= n) return;
+    if (blockIdx.z != 0 || threadIdx.x >= n) return;
     const size_t i = a.hfList[tile * 256 + threadIdx.x];
     history_fix_px(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i);
 }
@@ -1295,7 +1306,12 @@ hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_history_fix, grid16(a), dim3(256), 0, st, a);
+    // steady state on the C3 bench: ~3000 listed pixels in ~960 of 8160 tiles, at most ~21 per tile
+    // (tools/hf_stats.py); VXPT_HF_SPLIT workgroups per tile
+    static const int split = getenv("VXPT_HF_SPLIT") ? std::max(1, atoi(getenv("VXPT_HF_SPLIT"))) : 4;
+    dim3 g = grid16(a);
+    g.z = (unsigned)split;
+    hipLaunchKernelGGL(k_history_fix, g, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 // tile edge of the LDS-staged 5x5 stencils (history clamping, the first a-trous): 32 stages the
