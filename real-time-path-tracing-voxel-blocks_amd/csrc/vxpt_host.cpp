@@ -171,6 +171,12 @@ struct vxpt_ctx {
     std::vector<uint8_t> hIds, hBricks, hOd;
     std::vector<uint64_t> hMacro, hCell;
     std::vector<int> topCount;  // cube cells per 64^3 block
+    // world edits / uploads so far, and the last nearest-surface search (band halos of a moving
+    // camera): a later position p reuses it as nearDist - |p - nearPos| (1-Lipschitz) while the
+    // world is unchanged and that keeps >= 3/4 of the searched distance
+    unsigned worldVersion = 0, nearVersion = ~0u;
+    V3 nearPos{0.0f, 0.0f, 0.0f};
+    float nearDist = 0.0f;
     int prevSceneEmpty = 0;     // the next trace pass's temporal visibility sees no previous scene
     MatDev mats[32] = {};  // by block id: 1..12 cubes (kernel arguments), 13..29 instanced meshes (meshMats)
     CamDev cam{}, prevCam{};
@@ -725,6 +731,7 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
     if (old == id) return 0;
     hipStream_t st = c->stream;
     c->hIds[ci] = (uint8_t)id;
+    ++c->worldVersion;
     HIPCHK(c, hipMemcpyAsync(c->voxels.p + ci, &c->hIds[ci], 1, hipMemcpyHostToDevice, st));
     const size_t b = brick_lin(c, x >> 2, y >> 2, z >> 2);
     const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
@@ -1317,9 +1324,27 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         // a translated camera: the nearest surface bounds every primary hit's distance
         const bool moved = c0->cam.pos.x != c0->prevCam.pos.x || c0->cam.pos.y != c0->prevCam.pos.y ||
                            c0->cam.pos.z != c0->prevCam.pos.z;
-        const float nearDepth = moved ? nearest_surface(c0, c0->cam.pos) : 0.0f;
-        if (!band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err, nearDepth))
-            return fail(c0, VXPT_ERR_STATE, err.c_str());
+        float nearDepth = 0.0f;
+        bool reused = false;
+        auto search = [&]() {
+            nearDepth = nearest_surface(c0, c0->cam.pos);
+            c0->nearPos = c0->cam.pos;
+            c0->nearDist = nearDepth;
+            c0->nearVersion = c0->worldVersion;
+        };
+        if (moved) {
+            const V3 dp = c0->cam.pos - c0->nearPos;
+            const float reuse = c0->nearDist - std::sqrt(dp.x * dp.x + dp.y * dp.y + dp.z * dp.z);
+            reused = c0->nearVersion == c0->worldVersion && reuse >= 0.75f * c0->nearDist && reuse > 0.0f;
+            if (reused) nearDepth = reuse;
+            else search();
+        }
+        bool ok = band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err, nearDepth);
+        if (!ok && reused) {  // the reused bound is looser than a fresh search: search before refusing
+            search();
+            ok = band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err, nearDepth);
+        }
+        if (!ok) return fail(c0, VXPT_ERR_STATE, err.c_str());
     }
     if (frame > 0 && (traceRows > cs[0]->haloTraceRows || histRows > cs[0]->haloHistRows)) {
         std::vector<std::pair<int, int>> br;
@@ -1739,6 +1764,7 @@ int vxpt_upload_voxels(vxpt_ctx *c, const uint8_t *ids, int cxn, int cyn, int cz
     c->cx = cxn; c->cy = cyn; c->cz = czn;
     const size_t n = (size_t)cxn * cyn * czn * 32768;
     c->hIds.assign(ids, ids + n);
+    ++c->worldVersion;
     if (int r = upload_vec(c, c->voxels, c->hIds.data(), n)) return r;
     if (int r = build_occupancy(c, c->hIds.data())) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
