@@ -404,6 +404,31 @@ def test_gpu_linked_bands_follow_a_turning_camera(n, w, h, turns):
 
 
 @pytest.mark.gpu
+def test_gpu_nearest_surface_matches_restatement():
+    """vxpt_nearest_surface over the host mirror of the world equals the brute-force restatement over
+    the oracle's voxels (nearest non-air cell grown by one cell, capped at 62) at random positions in
+    and around the C1 world, before and after a block edit next to the probe."""
+    import vxpt
+    r = vxpt.Renderer(32, 32)
+    r.load_settings()
+    r.generate_terrain((2, 1, 2))
+    o = oracle.Oracle(8, 8)
+    o.terrain((2, 1, 2))
+    near_of = _near_bound(o)
+    rng = np.random.default_rng(11)
+    pts = rng.uniform([-20.0, -10.0, -20.0], [84.0, 60.0, 84.0], size=(200, 3))
+    for p in pts:
+        assert abs(r.nearest_surface(p) - near_of(p)) < 1e-4, p
+    # a block placed in the air beside a probe point: the bound drops to it
+    p = (35.6, 29.3, 42.1)  # ~17.6 above the terrain there
+    before = r.nearest_surface(p)
+    r.set_block(35, 31, 42, 1)
+    after = r.nearest_surface(p)
+    assert after < before and abs(after - 0.7) < 1e-4, (before, after)
+    r.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,w,h", [(2, 96, 320), (8, 640, 640)])
 def test_gpu_linked_bands_follow_a_translating_camera(n, w, h):
     """A camera that moves (and turns) between frames: the banded frame takes its halo depths from
