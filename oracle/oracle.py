@@ -67,6 +67,7 @@ def lib():
             "orc_copy_camera_to_prev": (None, [P]),
             "orc_trace": (None, [P, I, I, I, I]),
             "orc_post_trace": (None, [P]),
+            "orc_trace_frame_spp": (None, [P, I, I]),
             "orc_set_denoise_params": (None, [P, P, P]),
             "orc_denoise": (None, [P, I, I]),
             "orc_pass": (None, [P, I, I, I]),
@@ -297,6 +298,23 @@ class Oracle:
         if self._lights_dirty and (y1 is None or y1 >= self.H):
             self._lights_dirty = False
             self.L.orc_set_light_remap(self.h, _p(self._remap_keep), 0, 0)
+
+    def render_frame(self, frame, spp=1, denoise=True):
+        """One OfflineBackend::renderFrame (OfflineBackend.cpp:46-89) at spp samples per pixel, as
+        vxpt_render_frame defines it: spp 1-spp passes at iterationIndex
+        frame*spp + s, radiance averaged in pass order, the G-buffer and depth of the last pass, one
+        denoise (frameNum = frame, iterationIndex = frame*spp + spp).  orc_trace_frame_spp."""
+        it0 = frame * spp
+        if spp == 1:
+            self.trace(it0)
+            self.post_trace()
+        else:
+            self.L.orc_trace_frame_spp(self.h, it0, spp)
+            if self._lights_dirty:  # held for the frame's first pass (cleared there by the C side)
+                self._lights_dirty = False
+                self.L.orc_set_light_remap(self.h, _p(self._remap_keep), 0, 0)
+        if denoise:
+            self.denoise(frame, it0 + spp)
 
     def set_textures(self, chains):
         """chains: list of mip-level lists (level l = (S>>l, S>>l, 4) uint8 RGBA)."""

@@ -157,6 +157,55 @@ void orc_trace(void *p, int it, int y0, int y1, int primaryOnly) {
     trace_frame(c->s, c->f, it, y0, y1, primaryOnly != 0);
 }
 void orc_post_trace(void *p) { post_trace_copies(static_cast<Ctx *>(p)->f); }
+
+// The trace passes of one spp > 1 frame (the benchmarked frame): spp
+// 1-spp passes (RayGen.cu:102-182 each) at iterationIndex it0 + s, s = 0..spp-1.
+// - Pass s > 0 takes pass s-1 as its ReSTIR history (Restir.h:348-381 GetPrevSurface reads the
+//   previous pass's depth / normal / material, reservoirs by iterationIndex parity, Restir.h:13,50)
+//   and pass s-1's camera, the frame's own: prevCam = cam.  Pass 0 reads the previous frame's last
+//   pass through the denoiser's history copies (Denoiser.cu:394-407) and the frame's history camera.
+// - Radiance averaged in pass order, acc = acc + r * (1/spp) per channel in binary32 (first pass
+//   from 0); .w, depth and every G-buffer plane are the last pass's.
+// - The light-id remap and the empty previous scene of an edit hold for the frame's first pass only.
+// Leaves the average in illum for denoise_frame(frameNum, it0 + spp) and the denoiser's history
+// copies (prevNormalRough / prevDepth / prevMaterial) as the previous frame left them.
+void orc_trace_frame_spp(void *p, int it0, int spp) {
+    auto *c = static_cast<Ctx *>(p);
+    Scene &s = c->s;
+    Frame &f = c->f;
+    const size_t n = (size_t)f.W * f.H;
+    const std::vector<F4> histNr = f.prevNormalRough;
+    const std::vector<float> histDepth = f.prevDepth, histMat = f.prevMaterial;
+    const Camera histCam = s.prevCam;
+    std::vector<F4> acc(n);
+    const float scale = 1.0f / (float)spp;
+    for (int k = 0; k < spp; ++k) {
+        if (k > 0) {
+            f.prevNormalRough = f.normalRough;
+            f.prevDepth = f.depth;
+            f.prevMaterial = f.material;
+            s.prevCam = s.cam;
+        }
+        trace_frame(s, f, it0 + k, 0, f.H, false);
+        post_trace_copies(f);
+        s.lightsDirty = false;
+        s.prevSceneEmpty = false;
+        for (size_t i = 0; i < n; ++i) {
+            const F4 r = f.illum[i];
+            F4 a = k == 0 ? F4(0.0f) : acc[i];
+            a.x = a.x + r.x * scale;
+            a.y = a.y + r.y * scale;
+            a.z = a.z + r.z * scale;
+            a.w = r.w;
+            acc[i] = a;
+        }
+    }
+    f.prevNormalRough = histNr;
+    f.prevDepth = histDepth;
+    f.prevMaterial = histMat;
+    s.prevCam = histCam;
+    f.illum = acc;
+}
 void orc_set_prev_scene_empty(void *p, int on) { static_cast<Ctx *>(p)->s.prevSceneEmpty = on != 0; }
 // the light-id remap of the next pass (dirty = 0: the pass after it, no remap)
 void orc_set_light_remap(void *p, const int *remap, int prevNumLights, int dirty) {

@@ -835,7 +835,9 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
         a.numLights = (int)c->nLights;
     }
     a.cam = c->cam;
-    a.prevCam = c->prevCam;
+    // the temporal taps reproject into the previous pass's view: the frame's history camera for its
+    // first pass, the frame's own camera for the later passes of an accumulation
+    a.prevCam = (accumulate && !accumFirst) ? c->cam : c->prevCam;
     // the slot this pass writes: not the previous pass's (its temporal taps), not the denoiser's
     // history, and not the one the previous pass's second half may still be reading
     int next = 0;

@@ -1,0 +1,288 @@
+"""GPU parity of the benchmarked frames, at the configs' own sizes.
+
+- The C3 frame: vxpt_render_frame / vxpt_render_frames at 4 spp = 4 1-spp passes at
+  iterationIndex f*4 + s (RayGen.cu:102-182), the passes' radiance averaged, depth and G-buffer
+  from the last pass, ReSTIR reuse between the passes (Restir.h:13,50, 348-381) and one denoise
+  of the average (Denoiser.cu:24-408) -- against Oracle.render_frame (orc_trace_frame_spp), on the
+  C3 world (256^3) at 256x144 over 3 frames and at 1920x1080 (the bench's pipelined frame loop).
+- C2 at 1920x1080 on the C1 scene: primary rays + sky + G-buffer (DDA hits bit for bit).
+- C5 at 1920x1080: 64 frames x 1 spp of the C1 scene (mainOffline.cpp:423-498's canonical
+  render), relative RMS of the denoised output and the radiance.
+
+Bars: test_gpu_parity.check_radiance (north_star's per-pixel L2 < 1e-3) at 256x144.  At 1080p
+(2 M pixels per frame) a 1-ulp libm difference (ocml vs glibc) flips a threshold test on a few
+pixels; such a pixel then selects another light sample.  So at 1080p every pixel at or above 1e-3
+is listed with its cause and must have one:
+- radiance: the pixel's final reservoir differs from the oracle's (another light / uv / M was
+  selected -- a branch flip, not an arithmetic drift);
+- denoised output: a radiance or reservoir difference inside the filter footprint (34 px: the
+  a-trous steps 1..8 and the 5x5 / 7x7 stencils), or, past 4 frames of history, the history clamp's
+  x-only Float3 min / max (HistoryClamping.h:124-125, LinearMath.h:526-529) -- the reference's
+  own sensitivity (test_denoise_host.py::test_reference_denoiser_is_chaotic_once_history_exceeds_four_frames).
+and at most 1e-4 of the pixels may be listed (C5: 1e-3, and no more than twice as many pixels as
+a second oracle diverges from the first under a 1e-6 perturbation of its denoiser input).
+"""
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+import vxpt
+from golden.make_golden import C1_CAMERA
+from test_gpu_parity import DN_FLOATS, DN_INTS, E_MAX, _dn_params, _inject_sky, check_radiance, pixel_l2
+
+pytestmark = pytest.mark.gpu
+
+C3_CHUNKS = (8, 8, 8)
+GBUF = ("DEPTH", "NORMAL_ROUGH", "MATERIAL", "ALBEDO", "MAT_PARAM")
+FOOTPRINT = 34  # rows / columns a denoised pixel reads around itself
+LISTED_MAX = 1e-4  # fraction of pixels allowed at or above 1e-3 at 1080p, each with its cause
+
+
+def _c3_pair(w, h):
+    pos = tuple(p * 4 for p in C1_CAMERA[0])
+    r = vxpt.Renderer(w, h)
+    r.load_settings()
+    r.generate_terrain(C3_CHUNKS, height_scale=128.0, freq_den=256.0, global_y=True)
+    r.set_camera(pos, C1_CAMERA[1], fov=90.0, prev=(pos, C1_CAMERA[1], 90.0))
+    r.set_sky(0.25, 45.0, 0.0, 1.0)
+    o = oracle.Oracle(w, h)
+    o.terrain(C3_CHUNKS, height_scale=128.0, freq_den=256.0, global_y=True)
+    o.set_camera(pos, C1_CAMERA[1], fov=90.0)
+    o.set_camera(pos, C1_CAMERA[1], fov=90.0, which=1)
+    o.set_denoise_params(DN_FLOATS, DN_INTS)
+    _inject_sky(r, o)
+    return r, o
+
+
+def _c1_pair(w, h):
+    r = vxpt.Renderer(w, h)
+    r.load_settings()
+    r.generate_terrain((2, 1, 2), height_scale=32.0)
+    cam = C1_CAMERA
+    r.set_camera(cam[0], cam[1], fov=cam[2], prev=cam)
+    r.set_sky(0.25, 45.0, 0.0, 1.0)
+    o = oracle.Oracle(w, h)
+    o.terrain((2, 1, 2))
+    o.set_camera(cam[0], cam[1], fov=cam[2])
+    o.set_camera(cam[0], cam[1], fov=cam[2], which=1)
+    o.set_denoise_params(DN_FLOATS, DN_INTS)
+    _inject_sky(r, o)
+    return r, o
+
+
+def _gbuffer_equal(r, o, tag):
+    for name in GBUF:
+        g, c = r.read(name), o.read(vxpt.BUF[name])
+        bad = ~np.isclose(g, c, rtol=1e-6, atol=1e-7)
+        assert not bad.any(), (tag, name, bad.mean(), np.argwhere(bad)[:5])
+
+
+def _reservoir_diff(r, o, it):
+    """Per pixel: the reservoir of the pass of iterationIndex `it` differs from the oracle's beyond
+    arithmetic noise -- another light sample (lightData, uvData or M differ), or a weightSum more
+    than 1e-4 apart, which temporal reuse carries over from an earlier pass's different sample."""
+    g, c = r.read("RESERVOIRS"), o.read(vxpt.BUF["RESERVOIRS"])
+    n = r.W * r.H
+    par = it % 2
+    g, c = g[par * n:(par + 1) * n], c[par * n:(par + 1) * n]
+    d = (g["lightData"] != c["lightData"]) | (g["uvData"] != c["uvData"]) | (g["M"] != c["M"])
+    ws = np.abs(g["weightSum"] - c["weightSum"]) > 1e-4 * np.maximum(np.abs(c["weightSum"]), 1e-30)
+    return (d | ws).reshape(r.H, r.W)
+
+
+def _dilate(mask, k):
+    """Pixels within k (Chebyshev) of a set pixel."""
+    if not mask.any():
+        return mask
+    out = mask.copy()
+    ys, xs = np.nonzero(mask)
+    for y, x in zip(ys, xs):
+        out[max(0, y - k):y + k + 1, max(0, x - k):x + k + 1] = True
+    return out
+
+
+def _listed(e, causes, tag, listed_max=LISTED_MAX):
+    """The pixels at or above 1e-3 and their causes (each must have one, at most listed_max of the
+    frame).  causes: [(name, bool mask)] in order; a pixel takes the first cause that covers it."""
+    over = e >= E_MAX
+    rows = []
+    left = over.copy()
+    for name, m in causes:
+        hit = left & m
+        rows.append("%s %d" % (name, int(hit.sum())))
+        left &= ~m
+    worst = np.unravel_index(e.argmax(), e.shape)
+    msg = "%s: %d pixels >= 1e-3 (%.2e of the frame; max e %.3g at %s): %s; unexplained %d at %s" % (
+        tag, int(over.sum()), over.mean(), e.max(), tuple(int(v) for v in worst), ", ".join(rows), int(left.sum()),
+        np.argwhere(left)[:8].tolist())
+    print(msg, flush=True)
+    assert not left.any(), msg
+    assert over.mean() <= listed_max, msg
+    return msg
+
+
+def _check_means(r, o, tag):
+    for name, g, c in (("radiance", r.read("ILLUM"), o.read(0)), ("output", r.read("OUTPUT"), o.read(21))):
+        mg, mc = g[..., :3].mean(), c[..., :3].mean()
+        assert abs(mg - mc) <= 1e-5 * abs(mc), (tag, name, mg, mc)
+
+
+def test_c3_spp4_frames_match_oracle():
+    """C3 world at 256x144, 3 frames of vxpt_render_frame(spp = 4): the accumulated radiance, the
+    last pass's G-buffer and reservoirs, and the denoised average."""
+    r, o = _c3_pair(256, 144)
+    p = _dn_params()
+    try:
+        for f in range(3):
+            r.render_frame(f, 4, p)
+            o.render_frame(f, 4)
+            _gbuffer_equal(r, o, "frame %d" % f)
+            flips = _reservoir_diff(r, o, f * 4 + 3)
+            assert flips.mean() < 1e-3, (f, flips.sum())
+            check_radiance(r.read("ILLUM"), o.read(0), "c3 spp4 frame%d radiance" % f)
+            check_radiance(r.read("OUTPUT"), o.read(21), "c3 spp4 frame%d output" % f)
+            assert (r.read("HIST_LEN") == o.read(19)).mean() >= 0.999, f
+    finally:
+        r.close()
+
+
+def test_c3_spp4_moving_camera_matches_oracle():
+    """The later passes of a frame reproject into the frame's own camera (the previous pass's),
+    the first pass into the history camera: 3 frames with the camera moving and turning."""
+    r, o = _c3_pair(192, 108)
+    p = _dn_params()
+    pos, d = tuple(v * 4 for v in C1_CAMERA[0]), C1_CAMERA[1]
+    cams = [(pos, d), ((pos[0] + 0.6, pos[1] + 0.1, pos[2] - 0.4), d),
+            ((pos[0] + 0.9, pos[1] + 0.1, pos[2] - 0.7), (d[0] + 0.04, d[1] + 0.02, d[2]))]
+    prev = cams[0]
+    try:
+        for f, cur in enumerate(cams):
+            r.set_camera(*cur, fov=90.0, prev=(prev[0], prev[1], 90.0))
+            o.set_camera(*cur, fov=90.0)
+            o.set_camera(*prev, fov=90.0, which=1)
+            r.render_frame(f, 4, p)
+            o.render_frame(f, 4)
+            _gbuffer_equal(r, o, "frame %d" % f)
+            check_radiance(r.read("ILLUM"), o.read(0), "moving spp4 frame%d radiance" % f)
+            check_radiance(r.read("OUTPUT"), o.read(21), "moving spp4 frame%d output" % f)
+            prev = cur
+    finally:
+        r.close()
+
+
+def test_c3_1080p_bench_frames_match_oracle():
+    """The bench's workload itself: 1920x1080, 4 spp, C3 world, frames 0 and 1 through
+    vxpt_render_frames (the pipelined loop bench.py times), against two oracle frames.  Measured
+    (round 4): 1 pixel of 2 M at or above 1e-3 (e 2.1e-3, its reservoir's weightSum 1.4e-3 apart:
+    an earlier pass's different sky-sample uv carried by temporal reuse); outputs max e 4.5e-5."""
+    r, o = _c3_pair(1920, 1080)
+    p = _dn_params()
+    try:
+        t0 = time.time()
+        r.render_frames(0, 2, 4, p)
+        for f in range(2):
+            o.render_frame(f, 4)
+        print("oracle: 2 frames of 4 passes at 1080p in %.1f s" % (time.time() - t0), flush=True)
+        tag = "C3 1080p frame 1"
+        _gbuffer_equal(r, o, tag)
+        e_in = pixel_l2(r.read("ILLUM"), o.read(0))
+        res = _reservoir_diff(r, o, 7)
+        print("%s: radiance e<1e-4 %.6f, reservoirs differing %d" % (tag, (e_in < 1e-4).mean(), int(res.sum())))
+        assert (e_in < 1e-4).mean() >= 0.999, tag
+        _listed(e_in, [("the pixel's reservoir differs (another sample, or its weight carried from one)", res)],
+                tag + " radiance")
+        e_out = pixel_l2(r.read("OUTPUT"), o.read(21))
+        assert (e_out < 1e-4).mean() >= 0.999, tag
+        near = _dilate(res | (e_in >= 1e-4), FOOTPRINT)
+        _listed(e_out, [("radiance / reservoir difference within the filter footprint", near)], tag + " output")
+        _check_means(r, o, tag)
+    finally:
+        r.close()
+
+
+def test_c2_1080p_primary_gbuffer_on_c1_scene():
+    """C2: 1920x1080 primary rays + sky + SoA G-buffer on the C1 scene; the DDA's hit
+    distances / normals / materials equal the oracle's (<= 1e-6), the sky radiance <= 1e-5."""
+    r, o = _c1_pair(1920, 1080)
+    try:
+        for it in (0, 1):
+            r.trace(it, primary_only=True)
+            o.trace(it, primary_only=True)
+            for name in ("DEPTH", "NORMAL_ROUGH", "GEO_NORMAL_THIN", "ALBEDO", "MATERIAL", "MAT_PARAM"):
+                g, c = r.read(name), o.read(vxpt.BUF[name])
+                bad = ~np.isclose(g, c, rtol=1e-6, atol=1e-7)
+                assert not bad.any(), (it, name, bad.mean(), np.argwhere(bad)[:5])
+            np.testing.assert_allclose(r.read("ILLUM"), o.read(0), rtol=1e-5, atol=1e-6)
+        assert 0.3 < (r.read("DEPTH") < 1e20).mean() < 0.99
+    finally:
+        r.close()
+
+
+@pytest.mark.timeout(900)
+def test_c5_1080p_64_frames_match_oracle():
+    run_c5(1920, 1080, 64)
+
+
+def run_c5(w, h, frames):
+    """C5 (mainOffline.cpp:423-498): `frames` frames x 1 spp of the C1 scene at w x h.
+    Relative RMS over non-sky pixels < 1e-3 (denoised output) and < 1e-5 (radiance).  Past 4 frames
+    of history the reference's denoiser is chaotic (the history clamp's x-only Float3 min / max,
+    HistoryClamping.h:124-125, LinearMath.h:526-529): a second oracle whose radiance is
+    perturbed by 1e-6 relative before each denoise diverges from the first on as many pixels.  So
+    the GPU's output must stay within 2x that self-divergence (pixels at or above 1e-3, and RMS), and
+    every GPU pixel at or above 1e-3 is listed with a cause.  Measured (round 4): GPU 251 pixels
+    >= 1e-3, RMS 4.8e-5; perturbed oracle 174 pixels, RMS 3.7e-5."""
+    r, o = _c1_pair(w, h)
+    o2 = oracle.Oracle(w, h)  # the same scene, its denoiser input perturbed
+    o2.terrain((2, 1, 2))
+    o2.set_camera(C1_CAMERA[0], C1_CAMERA[1], fov=C1_CAMERA[2])
+    o2.set_camera(C1_CAMERA[0], C1_CAMERA[1], fov=C1_CAMERA[2], which=1)
+    o2.set_denoise_params(DN_FLOATS, DN_INTS)
+    _inject_sky(r, o2)
+    p = _dn_params()
+    flips = np.zeros((h, w), bool)  # pixels whose radiance took another sample in some frame
+    t0 = time.time()
+    try:
+        for f in range(frames):
+            r.render_frame(f, 1, p)
+            o.render_frame(f, 1)
+            o2.render_frame(f, 1, denoise=False)
+            il = o2.read(0)
+            il[..., :3] *= np.float32(1.0 + 1e-6)
+            o2.write(0, il)
+            o2.denoise(f, f + 1)
+            e_in = pixel_l2(r.read("ILLUM"), o.read(0))
+            flips |= _reservoir_diff(r, o, f) & (e_in >= 1e-4)
+            if f % 16 == 15:
+                print("C5 frame %d, %.0f s" % (f, time.time() - t0), flush=True)
+        mask = r.read("DEPTH") < 1e20
+        assert mask.mean() > 0.3
+        rms = {}
+        for name, g, c in (("OUTPUT", r.read("OUTPUT"), o.read(21)), ("ILLUM", r.read("ILLUM"), o.read(0)),
+                           ("OUTPUT perturbed oracle", o2.read(21), o.read(21))):
+            g, c = g[..., :3][mask], c[..., :3][mask]
+            rms[name] = np.sqrt(((g - c) ** 2).mean()) / np.sqrt((c ** 2).mean())
+            print("C5 %dx%d %s relative RMS %.3e" % (w, h, name, rms[name]), flush=True)
+        assert rms["OUTPUT"] < 1e-3 and rms["ILLUM"] < 1e-5, rms
+        assert rms["OUTPUT"] <= 2 * rms["OUTPUT perturbed oracle"], rms
+        tag = "C5 %dx%d frame %d" % (w, h, frames - 1)
+        _gbuffer_equal(r, o, tag)
+        e_in = pixel_l2(r.read("ILLUM"), o.read(0))
+        res = _reservoir_diff(r, o, frames - 1)
+        _listed(e_in, [("the pixel's reservoir differs (another sample, or its weight carried from one)", res)],
+                tag + " radiance")
+        e_out = pixel_l2(r.read("OUTPUT"), o.read(21))
+        e_self = pixel_l2(o2.read(21), o.read(21))
+        n_gpu, n_self = int((e_out >= E_MAX).sum()), int((e_self >= E_MAX).sum())
+        print("%s: output pixels >= 1e-3: GPU %d, perturbed oracle %d" % (tag, n_gpu, n_self), flush=True)
+        assert n_gpu <= 2 * n_self, (n_gpu, n_self)
+        _listed(e_out, [("a radiance sample flip within the filter footprint in some frame", _dilate(flips, FOOTPRINT)),
+                        ("history clamp x-only min/max past 4 frames of history", r.read("HIST_LEN") > 4),
+                        ("a history length unlike the oracle's within the 5x5 stencil (a disocclusion test decided "
+                         "the other way)", _dilate(r.read("HIST_LEN") != o.read(19), 2)),
+                        ("the oracle itself moves >= 1e-4 here under a 1e-6 input perturbation", e_self >= 1e-4)],
+                tag + " output", listed_max=1e-3)
+    finally:
+        r.close()

@@ -182,14 +182,17 @@ def test_tap_records_rebuilt_after_a_plane_upload():
 
 # Radiance bars (per pixel, RGB): relative L2 error e = |g - c|_2 / max(|c|_2, 1e-3).
 # North_star's per-pixel L2 tolerance is 1e-3; ocml vs glibc transcendentals can flip a
-# threshold test on a handful of pixels, so: >= 99.9 % of pixels with e < 1e-4, >= 99.95 %
-# with e < 1e-3, image mean within 1e-5, and NO pixel above E_MAX.  Measured (round 3, every
-# GPU test): radiance max e 7.6e-5 except a 4-bounce chain's frame 3 (4.1e-4); denoised outputs
-# max e 1.0e-5, except 2.0e-3 on single pixels of the textured sequence (the denoiser amplifies
-# ulp-level input differences once history passes 4 frames) -- so E_MAX = 5e-3.  Only the 64-frame C5 gate passes a wider e_max (see its test).
+# threshold test on a handful of pixels, so: >= 99.9 % of pixels with e < 1e-4, image mean within
+# 1e-5, and NO pixel at or above E_MAX = north_star's 1e-3.  Measured (round 3, every GPU test):
+# radiance max e 7.6e-5 except a 4-bounce chain's frame 3 (4.1e-4); denoised outputs max e
+# 1.0e-5.  Textured frames have their own bar, E_MAX_TEXTURED: their denoised outputs reached
+# 2.0e-3 on single pixels (RGBA8 texel filtering in float weights on both sides, whose ulp-level
+# albedo differences the denoiser's demodulation amplifies).  The 1080p tests and the
+# 64-frame C5 gate list the pixels above 1e-3 with their cause instead (test_gpu_frames_spp.py).
 E_TIGHT, FRAC_TIGHT = 1e-4, 0.999
-E_L2, FRAC_L2 = 1e-3, 0.9995
-E_MAX = 5e-3
+E_L2, FRAC_L2 = 1e-3, 1.0
+E_MAX = 1e-3
+E_MAX_TEXTURED = 5e-3
 MEAN_TOL_L2 = 1e-5
 
 
@@ -198,7 +201,9 @@ def pixel_l2(g, c):
     return np.linalg.norm(g - c, axis=-1) / np.maximum(np.linalg.norm(c, axis=-1), 1e-3)
 
 
-def check_radiance(g, c, what, frac_tight=FRAC_TIGHT, frac_l2=FRAC_L2, e_max=E_MAX):
+def check_radiance(g, c, what, frac_tight=FRAC_TIGHT, frac_l2=None, e_max=E_MAX):
+    if frac_l2 is None:  # a wider e_max (textured frames) keeps >= 99.95 % of pixels below 1e-3
+        frac_l2 = FRAC_L2 if e_max <= E_L2 else 0.9995
     assert np.isfinite(g).all(), what
     e = pixel_l2(g, c)
     ft, fl = (e < E_TIGHT).mean(), (e < E_L2).mean()
@@ -212,8 +217,8 @@ def check_radiance(g, c, what, frac_tight=FRAC_TIGHT, frac_l2=FRAC_L2, e_max=E_M
     return e
 
 
-def _compare_radiance(g, c, what):
-    check_radiance(g, c, what)
+def _compare_radiance(g, c, what, e_max=E_MAX):
+    check_radiance(g, c, what, e_max=e_max)
 
 
 def test_full_trace_frame0(pair):

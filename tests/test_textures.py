@@ -22,7 +22,7 @@ import pytest
 import oracle
 import vxpt
 from golden.make_golden import C1_CAMERA
-from test_gpu_parity import _compare_radiance, _inject_sky, DN_FLOATS, DN_INTS
+from test_gpu_parity import E_MAX_TEXTURED, _compare_radiance, _inject_sky, DN_FLOATS, DN_INTS
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DATA = os.path.join(REPO, "data")
@@ -204,7 +204,7 @@ def test_textured_frames_match_oracle(textured):
         assert bad.mean() < 1e-3, (name, bad.mean(), np.argwhere(bad)[:5])
     alb = r.read("ALBEDO")[..., :3]
     assert alb.std() > 0.05  # the textures really modulate the albedo
-    _compare_radiance(r.read("ILLUM"), o.read(0), "textured frame0")
+    _compare_radiance(r.read("ILLUM"), o.read(0), "textured frame0", E_MAX_TEXTURED)
     p = vxpt.DenoiseParams(*DN_FLOATS, *DN_INTS)
     r.denoise(0, 1, p)
     o.post_trace()
@@ -215,8 +215,8 @@ def test_textured_frames_match_oracle(textured):
         o.trace(f)
         o.post_trace()
         o.denoise(f, f + 1)
-        _compare_radiance(r.read("ILLUM"), o.read(0), "textured frame%d" % f)
-        _compare_radiance(r.read("OUTPUT"), o.read(21), "textured output %d" % f)
+        _compare_radiance(r.read("ILLUM"), o.read(0), "textured frame%d" % f, E_MAX_TEXTURED)
+        _compare_radiance(r.read("OUTPUT"), o.read(21), "textured output %d" % f, E_MAX_TEXTURED)
     # textures off again: the untextured path
     r.enable_textures(False)
     r.trace(3)
