@@ -38,10 +38,34 @@ C1_DIR = (-0.321564, -0.0129988, -0.946799)
 
 
 def scene_args(a):
+    """(chunks, height scale, frequency denominator, world-y heights, camera position) of the run's
+    scene: c1 = mainOffline's default scene (2x1x2 chunks, VoxelSceneGen.cu:341-388's terrain; SURVEY
+    §8d C1 / C2 / C5), c3 = the 256^3 world (C1 terrain scaled by world/64: heights and frequency
+    scaled, world-y heights, camera position scaled)."""
+    if a.scene == "c1":
+        return (2, 1, 2), 32.0, 64.0, False, C1_POS
     scale = a.world // 64
     pos = tuple(p * scale for p in C1_POS)
     chunks = (a.world // 32, a.world // 32, a.world // 32)
-    return chunks, 32.0 * scale, 64.0 * scale, pos
+    return chunks, 32.0 * scale, 64.0 * scale, True, pos
+
+
+def run_mode(a, spp):
+    """What a committed profile must have been measured on to be attached to this run's line."""
+    return {"scene": a.scene, "world": a.world if a.scene == "c3" else 64, "width": a.width, "height": a.height,
+            "spp": spp, "bounces": "%d/%d" % a.bounce_limits, "primary_only": bool(a.primary_only),
+            "tune": dict(sorted(a.tune.items()))}
+
+
+def matching_profile(pattern, mode):
+    """The newest committed profile JSON under profiles/ whose recorded `mode` equals this run's
+    (tools/pmc_traffic.py / valu_util.py copy it from the profiled bench line), or (None, None)."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("mode") == mode:
+            return d, os.path.relpath(path, REPO)
+    return None, None
 
 
 def native_oracle():
@@ -68,9 +92,9 @@ def cpu_baseline(a, target_s):
     os.environ["ORACLE_LIB"] = lib
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
-    chunks, hs, fd, pos = scene_args(a)
+    chunks, hs, fd, gy, pos = scene_args(a)
     o = oracle.Oracle(a.width, a.height, bounces=a.bounce_limits)
-    o.terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
+    o.terrain(chunks, height_scale=hs, freq_den=fd, global_y=gy)
     o.set_camera(pos, C1_DIR, 90.0)
     o.set_camera(pos, C1_DIR, 90.0, which=1)
     o.set_sky()
@@ -121,8 +145,13 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=4)
-    ap.add_argument("--world", type=int, default=256, help="world edge in voxels (multiple of 64)")
+    ap.add_argument("--world", type=int, default=256, help="c3 scene: world edge in voxels (multiple of 64)")
     ap.add_argument("--primary-only", action="store_true", help="C2: primary rays + sky + G-buffer, no denoiser")
+    ap.add_argument("--scene", choices=("c1", "c3"), default=None,
+                    help="c1: mainOffline's default 64x32x64 scene (SURVEY §8d C2's); c3: the --world^3 world "
+                         "(default: c1 with --primary-only, else c3)")
+    ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE",
+                    help="a vxpt_tuning field for this run (schedule only; results are unchanged)")
     ap.add_argument("--bounces", default="3/1",
                     help="total/diffuse bounce limits: 3/1 = the reference's (RayGen.cu:146-147); 4/4 = the "
                          "'4 bounces' of BASELINE.json's config line, labelled as such")
@@ -132,6 +161,9 @@ def main():
                     help="time K vxpt_render_frame calls instead of one pipelined vxpt_render_frames(K)")
     a = ap.parse_args()
     a.bounce_limits = tuple(int(v) for v in a.bounces.split("/"))
+    if a.scene is None:
+        a.scene = "c1" if a.primary_only else "c3"
+    a.tune = {k: int(v) for k, v in (t.split("=", 1) for t in a.tune)}
     assert len(a.bounce_limits) == 2 and a.bounce_limits[0] >= a.bounce_limits[1] >= 1, a.bounces
 
     rank = int(os.environ.get("RANK", 0))
@@ -148,10 +180,12 @@ def main():
     import vxpt
     import bands
 
-    chunks, hs, fd, pos = scene_args(a)
+    chunks, hs, fd, gy, pos = scene_args(a)
     r = vxpt.Renderer(a.width, a.height, device=local, bounces=a.bounce_limits)
     r.load_settings()
-    r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
+    if a.tune:
+        r.set_tuning(**a.tune)
+    r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=gy)
     r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
     r.set_sky()
     params = vxpt.DenoiseParams.defaults()
@@ -238,22 +272,16 @@ def main():
     else:
         alg_bytes, dur_ms, kern = B_ALG_PER_PX * band_px, avg_dn, "denoiser chain"
     achieved = alg_bytes / (dur_ms * 1e-3) / 1e9
-    # measured HBM bytes of the chain per frame: committed rocprofv3 PMC passes
-    # (tools/gpu_pmc.sh -> profiles/*_pmc_denoise.json); PMC cannot run inside this timed process
-    traffic, traffic_src = None, None
-    pmc = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_denoise.json")))
-    if pmc and not a.primary_only and a.width == 1920 and a.height == 1080:
-        with open(pmc[-1]) as f:
-            traffic = json.load(f)["traffic_bytes_per_frame"] * band_px / (a.width * a.height)
-        traffic_src = os.path.relpath(pmc[-1], REPO)
-    # VALU issue utilisation of the trace kernels from the committed PMC pass (tools/valu_util.py ->
-    # profiles/*_valu_util.json): how much of the chip's VALU issue the traversal / shading keeps busy
-    valu, valu_src = None, None
-    vu = sorted(glob.glob(os.path.join(REPO, "profiles", "*_valu_util.json")))
-    if vu and not a.primary_only and a.width == 1920 and a.height == 1080:
-        with open(vu[-1]) as f:
-            valu = json.load(f)["trace_valu_util"]
-        valu_src = os.path.relpath(vu[-1], REPO)
+    # measured HBM bytes of the chain per frame: committed rocprofv3 PMC passes (tools/gpu_pmc.sh ->
+    # profiles/*_pmc_denoise.json) of this same mode only; PMC cannot run inside this timed process
+    mode = run_mode(a, 1 if a.primary_only else a.spp)
+    traffic, traffic_src, valu, valu_src = None, None, None, None
+    if not a.primary_only and world == 1:
+        d, traffic_src = matching_profile("*_pmc_denoise.json", mode)
+        traffic = d["traffic_bytes_per_frame"] if d else None
+        # VALU issue utilisation of the trace kernels (tools/valu_util.py -> profiles/*_valu_util.json)
+        d, valu_src = matching_profile("*_valu_util.json", mode)
+        valu = d["trace_valu_util"] if d else None
     # the box's practical HBM ceiling ("record the measured copy-kernel bandwidth"): a
     # 1 GiB device-to-device copy, read + write bytes / time, best of 5
     copy_gbs = None
@@ -285,15 +313,21 @@ def main():
             "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "C2: %dx%d primary-only DDA + sky + G-buffer" % (a.width, a.height) if
-                       a.primary_only else "C3: %dx%d, %d spp full path + ReLAX denoiser" % (a.width, a.height, a.spp),
-                       "width": a.width, "height": a.height, "spp": spp, "world": "%d^3 voxels, Perlin seed 124" % a.world,
+            "config": {"workload": ("C2: %dx%d primary-only DDA + sky + G-buffer" % (a.width, a.height) if
+                                    a.primary_only else "C3: %dx%d, %d spp full path + ReLAX denoiser" % (
+                                        a.width, a.height, a.spp)) + (
+                           " on the C1 scene" if a.scene == "c1" else " on the %d^3 world" % a.world),
+                       "width": a.width, "height": a.height, "spp": spp,
+                       "world": ("C1 scene: 64x32x64 voxels (2x1x2 chunks), Perlin seed 124" if a.scene == "c1" else
+                                 "%d^3 voxels, Perlin seed 124" % a.world),
                        "bounces": "%d total / %d diffuse%s" % (
                            a.bounce_limits + ((" (the reference's RayGen.cu:146-147 limits)",) if a.bounce_limits == (3, 1)
                                               else (" (BASELINE.json's '4 bounces' reading; the reference renders 3/1)",)
                                               if a.bounce_limits == (4, 4) else ("",))),
                        "parallelism": ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU",
-                       "frame_loop": "vxpt_render_frames (pipelined)" if pipelined else "vxpt_render_frame per step"},
+                       "frame_loop": "vxpt_render_frames (pipelined)" if pipelined else "vxpt_render_frame per step",
+                       "tuning": a.tune or "defaults"},
+            "mode": mode,
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,

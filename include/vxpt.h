@@ -132,6 +132,33 @@ typedef struct vxpt_timing {  /* HIP-event times of the last frame, ms (replaces
     float frame_ms;
 } vxpt_timing;
 
+/* Schedule and traversal tuning of a context (no reference counterpart: the reference's OptiX
+ * launch has no such knobs).  No field changes a result, only how long a frame takes; the defaults
+ * (vxpt_tuning_defaults) are the measured best.  The library reads no
+ * environment variable: this struct is the only way to change its schedule. */
+typedef struct vxpt_tuning {
+    int32_t dda_boxes;        /* 1: the walk skips empty space with empty-box tables; 0: cube tables   (1) */
+    int32_t box_cap;          /* box growth limit in bricks, sideways octants, 1..255                   (8) */
+    int32_t box_cap_up;       /* the same for the upward octants                                        (8) */
+    int32_t brick_steps;      /* in-brick cell crossings before a queued walk yields, 1..64            (3) */
+    int32_t cam_steps;        /* the same for camera / continuing path rays (k_closest), 1..64         (10) */
+    int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (6) */
+    int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024      (0) */
+    int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (16) */
+    int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (0) */
+    int32_t overlap;          /* 1: pass halves and pipelined frames on two streams; 0: in order        (1) */
+    int32_t state_sets;       /* wavefront state sets, 2..3                                             (2) */
+    int32_t firefly_fused;    /* 1: the detecting wave filters its fireflies; 0: a second launch        (1) */
+    int32_t ta_supertiles;    /* 1: temporal accumulation on XCD supertiles; 0: raster tiles            (1) */
+    int32_t hf_split;         /* history-fix workgroups per tile, 1..16                                 (4) */
+    int32_t stencil_tile;     /* tile edge of the history clamp and the first a-trous, 16 or 32        (16) */
+} vxpt_tuning;
+int vxpt_tuning_defaults(vxpt_tuning *out);
+int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);
+/* between frames; dda_boxes / box caps rebuild the current world's skip tables (VXPT_ERR_ARG for a
+ * field out of range, nothing changed then) */
+int vxpt_set_tuning(vxpt_ctx *ctx, const vxpt_tuning *t);
+
 /* replaces OfflineBackend::init(w,h) + BufferManager::init (OfflineBackend.h:30, BufferManager.cpp:107) */
 int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out);
 /* replaces OfflineBackend::clear (OfflineBackend.h:31) */
@@ -260,8 +287,9 @@ int vxpt_render_frame(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame
 /* n_frames consecutive vxpt_render_frame calls (frames frame0 .. frame0+n_frames-1) with the
  * camera, world and lights left as they are: mainOffline's frame loop for a static camera.  The
  * buffers afterwards equal those calls' bit for bit; each frame's first trace pass is enqueued
- * beside the previous frame's last one, so the sequence takes less time.  Timing: frame_ms is the
- * mean per frame, denoise_ms the last frame's, trace_ms the mean per frame without the denoiser. */
+ * beside the previous frame's last one, so the sequence takes less time.  Timing (HIP events):
+ * frame_ms is the mean per frame, denoise_ms the mean of the frames' denoiser chains (each timed on
+ * its own; they run alone), trace_ms the mean per frame without them. */
 int vxpt_render_frames(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame0, int32_t n_frames,
                        int32_t spp);
 /* the denoiser parameters of global_settings.yaml's `denoising` section (GlobalSettings.h:82-141),

@@ -464,10 +464,8 @@ VX_HD V3 bicubic_smoothstep3(const L &ld, int W, int H, V2 uv) {
     return out;
 }
 
-// The planes temporal_px reads around a pixel: edge-clamped global loads (TaGlobal), or the
-// k_temporal workgroup's LDS window (TaLds: the previous frame's planes over the tile + a 2-pixel
-// apron, the current normals over the tile + 1).  A window entry holds the edge-clamped pixel's
-// value, so a tap inside the window reads exactly what ld4 / ld1 would.
+// The planes temporal_px reads around a pixel: edge-clamped global loads.  (A workgroup window of
+// them staged in LDS was measured slower -- 95 -> 109 us, 137 VGPRs -- and removed)
 struct TaGlobal {
     const DenoiseArgs *a;
     VX_HD V4 n(int x, int y) const { return ld4(a->normalRough, a->W, a->H, x, y); }
@@ -476,19 +474,6 @@ struct TaGlobal {
     VX_HD V4 pi(int x, int y) const { return ld4(a->prevIllum, a->W, a->H, x, y); }
     VX_HD V4 pf(int x, int y) const { return ld4(a->prevFast, a->W, a->H, x, y); }
     VX_HD float ph(int x, int y) const { return ld1(a->prevHistLen, a->W, a->H, x, y); }
-};
-constexpr int kTaWin = 20, kTaNWin = 18;  // window edges: the 16x16 tile + 2 (history taps) / + 1 (normals)
-struct TaLds {
-    const float4 *sN, *sPN, *sPI, *sPF;
-    const float *sPZ, *sPH;
-    int x0, y0;  // the window's first pixel (tile origin - 2)
-    VX_HD int w(int x, int y) const { return (y - y0) * kTaWin + (x - x0); }
-    VX_HD V4 n(int x, int y) const { return f4(sN[(y - y0 - 1) * kTaNWin + (x - x0 - 1)]); }
-    VX_HD float pz(int x, int y) const { return sPZ[w(x, y)]; }
-    VX_HD V4 pn(int x, int y) const { return f4(sPN[w(x, y)]); }
-    VX_HD V4 pi(int x, int y) const { return f4(sPI[w(x, y)]); }
-    VX_HD V4 pf(int x, int y) const { return f4(sPF[w(x, y)]); }
-    VX_HD float ph(int x, int y) const { return sPH[w(x, y)]; }
 };
 
 // The reprojected history of a pixel (TemporalAccumulation.h loadSurfaceMotionBasedPrevData):
@@ -550,21 +535,19 @@ VX_HD TaHist ta_history(const T &t, int W, int H, const Qt &rot, V3 nIn, V2 prev
 
 // Returns whether the history fix must filter the pixel (HistoryFix.h:20-22:
 // non-sky and history <= 4; pixels past the denoising range keep last frame's length).
-// `lds`: the workgroup's window (k_temporal<.., true>); the history taps read it when their
-// 4x4 footprint lies inside it, the global planes otherwise.
-VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol, const TaLds *lds = nullptr) {
+VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol) {
     const int W = a.W, H = a.H;
     const size_t i = (size_t)y * W + x;
     const float z = a.depth[i];
     if (z > a.p.denoisingRange) return z <= kRange && a.histLen[i] <= 4.0f;
     const CamDev &cam = a.cam, &pc = a.prevCam;
     const TaGlobal g{&a};
-    const V3 cN = (lds ? lds->n(x, y) : f4(a.normalRough[i])).xyz();
+    const V3 cN = f4(a.normalRough[i]).xyz();
     V3 avgN = cN;
     for (int ax = -1; ax <= 1; ++ax)
         for (int by = -1; by <= 1; ++by) {
             if (ax == 0 && by == 0) continue;
-            avgN += (lds ? lds->n(x + ax, y + by) : g.n(x + ax, y + by)).xyz();
+            avgN += g.n(x + ax, y + by).xyz();
         }
     avgN /= 9.0f;
     const V2 pixelUv = (V2((float)x, (float)y) + 0.5f) * V2(a.invW, a.invH);
@@ -608,11 +591,7 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
     }
     thr4 -= 1e-6f;
     const float thrv[4] = {thr4.x, thr4.y, thr4.z, thr4.w};
-    // every tap of the history lies in [ox - 1, ox + 2] x [oy - 1, oy + 2]
-    const bool inWin = lds && ox - 1 >= lds->x0 && ox + 2 < lds->x0 + kTaWin && oy - 1 >= lds->y0 &&
-                       oy + 2 < lds->y0 + kTaWin;
-    const TaHist hh = inWin ? ta_history(*lds, W, H, rot, nIn, prevUV, ox, oy, estDepth, thrv)
-                            : ta_history(g, W, H, rot, nIn, prevUV, ox, oy, estDepth, thrv);
+    const TaHist hh = ta_history(g, W, H, rot, nIn, prevUV, ox, oy, estDepth, thrv);
     const V4 prevI = hh.prevI;
     const V3 prevF = hh.prevF;
     const float found = hh.found;
@@ -647,21 +626,14 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
 // 123 VGPRs (4 waves/SIMD); bounding it to 5 waves spills 80-116 B/lane and was slower (89 -> 105 us),
 // and fetching the pixel's inputs before the depth test or the history taps with the depth taps
 // raised it to 130 (3 waves: 100-103 us)
-// LDS = true: the workgroup first stages its window of the previous frame's depth, normal, history,
-// fast history and history length (20x20) and of the current normals (18x18) -- one round of
-// independent loads -- and the pixels' history taps read LDS while they stay inside the window
-// (a static or slowly moving camera); tiles without a pixel in the denoising range stage nothing.
 #ifndef VX_WPE_TA
 #define VX_WPE_TA 1  // occupancy bound of k_temporal (waves per SIMD; 1 = the compiler's choice)
 #endif
-template <bool ST, bool LDS>
+template <bool ST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_TA))) void k_temporal(DenoiseArgs a, Qt rot) {
     __shared__ unsigned sTot[4], sFFn, sFFmask[8];
     __shared__ float4 sFF[256];
-    __shared__ float4 sN[LDS ? kTaNWin * kTaNWin : 1], sPN[LDS ? kTaWin * kTaWin : 1], sPI[LDS ? kTaWin * kTaWin : 1],
-        sPF[LDS ? kTaWin * kTaWin : 1];
-    __shared__ float sPZ[LDS ? kTaWin * kTaWin : 1], sPH[LDS ? kTaWin * kTaWin : 1];
-    int tx, ty;  // supertiles (default) or raster tiles (VXPT_TA_ST=0)
+    int tx, ty;  // supertiles (default) or raster tiles (vxpt_tuning.ta_supertiles = 0)
     if (!map_tile<ST>(a, tx, ty)) return;
     const unsigned tile = ty * ((a.W + 15) / 16) + tx;
     if (threadIdx.x == 0) {
@@ -685,28 +657,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_TA))
     }
     const bool own = nff && ((sFFmask[threadIdx.x >> 5] >> (threadIdx.x & 31)) & 1u);
     const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);
-    bool fix;
-    if (LDS) {
-        const int W = a.W, H = a.H, x0 = tx * 16 - 2, y0 = a.y0 + ty * 16 - 2;
-        const bool act = x < W && y < a.y1 && a.depth[(size_t)y * W + x] <= a.p.denoisingRange;
-        if (__syncthreads_or(act)) {
-            for (int k = threadIdx.x; k < kTaWin * kTaWin; k += 256) {
-                const size_t j = (size_t)cl(y0 + k / kTaWin, H) * W + cl(x0 + k % kTaWin, W);
-                sPZ[k] = a.prevDepth[j];
-                sPN[k] = a.prevNormalRough[j];
-                sPI[k] = a.prevIllum[j];
-                sPF[k] = a.prevFast[j];
-                sPH[k] = a.prevHistLen[j];
-            }
-            for (int k = threadIdx.x; k < kTaNWin * kTaNWin; k += 256)
-                sN[k] = a.normalRough[(size_t)cl(y0 + 1 + k / kTaNWin, H) * W + cl(x0 + 1 + k % kTaNWin, W)];
-            __syncthreads();
-        }
-        const TaLds w{sN, sPN, sPI, sPF, sPZ, sPH, x0, y0};
-        fix = x < W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr, &w);
-    } else {
-        fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr);
-    }
+    const bool fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr);
     const unsigned long long m = __ballot(fix);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0) sTot[wv] = (unsigned)__popcll(m);
@@ -1270,8 +1221,9 @@ inline dim3 grid1d(const DenoiseArgs &a) { return dim3((unsigned)(((size_t)(a.y1
 // written back here rather than by the next k_temporal
 hipError_t launch_firefly(const DenoiseArgs &a, int wy0, int wy1, bool detect, bool apply, hipStream_t st) {
     // the detecting wave filters its own fireflies (84 VGPRs, 5 waves/SIMD, for the ~100 pixels of a
-    // frame) instead of a second launch: chain 0.3745 -> 0.3709 ms; VXPT_FF_FUSED=0 keeps k_firefly_filter
-    static const bool fused = !(getenv("VXPT_FF_FUSED") && atoi(getenv("VXPT_FF_FUSED")) == 0);
+    // frame) instead of a second launch: chain 0.3745 -> 0.3709 ms; tuning firefly_fused = 0 keeps
+    // k_firefly_filter
+    const bool fused = a.tune.ffFused != 0;
     const dim3 g((a.W + 63) / 64, (wy1 - wy0 + 3) / 4);
     if (fused) hipLaunchKernelGGL(k_firefly<true>, g, dim3(256), 0, st, a, wy0, wy1, detect ? 1 : 0);
     else hipLaunchKernelGGL(k_firefly<false>, g, dim3(256), 0, st, a, wy0, wy1, detect ? 1 : 0);
@@ -1292,43 +1244,30 @@ inline dim3 grid_st(const DenoiseArgs &a) {
 hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st) {
     const Qt rot = q_rotation_between(a.prevCam.dir, a.cam.dir);
     // supertiles: the taps' history rows stay in the XCD's L2 (351 -> 266 MB per frame, time even);
-    // VXPT_TA_ST=0: raster tiles
-    static const bool stT = !(getenv("VXPT_TA_ST") && atoi(getenv("VXPT_TA_ST")) == 0);
-    // VXPT_TA_LDS=1: the LDS window (measured slower: 95 -> 109 us at 137 VGPRs / 3 waves, 0.367 ->
-    // 0.382 ms chain; bounded to 4 waves it spills 48 B/lane, 0.378 ms)
-    // (read per launch: a test switches it between frames)
-    const char *ldsEnv = getenv("VXPT_TA_LDS");
-    const bool lds = ldsEnv && atoi(ldsEnv) == 1;
-    if (stT && lds) hipLaunchKernelGGL((k_temporal<true, true>), grid_st(a), dim3(256), 0, st, a, rot);
-    else if (stT) hipLaunchKernelGGL((k_temporal<true, false>), grid_st(a), dim3(256), 0, st, a, rot);
-    else if (lds) hipLaunchKernelGGL((k_temporal<false, true>), grid16(a), dim3(256), 0, st, a, rot);
-    else hipLaunchKernelGGL((k_temporal<false, false>), grid16(a), dim3(256), 0, st, a, rot);
+    // tuning ta_supertiles = 0: raster tiles
+    if (a.tune.taSupertiles) hipLaunchKernelGGL((k_temporal<true>), grid_st(a), dim3(256), 0, st, a, rot);
+    else hipLaunchKernelGGL((k_temporal<false>), grid16(a), dim3(256), 0, st, a, rot);
     return hipGetLastError();
 }
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {
     // steady state on the C3 bench: ~3000 listed pixels in ~960 of 8160 tiles, at most ~21 per tile
-    // (tools/hf_stats.py); VXPT_HF_SPLIT workgroups per tile
-    static const int split = getenv("VXPT_HF_SPLIT") ? std::max(1, atoi(getenv("VXPT_HF_SPLIT"))) : 4;
+    // (tools/hf_stats.py); tuning hf_split workgroups per tile
     dim3 g = grid16(a);
-    g.z = (unsigned)split;
+    g.z = (unsigned)a.tune.hfSplit;
     hipLaunchKernelGGL(k_history_fix, g, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 // tile edge of the LDS-staged 5x5 stencils (history clamping, the first a-trous): 32 stages the
 // 2-pixel apron at 1.27x the tile's pixels instead of 1.56x (both kernels run at the HBM's rate on
 // their fetched bytes)
-inline int stencil_tile() {
-    static const int ts = getenv("VXPT_STENCIL_TILE") ? atoi(getenv("VXPT_STENCIL_TILE")) : 16;
-    return ts;
-}
 inline dim3 grid_ts(const DenoiseArgs &a, int ts) { return dim3((a.W + ts - 1) / ts, (a.y1 - a.y0 + ts - 1) / ts); }
 hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st) {
-    if (stencil_tile() == 32) hipLaunchKernelGGL((k_history_clamp<32, false>), grid_ts(a, 32), dim3(1024), 0, st, a);
+    if (a.tune.stencilTile == 32) hipLaunchKernelGGL((k_history_clamp<32, false>), grid_ts(a, 32), dim3(1024), 0, st, a);
     else hipLaunchKernelGGL((k_history_clamp<16, true>), grid_st(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st) {
-    if (stencil_tile() == 32) hipLaunchKernelGGL((k_atrous_smem<32, false>), grid_ts(a, 32), dim3(1024), 0, st, a);
+    if (a.tune.stencilTile == 32) hipLaunchKernelGGL((k_atrous_smem<32, false>), grid_ts(a, 32), dim3(1024), 0, st, a);
     else hipLaunchKernelGGL((k_atrous_smem<16, true>), grid_st(a), dim3(256), 0, st, a);
     return hipGetLastError();
 }

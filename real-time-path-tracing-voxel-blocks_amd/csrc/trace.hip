@@ -384,56 +384,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_QUEU
     }
 }
 
-// Persistent traversal of queue q: every wave keeps up to 64 walks in flight and refills the
-// lanes whose walk has ended from the queue's head (qCount[kQueues + q], one atomic per refill), once
-// at least `refill` lanes are idle; a wave leaves when the queue is drained and its last walk has
-// ended.  The lanes stay busy with live walks instead of waiting for the wave's longest one, so no
-// iteration cap and no straggler pass are needed.  Each walk is the same sequence of dda_iter
-// steps as in k_queue, so the results are identical.
-template <bool OCC, bool BOX>
-__global__ __launch_bounds__(256) void k_persist(TraceArgs a, int q, int refill) {
-    const WaveBufs &w = a.wb;
-    const unsigned n = w.qCount[q];
-    unsigned *head = w.qCount + kQueues + q;
-    const int lane = threadIdx.x & 63;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
-    Dda st;
-    int id = 0;
-    bool active = false, drained = false;
-    for (;;) {
-        const unsigned long long im = __ballot(!active);
-        const int nIdle = __popcll(im);
-        if (!drained && nIdle >= refill) {
-            unsigned base = 0;
-            if (lane == 0) base = atomicAdd(head, (unsigned)nIdle);
-            base = __shfl(base, 0);
-            if (base + (unsigned)nIdle >= n) drained = true;
-            if (!active) {
-                const unsigned i = base + (unsigned)__popcll(im & below);
-                if (i < n) {
-                    const float4 ro = w.qO[i], rd = w.qD[i];
-                    id = w.qId[i];
-                    h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
-                    const int rc = dda_begin<OCC, BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
-                    if (rc == DdaRun) active = true;
-                    else store_result<OCC>(w, id, rc, h, a.mesh.nInst == 0);
-                }
-            }
-        }
-        if (__ballot(active) == 0ull) {
-            if (drained) break;
-            continue;
-        }
-        if (active) {
-            const int rc = dda_iter<OCC, BOX>(a.world, st, h, nullptr);
-            if (rc != DdaRun) {
-                store_result<OCC>(w, id, rc, h, a.mesh.nInst == 0);
-                active = false;
-            }
-        }
-    }
-}
+// (A persistent traversal that keeps 64 walks per wave in flight and refills finished lanes from the
+// queue head was measured slower than the capped walks + straggler resume below, 7.5-14.4 against
+// 6.1 ms of trace per C3 frame, and removed: DESIGN.md §3.)
 
 // Resumes the level-`level` stragglers of queue q (level 1: from k_queue,
 // level 2: from the level-1 resume).  Each wave serves one shard (wave index
@@ -1486,22 +1439,10 @@ struct Launcher {
     }
     // a ray queue's traversal: iteration-capped pass + straggler continuation (+ the mesh pass).  The
     // stragglers' grid: a fixed number of workgroups per CU (their count is on the device; each wave
-    // reads it and strides over its shard), VXPT_RESUME_WG per CU for the sweep in DESIGN.md
+    // reads it and strides over its shard), vxpt_tuning.resume_wg_per_cu per CU (the sweep in DESIGN.md)
     void trav(bool occ, int q, int cap) {
         const dim3 gr(a.numCU * (a.resumeWgPerCU > 0 ? a.resumeWgPerCU : 16));
         const dim3 gq((cap + 255) / 256);
-        if (a.persistWg > 0) {
-            const dim3 gp(a.numCU * a.persistWg);
-            if (occ && box) hipLaunchKernelGGL((k_persist<true, true>), gp, b, 0, st, a, q, a.persistRefill);
-            else if (occ) hipLaunchKernelGGL((k_persist<true, false>), gp, b, 0, st, a, q, a.persistRefill);
-            else if (box) hipLaunchKernelGGL((k_persist<false, true>), gp, b, 0, st, a, q, a.persistRefill);
-            else hipLaunchKernelGGL((k_persist<false, false>), gp, b, 0, st, a, q, a.persistRefill);
-            if (mesh) {
-                if (occ) hipLaunchKernelGGL(k_mesh_queue<true>, gq, b, 0, st, a, q);
-                else hipLaunchKernelGGL(k_mesh_queue<false>, gq, b, 0, st, a, q);
-            }
-            return;
-        }
         const int shardCap = (int)((gq.x + kShards - 1) / kShards) * 256;
         if (occ && box) {
             hipLaunchKernelGGL((k_queue<true, true>), gq, b, 0, st, a, q, a.iterCap, shardCap);

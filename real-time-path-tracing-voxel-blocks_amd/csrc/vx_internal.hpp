@@ -61,13 +61,13 @@ struct WorldDev {
     const uint8_t *bdist;     // 8 octant tables of nBricks bytes (brick index as cellMask): edge in bricks
                               // of the largest empty brick cube cornered at the brick and extending into
                               // the octant (0 = occupied, capped at 255); octant = (dx>0) | (dy>0)<<1 | (dz>0)<<2
-    const uint32_t *bbox;     // optional (VXPT_DDA_BOXES): 8 octant tables of nBricks words, an empty brick
+    const uint32_t *bbox;     // optional (vxpt_tuning.dda_boxes): 8 octant tables of nBricks words, an empty brick
                               // BOX's extents in bricks (x | y << 8 | z << 16; 0 = occupied) grown from the
                               // cube; null: the cube tables alone
     int nBricks;
     int brickSteps;           // cell crossings per brick walk before the walk yields an outer iteration
     int brickStepsCam;        // the same for the camera rays (k_closest, which runs every walk to its end)
-                              // (0 = 10: a whole brick); VXPT_BRICK_STEPS
+                              // (0 = 10: a whole brick); vxpt_tuning.brick_steps
     uint64_t top;
     int topValid;
     int cx, cy, cz;       // chunks
@@ -147,7 +147,7 @@ struct WaveBufs {
     // result id; one storage reused by the pass's queues, counters 4 per segment
     float4 *qO, *qD;
     int *qId;
-    unsigned *qCount;  // kQueueWords: kQueues queue counters, kQueues queue heads (k_persist), then per straggler level (1-3) kQueues queues x kShards shard counters 16 words apart
+    unsigned *qCount;  // kQueueWords: kQueues queue counters, kQueues unused words, then per straggler level (1-3) kQueues queues x kShards shard counters 16 words apart
     // straggler queues (ping-pong by level): walk state of rays stopped at an iteration cap (DdaSaved)
     int4 *sCell[2];
     float4 *sT[2];
@@ -232,8 +232,6 @@ struct TraceArgs {
     int resumeWgPerCU;  // k_resume workgroups per CU (0: 16)
     int sortMode;       // ray queues grouped by direction class per workgroup (0 off, 1 octant, 2 octant x axis)
     int writeMotion;    // store the (zero) motion vectors: the plane may hold a host upload
-    int persistWg;      // > 0: queue traversal by a persistent grid of this many workgroups per CU (k_persist)
-    int persistRefill;  // k_persist: a wave refills its finished lanes once at least this many are idle
 };
 
 // kernel launchers (defined in the .hip translation units)
@@ -293,6 +291,10 @@ struct DenoiseArgs {
     // thresholds, the frustum scale tanHalfFov.x / (res.x / 2), 1/(maxAcc+1),
     // 1/(maxFast+1)
     float invW, invH, thrB, thrA, frustumK, invAcc1, invFast1;
+    // launch shapes (vxpt_tuning; host side only: read by the launch functions)
+    struct {
+        int ffFused, taSupertiles, hfSplit, stencilTile;
+    } tune;
 };
 
 // post-processing (postprocess.hip; ToneMappingParams + PostProcessingPipelineParams, GlobalSettings.h:10-186)

@@ -142,6 +142,35 @@ constexpr int kBlockTypes = 30;  // BlockTypeNum (generated/voxelengine/BlockTyp
 constexpr int kPostHist = 257;   // 256 luminance bins + the lens flare's sun flag
 constexpr int kMaxSets = 3;      // wavefront state sets (vxpt_ctx::nSets)
 
+// the measured best schedule; vxpt_set_tuning changes it per context
+vxpt_tuning tuning_defaults() {
+    vxpt_tuning t{};
+    t.dda_boxes = 1;          // empty-box tables: 7.56 -> 7.06 ms of trace per C3 frame (round 3)
+    t.box_cap = kBoxCap;      // growth limits swept flat (8:8 .. 32:64 within 0.03 ms)
+    t.box_cap_up = kBoxCap;
+    t.brick_steps = 3;        // in-brick walks yield after 3 crossings: 6.44 -> 6.26 ms
+    t.cam_steps = 10;         // camera rays walk whole bricks
+    t.iter_cap = 6;           // caps 4 / 6 / 8 / 12: 7.02 / 6.84 / 7.07 / 7.63 ms
+    t.iter_cap2 = 0;          // a second level (6 + 16): 7.59 ms
+    t.resume_wg_per_cu = 16;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms
+    t.sort_mode = 0;          // direction-class sort: 1.5 % faster traversal, producers pay it back
+    t.overlap = 1;            // pass halves on two streams: 6.84 -> 6.06 ms
+    t.state_sets = 2;         // 3 sets: 6.40 -> 6.39 ms
+    t.firefly_fused = 1;      // -4 us per chain
+    t.ta_supertiles = 1;      // temporal pass traffic 351 -> 266 MB per frame
+    t.hf_split = 4;           // 16.3 -> 11.8 us history fix (with readlane sums)
+    t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
+    return t;
+}
+bool tuning_valid(const vxpt_tuning &t) {
+    auto in = [](int v, int lo, int hi) { return v >= lo && v <= hi; };
+    return in(t.dda_boxes, 0, 1) && in(t.box_cap, 1, 255) && in(t.box_cap_up, 1, 255) && in(t.brick_steps, 1, 64) &&
+           in(t.cam_steps, 1, 64) && in(t.iter_cap, 1, 1024) && in(t.iter_cap2, 0, 1024) &&
+           in(t.resume_wg_per_cu, 1, 64) && in(t.sort_mode, 0, 2) && in(t.overlap, 0, 1) &&
+           in(t.state_sets, 2, kMaxSets) && in(t.firefly_fused, 0, 1) && in(t.ta_supertiles, 0, 1) &&
+           in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32);
+}
+
 struct vxpt_ctx {
     int W = 0, H = 0, dev = 0, rowBegin = 0, rowEnd = 0;
     int totalBounce = 3, diffuseBounce = 1;
@@ -150,6 +179,7 @@ struct vxpt_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     vxpt_timing timing{};
+    vxpt_tuning tune = tuning_defaults();
 
     // scene
     int cx = 0, cy = 0, cz = 0;
@@ -157,8 +187,8 @@ struct vxpt_ctx {
     DBuf<uint8_t> bricks;
     DBuf<uint64_t> macro, cellMask;
     DBuf<uint8_t> bdist;
-    // optional empty-box skip tables (VXPT_DDA_BOXES=1 at vxpt_create; box_tables.hpp)
-    bool useBoxes = false;
+    // optional empty-box skip tables (vxpt_tuning.dda_boxes; box_tables.hpp)
+    bool useBoxes = true;
     BrickPrefix brickPrefix;
     int boxCap = kBoxCap, boxCapUp = kBoxCap;  // box growth limits (box_tables.hpp)
     std::vector<uint32_t> hBox;
@@ -260,7 +290,7 @@ struct vxpt_ctx {
     // end hands the last slot to the denoiser by index instead of copying planes.
     // Two more slots let first halves (camera rays .. NEE visibility, which read no previous pass)
     // run ahead while up to two second halves still read their previous passes' slots, and one more
-    // keeps the denoiser's previous history slot while a split denoiser chain may still read it.
+    // keeps the denoiser's previous history slot (histOld) out of the pipelined next frame's reach.
     GSlot gb[6];
     int last = 0;              // slot of the most recent trace output
     int tracePrev = 0;         // slot the most recent trace read as its previous pass
@@ -295,12 +325,7 @@ struct vxpt_ctx {
     int lastSet = 0;           // the set of the most recent pass
     hipStream_t frontStream = nullptr;
     hipEvent_t frontDone[kMaxSets] = {}, backDone[kMaxSets] = {}, frontGate = nullptr;
-    // split denoiser chains (vxpt_render_frames): the firefly stage on the context stream, the rest
-    // (temporal .. a-trous) on dnStream beside the next frame's first pass
-    hipStream_t dnStream = nullptr;
-    hipEvent_t dnStart = nullptr, dnDone = nullptr;
-    bool dnOutstanding = false;  // a split chain not yet waited for by the context stream
-    int dnBacks = 0;             // second halves enqueued since it
+    std::vector<hipEvent_t> chainEv;  // vxpt_render_frames: around each frame's denoiser chain
     int numCU = 256;
     std::vector<void *> allocs;
 
@@ -469,12 +494,10 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.bdist = c->bdist.p;
     w.bbox = c->useBoxes ? c->bbox.p : nullptr;
     w.nBricks = c->nBricks;
-    // a brick walk yields its lanes back to the outer loop after 4 crossings (fewer lanes idle behind
-    // long in-brick walks; C3 trace 6.44 -> 6.27 ms per frame)
-    static const int brickSteps = getenv("VXPT_BRICK_STEPS") ? atoi(getenv("VXPT_BRICK_STEPS")) : 3;
-    w.brickSteps = brickSteps;
-    static const int camSteps = getenv("VXPT_CAM_STEPS") ? atoi(getenv("VXPT_CAM_STEPS")) : 10;
-    w.brickStepsCam = camSteps;
+    // a brick walk yields its lanes back to the outer loop after brick_steps (3) crossings (fewer lanes
+    // idle behind long in-brick walks; C3 trace 6.44 -> 6.26 ms per frame)
+    w.brickSteps = c->tune.brick_steps;
+    w.brickStepsCam = c->tune.cam_steps;
     w.top = c->top;
     w.topValid = c->topValid;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
@@ -525,6 +548,10 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.frustumK = c->cam.tanHalfFov.x / (c->cam.res.x / 2);
     a.invAcc1 = 1.0f / (a.p.maxAcc + 1.0f);
     a.invFast1 = 1.0f / (a.p.maxFast + 1.0f);
+    a.tune.ffFused = c->tune.firefly_fused;
+    a.tune.taSupertiles = c->tune.ta_supertiles;
+    a.tune.hfSplit = c->tune.hf_split;
+    a.tune.stencilTile = c->tune.stencil_tile;
 }
 
 // GlobalSettings.h:10-186 defaults (the reference yaml overrides most of them: vxpt_load_settings)
@@ -858,8 +885,8 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     const size_t n = (size_t)c->W * c->H;
     a.resCur = c->res + (size_t)(((it % 2) + 2) % 2) * n;
     a.resPrev = c->res + (size_t)((((it + 1) % 2) + 2) % 2) * n;
-    // the first pass of an accumulation writes the other buffer: a denoiser chain still reading the
-    // previous accumulation (split chains) keeps its input; trace_back makes it current
+    // the first pass of an accumulation writes the other buffer (the previous accumulation, the
+    // pipelined denoiser's input, stays intact); trace_back makes it current
     a.accum = accumulate ? (accumFirst ? (c->accum == c->accumBuf[0] ? c->accumBuf[1] : c->accumBuf[0]) : c->accum)
                          : nullptr;
     a.accumScale = accumScale;
@@ -881,20 +908,17 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.primaryOnly = (flags & VXPT_TRACE_PRIMARY_ONLY) ? 1 : 0;
     a.tilesX = (c->W + 7) / 8;
     a.nSlots = a.tilesX * ((a.y1 - a.y0 + 7) / 8) * 64;
-    // VXPT_OVERLAP=0 (diagnostics): every first half after the previous pass, kernels one at a time
-    static const bool overlapOk = !(getenv("VXPT_OVERLAP") && atoi(getenv("VXPT_OVERLAP")) == 0);
-    if (!overlapOk) overlap = false;
+    // tuning overlap = 0 (diagnostics): every first half after the previous pass, kernels one at a time
+    if (!c->tune.overlap) overlap = false;
     bool fresh;
     if (int r = ensure_wave(c, set, (size_t)a.nSlots, fresh)) return r;
     if (fresh) overlap = false;  // the first half must follow the new buffers' zero fill
     a.wb = c->wb[set];
     a.numCU = c->numCU;
-    a.iterCap = getenv("VXPT_ITER_CAP") ? atoi(getenv("VXPT_ITER_CAP")) : 6;
-    a.iterCap2 = getenv("VXPT_ITER_CAP2") ? atoi(getenv("VXPT_ITER_CAP2")) : 0;
-    a.resumeWgPerCU = getenv("VXPT_RESUME_WG") ? atoi(getenv("VXPT_RESUME_WG")) : 16;
-    a.sortMode = getenv("VXPT_SORT") ? atoi(getenv("VXPT_SORT")) : 0;
-    a.persistWg = getenv("VXPT_PERSIST") ? atoi(getenv("VXPT_PERSIST")) : 0;
-    a.persistRefill = getenv("VXPT_REFILL") ? std::max(1, std::min(64, atoi(getenv("VXPT_REFILL")))) : 32;
+    a.iterCap = c->tune.iter_cap;
+    a.iterCap2 = c->tune.iter_cap2;
+    a.resumeWgPerCU = c->tune.resume_wg_per_cu;
+    a.sortMode = c->tune.sort_mode;
     a.prevSceneEmpty = c->prevSceneEmpty;
     // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
     a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;
@@ -929,14 +953,6 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
 // The second half of the planned pass, on the context stream, and the ring bookkeeping.
 int trace_back(vxpt_ctx *c, const PassPlan &pl) {
     const int set = pl.set;
-    // the second half after a split denoiser chain's first overlapping one waits for it: everything
-    // behind it on this stream -- the next accumulation into the chain's input, the next firefly
-    // stage, and (through their backDone events) the first halves that may reuse its G-buffer
-    // slots -- then follows the chain
-    if (c->dnOutstanding && ++c->dnBacks == 2) {
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->dnDone, 0));
-        c->dnOutstanding = false;
-    }
     if (!pl.a.primaryOnly) {
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[set], 0));
         HIPCHK(c, launch_trace_back(pl.a, c->stream, c->haloPending ? c->haloDone : nullptr));
@@ -980,28 +996,18 @@ hipError_t firefly_band(const DenoiseArgs &a, bool detect, bool apply, hipStream
     return launch_firefly(a, std::max(0, a.y0 - kWposHalo), std::min(a.H, a.y1 + kWposHalo), detect, apply, st);
 }
 
-// split (vxpt_render_frames): the firefly stage -- which writes the filtered reservoirs the next
-// pass's temporal reuse reads -- runs on the context stream, the rest of the chain on dnStream, where
-// it runs beside the next frame's first pass (which writes the other accumulation buffer and a
-// G-buffer slot that is neither this chain's input nor its history)
-int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it, bool split = false) {
+// Denoiser::run (Denoiser.cu:24-408) on the context stream.  (Running all of it but the firefly
+// stage on a third stream beside the next frame's first pass was measured and removed)
+int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) {
     if (!p) p = &c->yamlDenoise;
     const int used = it > 0 ? it - 1 : 0;
     DenoiseArgs a{};
     fill_denoise(c, p, a, used & 1);
-    // the previous split chain reads the firefly lists and world positions this one rewrites
-    if (c->dnOutstanding) HIPCHK(c, hipStreamWaitEvent(c->stream, c->dnDone, 0));
-    c->dnOutstanding = false;
     HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
-    // the temporal pass applies the firefly lists when it runs (split: the firefly launch does)
-    const bool ffFold = p->enable_temporal_accumulation && frameNum > 0 && !split;
+    // the temporal pass applies the firefly lists when it runs
+    const bool ffFold = p->enable_temporal_accumulation && frameNum > 0;
     HIPCHK(c, firefly_band(a, p->enable_firefly_filter, !ffFold, c->stream));
     hipStream_t st = c->stream;
-    if (split) {
-        HIPCHK(c, hipEventRecord(c->dnStart, c->stream));
-        HIPCHK(c, hipStreamWaitEvent(c->dnStream, c->dnStart, 0));
-        st = c->dnStream;
-    }
     if (frameNum == 0) HIPCHK(c, launch_frame0_init(a, st));
     int fin = 0;  // 0 illum, 1 ping, 2 pong, 3 prevIllum
     if (p->enable_temporal_accumulation && frameNum > 0) {
@@ -1035,11 +1041,6 @@ int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it, 
     }
     HIPCHK(c, history_copies(c));
     HIPCHK(c, hipEventRecord(c->ev[3], st));
-    if (split) {
-        HIPCHK(c, hipEventRecord(c->dnDone, st));
-        c->dnOutstanding = true;
-        c->dnBacks = 0;
-    }
     return 0;
 }
 
@@ -1469,36 +1470,19 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (cfg->total_bounce_limit > 0) c->totalBounce = cfg->total_bounce_limit;
     if (cfg->diffuse_bounce_limit > 0) c->diffuseBounce = cfg->diffuse_bounce_limit;
     c->dataDir = cfg->data_dir ? cfg->data_dir : "data";
-    // the DDA's empty-box skip tables (box_tables.hpp; measured 7.56 -> 7.06 ms of trace per
-    // C3 frame); VXPT_DDA_BOXES=0 walks with the empty-cube tables alone
-    c->useBoxes = !(getenv("VXPT_DDA_BOXES") && atoi(getenv("VXPT_DDA_BOXES")) == 0);
-    if (getenv("VXPT_BOX_CAP")) c->boxCap = std::max(1, std::min(255, atoi(getenv("VXPT_BOX_CAP"))));
-    if (getenv("VXPT_BOX_CAP_UP")) c->boxCapUp = std::max(1, std::min(255, atoi(getenv("VXPT_BOX_CAP_UP"))));
     c->yamlPost = default_post();
     c->yamlDenoise = default_denoise();
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(c, hipStreamCreateWithFlags(&c->frontStream, hipStreamNonBlocking));
-    // VXPT_SETS=3: a third wavefront state set, so a first half may run beside the two previous
-    // second halves (C3: 6.40 -> 6.39 ms per frame, within noise: the overlapped halves already
-    // fill the chip; two sets are the default)
-    if (getenv("VXPT_SETS")) c->nSets = std::max(2, std::min(kMaxSets, atoi(getenv("VXPT_SETS"))));
+    // tuning state_sets = 3: a third wavefront state set, so a first half may run beside the two
+    // previous second halves (C3: 6.40 -> 6.39 ms per frame, within noise: the overlapped halves
+    // already fill the chip; two sets are the default)
     for (int k = 0; k < kMaxSets; ++k)
         for (hipEvent_t *e : {&c->frontDone[k], &c->backDone[k]})
             HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(c, hipEventCreateWithFlags(&c->frontGate, hipEventDisableTiming | hipEventDisableSystemFence));
-    {
-        // the split denoiser chains' stream at the lowest priority: beside the next frame's trace the
-        // dispatcher places their workgroups behind the trace's (C3 frame 6.02 -> 5.95 ms at equal
-        // priority, 5.92 at the lowest; VXPT_DN_PRIO=0 equal)
-        int least = 0, greatest = 0;
-        HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
-        const bool low = !(getenv("VXPT_DN_PRIO") && atoi(getenv("VXPT_DN_PRIO")) == 0);
-        HIPCHK(c, hipStreamCreateWithPriority(&c->dnStream, hipStreamNonBlocking, low ? least : 0));
-    }
-    HIPCHK(c, hipEventCreateWithFlags(&c->dnStart, hipEventDisableTiming | hipEventDisableSystemFence));
-    HIPCHK(c, hipEventCreateWithFlags(&c->dnDone, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(c, hipDeviceGetAttribute(&c->numCU, hipDeviceAttributeMultiprocessorCount, c->dev));
     // timing markers only (every read of them follows a stream synchronisation): no system-scope
     // fence, so a marker neither writes back / invalidates the L2 nor delays the next kernel
@@ -1521,7 +1505,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     c->illumSet[0] = c->illum;
     c->accumBuf[0] = c->accum;
     if (dalloc(c, c->accumBuf[1], n)) return VXPT_ERR_HIP;
-    for (int k = 1; k < c->nSets; ++k)
+    for (int k = 1; k < kMaxSets; ++k)  // (a third set's plane too: vxpt_set_tuning may enable it)
         if (dalloc(c, c->illumSet[k], n)) return VXPT_ERR_HIP;
     // tables
     const std::string t = c->dataDir + "/tables/";
@@ -1549,7 +1533,6 @@ void vxpt_destroy(vxpt_ctx *c) {
     if (!c) return;
     hipSetDevice(c->dev);
     if (c->frontStream) hipStreamSynchronize(c->frontStream);
-    if (c->dnStream) hipStreamSynchronize(c->dnStream);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void *p : c->allocs) hipFree(p);
     for (int k = 0; k < kMaxSets; ++k)
@@ -1557,9 +1540,7 @@ void vxpt_destroy(vxpt_ctx *c) {
             if (e) hipEventDestroy(e);
     if (c->frontGate) hipEventDestroy(c->frontGate);
     if (c->frontStream) hipStreamDestroy(c->frontStream);
-    for (hipEvent_t e : {c->dnStart, c->dnDone})
-        if (e) hipEventDestroy(e);
-    if (c->dnStream) hipStreamDestroy(c->dnStream);
+    for (hipEvent_t e : c->chainEv) hipEventDestroy(e);
     for (auto &e : c->ev)
         if (e) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -2624,16 +2605,13 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         return VXPT_OK;
     }
     const float scale = 1.0f / (float)spp;
-    // Split denoiser chains (VXPT_DN_SPLIT=1; default: each chain after the next frame's first half,
-    // alone): an accumulated frame's chain reads its own accumulation buffer and G-buffer slots, which
-    // the next frame's passes leave alone, so all of it but the firefly stage can overlap the next
-    // frame's trace.  Measured: C3 frame 6.02 -> 5.92 ms, but the overlapped chains take ~3x as long
-    // and k_restir beside them +0.5 ms, and the chain's kernel timings stop being its
-    // own -- not the default.
-    const bool splitOk = getenv("VXPT_DN_SPLIT") && atoi(getenv("VXPT_DN_SPLIT")) == 1;  // read per call
-    // (the first halves not ordered behind the chain through the wait in trace_back are the nSets
-    // after it, all enqueued before the next chain moves the history: nSets <= spp)
-    const bool split = splitOk && spp > 1 && c->nSets <= spp;
+    // an event pair around every denoiser chain: the chains run alone (below), so the frames' trace
+    // time is the whole minus their sum
+    while (c->chainEv.size() < (size_t)2 * nFrames) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+        c->chainEv.push_back(e);
+    }
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     PassPlan pend;
     bool havePend = false;
@@ -2658,30 +2636,32 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             // motion plane it stores is all zeros (static world) like the one the denoiser reads.
             if (int r = trace_front(c, it0 + spp, 0, spp > 1, true, scale, true, pend)) return r;
             havePend = true;
-            if (!split) {
-                // the denoiser starts after it, so it runs alone and its timing stays its own
-                if (!pend.a.primaryOnly) HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
-            }
+            // the denoiser starts after it, so it runs alone and its timing stays its own.  (Running
+            // all of the chain but its firefly stage on a third stream beside the next frame's first
+            // pass was measured: 6.02 -> 5.92 ms per frame, but the overlapped chain took ~3x as long
+            // and k_restir beside it +0.5 ms; removed)
+            if (!pend.a.primaryOnly) HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
         }
         c->denoiseInputIsAccum = spp > 1;
-        // split chains: every one but the last runs beside the next frame's first pass
-        if (int r = do_denoise(c, p, frame0 + f, it0 + spp, split && f + 1 < nFrames)) return r;
-        if (havePend && !split) {  // later first halves wait for the denoiser (it reads the old history slot)
+        HIPCHK(c, hipEventRecord(c->chainEv[2 * f], c->stream));
+        if (int r = do_denoise(c, p, frame0 + f, it0 + spp)) return r;
+        HIPCHK(c, hipEventRecord(c->chainEv[2 * f + 1], c->stream));
+        if (havePend) {  // later first halves wait for the denoiser (it reads the old history slot)
             HIPCHK(c, hipEventRecord(c->frontGate, c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->frontStream, c->frontGate, 0));
         }
     }
-    if (c->dnOutstanding) HIPCHK(c, hipStreamWaitEvent(c->stream, c->dnDone, 0));
-    c->dnOutstanding = false;
     HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    float d = 0, f = 0;
-    hipEventElapsedTime(&d, c->ev[2], c->ev[3]);  // the last chain: alone, after every pass
+    float dsum = 0, f = 0;
+    for (int k = 0; k < nFrames; ++k) {
+        float d = 0;
+        hipEventElapsedTime(&d, c->chainEv[2 * k], c->chainEv[2 * k + 1]);
+        dsum += d;
+    }
     hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
-    // per frame, denoiser runs excluded (split: all but the last run beside the trace, which then
-    // carries whatever they cost it)
-    c->timing.trace_ms = (f - d * (split ? 1 : nFrames)) / (float)nFrames;
-    c->timing.denoise_ms = d;
+    c->timing.trace_ms = (f - dsum) / (float)nFrames;  // per frame, the chains excluded
+    c->timing.denoise_ms = dsum / (float)nFrames;        // the mean chain
     c->timing.frame_ms = f / (float)nFrames;
     return VXPT_OK;
 }
@@ -3089,6 +3069,43 @@ int vxpt_get_sky_alias(vxpt_ctx *c, float *q, float *p, int32_t *alias, float *s
         if (alias) alias[i] = c->hSkyAlias[i].alias;
     }
     if (sunDir) { sunDir[0] = c->sunDir.x; sunDir[1] = c->sunDir.y; sunDir[2] = c->sunDir.z; }
+    return VXPT_OK;
+}
+
+int vxpt_tuning_defaults(vxpt_tuning *out) {
+    if (!out) return VXPT_ERR_ARG;
+    *out = tuning_defaults();
+    return VXPT_OK;
+}
+
+int vxpt_get_tuning(vxpt_ctx *c, vxpt_tuning *out) {
+    if (!c || !out) return VXPT_ERR_ARG;
+    *out = c->tune;
+    return VXPT_OK;
+}
+
+int vxpt_set_tuning(vxpt_ctx *c, const vxpt_tuning *t) {
+    if (!c || !t) return VXPT_ERR_ARG;
+    if (!tuning_valid(*t)) return fail(c, VXPT_ERR_ARG, "tuning field out of range");
+    HIPCHK(c, hipSetDevice(c->dev));
+    // whatever is in flight used the old schedule's buffers
+    HIPCHK(c, hipStreamSynchronize(c->frontStream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const bool tables = t->dda_boxes != c->tune.dda_boxes || t->box_cap != c->tune.box_cap ||
+                        t->box_cap_up != c->tune.box_cap_up;
+    c->tune = *t;
+    c->nSets = t->state_sets;
+    c->useBoxes = t->dda_boxes != 0;
+    c->boxCap = t->box_cap;
+    c->boxCapUp = t->box_cap_up;
+    if (tables && c->useBoxes && c->nBricks > 0) {  // the current world's box tables, rebuilt whole
+        const int BX = c->cx * 8, BY = c->cy * 8, BZ = c->cz * 8;
+        brick_prefix(c);
+        c->hBox.assign((size_t)8 * c->nBricks, 0u);
+        for (int oct = 0; oct < 8; ++oct) box_fill(c, oct, 0, BX - 1, 0, BY - 1, 0, BZ - 1);
+        if (int r = upload_vec(c, c->bbox, c->hBox.data(), c->hBox.size())) return r;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     return VXPT_OK;
 }
 

@@ -90,6 +90,19 @@ class ImageDiffResult(ctypes.Structure):
                 ("is_identical", ctypes.c_int32), ("is_very_close", ctypes.c_int32), ("is_close", ctypes.c_int32)]
 
 
+TUNING_FIELDS = ("dda_boxes", "box_cap", "box_cap_up", "brick_steps", "cam_steps", "iter_cap", "iter_cap2",
+                 "resume_wg_per_cu", "sort_mode", "overlap", "state_sets", "firefly_fused", "ta_supertiles",
+                 "hf_split", "stencil_tile")
+
+
+class Tuning(ctypes.Structure):
+    """vxpt_tuning: the context's schedule (no field changes a result)."""
+    _fields_ = [(n, ctypes.c_int32) for n in TUNING_FIELDS]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n in TUNING_FIELDS}
+
+
 class Timing(ctypes.Structure):
     _fields_ = [("trace_ms", ctypes.c_float), ("denoise_ms", ctypes.c_float), ("sky_ms", ctypes.c_float),
                 ("frame_ms", ctypes.c_float)]
@@ -146,6 +159,9 @@ def load_library(path=LIB_PATH):
         "vxpt_upload": (I, [P, I, P, ctypes.c_size_t]),
         "vxpt_get_sky_alias": (I, [P, P, P, P, P]),
         "vxpt_timings": (I, [P, ctypes.POINTER(Timing)]),
+        "vxpt_tuning_defaults": (I, [ctypes.POINTER(Tuning)]),
+        "vxpt_get_tuning": (I, [P, ctypes.POINTER(Tuning)]),
+        "vxpt_set_tuning": (I, [P, ctypes.POINTER(Tuning)]),
         "vxpt_sync": (I, [P]),
         "vxpt_stream": (P, [P]),
         "vxpt_probe_rays": (I, [P, I, P, P, P, I]),
@@ -496,6 +512,21 @@ class Renderer:
         first trace pass overlapping the previous frame's last (same buffers as render_frame calls)."""
         p = params or DenoiseParams.defaults()
         self._chk(self.lib.vxpt_render_frames(self.ctx, ctypes.byref(p), frame0, n_frames, spp), "vxpt_render_frames")
+
+    def tuning(self):
+        t = Tuning()
+        self._chk(self.lib.vxpt_get_tuning(self.ctx, ctypes.byref(t)), "vxpt_get_tuning")
+        return t.as_dict()
+
+    def set_tuning(self, **fields):
+        """vxpt_set_tuning with the named fields changed (the rest as they are)."""
+        t = Tuning()
+        self._chk(self.lib.vxpt_get_tuning(self.ctx, ctypes.byref(t)), "vxpt_get_tuning")
+        for k, v in fields.items():
+            if k not in TUNING_FIELDS:
+                raise VxptError("unknown tuning field " + k)
+            setattr(t, k, int(v))
+        self._chk(self.lib.vxpt_set_tuning(self.ctx, ctypes.byref(t)), "vxpt_set_tuning")
 
     def timings(self):
         t = Timing()

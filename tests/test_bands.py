@@ -535,14 +535,15 @@ def test_gpu_c4_eight_bands_4k_c3_world():
 
     class A:
         world = 256
+        scene = "c3"
 
-    chunks, hs, fd, pos = scene_args(A)
+    chunks, hs, fd, gy, pos = scene_args(A)
     w, h, spp, n = 3840, 2160, 4, 8
 
     def make():
         r = vxpt.Renderer(w, h)
         r.load_settings()
-        r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)
+        r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=gy)
         r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
         r.set_sky()
         return r

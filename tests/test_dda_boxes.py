@@ -1,5 +1,5 @@
 """The voxel walk's empty-box skip tables (csrc/box_tables.hpp; the default walk since round 3,
-VXPT_DDA_BOXES=0 walks with the empty-cube tables alone).
+vxpt_tuning.dda_boxes = 0 walks with the empty-cube tables alone).
 
 CPU: the library's own walk (vx_device.hpp is host + device code) runs on the host in a driver
 compiled with hipcc (no kernel launch), once with the default empty-cube tables and once with the
@@ -72,12 +72,18 @@ def test_box_tables_walk_equals_cube_walk(driver, world, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("boxes", ["1", "0"])
+@pytest.mark.parametrize("boxes", [1, 0, "rebuilt"])
 @pytest.mark.parametrize("outside", [False, True])
-def test_dda_probe_with_box_tables_bit_exact(outside, boxes, monkeypatch):
+def test_dda_probe_with_box_tables_bit_exact(outside, boxes):
+    """boxes 1 / 0: the tables the world was uploaded with; "rebuilt": the box tables turned off and
+    on again through vxpt_set_tuning after the upload, with other growth caps (rebuilt whole)."""
     from test_gpu_parity import _random_rays, _setup
-    monkeypatch.setenv("VXPT_DDA_BOXES", boxes)
     r, o = _setup()
+    if boxes == "rebuilt":
+        r.set_tuning(dda_boxes=0)
+        r.set_tuning(dda_boxes=1, box_cap=5, box_cap_up=12)
+    else:
+        r.set_tuning(dda_boxes=boxes)
     try:
         rays = _random_rays(20000, 31 + outside, outside=outside)
         g, tg = r.probe_rays(rays, 0)

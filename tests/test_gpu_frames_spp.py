@@ -275,14 +275,18 @@ def run_c5(w, h, frames):
                 tag + " radiance")
         e_out = pixel_l2(r.read("OUTPUT"), o.read(21))
         e_self = pixel_l2(o2.read(21), o.read(21))
+        hist = r.read("HIST_LEN")
         n_gpu, n_self = int((e_out >= E_MAX).sum()), int((e_self >= E_MAX).sum())
         print("%s: output pixels >= 1e-3: GPU %d, perturbed oracle %d" % (tag, n_gpu, n_self), flush=True)
         assert n_gpu <= 2 * n_self, (n_gpu, n_self)
         _listed(e_out, [("a radiance sample flip within the filter footprint in some frame", _dilate(flips, FOOTPRINT)),
-                        ("history clamp x-only min/max past 4 frames of history", r.read("HIST_LEN") > 4),
+                        ("history clamp x-only min/max past 4 frames of history", hist > 4),
                         ("a history length unlike the oracle's within the 5x5 stencil (a disocclusion test decided "
                          "the other way)", _dilate(r.read("HIST_LEN") != o.read(19), 2)),
-                        ("the oracle itself moves >= 1e-4 here under a 1e-6 input perturbation", e_self >= 1e-4)],
+                        ("the oracle itself moves >= 1e-4 here under a 1e-6 input perturbation", e_self >= 1e-4),
+                        ("the history fix (history <= 4) gathering, up to 34 px away (HistoryFix.h:20-60), from "
+                         "pixels past 4 frames that moved >= 1e-4",
+                         (hist <= 4) & _dilate((e_out >= 1e-4) & (hist > 4), FOOTPRINT))],
                 tag + " output", listed_max=1e-3)
     finally:
         r.close()

@@ -333,27 +333,47 @@ def test_denoiser_history_fix_after_camera_move():
     r.close()
 
 
-def test_temporal_lds_window_equals_global_taps(monkeypatch):
-    """The opt-in LDS window of the temporal accumulation (VXPT_TA_LDS=1, read per launch) gives the
-    global-tap kernel's results bit for bit: 8 frames with the camera held, turned and moved (taps
-    outside the window fall back to the global planes)."""
-    rs = [_setup(100, 70)[0] for _ in range(2)]
+TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=3), dict(sort_mode=1), dict(sort_mode=2),
+                   dict(iter_cap=2, iter_cap2=3, resume_wg_per_cu=3), dict(brick_steps=1, cam_steps=2),
+                   dict(dda_boxes=0), dict(box_cap=2, box_cap_up=40), dict(firefly_fused=0), dict(ta_supertiles=0),
+                   dict(hf_split=1), dict(stencil_tile=32)]
+
+
+@pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
+def test_tuning_changes_no_result(variant):
+    """vxpt_tuning changes the schedule only: 4 frames of 4 spp (camera held, then moved) with a
+    non-default setting equal the defaults' frames bit for bit -- trace buffers, reservoirs,
+    denoiser state and output."""
+    a, _ = _setup(100, 70)
+    b, _ = _setup(100, 70)
+    b.set_tuning(**TUNING_VARIANTS[variant])
     p = _dn_params()
     pos, d, fov = C1_CAMERA[0], C1_CAMERA[1], C1_CAMERA[2]
-    cams = [(pos, d)] * 4 + [((pos[0] + 0.3, pos[1], pos[2] - 0.2), d)] + \
-        [((pos[0] + 0.3, pos[1], pos[2] - 0.2), (d[0] + 0.05, d[1] + 0.03, d[2]))] * 3
-    prev = (pos, d)
-    for f, cur in enumerate(cams):
-        outs = []
-        for k, r in enumerate(rs):
-            monkeypatch.setenv("VXPT_TA_LDS", str(k))
-            r.set_camera(*cur, fov=fov, prev=(prev[0], prev[1], fov))
-            r.render_frame(f, 1, p)
-            outs.append([r.read(n).view(np.uint32) for n in ("OUTPUT", "PREV_ILLUM", "PREV_FAST", "HIST_LEN")])
-        for a, b in zip(*outs):
-            np.testing.assert_array_equal(a, b, err_msg="frame %d" % f)
-        prev = cur
-    for r in rs:
+    moved = (pos[0] + 0.3, pos[1], pos[2] - 0.2)
+    try:
+        a.render_frames(0, 2, 4, p)
+        b.render_frames(0, 2, 4, p)
+        for f, cur in ((2, (pos, d)), (3, (moved, d))):
+            for r in (a, b):
+                r.set_camera(cur[0], cur[1], fov=fov, prev=(pos, d, fov))
+                r.render_frame(f, 4, p)
+        for name in ("ILLUM", "DEPTH", "NORMAL_ROUGH", "TAP_RECORD", "RES_EVEN", "RES_ODD", "PREV_ILLUM",
+                     "PREV_FAST", "HIST_LEN", "OUTPUT"):
+            np.testing.assert_array_equal(a.read(name).view(np.uint8), b.read(name).view(np.uint8), err_msg=name)
+    finally:
+        a.close()
+        b.close()
+
+
+def test_tuning_rejects_out_of_range_fields():
+    r, _ = _setup(32, 16)
+    try:
+        before = r.tuning()
+        for bad in (dict(state_sets=4), dict(stencil_tile=24), dict(iter_cap=0), dict(sort_mode=3)):
+            with pytest.raises(vxpt.VxptError):
+                r.set_tuning(**bad)
+            assert r.tuning() == before
+    finally:
         r.close()
 
 
@@ -379,14 +399,11 @@ def test_overlapped_passes_equal_sequential_passes(w, h):
         b.close()
 
 
-@pytest.mark.parametrize("spp,split", [(4, "0"), (1, "0"), (4, "1")])
-def test_pipelined_frames_equal_frame_calls(spp, split, monkeypatch):
+@pytest.mark.parametrize("spp", [4, 1])
+def test_pipelined_frames_equal_frame_calls(spp):
     """vxpt_render_frames enqueues each frame's first pass-half beside the previous frame's last
-    second half, and (spp > 1, VXPT_DN_SPLIT=1) every denoiser chain but the last after its firefly
-    stage on a stream of its own beside the next frame's first pass (the other accumulation buffer, a G-buffer slot
-    outside the chain's two); after 4 frames every trace and denoiser buffer equals 4
-    vxpt_render_frame calls bit for bit, and a frame rendered after it (fresh call) still does."""
-    monkeypatch.setenv("VXPT_DN_SPLIT", split)
+    second half; after 4 frames every trace and denoiser buffer equals 4 vxpt_render_frame calls
+    bit for bit, and a frame rendered after it (fresh call) still does."""
     a, _ = _setup(96, 72)
     b, _ = _setup(96, 72)
     p = _dn_params()

@@ -3,11 +3,9 @@
 # GPU fault / timeout.  Usage (on the box): tools/gpu_batch.sh STEP...   steps:
 #   tests    pytest -m gpu on the files in $TESTS (default: all)
 #   bench    bench.py --steps 20 --warmup 6 --no-cpu-baseline  -> gpurun_out/b_default.json
-#   caps     trace iteration-cap sweep (VXPT_ITER_CAP / VXPT_ITER_CAP2)   -> gpurun_out/b_cap*.json
 #   full     bench.py (defaults, CPU baseline on)                          -> gpurun_out/b_full.json
 #   c2       bench.py --primary-only                                       -> gpurun_out/b_c2.json
 #   b44      bench.py --bounces 4/4 --no-cpu-baseline                      -> gpurun_out/b_44.json
-#   boxes    bench.py with the DDA's empty-box tables (VXPT_DDA_BOXES=1)   -> gpurun_out/b_boxes.json
 #   counters rocprofv3 -L                                                  -> gpurun_out/counters.txt
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -25,19 +23,9 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest -v --timeout 240 --timeout-method thread -m gpu ${TESTS:-tests} \
                > gpurun_out/tests.log 2>&1 || exit $? ;;
     bench) run bench 200 python -u bench.py --steps 20 --warmup 6 --no-cpu-baseline > gpurun_out/b_default.json 2> gpurun_out/b_default.err || exit $? ;;
-    caps) for c in 4:0 6:0 8:0 6:16 12:0; do
-              VXPT_ITER_CAP=${c%%:*} VXPT_ITER_CAP2=${c##*:} run cap$c 200 python -u bench.py --steps 20 --warmup 6 \
-                  --no-cpu-baseline > gpurun_out/b_cap${c/:/_}.json 2>/dev/null || exit $?
-          done
-          for g in 4 8 32; do
-              VXPT_RESUME_WG=$g run wg$g 200 python -u bench.py --steps 20 --warmup 6 --no-cpu-baseline \
-                  > gpurun_out/b_wg$g.json 2>/dev/null || exit $?
-          done ;;
     full) run full 400 python -u bench.py > gpurun_out/b_full.json 2> gpurun_out/b_full.err || exit $? ;;
     c2) run c2 300 python -u bench.py --primary-only --cpu-seconds 8 > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || exit $? ;;
     b44) run b44 200 python -u bench.py --bounces 4/4 --steps 10 --warmup 4 --no-cpu-baseline > gpurun_out/b_44.json 2> gpurun_out/b_44.err || exit $? ;;
-    boxes) VXPT_DDA_BOXES=1 run boxes 200 python -u bench.py --steps 20 --warmup 6 --no-cpu-baseline \
-               > gpurun_out/b_boxes.json 2> gpurun_out/b_boxes.err || exit $? ;;
     counters) (cd /tmp && TMPDIR=/tmp timeout -k 5 60 rocprofv3 -L > "$GRAFT_REPO_ROOT/gpurun_out/counters.txt" 2>&1); true ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel-trace profile of the bench workload, plus the traversal statistics build.
 # Usage (on the box): tools/gpu_kt.sh TAG [bench args]   -> gpurun_out/TAG_kt.txt, gpurun_out/TAG_stats.txt
-# Environment variables (VXPT_*) pass through to both runs.
+# Bench args (e.g. --tune overlap=0) pass through to the kernel trace.
 TAG=${1:-kt}; shift
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1

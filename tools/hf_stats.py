@@ -15,9 +15,10 @@ from bench import C1_DIR, scene_args  # noqa: E402
 
 class A:
     world = 256
+    scene = "c3"
 
 
-chunks, hs, fd, pos = scene_args(A)
+chunks, hs, fd, _, pos = scene_args(A)
 w, h = 1920, 1080
 r = vxpt.Renderer(w, h)
 r.load_settings()

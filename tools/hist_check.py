@@ -13,9 +13,10 @@ from bench import C1_DIR, scene_args  # noqa: E402
 
 class A:
     world = 256
+    scene = "c3"
 
 
-chunks, hs, fd, pos = scene_args(A)
+chunks, hs, fd, _, pos = scene_args(A)
 r = vxpt.Renderer(1920, 1080, device=0)
 r.load_settings()
 r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)

@@ -1,6 +1,8 @@
 """HBM traffic of the denoiser chain per frame from rocprofv3 PMC passes.
 
-Usage: python tools/pmc_traffic.py FETCH_DB WRITE_DB STATS_DB FRAMES OUT_JSON [CALIB_JSON]
+Usage: python tools/pmc_traffic.py FETCH_DB WRITE_DB STATS_DB FRAMES OUT_JSON [CALIB_JSON [BENCH_LOG]]
+  BENCH_LOG: the profiled bench run's output; its line's `mode` is recorded, and bench.py attaches
+  the result only to lines of the same mode.
   FETCH_DB / WRITE_DB: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE runs (separate passes) of
   `bench.py --warmup W --steps S --no-cpu-baseline`; STATS_DB: a --kernel-trace run of the same
   command.  Only the last FRAMES frames' dispatches are used (steady state: converged history).
@@ -57,12 +59,20 @@ def durations(path):
     return d
 
 
+def bench_mode(log):
+    """The `mode` of the last bench.py JSON line in a log."""
+    lines = [ln for ln in open(log) if ln.startswith("{")]
+    return json.loads(lines[-1]).get("mode") if lines else None
+
+
 def main():
     fetch_db, write_db, stats_db, frames, out = sys.argv[1:6]
-    calib = None
+    calib, mode = None, None
     if len(sys.argv) > 6:
         with open(sys.argv[6]) as fc:
             calib = json.load(fc)
+    if len(sys.argv) > 7:
+        mode = bench_mode(sys.argv[7])
     frames = int(frames)
     fetch, write, dur = counters(fetch_db, "FETCH_SIZE"), counters(write_db, "WRITE_SIZE"), durations(stats_db)
     kern, total_f, total_w, total_ns = {}, 0.0, 0.0, 0.0
@@ -98,6 +108,7 @@ def main():
         "traffic_bytes_per_frame": total_f + total_w,
         "algorithmic_bytes_per_frame": B_ALG * 1920 * 1080,
         "chain_kernel_ns_per_frame": total_ns,
+        "mode": mode,
     }
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)

@@ -23,12 +23,13 @@ KINDS = {0: "path rays", 1: "BRDF candidate", 2: "camera", 3: "visibility x4 (Re
 
 class A:
     world = int(os.environ.get("WORLD", 256))
+    scene = "c3"
 
 
 def main():
     lib = vxpt.load_library()
     lib.vxpt_debug_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    chunks, hs, fd, pos = scene_args(A)
+    chunks, hs, fd, _, pos = scene_args(A)
     r = vxpt.Renderer(1920, 1080, device=0)
     r.load_settings()
     r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=True)

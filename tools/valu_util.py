@@ -81,6 +81,9 @@ def main():
            "kernel_time_weighted_issue_util": round(agg, 4),
            "kernels": out,
            "note": "trace_valu_util = the trace kernels' SQ_INSTS_VALU x 2 cycles / (the time any trace kernel runs x 2.4 GHz x 1024 SIMDs); per kernel issue util = SQ_INSTS_VALU x 2 / (its duration x 2.4 GHz x 1024) -- with the pass halves on two streams a kernel's duration includes the other stream's work; lane util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU), time-weighted"}
+    if len(sys.argv) > 4:  # the profiled bench run's log: its mode (bench.py attaches matching modes only)
+        from pmc_traffic import bench_mode
+        res["mode"] = bench_mode(sys.argv[4])
     print(json.dumps(res, indent=1))
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as f:
