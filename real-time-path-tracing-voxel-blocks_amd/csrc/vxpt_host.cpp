@@ -351,7 +351,8 @@ struct vxpt_ctx {
     // pass up to its temporal-reuse kernel (haloDone: recorded after the exchange)
     hipStream_t commStream = nullptr;
     hipEvent_t haloReady = nullptr, haloDone = nullptr;
-    int haloTraceRows = 72, haloHistRows = 2;  // halo depths the last banded frame exchanged
+    // halo depths the last banded frame exchanged: tap records + reservoirs, histories, G-buffer planes
+    int haloTraceRows = 72, haloHistRows = 2, haloPlaneRows = 40;
     bool haloPending = false;
 };
 
@@ -992,6 +993,7 @@ hipError_t history_copies(vxpt_ctx *c) {
 // launch (`detect`: the filter over the band; `apply`: write the filtered pixels
 // back in this launch rather than in the next k_temporal)
 constexpr int kWposHalo = 40;
+constexpr int kDenoiseRows = kWposHalo;  // the deepest read of the current G-buffer planes by the denoiser
 hipError_t firefly_band(const DenoiseArgs &a, bool detect, bool apply, hipStream_t st) {
     return launch_firefly(a, std::max(0, a.y0 - kWposHalo), std::min(a.H, a.y1 + kWposHalo), detect, apply, st);
 }
@@ -1079,8 +1081,13 @@ int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int a
 // context stream behind the kernels that produced the rows -- no packing, no
 // host synchronisation.
 constexpr int kTraceHalo = 72;  // ReSTIR temporal taps: 64-pixel disk + reprojection (Restir.h:348-381)
-const int kGbufBufs[] = {VXPT_BUF_DEPTH, VXPT_BUF_NORMAL_ROUGH, VXPT_BUF_GEO_NORMAL_THIN,
-                         VXPT_BUF_ALBEDO, VXPT_BUF_MATERIAL, VXPT_BUF_MAT_PARAM, VXPT_BUF_TAP_RECORD};
+// The next pass's temporal taps read only the previous pass's tap records (GBuf::rec) and reservoirs,
+// so a pass hands its neighbours those two, 52 B/px, at the trace depth; the G-buffer planes are
+// read by the denoiser alone (after the frame's last pass, within kDenoiseRows of the band: the
+// world positions of k_firefly at kWposHalo, the history fix's taps at 34) and by the next frame's
+// temporal accumulation as its history (histRows), so they travel once per frame.
+const int kGbufPlanes[] = {VXPT_BUF_DEPTH, VXPT_BUF_NORMAL_ROUGH, VXPT_BUF_GEO_NORMAL_THIN,
+                           VXPT_BUF_ALBEDO, VXPT_BUF_MATERIAL, VXPT_BUF_MAT_PARAM};
 // a host-side write to a G-buffer plane leaves the slots' tap records stale (rebuilt before the next
 // trace reads them)
 bool is_gbuf_plane(int which) { return (which >= VXPT_BUF_DEPTH && which <= VXPT_BUF_MAT_PARAM) ||
@@ -1272,16 +1279,21 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
             st = c->commStream;
         }
         if (ncclGroupStart() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupStart");
+        ncclResult_t rc = ncclSuccess;
         for (const auto &br : bufRows)
             for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, br.second)) {
                 const int b = br.first;
                 size_t rb;
                 char *send = buffer_rows(c, b, h.sy, rb);
                 char *recv = buffer_rows(c, b, h.ry, rb);
-                ncclSend(send, (size_t)h.sn * rb, ncclUint8, h.peer, c->comm, st);
-                ncclRecv(recv, (size_t)h.rn * rb, ncclUint8, h.peer, c->comm, st);
+                if (rc == ncclSuccess) rc = ncclSend(send, (size_t)h.sn * rb, ncclUint8, h.peer, c->comm, st);
+                if (rc == ncclSuccess) rc = ncclRecv(recv, (size_t)h.rn * rb, ncclUint8, h.peer, c->comm, st);
             }
-        if (ncclGroupEnd() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupEnd (halo exchange)");
+        const ncclResult_t re = ncclGroupEnd();  // closes the group whatever failed inside it
+        if (rc != ncclSuccess)
+            return fail(c, VXPT_ERR_HIP, std::string("ncclSend/ncclRecv (halo exchange): ") + ncclGetErrorString(rc));
+        if (re != ncclSuccess)
+            return fail(c, VXPT_ERR_HIP, std::string("ncclGroupEnd (halo exchange): ") + ncclGetErrorString(re));
         if (overlap) {
             HIPCHK(c, hipEventRecord(c->haloDone, c->commStream));
             c->haloPending = true;
@@ -1349,30 +1361,38 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         }
         if (!ok) return fail(c0, VXPT_ERR_STATE, err.c_str());
     }
-    if (frame > 0 && (traceRows > cs[0]->haloTraceRows || histRows > cs[0]->haloHistRows)) {
+    // the G-buffer planes' depth: the denoiser's reads, or the next temporal accumulation's history
+    const int planeRows = std::max(kDenoiseRows, histRows);
+    if (frame > 0 && (traceRows > cs[0]->haloTraceRows || histRows > cs[0]->haloHistRows ||
+                      planeRows > cs[0]->haloPlaneRows)) {
         std::vector<std::pair<int, int>> br;
-        for (int b : kGbufBufs) br.emplace_back(b, traceRows);
+        br.emplace_back(VXPT_BUF_TAP_RECORD, traceRows);
         br.emplace_back(((it0 - 1) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows);
+        for (int b : kGbufPlanes) br.emplace_back(b, planeRows);
         for (int b : kHistoryBufs) br.emplace_back(b, histRows);
         BANDCHK(exchange_set(cs, br, false));
     }
     for (vxpt_ctx *c : cs) {
         c->haloTraceRows = traceRows;
         c->haloHistRows = histRows;
+        c->haloPlaneRows = planeRows;
     }
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
         FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0));
-        std::vector<std::pair<int, int>> br;
-        for (int b : kGbufBufs) br.emplace_back(b, traceRows);
-        br.emplace_back(((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows);
+        const int res = ((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN;
         if (s + 1 < spp) {
-            // all but the last pass: overlapped with the next pass up to its temporal reuse
-            BANDCHK(exchange_set(cs, br, true));
+            // all but the last pass: the next pass's temporal taps' inputs, overlapped with that pass
+            // up to its temporal reuse
+            BANDCHK(exchange_set(cs, {{VXPT_BUF_TAP_RECORD, traceRows}, {res, traceRows}}, true));
         } else {
-            // the last pass's rows travel with the denoiser input's (radiance, or the spp average)
+            // the last pass: its planes for the denoiser, and the denoiser input (radiance, or the spp
+            // average) for the firefly filter's 3x3 neighbours.  Its reservoirs go out at the trace
+            // depth after the firefly filter has rewritten them (below); without the filter, here.
             for (vxpt_ctx *c : cs) c->denoiseInputIsAccum = spp > 1;
-            br.emplace_back(VXPT_BUF_ILLUM, 2);
+            std::vector<std::pair<int, int>> br{{VXPT_BUF_TAP_RECORD, traceRows}, {VXPT_BUF_ILLUM, 2},
+                                                {res, p->enable_firefly_filter ? 2 : traceRows}};
+            for (int b : kGbufPlanes) br.emplace_back(b, planeRows);
             BANDCHK(exchange_set(cs, br, false));
         }
     }
@@ -1385,6 +1405,7 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     if (!p->enable_firefly_filter) FOR_BANDS(run_pass(c, p, 11, 0, 0));
     if (p->enable_firefly_filter) {  // + world positions
         FOR_BANDS(run_pass(c, p, 0, used & 1, 0));
+        // the filtered reservoirs: the next frame's first temporal taps read them at the trace depth
         BANDCHK(exchange_set(cs, {{(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows}, {VXPT_BUF_ILLUM, 2}}));
     }
     const std::vector<int> hist(std::begin(kHistoryBufs), std::end(kHistoryBufs));
@@ -2920,19 +2941,24 @@ int band_gather(std::vector<vxpt_ctx *> &cs, int which, int root) {
     if (cs.size() == 1 && c0->comm) {
         size_t rb;
         if (ncclGroupStart() != ncclSuccess) return fail(c0, VXPT_ERR_HIP, "ncclGroupStart");
+        ncclResult_t rc = ncclSuccess;
         if (c0->rank == root) {
-            for (int r = 0; r < world; ++r) {
+            for (int r = 0; r < world && rc == ncclSuccess; ++r) {
                 int y0, y1;
                 band_rows(c0->H, world, r, y0, y1);
                 if (r == root || y1 <= y0) continue;
                 char *dst = buffer_rows(c0, which, y0, rb);
-                ncclRecv(dst, (size_t)(y1 - y0) * rb, ncclUint8, r, c0->comm, c0->stream);
+                rc = ncclRecv(dst, (size_t)(y1 - y0) * rb, ncclUint8, r, c0->comm, c0->stream);
             }
         } else if (c0->rowEnd > c0->rowBegin) {
             char *src = buffer_rows(c0, which, c0->rowBegin, rb);
-            ncclSend(src, (size_t)(c0->rowEnd - c0->rowBegin) * rb, ncclUint8, root, c0->comm, c0->stream);
+            rc = ncclSend(src, (size_t)(c0->rowEnd - c0->rowBegin) * rb, ncclUint8, root, c0->comm, c0->stream);
         }
-        if (ncclGroupEnd() != ncclSuccess) return fail(c0, VXPT_ERR_HIP, "ncclGroupEnd (gather)");
+        const ncclResult_t re = ncclGroupEnd();
+        if (rc != ncclSuccess)
+            return fail(c0, VXPT_ERR_HIP, std::string("ncclSend/ncclRecv (gather): ") + ncclGetErrorString(rc));
+        if (re != ncclSuccess)
+            return fail(c0, VXPT_ERR_HIP, std::string("ncclGroupEnd (gather): ") + ncclGetErrorString(re));
         HIPCHK(c0, hipStreamSynchronize(c0->stream));
         return VXPT_OK;
     }

@@ -241,3 +241,43 @@ def test_denoised_frames_across_lantern_edits(mesh_scene):
     each edit (histories reset where a lantern vanished or reappeared, the light-id remap applied)
     denoise as the oracle does."""
     _lantern_edits(mesh_scene, output=True)
+
+
+def test_base_only_edits_follow_the_grid(mesh_scene):
+    """A lantern base placed and removed on its own (defined deviation): the library's
+    instance set is always collectInstanceTransforms of the edited grid (VoxelEngine.cu:323-384), so a
+    bare base cell carries its light's instance as at load, and its edit is that light's incremental
+    light update (the reference's incremental addInstancedBlock of a bare base registers no light,
+    VoxelEngine.cu:1278-1284, and deleting one leaves a stale light instance).  The oracle restates
+    the same rule (collect_instances + light_edit of the light instance): the instance rows, the
+    light remap of each update and the traced frames agree."""
+    r, o, rows, placed, ex = mesh_scene
+    models, defs = ex["models"], ex["defs"]
+    first, width = min(defs), CH[0] * 32
+    leaves = [p for p in placed if p[3] == LEAVES]
+    x, y, z = leaves[0][0], leaves[0][1] + 1, leaves[0][2]
+    assert r.read("VOXELS")[_idx(x, y, z)] == 0
+    p = _dn_params()
+    f = 0
+    for _ in range(2):
+        _frame(r, o, f, p, "pre frame%d" % f, False)
+        f += 1
+    light_iid = oracle.instance_id(first, width, LIGHT - 1, x, y, z)
+    for k, block in enumerate((BASE, 0)):
+        r.set_block(x, y, z, block)
+        o.set_voxels(r.read("VOXELS"), CH)
+        o.set_prev_scene_empty(True)
+        o.light_edit(light_iid, removed=block == 0)
+        got_rows = o.set_meshes(models, defs, light_update="update")
+        inst = r.instances()
+        np.testing.assert_array_equal(inst[:, 0] + 1, got_rows[:, 0])
+        np.testing.assert_array_equal(inst[:, 2:5], got_rows[:, 1:4])
+        # the bare base carries a light instance (and its own base instance) while it stands
+        at = [tuple(int(v) for v in row) for row in inst if (row[2], row[3], row[4]) == (x, y, z)]
+        assert (len(at) == 2) == (block == BASE), at
+        remap, pending = r.light_remap()
+        assert pending and len(remap) == o._lights_prev, (k, len(remap))
+        np.testing.assert_array_equal(remap, o._remap_keep[:len(remap)], err_msg="base edit %d remap" % k)
+        for _ in range(2):
+            _frame(r, o, f, p, "base edit%d frame%d" % (k, f), False)
+            f += 1

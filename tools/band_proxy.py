@@ -1,0 +1,121 @@
+"""One-GPU proxy of the multi-GPU band partition: every rank's band of the C3 frame
+(1920x1080 by default, or 3840x2160 for C4) rendered alone by a single context in band mode
+(vxpt_config row_begin / row_end: the trace and denoiser over the band's rows only, no exchange),
+for N = 1 / 2 / 4 / 8 bands, plus the halo bytes the library's band schedule moves per rank and frame
+(band_frame in vxpt_host.cpp) and their time on one xGMI link.
+
+python tools/band_proxy.py [WIDTH HEIGHT] [--out profiles/r04_band_proxy.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "real-time-path-tracing-voxel-blocks_amd"))
+import vxpt  # noqa: E402
+from bench import C1_DIR  # noqa: E402
+
+XGMI_GBS = 153.0   # one xGMI link, one direction (MI355X_MICROARCH.md: 7 links x ~153 GB/s per GPU)
+TRACE_ROWS, HIST_ROWS, PLANE_ROWS = 72, 2, 40   # static camera (vxpt_host.cpp band_frame)
+PLANE_B = 16 + 16 + 16 + 16 + 4 + 4             # depth, normalRough, geoNormalThin, albedo, material, matParam
+
+
+def atrous_rows(step):
+    return step + (step // 4 if step > 4 else 0)
+
+
+def halo_bytes(width, spp, rows_avail):
+    """Bytes one rank sends to ONE neighbour per frame (it receives as many), static camera, the
+    library's schedule: (overlapped, in stream order).  rows_avail caps every depth at the bands'
+    height (vxpt_halo_plan moves min(rows, both band heights))."""
+    r = lambda n: min(n, rows_avail)  # noqa: E731
+    per_pass = (32 + 20) * r(TRACE_ROWS)                         # tap records + reservoirs
+    overlapped = (spp - 1) * per_pass * width
+    last = 32 * r(TRACE_ROWS) + 16 * r(2) + 20 * r(2) + PLANE_B * r(PLANE_ROWS)
+    ff = 20 * r(TRACE_ROWS) + 16 * r(2)                           # filtered reservoirs + radiance
+    ta = 16 * r(34) + 16 * r(2)                                   # ping for the history fix, pong
+    hf = 16 * r(2)
+    hc = (16 + 16 + 4) * r(HIST_ROWS)
+    at = 16 * r(atrous_rows(2)) + 16 * r(atrous_rows(4)) + 16 * r(atrous_rows(8))
+    ordered = (last + ff + ta + hf + hc + at) * width
+    return overlapped, ordered
+
+
+def band_rows(h, n, k):
+    per = (h + 8 * n - 1) // (8 * n) * 8
+    y0 = min(h, k * per)
+    return y0, min(h, y0 + per)
+
+
+def time_band(w, h, rows, frames, warmup, spp):
+    pos = tuple(p * 4 for p in (35.6184, 11.8733, 42.0387))
+    r = vxpt.Renderer(w, h, rows=rows)
+    try:
+        r.load_settings()
+        r.generate_terrain((8, 8, 8), height_scale=128.0, freq_den=256.0, global_y=True)
+        r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
+        r.set_sky()
+        p = vxpt.DenoiseParams.defaults()
+        r.render_frames(0, warmup, spp, p)
+        r.sync()
+        t0 = time.perf_counter()
+        r.render_frames(warmup, frames, spp, p)
+        r.sync()
+        wall = (time.perf_counter() - t0) / frames * 1e3
+        t = r.timings()
+        return dict(frame_ms=round(wall, 4), trace_ms=round(t["trace_ms"], 4), denoise_ms=round(t["denoise_ms"], 4))
+    finally:
+        r.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("size", nargs="*", type=int, default=[1920, 1080])
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--spp", type=int, default=4)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    w, h = a.size
+    res = {"what": "one-GPU proxy of the band partition: each rank's band of the C3 frame rendered alone "
+                   "(single context in band mode, no exchange), and the halo bytes per rank and frame of the "
+                   "library's schedule on one xGMI link (%.0f GB/s per direction)" % XGMI_GBS,
+           "width": w, "height": h, "spp": a.spp, "ranks": {}}
+    one = None
+    for n in (1, 2, 4, 8):
+        bands = [band_rows(h, n, k) for k in range(n)]
+        per = []
+        for k, rows in enumerate(bands):
+            t = time_band(w, h, rows, a.frames, a.warmup, a.spp)
+            t.update(rank=k, rows=list(rows))
+            per.append(t)
+            print(n, k, rows, t, flush=True)
+        slow = max(per, key=lambda t: t["frame_ms"])
+        min_rows = min(y1 - y0 for y0, y1 in bands)
+        ov, od = halo_bytes(w, a.spp, min_rows) if n > 1 else (0, 0)
+        # an interior rank talks to two neighbours over two links at once: the time of one link's bytes
+        link_ms_ordered = od / (XGMI_GBS * 1e9) * 1e3
+        link_ms_overlapped = ov / (XGMI_GBS * 1e9) * 1e3
+        proj = slow["frame_ms"] + link_ms_ordered
+        if n == 1:
+            one = slow["frame_ms"]
+        res["ranks"][str(n)] = {
+            "bands": per, "slowest_band_ms": slow["frame_ms"], "mean_band_ms": round(sum(t["frame_ms"] for t in per) / n, 4),
+            "halo_mb_per_neighbour_per_frame": {"overlapped": round(ov / 1e6, 3), "in_stream_order": round(od / 1e6, 3)},
+            "link_ms": {"overlapped": round(link_ms_overlapped, 4), "in_stream_order": round(link_ms_ordered, 4)},
+            "projected_frame_ms": round(proj, 4),
+            "projected_speedup": round(one / proj, 3) if one else None,
+            "balanced_speedup_bound": round(one / (sum(t["frame_ms"] for t in per) / n + link_ms_ordered), 3)
+            if one else None,
+        }
+    print(json.dumps(res, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
