@@ -355,8 +355,9 @@ int vxpt_band_halo_rows(const vxpt_camera *cur, const vxpt_camera *prev, int wid
 /* the same for a camera that may also translate: near_depth > 0 bounds every primary hit's distance
  * from the camera (a pixel's reprojected row is monotone in its hit distance, so the rows at
  * near_depth and at infinity bound it).  vxpt_render_frame / _linked use the world's own bound,
- * vxpt_nearest_surface: the distance from pos to the nearest non-air cell grown by one cell (mesh
- * overhang), searched up to 64 cells (host mirror of the world; no GPU work). */
+ * vxpt_nearest_surface: the distance from pos to the nearest non-air cell grown by one cell, or by
+ * the loaded meshes' largest overhang past their cell when that is more (vxpt_load_models), searched
+ * up to 64 cells (host mirror of the world; no GPU work). */
 int vxpt_band_halo_rows_near(const vxpt_camera *cur, const vxpt_camera *prev, int width, int height, int nranks,
                              float near_depth, int *trace_rows, int *history_rows);
 int vxpt_nearest_surface(vxpt_ctx *ctx, const float pos[3], float *dist);
@@ -382,7 +383,13 @@ int vxpt_band_link(vxpt_ctx **ctxs, int n);
 int vxpt_render_frame_linked(vxpt_ctx **ctxs, int n, const vxpt_denoise_params *p, int32_t frame_num,
                              int32_t spp);
 
-/* copy any logical buffer to/from host memory (parity hooks, PNG output) */
+/* copy any logical buffer to/from host memory (parity hooks, PNG output).  Uploads of G-buffer planes
+ * mark the slots' ReSTIR tap records stale; the next trace rebuilds them from NORMAL_ROUGH, ALBEDO,
+ * MAT_PARAM.x and DEPTH (k_pack_rec).  The taps take their geometric normal from NORMAL_ROUGH: the trace
+ * writes the same normal to both planes, so an uploaded GEO_NORMAL_THIN that differs from
+ * NORMAL_ROUGH.xyz is not seen by the temporal taps (GetPrevSurface, Restir.h:359-378, reads it).  In a
+ * banded context such an upload must also cover the trace halo rows (the library's own exchanges move
+ * the records, not the planes, between passes). */
 int vxpt_readback(vxpt_ctx *ctx, int which, void *host, size_t bytes);
 int vxpt_upload(vxpt_ctx *ctx, int which, const void *host, size_t bytes);
 /* sky alias table (Vose, AliasTable.cu:66-153): q,p floats and alias ints, 1024*512 each */

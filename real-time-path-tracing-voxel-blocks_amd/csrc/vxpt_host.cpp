@@ -201,6 +201,10 @@ struct vxpt_ctx {
     std::vector<uint8_t> hIds, hBricks, hOd;
     std::vector<uint64_t> hMacro, hCell;
     std::vector<int> topCount;  // cube cells per 64^3 block
+    std::vector<uint8_t> hNonAir;  // non-air cells (any id, instanced ones too) per 4^3 brick (brick_lin order)
+    // how far an instanced block's mesh reaches outside its cell (the largest vertex overhang of the
+    // loaded meshes, at least 1): nearest_surface grows every non-air cell by it
+    float meshGrow = 1.0f;
     // world edits / uploads so far, and the last nearest-surface search (band halos of a moving
     // camera): a later position p reuses it as nearDist - |p - nearPos| (1-Lipschitz) while the
     // world is unchanged and that keeps >= 3/4 of the searched distance
@@ -708,6 +712,7 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     c->hCell.assign((size_t)mx * my * mz * 64, 0ull);
     const int tx = (wx + 63) / 64, ty = (wy + 63) / 64, tz = (wz + 63) / 64;
     c->topCount.assign((size_t)tx * ty * tz, 0);
+    c->hNonAir.assign((size_t)mx * my * mz * 64, 0);
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -717,6 +722,7 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
                 const size_t b = brick_lin(c, x >> 2, y >> 2, z >> 2);
                 const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
                 c->hBricks[b * 64 + lc] = id;
+                c->hNonAir[b]++;
                 // only cube ids (1..12) make a brick visible to the DDA; other ids are empty for it
                 if (is_cube(id)) {
                     c->hMacro[b / 64] |= 1ull << (b % 64);
@@ -764,6 +770,7 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
     const size_t b = brick_lin(c, x >> 2, y >> 2, z >> 2);
     const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
     c->hBricks[b * 64 + lc] = (uint8_t)id;
+    c->hNonAir[b] += (id != 0 ? 1 : 0) - (old != 0 ? 1 : 0);
     HIPCHK(c, hipMemcpyAsync(c->bricks.p + b * 64 + lc, &c->hBricks[b * 64 + lc], 1, hipMemcpyHostToDevice, st));
     if (is_cube(old) != is_cube(id)) {
         const uint64_t before = c->hCell[b];
@@ -1206,43 +1213,56 @@ bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, int world
 }
 
 // A lower bound on the distance from p to any primary hit: the nearest non-air cell's box, grown by
-// one cell on every side (instanced meshes may overhang their cell), over the host mirror of the
-// world, searched in Chebyshev rings around p's cell up to 64 cells (beyond that, 63 is the bound).
-// Empty space outside the world holds no geometry.
+// meshGrow cells on every side (instanced meshes may overhang their cell; 1 unless a loaded mesh
+// reaches further), over the host mirror of the world, within 64 cells of p's cell (beyond that,
+// 63 - grow is the bound).  Empty space outside the world holds no geometry.  The search walks
+// Chebyshev rings of 4^3 bricks around p's brick, visits the cells of non-empty bricks only
+// (hNonAir) and stops once a ring cannot hold anything closer.
 float nearest_surface(const vxpt_ctx *c, V3 p) {
     const int WX = c->cx * 32, WY = c->cy * 32, WZ = c->cz * 32;
-    if (c->hIds.empty() || WX == 0) return 1e30f;
-    const int px = (int)std::floor(p.x), py = (int)std::floor(p.y), pz = (int)std::floor(p.z);
+    if (c->hIds.empty() || WX == 0 || c->hNonAir.empty()) return 1e30f;
     constexpr int kRings = 64;
-    constexpr float kGrow = 1.0f;
+    const float grow = c->meshGrow;
+    const float cap = (float)(kRings - 1) - grow;
+    auto gap = [&](float v, float lo, float hi) { return v < lo ? lo - v : (v > hi ? v - hi : 0.0f); };
+    const int px = (int)std::floor(p.x), py = (int)std::floor(p.y), pz = (int)std::floor(p.z);
+    const int bx0 = px >> 2, by0 = py >> 2, bz0 = pz >> 2;  // (arithmetic shift: floor for negatives)
+    const int BX = WX / 4, BY = WY / 4, BZ = WZ / 4;
     float best = 1e30f;
-    auto cell = [&](int x, int y, int z) {
-        if (x < 0 || y < 0 || z < 0 || x >= WX || y >= WY || z >= WZ) return;
-        if (c->hIds[(size_t)((x >> 5) + c->cx * ((z >> 5) + c->cz * (y >> 5))) * 32768 + (x & 31) +
-                    32 * ((z & 31) + 32 * (y & 31))] == 0)
-            return;
-        auto ax = [&](float v, int lo) {
-            const float a = (float)lo - kGrow, b = (float)(lo + 1) + kGrow;
-            return v < a ? a - v : (v > b ? v - b : 0.0f);
-        };
-        const float dx = ax(p.x, x), dy = ax(p.y, y), dz = ax(p.z, z);
-        best = std::min(best, std::sqrt(dx * dx + dy * dy + dz * dz));
+    auto brick = [&](int bx, int by, int bz) {
+        if (bx < 0 || by < 0 || bz < 0 || bx >= BX || by >= BY || bz >= BZ) return;
+        const size_t b = brick_lin(c, bx, by, bz);
+        if (!c->hNonAir[b]) return;
+        const float dx = gap(p.x, 4.0f * bx - grow, 4.0f * bx + 4.0f + grow);
+        const float dy = gap(p.y, 4.0f * by - grow, 4.0f * by + 4.0f + grow);
+        const float dz = gap(p.z, 4.0f * bz - grow, 4.0f * bz + 4.0f + grow);
+        if (std::sqrt(dx * dx + dy * dy + dz * dz) >= best) return;
+        for (int lc = 0; lc < 64; ++lc) {
+            if (!c->hBricks[b * 64 + lc]) continue;
+            const int x = bx * 4 + (lc & 3), z = bz * 4 + ((lc >> 2) & 3), y = by * 4 + (lc >> 4);
+            const float ex = gap(p.x, (float)x - grow, (float)(x + 1) + grow);
+            const float ey = gap(p.y, (float)y - grow, (float)(y + 1) + grow);
+            const float ez = gap(p.z, (float)z - grow, (float)(z + 1) + grow);
+            best = std::min(best, std::sqrt(ex * ex + ey * ey + ez * ez));
+        }
     };
-    for (int r = 0; r <= kRings; ++r) {
-        // every cell of ring r is at least r - 1 - kGrow away along its farthest axis
-        if (best <= (float)(r - 1) - kGrow) break;
+    // cells within Chebyshev distance 64 of p's cell lie within 17 bricks of p's brick; a cell
+    // further out is >= 64 - grow away, past the cap
+    for (int r = 0; r <= kRings / 4 + 1; ++r) {
+        // every brick of ring r is at least 4 (r - 1) - grow away along its farthest axis
+        if (best <= 4.0f * (float)(r - 1) - grow) break;
         for (int dy = -r; dy <= r; ++dy)
             for (int dz = -r; dz <= r; ++dz) {
                 const bool face = dy == -r || dy == r || dz == -r || dz == r;
                 if (face) {
-                    for (int dx = -r; dx <= r; ++dx) cell(px + dx, py + dy, pz + dz);
+                    for (int dx = -r; dx <= r; ++dx) brick(bx0 + dx, by0 + dy, bz0 + dz);
                 } else {
-                    cell(px - r, py + dy, pz + dz);
-                    if (r > 0) cell(px + r, py + dy, pz + dz);
+                    brick(bx0 - r, by0 + dy, bz0 + dz);
+                    if (r > 0) brick(bx0 + r, by0 + dy, bz0 + dz);
                 }
             }
     }
-    return std::min(best, (float)(kRings - 1) - kGrow);
+    return std::min(best, cap);
 }
 
 char *buffer_rows(vxpt_ctx *c, int which, int y, size_t &rowBytes) {
@@ -2275,6 +2295,12 @@ int vxpt_load_models(vxpt_ctx *c, const char *root, int *loaded) {
     }
     c->modelsLoaded = true;
     if (loaded) *loaded = nLoaded;
+    // the farthest any loaded mesh reaches outside its unit cell (its instance is the cell's
+    // translation): banded frames bound the primary hits' distance with it (nearest_surface)
+    c->meshGrow = 1.0f;
+    for (int b = 0; b < kBlockTypes; ++b)
+        for (float v : c->blocks[b].pos) c->meshGrow = std::max(c->meshGrow, std::max(-v, v - 1.0f));
+    ++c->worldVersion;  // a cached nearest-surface search used the old growth
     HIPCHK(c, hipSetDevice(c->dev));
     if (int r = build_blas(c)) return r;
     return refresh_instances(c, true, true);

@@ -122,7 +122,7 @@ def _rays_toward(origins, target, n, seed, spread=0.6):
     r[:, 0:3] = origins[rng.integers(0, len(origins), n)]
     tgt = np.asarray(target, np.float32) + rng.uniform(-spread, spread, (n, 3)).astype(np.float32)
     d = tgt - r[:, 0:3]
-    d[: n // 8, 1] = 0.0  # level rays too (the exit also takes d.y == 0)
+    d[: n // 8, 1] = 0.0  # level rays too: walks that stay in one layer of cells above the terrain
     r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
     r[:, 6] = 0.0
     r[:, 7] = 1e20
