@@ -92,7 +92,7 @@ class ImageDiffResult(ctypes.Structure):
 
 TUNING_FIELDS = ("dda_boxes", "box_cap", "box_cap_up", "brick_steps", "cam_steps", "iter_cap", "iter_cap2",
                  "resume_wg_per_cu", "sort_mode", "overlap", "state_sets", "firefly_fused", "ta_supertiles",
-                 "hf_split", "stencil_tile")
+                 "hf_split", "stencil_tile", "front_streams")
 
 
 class Tuning(ctypes.Structure):
@@ -561,7 +561,7 @@ class Renderer:
         if which in FLOAT1_BUFS:
             return np.zeros((self.H, self.W), np.float32)
         if which == BUF["TAP_RECORD"]:
-            return np.zeros((self.H, self.W, 8), np.float32)
+            return np.zeros((self.H, self.W, 16), np.float32)  # 64-byte tap records
         return np.zeros((self.H, self.W, 4), np.float32)
 
     def read(self, name):
