@@ -59,10 +59,9 @@ enum vxpt_buffer {
     VXPT_BUF_LIGHTS = 44,        /* nLights x 32 B LightInfo (Light.h:13-23)                     */
     VXPT_BUF_LIGHT_ALIAS = 45,   /* nLights x {f32 q, f32 p, i32 alias} (AliasTable.h bins)      */
     VXPT_BUF_BLOOM = 46,         /* post-process: the horizontally blurred bloom, Float4 per pixel */
-    VXPT_BUF_TAP_RECORD = 47,    /* read-only: the last pass's ReSTIR tap records, 64 B per pixel (normal xyz,
-                                  * roughness with the metallic flag in its sign bit; albedo xyz, depth;
-                                  * the pass's reservoir: lightData, uvData, weightSum, targetPdf; M, 0, 0, 0)
-                                  * -- what GetPrevSurface / LoadDIReservoir read (Restir.h:348-381, 48-79) */
+    VXPT_BUF_TAP_RECORD = 47,    /* read-only: the last pass's ReSTIR tap records, 32 B per pixel (normal xyz,
+                                  * roughness with the metallic flag in its sign bit; albedo xyz, depth) --
+                                  * the G-buffer planes GetPrevSurface reads (Restir.h:348-381), packed */
     VXPT_BUF_BOX_TABLES = 48     /* read-only: 8 x nBricks u32, the walk's empty-box extents per brick and ray
                                   * octant (x | y << 8 | z << 16 bricks; 0 = occupied), box_tables.hpp */
 };
@@ -153,7 +152,7 @@ typedef struct vxpt_tuning {
     int32_t ta_supertiles;    /* 1: temporal accumulation on XCD supertiles; 0: raster tiles            (1) */
     int32_t hf_split;         /* history-fix workgroups per tile, 1..16                                 (4) */
     int32_t stencil_tile;     /* tile edge of the history clamp and the first a-trous, 16 or 32        (16) */
-    int32_t front_streams;    /* first halves of consecutive passes on 1 stream, or 2 (side by side)    (2) */
+    int32_t front_streams;    /* streams for the passes' first halves (by state set), 1..3: side by side (2) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);

@@ -303,12 +303,7 @@ VX_D size_t ff_apply(const DenoiseArgs &a, unsigned tile, unsigned k, float4 &co
     const size_t i = (size_t)(a.y0 + (tile / tilesX) * 16 + (p >> 4)) * a.W + (tile % tilesX) * 16 + (p & 15);
     col = a.ffColor[s];
     a.illum[i] = col;
-    const Reservoir r = a.ffRes[s];
-    a.reservoir[i] = r;
-    // the next pass's temporal taps read the reservoir from the pass's tap record
-    a.rec[kRecF4 * i + 2] = make_float4(__int_as_float((int)r.lightData), __int_as_float((int)r.uvData), r.weightSum,
-                                        r.targetPdf);
-    a.rec[kRecF4 * i + 3] = make_float4(r.M, 0.0f, 0.0f, 0.0f);
+    a.reservoir[i] = a.ffRes[s];
     return i;
 }
 
@@ -1288,14 +1283,6 @@ hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, un
         hipLaunchKernelGGL((k_atrous_tile<4, 16>), grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, f);
     else  // step 8: a 34x34 staged apron for 16x16 pixels was measured slower (71 vs 65 us) than the taps
         hipLaunchKernelGGL(k_atrous, grid_xcd(a), dim3(256), 0, st, a, in, out, step, frameIndex, f);
-    return hipGetLastError();
-}
-// An empty launch that starts after every wait enqueued before it on the stream: a timing event
-// recorded behind it is not stamped before a pending cross-stream wait has resolved (a marker
-// right behind a wait measured ~30 us early on the C3 bench's chains)
-__global__ void k_gate() {}
-hipError_t launch_gate(hipStream_t st) {
-    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, st);
     return hipGetLastError();
 }
 hipError_t launch_copy_output(const DenoiseArgs &a, const float4 *in, hipStream_t st) {

@@ -448,17 +448,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESU
 // ----------------------------------------------------------------- shading
 // the pass's tap record (GBuf::rec) of pixel pi, written wherever the G-buffer planes are
 VX_D void store_rec(const TraceArgs &a, size_t pi, V3 n, float rough, bool metal, V3 alb, float depth) {
-    a.cur.rec[kRecF4 * pi] = make_float4(n.x, n.y, n.z, bits_as_float(float_as_bits(rough) | (metal ? (int)0x80000000u : 0)));
-    a.cur.rec[kRecF4 * pi + 1] = make_float4(alb.x, alb.y, alb.z, depth);
-}
-// the pass's reservoir of pixel pi: the reservoir plane and the tap record's copy
-VX_HD float4 res_word0(const Reservoir &r) {
-    return make_float4(bits_as_float((int)r.lightData), bits_as_float((int)r.uvData), r.weightSum, r.targetPdf);
-}
-VX_D void store_res(const TraceArgs &a, size_t pi, const Reservoir &r) {
-    a.resCur[pi] = r;
-    a.cur.rec[kRecF4 * pi + 2] = res_word0(r);
-    a.cur.rec[kRecF4 * pi + 3] = make_float4(r.M, 0.0f, 0.0f, 0.0f);
+    a.cur.rec[2 * pi] = make_float4(n.x, n.y, n.z, bits_as_float(float_as_bits(rough) | (metal ? (int)0x80000000u : 0)));
+    a.cur.rec[2 * pi + 1] = make_float4(alb.x, alb.y, alb.z, depth);
 }
 VX_D void store_rec_sky(const TraceArgs &a, size_t pi, float depth) {
     store_rec(a, pi, V3(0.0f, -1.0f, 0.0f), 0.0f, false, V3(1.0f), depth);
@@ -1044,9 +1035,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 1 : 
 // in the pass after a light update (a light that is gone empties it).  Taken literally: an empty
 // reservoir (lightData 0) reads as index 0 and is remapped as well.
 VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) {
-    // the tap record's copy: the same line as the tap's surface (prev_surface)
-    const float4 w0 = a.prev.rec[kRecF4 * i + 2], w1 = a.prev.rec[kRecF4 * i + 3];
-    Reservoir r{(uint32_t)float_as_bits(w0.x), (uint32_t)float_as_bits(w0.y), w0.z, w0.w, w1.x};
+    Reservoir r = a.resPrev[i];
     if (!a.lightsDirty) return r;
     const uint32_t li = r.lightData & 0x7FFFFFFFu;
     if (li >= 0x7FFFFFFDu || li >= (uint32_t)a.prevNumLights) return r;  // sun / sky, or not a previous light
@@ -1201,7 +1190,7 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     int4 meta = load_meta(w, s);
     const size_t pi = (size_t)py * a.W + px;
     if (meta.x & F_EMPTY) {
-        store_res(a, pi, empty_res());
+        a.resCur[pi] = empty_res();
         return;
     }
     if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
@@ -1234,7 +1223,7 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     }
     V3 segRad(0.0f);
     if (ls.type != LtInvalid && rr.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, rr);
-    store_res(a, pi, rr);
+    a.resCur[pi] = rr;
     // segment 0 (the only one with temporal reuse); travelled and the primary distance: its hit
     // distance (sPos.w).  A one-segment pass ends the path here (k_shade stored no continuation).
     const bool one = a.segments == 1;
@@ -1320,7 +1309,7 @@ __global__ __launch_bounds__(256) void k_primary_gbuffer(TraceArgs a) {
     const Hit h = unpack_hit(w.cHit[s], w.cT[s]);
     const V3 o = a.cam.pos, d = camera_ray(a, px, py);  // the camera ray, as k_closest traced it
     if (!h.hit) {
-        store_res(a, pi, empty_res());
+        a.resCur[pi] = empty_res();
         a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         a.cur.material[pi] = (float)0xFFFF;
         a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
@@ -1396,15 +1385,12 @@ __global__ __launch_bounds__(256) void k_probe_rng(BlueNoiseDev bn, int n, const
 }
 
 // rebuilds a slot's tap records from its planes (after a host write to the planes)
-__global__ __launch_bounds__(256) void k_pack_rec(GBuf g, const Reservoir *res, size_t n) {
+__global__ __launch_bounds__(256) void k_pack_rec(GBuf g, size_t n) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float4 nr = g.normalRough[i], al = g.albedo[i], mp = g.matParam[i];
-    g.rec[kRecF4 * i] = make_float4(nr.x, nr.y, nr.z, bits_as_float(float_as_bits(nr.w) | (mp.x == 1.0f ? (int)0x80000000u : 0)));
-    g.rec[kRecF4 * i + 1] = make_float4(al.x, al.y, al.z, g.depth[i]);
-    const Reservoir r = res[i];
-    g.rec[kRecF4 * i + 2] = res_word0(r);
-    g.rec[kRecF4 * i + 3] = make_float4(r.M, 0.0f, 0.0f, 0.0f);
+    g.rec[2 * i] = make_float4(nr.x, nr.y, nr.z, bits_as_float(float_as_bits(nr.w) | (mp.x == 1.0f ? (int)0x80000000u : 0)));
+    g.rec[2 * i + 1] = make_float4(al.x, al.y, al.z, g.depth[i]);
 }
 
 }  // namespace
@@ -1422,8 +1408,8 @@ extern "C" int vxpt_debug_stats(unsigned long long *out64, int reset) {
 }
 #endif
 
-hipError_t launch_pack_rec(const GBuf &g, const Reservoir *res, size_t n, hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_rec, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, res, n);
+hipError_t launch_pack_rec(const GBuf &g, size_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_rec, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, n);
     return hipGetLastError();
 }
 

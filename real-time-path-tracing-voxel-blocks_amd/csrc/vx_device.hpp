@@ -795,10 +795,10 @@ VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const 
     const size_t i = (size_t)y * a.W + x;
     // the previous pass's tap record (GBuf::rec): the planes' depth, normal (normalRough and
     // geoNormalThin hold the same one), roughness, metallic flag and albedo
-    const float4 b = a.prev.rec[kRecF4 * i + 1];
+    const float4 b = a.prev.rec[2 * i + 1];
     sf.depth = b.w;
     if (sf.depth == kRayMax) return false;
-    const float4 nr = a.prev.rec[kRecF4 * i];
+    const float4 nr = a.prev.rec[2 * i];
     V3 vd;
     if (vdIn) {
         vd = *vdIn;

@@ -91,16 +91,12 @@ struct BlueNoiseDev { const uint8_t *sobol, *scramble, *rank; };
 struct GBuf {
     float4 *normalRough, *geoNormalThin, *albedo, *matParam;
     float *depth, *material;
-    // what a ReSTIR temporal tap reads of this pass (Restir.h:348-381 GetPrevSurface, :48-79
-    // LoadDIReservoir), one 64-byte record per pixel, kRecF4 float4s: [0] = shading normal xyz (the
-    // geoNormalThin plane holds the same normal) + roughness with the metallic flag in its sign bit,
-    // [1] = albedo xyz + depth, [2] = the pass's reservoir (lightData, uvData bits, weightSum,
-    // targetPdf), [3].x = its M.  Written beside the planes and the reservoir plane by the trace (and
-    // by the firefly filter's write-back); a tap reads one aligned 64-byte line instead of five
-    // planes and a 20-byte reservoir.
+    // what a ReSTIR temporal tap reads of this pass's G-buffer (Restir.h:348-381 GetPrevSurface), one
+    // 32-byte record per pixel: [2i] = shading normal xyz (the geoNormalThin plane holds the same
+    // normal) + roughness with the metallic flag in its sign bit, [2i+1] = albedo xyz + depth.  Written
+    // beside the planes by the trace; a tap then reads one 32-byte record instead of five planes.
     float4 *rec;
 };
-constexpr int kRecF4 = 4;
 
 // Per-pixel state of the wavefront trace pass (trace.hip).  One slot per
 // pixel in 8x8-tile order (slot = tile*64 + lane, tiles row-major over the
@@ -248,8 +244,8 @@ hipError_t launch_sky_lower(float4 *sky, float *skyPdf, int skyW, int skyH, floa
 // halo exchange), or null
 hipError_t launch_trace_front(const TraceArgs &a, hipStream_t st);
 hipError_t launch_trace_back(const TraceArgs &a, hipStream_t st, hipEvent_t waitBeforeRestir);
-// GBuf::rec of the n pixels from the planes and the pass's reservoirs
-hipError_t launch_pack_rec(const GBuf &g, const Reservoir *res, size_t n, hipStream_t st);
+// GBuf::rec of the n pixels from the planes
+hipError_t launch_pack_rec(const GBuf &g, size_t n, hipStream_t st);
 hipError_t launch_probe_rng(const BlueNoiseDev &bn, int n, const int *q, float *out, hipStream_t st);
 
 struct DenoiseParamsDev {
@@ -295,9 +291,6 @@ struct DenoiseArgs {
     // thresholds, the frustum scale tanHalfFov.x / (res.x / 2), 1/(maxAcc+1),
     // 1/(maxFast+1)
     float invW, invH, thrB, thrA, frustumK, invAcc1, invFast1;
-    // the tap records of the frame's last pass (GBuf::rec): the firefly write-back keeps their
-    // reservoir copies in step with the reservoir plane
-    float4 *rec;
     // launch shapes (vxpt_tuning; host side only: read by the launch functions)
     struct {
         int ffFused, taSupertiles, hfSplit, stencilTile;
@@ -367,6 +360,5 @@ hipError_t launch_atrous_smem(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_atrous(const DenoiseArgs &a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex,
                          bool final, hipStream_t st);
 hipError_t launch_copy_output(const DenoiseArgs &a, const float4 *in, hipStream_t st);
-hipError_t launch_gate(hipStream_t st);
 
 }  // namespace vx

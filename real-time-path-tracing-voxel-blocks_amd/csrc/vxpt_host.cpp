@@ -45,7 +45,7 @@ struct DBuf {
 struct GSlot {
     float4 *normalRough = nullptr, *geoNormalThin = nullptr, *albedo = nullptr, *matParam = nullptr;
     float *depth = nullptr, *material = nullptr;
-    float4 *rec = nullptr;  // ReSTIR tap records (GBuf::rec), kRecF4 float4 (64 B) per pixel
+    float4 *rec = nullptr;  // ReSTIR tap records (GBuf::rec), 2 float4 per pixel
     bool recStale = false;  // the planes were written from the host since the records were
 };
 
@@ -170,7 +170,7 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.cam_steps, 1, 64) && in(t.iter_cap, 1, 1024) && in(t.iter_cap2, 0, 1024) &&
            in(t.resume_wg_per_cu, 1, 64) && in(t.sort_mode, 0, 2) && in(t.overlap, 0, 1) &&
            in(t.state_sets, 2, kMaxSets) && in(t.firefly_fused, 0, 1) && in(t.ta_supertiles, 0, 1) &&
-           in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, 2);
+           in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, kMaxSets);
 }
 
 struct vxpt_ctx {
@@ -329,10 +329,10 @@ struct vxpt_ctx {
     size_t wbSlots[kMaxSets] = {};
     int passCount = 0;         // trace passes so far (set = passCount % nSets)
     int lastSet = 0;           // the set of the most recent pass
-    // first halves: frontStream, or (tuning front_streams = 2) alternately frontStream / frontStream2 by
-    // state set, so a first half may run beside the previous pass's first half (it reads nothing a
-    // first half writes: the waits on backDone order it behind its set's last user only)
-    hipStream_t frontStream = nullptr, frontStream2 = nullptr;
+    // first halves: on front_streams streams by state set (set % front_streams), so a first half may run
+    // beside the previous passes' first halves (it reads nothing a first half writes: the waits on
+    // backDone order it behind its set's last user only)
+    hipStream_t frontStreams[kMaxSets] = {};
     hipEvent_t frontDone[kMaxSets] = {}, backDone[kMaxSets] = {}, frontGate = nullptr;
     std::vector<hipEvent_t> chainEv;  // vxpt_render_frames: around each frame's denoiser chain
     int numCU = 256;
@@ -558,7 +558,6 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.frustumK = c->cam.tanHalfFov.x / (c->cam.res.x / 2);
     a.invAcc1 = 1.0f / (a.p.maxAcc + 1.0f);
     a.invFast1 = 1.0f / (a.p.maxFast + 1.0f);
-    a.rec = c->gb[c->last].rec;
     a.tune.ffFused = c->tune.firefly_fused;
     a.tune.taSupertiles = c->tune.ta_supertiles;
     a.tune.hfSplit = c->tune.hf_split;
@@ -634,7 +633,7 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_TEXELS: p = c->texels.p; bytes = c->nTexels * 4; return !forWrite && c->texels.p;
         case VXPT_BUF_BLOOM: p = c->bloomB; bytes = n * 16; return c->bloomB != nullptr;
         case VXPT_BUF_LIGHTS: p = c->lights.p; bytes = (size_t)c->nLights * sizeof(LightInfo); return !forWrite && c->nLights;
-        case VXPT_BUF_TAP_RECORD: p = g.rec; bytes = n * 16 * kRecF4; return !forWrite;
+        case VXPT_BUF_TAP_RECORD: p = g.rec; bytes = n * 32; return !forWrite;
         case VXPT_BUF_BOX_TABLES: p = c->bbox.p; bytes = (size_t)8 * c->nBricks * 4; return !forWrite && c->bbox.p;
         case VXPT_BUF_LIGHT_ALIAS:
             p = c->lightAlias.p; bytes = (size_t)c->nLights * sizeof(AliasBin); return !forWrite && c->nLights;
@@ -851,9 +850,7 @@ struct PassPlan {
 // half (it then waits only for the pass before that to release its state set).  Otherwise it starts
 // after everything enqueued on the context stream.  A primary-only pass runs whole on the context
 // stream here.
-hipStream_t front_stream(const vxpt_ctx *c, int set) {
-    return (c->tune.front_streams > 1 && (set & 1)) ? c->frontStream2 : c->frontStream;
-}
+hipStream_t front_stream(const vxpt_ctx *c, int set) { return c->frontStreams[set % c->tune.front_streams]; }
 
 int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
                 bool overlap, PassPlan &pl) {
@@ -892,7 +889,7 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.cur = {cur.normalRough, cur.geoNormalThin, cur.albedo, cur.matParam, cur.depth, cur.material, cur.rec};
     a.prev = {prev.normalRough, prev.geoNormalThin, prev.albedo, prev.matParam, prev.depth, prev.material, prev.rec};
     if (prev.recStale) {  // planes uploaded or copied in from the host: rebuild the taps' records
-        HIPCHK(c, launch_pack_rec(a.prev, a.resPrev, (size_t)c->W * c->H, c->stream));
+        HIPCHK(c, launch_pack_rec(a.prev, (size_t)c->W * c->H, c->stream));
         c->gb[c->last].recStale = false;
     }
     c->gb[next].recStale = false;  // this pass writes both
@@ -1099,18 +1096,17 @@ int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int a
 // context stream behind the kernels that produced the rows -- no packing, no
 // host synchronisation.
 constexpr int kTraceHalo = 72;  // ReSTIR temporal taps: 64-pixel disk + reprojection (Restir.h:348-381)
-// The next pass's temporal taps read only the previous pass's tap records (GBuf::rec: surface and
-// reservoir), so a pass hands its neighbours those, 64 B/px, at the trace depth; the G-buffer planes are
+// The next pass's temporal taps read only the previous pass's tap records (GBuf::rec) and reservoirs,
+// so a pass hands its neighbours those two, 52 B/px, at the trace depth; the G-buffer planes are
 // read by the denoiser alone (after the frame's last pass, within kDenoiseRows of the band: the
 // world positions of k_firefly at kWposHalo, the history fix's taps at 34) and by the next frame's
 // temporal accumulation as its history (histRows), so they travel once per frame.
 const int kGbufPlanes[] = {VXPT_BUF_DEPTH, VXPT_BUF_NORMAL_ROUGH, VXPT_BUF_GEO_NORMAL_THIN,
                            VXPT_BUF_ALBEDO, VXPT_BUF_MATERIAL, VXPT_BUF_MAT_PARAM};
-// a host-side write to a G-buffer plane or to reservoirs leaves the slots' tap records stale (rebuilt
-// before the next trace reads them)
+// a host-side write to a G-buffer plane leaves the slots' tap records stale (rebuilt before the next
+// trace reads them)
 bool is_gbuf_plane(int which) { return (which >= VXPT_BUF_DEPTH && which <= VXPT_BUF_MAT_PARAM) ||
-                                       (which >= VXPT_BUF_PREV_NORMAL_ROUGH && which <= VXPT_BUF_RESERVOIRS) ||
-                                       which == VXPT_BUF_RES_EVEN || which == VXPT_BUF_RES_ODD; }
+                                       (which >= VXPT_BUF_PREV_NORMAL_ROUGH && which <= VXPT_BUF_PREV_MATERIAL); }
 void gbuf_written(vxpt_ctx *c, int which) {
     if (which == VXPT_BUF_MOTION) c->motionZero = false;
     if (is_gbuf_plane(which))
@@ -1399,6 +1395,7 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
                       planeRows > cs[0]->haloPlaneRows)) {
         std::vector<std::pair<int, int>> br;
         br.emplace_back(VXPT_BUF_TAP_RECORD, traceRows);
+        br.emplace_back(((it0 - 1) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows);
         for (int b : kGbufPlanes) br.emplace_back(b, planeRows);
         for (int b : kHistoryBufs) br.emplace_back(b, histRows);
         BANDCHK(exchange_set(cs, br, false));
@@ -1415,13 +1412,14 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         if (s + 1 < spp) {
             // all but the last pass: the next pass's temporal taps' inputs, overlapped with that pass
             // up to its temporal reuse
-            BANDCHK(exchange_set(cs, {{VXPT_BUF_TAP_RECORD, traceRows}}, true));
+            BANDCHK(exchange_set(cs, {{VXPT_BUF_TAP_RECORD, traceRows}, {res, traceRows}}, true));
         } else {
             // the last pass: its planes for the denoiser, and the denoiser input (radiance, or the spp
             // average) for the firefly filter's 3x3 neighbours.  Its reservoirs go out at the trace
             // depth after the firefly filter has rewritten them (below); without the filter, here.
             for (vxpt_ctx *c : cs) c->denoiseInputIsAccum = spp > 1;
-            std::vector<std::pair<int, int>> br{{VXPT_BUF_TAP_RECORD, traceRows}, {VXPT_BUF_ILLUM, 2}, {res, 2}};
+            std::vector<std::pair<int, int>> br{{VXPT_BUF_TAP_RECORD, traceRows}, {VXPT_BUF_ILLUM, 2},
+                                                {res, p->enable_firefly_filter ? 2 : traceRows}};
             for (int b : kGbufPlanes) br.emplace_back(b, planeRows);
             BANDCHK(exchange_set(cs, br, false));
         }
@@ -1435,10 +1433,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     if (!p->enable_firefly_filter) FOR_BANDS(run_pass(c, p, 11, 0, 0));
     if (p->enable_firefly_filter) {  // + world positions
         FOR_BANDS(run_pass(c, p, 0, used & 1, 0));
-        // the filtered reservoirs: the next frame's first temporal taps read them (in the tap records)
-        // at the trace depth, the filter itself its 3x3 neighbours' (the reservoir plane)
-        BANDCHK(exchange_set(cs, {{VXPT_BUF_TAP_RECORD, traceRows},
-                                  {(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, 2}, {VXPT_BUF_ILLUM, 2}}));
+        // the filtered reservoirs: the next frame's first temporal taps read them at the trace depth
+        BANDCHK(exchange_set(cs, {{(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows}, {VXPT_BUF_ILLUM, 2}}));
     }
     const std::vector<int> hist(std::begin(kHistoryBufs), std::end(kHistoryBufs));
     if (frame == 0) {
@@ -1528,8 +1524,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(c, hipStreamCreateWithFlags(&c->frontStream, hipStreamNonBlocking));
-    HIPCHK(c, hipStreamCreateWithFlags(&c->frontStream2, hipStreamNonBlocking));
+    for (hipStream_t &fs : c->frontStreams) HIPCHK(c, hipStreamCreateWithFlags(&fs, hipStreamNonBlocking));
     // tuning state_sets = 3: a third wavefront state set, so a first half may run beside the two
     // previous second halves (C3: 6.40 -> 6.39 ms per frame, within noise: the overlapped halves
     // already fill the chip; two sets are the default)
@@ -1545,7 +1540,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     const size_t tiles16 = (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16);  // denoiser tiles
     for (auto &g : c->gb) {
         if (dalloc(c, g.normalRough, n) || dalloc(c, g.geoNormalThin, n) || dalloc(c, g.albedo, n) ||
-            dalloc(c, g.matParam, n) || dalloc(c, g.depth, n) || dalloc(c, g.material, n) || dalloc(c, g.rec, kRecF4 * n))
+            dalloc(c, g.matParam, n) || dalloc(c, g.depth, n) || dalloc(c, g.material, n) || dalloc(c, g.rec, 2 * n))
             return VXPT_ERR_HIP;
     }
     if (dalloc(c, c->illum, n) || dalloc(c, c->accum, n) || dalloc(c, c->motion, n) || dalloc(c, c->res, 2 * n) ||
@@ -1586,16 +1581,16 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
 void vxpt_destroy(vxpt_ctx *c) {
     if (!c) return;
     hipSetDevice(c->dev);
-    if (c->frontStream) hipStreamSynchronize(c->frontStream);
-    if (c->frontStream2) hipStreamSynchronize(c->frontStream2);
+    for (hipStream_t fs : c->frontStreams)
+        if (fs) hipStreamSynchronize(fs);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void *p : c->allocs) hipFree(p);
     for (int k = 0; k < kMaxSets; ++k)
         for (hipEvent_t e : {c->frontDone[k], c->backDone[k]})
             if (e) hipEventDestroy(e);
     if (c->frontGate) hipEventDestroy(c->frontGate);
-    if (c->frontStream) hipStreamDestroy(c->frontStream);
-    if (c->frontStream2) hipStreamDestroy(c->frontStream2);
+    for (hipStream_t fs : c->frontStreams)
+        if (fs) hipStreamDestroy(fs);
     for (hipEvent_t e : c->chainEv) hipEventDestroy(e);
     for (auto &e : c->ev)
         if (e) hipEventDestroy(e);
@@ -2667,9 +2662,12 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         return VXPT_OK;
     }
     const float scale = 1.0f / (float)spp;
-    // an event pair around every denoiser chain: the chains run alone (below), so the frames' trace
-    // time is the whole minus their sum
-    while (c->chainEv.size() < (size_t)2 * nFrames) {
+    // events around every denoiser chain: the chains run alone (below), so the frames' trace time is
+    // the whole minus their sum.  A chain starts when both the frame's last second half (context
+    // stream) and the next frame's first half (its front stream) have finished: a marker behind each,
+    // the later of the two is its start (a marker behind a cross-stream wait is not reliably stamped
+    // after the wait: measured 10-40 us early)
+    while (c->chainEv.size() < (size_t)3 * nFrames) {
         hipEvent_t e;
         HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         c->chainEv.push_back(e);
@@ -2702,28 +2700,34 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             // all of the chain but its firefly stage on a third stream beside the next frame's first
             // pass was measured: 6.02 -> 5.92 ms per frame, but the overlapped chain took ~3x as long
             // and k_restir beside it +0.5 ms; removed)
+            // (chains after such a first half measure 0.40 instead of 0.36 ms, every chain kernel 5-10 %
+            // slower with the GPU idle beside them; an L2 write-back of the first half's dirty lines
+            // before the chain changed nothing -- the frame is still 0.14 ms shorter this way)
             if (!pend.a.primaryOnly) {
+                HIPCHK(c, hipEventRecord(c->chainEv[3 * f + 2], front_stream(c, pend.set)));
+                HIPCHK(c, hipEventRecord(c->chainEv[3 * f], c->stream));
                 HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
-                HIPCHK(c, launch_gate(c->stream));  // the chain's start event after that wait
             }
         }
         c->denoiseInputIsAccum = spp > 1;
-        HIPCHK(c, hipEventRecord(c->chainEv[2 * f], c->stream));
+        const bool waited = havePend && !pend.a.primaryOnly;
+        if (!waited) HIPCHK(c, hipEventRecord(c->chainEv[3 * f], c->stream));
         if (int r = do_denoise(c, p, frame0 + f, it0 + spp)) return r;
-        HIPCHK(c, hipEventRecord(c->chainEv[2 * f + 1], c->stream));
+        HIPCHK(c, hipEventRecord(c->chainEv[3 * f + 1], c->stream));
         if (havePend) {  // later first halves wait for the denoiser (it reads the old history slot)
             HIPCHK(c, hipEventRecord(c->frontGate, c->stream));
-            HIPCHK(c, hipStreamWaitEvent(c->frontStream, c->frontGate, 0));
-            HIPCHK(c, hipStreamWaitEvent(c->frontStream2, c->frontGate, 0));
+            for (hipStream_t fs : c->frontStreams) HIPCHK(c, hipStreamWaitEvent(fs, c->frontGate, 0));
         }
     }
     HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float dsum = 0, f = 0;
     for (int k = 0; k < nFrames; ++k) {
-        float d = 0;
-        hipEventElapsedTime(&d, c->chainEv[2 * k], c->chainEv[2 * k + 1]);
-        dsum += d;
+        float a = 0, b = 0, e = 0;
+        hipEventElapsedTime(&a, c->ev[6], c->chainEv[3 * k]);
+        hipEventElapsedTime(&e, c->ev[6], c->chainEv[3 * k + 1]);
+        if (k + 1 < nFrames && hipEventElapsedTime(&b, c->ev[6], c->chainEv[3 * k + 2]) == hipSuccess) a = std::max(a, b);
+        dsum += e - a;
     }
     hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
     c->timing.trace_ms = (f - dsum) / (float)nFrames;  // per frame, the chains excluded
@@ -3160,8 +3164,7 @@ int vxpt_set_tuning(vxpt_ctx *c, const vxpt_tuning *t) {
     if (!tuning_valid(*t)) return fail(c, VXPT_ERR_ARG, "tuning field out of range");
     HIPCHK(c, hipSetDevice(c->dev));
     // whatever is in flight used the old schedule's buffers
-    HIPCHK(c, hipStreamSynchronize(c->frontStream));
-    HIPCHK(c, hipStreamSynchronize(c->frontStream2));
+    for (hipStream_t fs : c->frontStreams) HIPCHK(c, hipStreamSynchronize(fs));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const bool tables = t->dda_boxes != c->tune.dda_boxes || t->box_cap != c->tune.box_cap ||
                         t->box_cap_up != c->tune.box_cap_up;

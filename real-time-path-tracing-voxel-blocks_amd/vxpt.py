@@ -561,7 +561,7 @@ class Renderer:
         if which in FLOAT1_BUFS:
             return np.zeros((self.H, self.W), np.float32)
         if which == BUF["TAP_RECORD"]:
-            return np.zeros((self.H, self.W, 16), np.float32)  # 64-byte tap records
+            return np.zeros((self.H, self.W, 8), np.float32)
         return np.zeros((self.H, self.W, 4), np.float32)
 
     def read(self, name):

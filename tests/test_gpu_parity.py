@@ -135,53 +135,42 @@ def test_primary_gbuffer(pair):
     np.testing.assert_allclose(g, c, rtol=1e-5, atol=1e-6)
 
 
-def _expected_tap_record(r, it):
-    """GBuf::rec restated from the G-buffer planes and the pass's reservoirs (iterationIndex it):
-    (normal xyz, roughness | metallic << 31), (albedo xyz, depth), (lightData, uvData, weightSum,
-    targetPdf), (M, 0, 0, 0) -- 64 bytes per pixel."""
+def _expected_tap_record(r):
+    """GBuf::rec restated from the G-buffer planes: (normal xyz, roughness | metallic << 31),
+    (albedo xyz, depth), 32 bytes per pixel."""
     nr, al, mp, d = r.read("NORMAL_ROUGH"), r.read("ALBEDO"), r.read("MAT_PARAM"), r.read("DEPTH")
-    res = r.read("RES_ODD" if it & 1 else "RES_EVEN")
-    exp = np.zeros(nr.shape[:2] + (16,), np.float32)
+    exp = np.zeros(nr.shape[:2] + (8,), np.float32)
     exp[..., :3], exp[..., 4:7], exp[..., 7] = nr[..., :3], al[..., :3], d
     rb = nr[..., 3].view(np.uint32) | np.where(mp[..., 0] == 1.0, np.uint32(0x80000000), np.uint32(0))
     exp[..., 3] = rb.view(np.float32)
-    res = res.reshape(nr.shape[:2])
-    exp[..., 8] = res["lightData"].view(np.float32)
-    exp[..., 9] = res["uvData"].view(np.float32)
-    exp[..., 10], exp[..., 11], exp[..., 12] = res["weightSum"], res["targetPdf"], res["M"]
     return exp
 
 
 @pytest.mark.parametrize("primary_only", [False, True])
 def test_tap_record_matches_planes(primary_only):
-    """The trace writes each pixel's ReSTIR tap record beside its G-buffer planes and reservoirs; the
-    record is the planes' and the pass's reservoir's values bit for bit (and the geoNormalThin plane
-    holds the normalRough normal, which the record stores once).  A primary-only pass stores no
-    reservoirs: its records' surface half only."""
+    """The trace writes each pixel's ReSTIR tap record beside its G-buffer planes; the record is
+    the planes' values bit for bit (and the geoNormalThin plane holds the normalRough normal, which
+    the record stores once)."""
     r, o = _setup(100, 62)
     try:
         for it in range(2):
             r.trace(it, primary_only=primary_only)
-            k = 8 if primary_only else 16
-            np.testing.assert_array_equal(r.read("TAP_RECORD")[..., :k].view(np.uint32),
-                                          _expected_tap_record(r, it)[..., :k].view(np.uint32))
+            np.testing.assert_array_equal(r.read("TAP_RECORD").view(np.uint32), _expected_tap_record(r).view(np.uint32))
             np.testing.assert_array_equal(r.read("GEO_NORMAL_THIN")[..., :3].view(np.uint32),
                                           r.read("NORMAL_ROUGH")[..., :3].view(np.uint32))
     finally:
         r.close()
 
 
-@pytest.mark.parametrize("plane", ["NORMAL_ROUGH", "RES_EVEN", "RESERVOIRS"])
-def test_tap_records_rebuilt_after_a_plane_upload(plane):
-    """A host write to a G-buffer plane or to the reservoirs marks the tap records stale; the next
-    trace rebuilds them from the planes and the previous pass's reservoirs (k_pack_rec) and renders
-    exactly what an untouched context renders."""
+def test_tap_records_rebuilt_after_a_plane_upload():
+    """A host write to a G-buffer plane marks the tap records stale; the next trace rebuilds them
+    from the planes (k_pack_rec) and renders exactly what an untouched context renders."""
     a, _ = _setup(100, 62)
     b, _ = _setup(100, 62)
     try:
         for r in (a, b):
             r.trace(0)
-        b.write(plane, b.read(plane))  # same values, through the upload path
+        b.write("NORMAL_ROUGH", b.read("NORMAL_ROUGH"))  # same values, through the upload path
         for r in (a, b):
             r.trace(1)
         for name in ("ILLUM", "RES_ODD", "TAP_RECORD"):
@@ -348,7 +337,7 @@ TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=3), dict(sort_mode=1), dict(
                    dict(iter_cap=2, iter_cap2=3, resume_wg_per_cu=3), dict(brick_steps=1, cam_steps=2),
                    dict(dda_boxes=0), dict(box_cap=2, box_cap_up=40), dict(firefly_fused=0), dict(ta_supertiles=0),
                    dict(hf_split=1), dict(stencil_tile=32), dict(front_streams=1),
-                   dict(front_streams=1, state_sets=3), dict(state_sets=3)]
+                   dict(front_streams=1, state_sets=3), dict(state_sets=3), dict(front_streams=3, state_sets=3)]
 
 
 @pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
