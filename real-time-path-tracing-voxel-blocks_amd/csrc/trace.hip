@@ -152,10 +152,56 @@ VX_D V3 camera_ray(const TraceArgs &a, int px, int py) {
     return a.cam.uv_to_dir(uv);
 }
 
+// North_star's "voxel bricks staged into LDS" for the camera walks (tuning lds_bricks): a workgroup's
+// 256 camera rays leave one origin through a narrow frustum and read few distinct bricks (8.7
+// distinct 128-B lines per workgroup on the C3 bench, tools/dda_sim), so each workgroup keeps a
+// direct-mapped cache of (brick, ray octant) -> box entry + cube mask in LDS.  An entry is filled
+// once, by the first lane that misses on an empty slot (atomicCAS claims it, the data is written,
+// then the key is published) and never evicted; a lane that finds another key, or a slot being
+// filled, reads global memory.  The entries are copies, so every walk is the global one.
+constexpr int kLdsBrickSlots = 512;
+struct BrickCacheLds {
+    int key[kLdsBrickSlots];
+    uint32_t box[kLdsBrickSlots];
+    uint64_t cm[kLdsBrickSlots];
+};
+struct LdsBricks {
+    BrickCacheLds *c;
+    template <bool BOX>
+    VX_D uint64_t fetch(const WorldDev &w, Dda &s, int nb) const {
+        static_assert(BOX, "the LDS brick cache holds box-table entries");
+        const int key = nb * 8 + octant_of(s.r);
+        const int slot = key & (kLdsBrickSlots - 1);
+        const int k = __hip_atomic_load(&c->key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint64_t m;
+        if (k == key) {
+            s.box = c->box[slot];
+            m = c->cm[slot];
+        } else {
+            m = w.cellMask[nb];
+            s.box = s.ob[nb];
+            if (k == -1 && atomicCAS(&c->key[slot], -1, -2) == -1) {
+                c->box[slot] = s.box;
+                c->cm[slot] = m;
+                __threadfence_block();
+                atomicExch(&c->key[slot], key);
+            }
+        }
+        s.dist = (int)(s.box & 0xFFu);
+        return m;
+    }
+};
+
 // mode 2: camera rays (RayGen.cu:102-126; initialises the path state);
 // mode 0: continuing path rays (BRDF-candidate rays go through the compacted queue).
-template <bool BOX>
+template <bool BOX, bool LDS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOSEST))) void k_closest(TraceArgs a, int mode) {
+    struct NoCache {};
+    __shared__ std::conditional_t<LDS, BrickCacheLds, NoCache> cache;
+    if constexpr (LDS) {
+        for (int k = threadIdx.x; k < kLdsBrickSlots; k += 256) cache.key[k] = -1;
+        __syncthreads();
+    }
     const int s = blockIdx.x * 256 + threadIdx.x;
     int px, py;
     bool active = slot_pixel(a, s, px, py);
@@ -193,7 +239,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOS
     if (active) {
         WorldDev wc = a.world;
         wc.brickSteps = wc.brickStepsCam;
-        const Hit h = dda_closest<BOX>(wc, o, d, tmax VX_IT);
+        Hit h;
+        if constexpr (LDS) h = dda_closest<BOX>(wc, o, d, tmax, nullptr, LdsBricks{&cache});
+        else h = dda_closest<BOX>(wc, o, d, tmax VX_IT);
         w.cHit[s] = pack_hit(h);
         w.cT[s] = h.t;
     }
@@ -1434,8 +1482,9 @@ struct Launcher {
         : a(a_), st(st_), g((a_.nSlots + 255) / 256), b(256), mesh(a_.mesh.nInst > 0), box(a_.world.bbox != nullptr) {}
     // the walks use the empty-box tables when the world has them, else the cubes
     void closest(int mode) {
-        if (box) hipLaunchKernelGGL(k_closest<true>, g, b, 0, st, a, mode);
-        else hipLaunchKernelGGL(k_closest<false>, g, b, 0, st, a, mode);
+        if (box && a.ldsBricks) hipLaunchKernelGGL((k_closest<true, true>), g, b, 0, st, a, mode);
+        else if (box) hipLaunchKernelGGL((k_closest<true, false>), g, b, 0, st, a, mode);
+        else hipLaunchKernelGGL((k_closest<false, false>), g, b, 0, st, a, mode);
     }
     // a ray queue's traversal: iteration-capped pass + straggler continuation (+ the mesh pass).  The
     // stragglers' grid: a fixed number of workgroups per CU (their count is on the device; each wave

@@ -186,12 +186,11 @@ struct Dda {
 };
 enum { DdaRun = 0, DdaEvent = 1, DdaNone = 2 };
 
-// brick data of the walk's current cell (cached per brick); returns the cube bit
-template <bool BOX = false>
-VX_HD bool locate(const WorldDev &w, Dda &s) {
-    const int nb = brick_index(w, s.c.x, s.c.y, s.c.z);
-    if (nb != s.nb) {
-        s.nb = nb;
+// Where a walk reads a brick's skip-table entry and cube mask: global memory (every kernel but the
+// LDS-cached camera walk of k_closest, trace.hip LdsBricks).  Sets s.box / s.dist; returns the mask.
+struct GlobalBricks {
+    template <bool BOX>
+    VX_HD uint64_t fetch(const WorldDev &w, Dda &s, int nb) const {
         // the brick's cube mask is fetched beside its table entry, not behind it: one memory
         // round trip per new brick (8 wasted bytes for an empty one) instead of two
         const uint64_t m = w.cellMask[nb];
@@ -201,6 +200,17 @@ VX_HD bool locate(const WorldDev &w, Dda &s) {
         } else {
             s.dist = s.od[nb];
         }
+        return m;
+    }
+};
+
+// brick data of the walk's current cell (cached per brick); returns the cube bit
+template <bool BOX = false, class F = GlobalBricks>
+VX_HD bool locate(const WorldDev &w, Dda &s, const F &f = F()) {
+    const int nb = brick_index(w, s.c.x, s.c.y, s.c.z);
+    if (nb != s.nb) {
+        s.nb = nb;
+        const uint64_t m = f.template fetch<BOX>(w, s, nb);
         s.cm = s.dist ? 0ull : m;
     }
     return (s.cm >> cell_of(s.c.x, s.c.y, s.c.z)) & 1ull;
@@ -294,8 +304,8 @@ VX_HD int brick_walk(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
 // plane is a chunk boundary, or a is outside the world.
 // Visibility rays (OCC = true): any face crossing with tmin <= t <= tmax (no
 // culling, so leaving a cube cell counts too).
-template <bool OCC, bool BOX = false>
-VX_HD int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s, Hit &h) {
+template <bool OCC, bool BOX = false, class F = GlobalBricks>
+VX_HD int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &s, Hit &h, const F &f = F()) {
     bool outside;
     int ax = -1;
     float tEnter = 0;
@@ -306,7 +316,7 @@ VX_HD int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &
     if constexpr (BOX) s.ob = w.bbox + (size_t)w.nBricks * octant_of(s.r);
     else s.od = w.bdist + (size_t)w.nBricks * octant_of(s.r);
     s.nb = -1;
-    const bool solid = locate<BOX>(w, s);
+    const bool solid = locate<BOX>(w, s, f);
     s.prevId = solid ? -1 : 0;
     s.prevLoc = s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z);
     if (outside) {
@@ -343,8 +353,8 @@ VX_HD void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, con
     s.steps = v.face.y >> 16;
 }
 
-template <bool OCC, bool BOX = false>
-VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
+template <bool OCC, bool BOX = false, class F = GlobalBricks>
+VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const F &f = F()) {
     if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;
     if (cnt) ++cnt[s.dist == 0 ? 3 : (s.dist == 1 ? 2 : 1)];
     if (s.dist == 0) {
@@ -371,7 +381,7 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
         // leaving the world: only a visibility ray leaving a cube cell sees a face
         return (OCC && t >= s.tmin && s.prevId != 0) ? DdaEvent : DdaNone;
     }
-    const bool solid = locate<BOX>(w, s);
+    const bool solid = locate<BOX>(w, s, f);
     if (solid || s.prevId != 0) {
         if (cross<OCC>(w, s, solid, s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z), chunkPlane, t, face, h))
             return DdaEvent;
@@ -379,12 +389,12 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr) {
     return DdaRun;
 }
 
-template <bool BOX = false>
-VX_HD Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax, int *iters = nullptr) {
+template <bool BOX = false, class F = GlobalBricks>
+VX_HD Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax, int *iters = nullptr, const F &f = F()) {
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
     Dda s;
-    int rc = dda_begin<false, BOX>(w, o, d, 0.0f, tmax, s, h);
-    while (rc == DdaRun) rc = dda_iter<false, BOX>(w, s, h, iters);
+    int rc = dda_begin<false, BOX>(w, o, d, 0.0f, tmax, s, h, f);
+    while (rc == DdaRun) rc = dda_iter<false, BOX>(w, s, h, iters, f);
     if (rc != DdaEvent) h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
     return h;
 }

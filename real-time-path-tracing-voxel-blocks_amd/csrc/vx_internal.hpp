@@ -231,6 +231,7 @@ struct TraceArgs {
     int lightsDirty;
     int resumeWgPerCU;  // k_resume workgroups per CU (0: 16)
     int sortMode;       // ray queues grouped by direction class per workgroup (0 off, 1 octant, 2 octant x axis)
+    int ldsBricks;      // k_closest reads bricks through a workgroup cache in LDS (trace.hip LdsBricks)
     int writeMotion;    // store the (zero) motion vectors: the plane may hold a host upload
 };
 
