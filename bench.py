@@ -18,7 +18,11 @@ horizontal bands; each rank's library context renders its band and enqueues
 the halo exchanges itself (RCCL over xGMI: grouped send/recv with the band
 neighbours on the context stream, vxpt_band_comm_init).  Total work is fixed
 (strong scaling); value = whole-frame paths / max-over-ranks time; roofline =
-the rank's band (its denoiser time includes the exchanges).
+the rank's band (its denoiser time includes the exchanges).  Before the run the
+band boundaries are balanced (vxpt_band_balance): every rank times its band of
+the frame alone (no exchange), the ranks share the times, and the boundaries
+move to equalise them -- rows near the horizon cost several times the ground's,
+so equal bands leave the slowest rank far above the mean (--equal-bands: off).
 """
 import argparse
 import glob
@@ -137,6 +141,39 @@ def cpu_baseline(a, target_s):
     return res
 
 
+def balance_bands(a, make, params, world, rank, dist, rounds=2, frames=6):
+    """Cost-balanced band boundaries (vxpt_band_balance): each round, every rank renders its band
+    of the current partition alone in a throwaway context (band mode, no exchange: its compute
+    only), the ranks all-gather the per-frame times, and every rank computes the same next
+    partition from them.  Returns (row boundaries, per-round log)."""
+    import vxpt
+    splits, cost, log = vxpt.equal_splits(a.height, world), None, []
+    for _ in range(rounds):
+        r = make()
+        try:
+            r.set_band(splits[rank], splits[rank + 1])
+
+            def run(f0, n):
+                if a.primary_only:
+                    for f in range(f0, f0 + n):
+                        r.trace(f, primary_only=True)
+                else:
+                    r.render_frames(f0, n, a.spp, params)
+                r.sync()
+            run(0, 3)
+            t0 = time.perf_counter()
+            run(3, frames)
+            ms = (time.perf_counter() - t0) / frames * 1e3
+        finally:
+            r.close()
+        times = [None] * world
+        dist.all_gather_object(times, ms)
+        log.append({"band_rows": splits, "band_ms": [round(t, 4) for t in times]})
+        splits, cost = vxpt.band_balance(a.height, splits, times, cost)
+    log.append({"band_rows": splits})
+    return splits, log
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +194,8 @@ def main():
                          "'4 bounces' of BASELINE.json's config line, labelled as such")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--equal-bands", action="store_true",
+                    help="N>1: keep the equal row bands instead of balancing the boundaries on measured band times")
     ap.add_argument("--frame-calls", action="store_true",
                     help="time K vxpt_render_frame calls instead of one pipelined vxpt_render_frames(K)")
     a = ap.parse_args()
@@ -185,14 +224,22 @@ def main():
     import bands
 
     chunks, hs, fd, gy, pos = scene_args(a)
-    r = vxpt.Renderer(a.width, a.height, device=local, bounces=a.bounce_limits)
-    r.load_settings()
-    if a.tune:
-        r.set_tuning(**a.tune)
-    r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=gy)
-    r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
-    r.set_sky()
     params = vxpt.DenoiseParams.defaults()
+
+    def make():
+        r = vxpt.Renderer(a.width, a.height, device=local, bounces=a.bounce_limits)
+        r.load_settings()
+        if a.tune:
+            r.set_tuning(**a.tune)
+        r.generate_terrain(chunks, height_scale=hs, freq_den=fd, global_y=gy)
+        r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
+        r.set_sky()
+        return r
+
+    splits, balance_log = None, None
+    if world > 1 and not a.equal_bands:
+        splits, balance_log = balance_bands(a, make, params, world, rank, dist)
+    r = make()
     band = None
     if world > 1:
         # the library renders this rank's band and enqueues the halo exchanges itself
@@ -201,7 +248,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         err = ""
         try:
-            r.band_comm_init(obj[0], world, rank)
+            r.band_comm_init(obj[0], world, rank, splits)
         except vxpt.VxptError as e:
             err = str(e)
         errs = [None] * world
@@ -214,7 +261,7 @@ def main():
             r.close()
             dist.destroy_process_group()
             sys.exit(3)
-        band = bands.band_rows(a.height, world, rank)
+        band = bands.band_rows(a.height, world, rank) if splits is None else (splits[rank], splits[rank + 1])
 
     def step(frame):
         if a.primary_only:
@@ -329,6 +376,8 @@ def main():
                                               else (" (BASELINE.json's '4 bounces' reading; the reference renders 3/1)",)
                                               if a.bounce_limits == (4, 4) else ("",))),
                        "parallelism": ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU",
+                       "band_rows": (splits or vxpt.equal_splits(a.height, world)) if world > 1 else None,
+                       "band_balance": balance_log,
                        "frame_loop": "vxpt_render_frames (pipelined)" if pipelined else "vxpt_render_frame per step",
                        "tuning": a.tune or "defaults"},
             "mode": mode,

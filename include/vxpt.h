@@ -379,9 +379,24 @@ int vxpt_band_gather_linked(vxpt_ctx **ctxs, int n, int which, int root);
  * halos (vxpt_band_halo_rows). */
 int vxpt_band_comm_id(void *id, size_t bytes);
 int vxpt_band_comm_init(vxpt_ctx *ctx, const void *id, size_t bytes, int nranks, int rank);
+/* the same with an uneven partition: band r = rows [row_splits[r], row_splits[r + 1]) of nranks + 1
+ * boundaries (0 first, height last, inner ones 8-aligned, every band >= 72 rows), the same array on
+ * every rank; NULL = the equal bands.  vxpt_band_balance proposes one from measured band times. */
+int vxpt_band_comm_init_rows(vxpt_ctx *ctx, const void *id, size_t bytes, int nranks, int rank,
+                             const int32_t *row_splits);
 /* The same schedule over n contexts of one process (tests, one-GPU boxes): context k owns band
  * k of n; halo rows move by device copies between the contexts. */
 int vxpt_band_link(vxpt_ctx **ctxs, int n);
+int vxpt_band_link_rows(vxpt_ctx **ctxs, int n, const int32_t *row_splits);
+/* cost-balanced boundaries (pure host function): band_ms[r] = the measured time of band r of the
+ * partition row_splits; block_cost = the frame's cost per 8-row block (ceil(height / 8) floats, kept
+ * by the caller between calls; first entry < 0 = no estimate yet) is refined with them -- each band's
+ * blocks scaled to sum to its time -- and out_splits (nranks + 1) cut the cumulative cost into equal
+ * parts on block boundaries, every band >= 72 rows.  Screen rows cost unevenly (a band that sees
+ * the horizon walks far more cells than one that sees the ground under the camera), so equal bands
+ * leave the slowest rank well above the mean. */
+int vxpt_band_balance(int height, int nranks, const int32_t *row_splits, const float *band_ms, float *block_cost,
+                      int32_t *out_splits);
 int vxpt_render_frame_linked(vxpt_ctx **ctxs, int n, const vxpt_denoise_params *p, int32_t frame_num,
                              int32_t spp);
 

@@ -356,6 +356,7 @@ struct vxpt_ctx {
     // transport its halo rows move by -- an RCCL communicator (one process per
     // GPU) or the other contexts of this process (vxpt_band_link)
     int nranks = 1, rank = 0;
+    std::vector<int> splits;  // nranks + 1 band boundaries (row_splits, or the equal bands)
     ncclComm_t comm = nullptr;
     std::vector<vxpt_ctx *> linked;
     // the trace-halo exchange runs on its own stream, overlapped with the next
@@ -1123,26 +1124,43 @@ void band_rows(int H, int world, int rank, int &y0, int &y1) {
     y1 = std::min(H, y0 + per);
 }
 
+// the equal bands' boundaries: band r = rows [s[r], s[r + 1])
+std::vector<int> equal_splits(int H, int world) {
+    std::vector<int> s(world + 1, 0);
+    for (int r = 0; r < world; ++r) band_rows(H, world, r, s[r], s[r + 1]);
+    return s;
+}
+
+// an uneven partition (vxpt_band_comm_init_rows): 0 = s[0] < s[1] < ... < s[n] = H, inner
+// boundaries 8-aligned (vxpt_set_band), every band at least the ReSTIR halo tall when n > 1
+bool splits_valid(const int32_t *s, int n, int H, int minRows) {
+    if (!s || n < 1 || s[0] != 0 || s[n] != H) return false;
+    for (int k = 0; k < n; ++k)
+        if (s[k + 1] - s[k] < (n > 1 ? minRows : 1) || (k > 0 && (s[k] & 7))) return false;
+    return true;
+}
+
 struct Halo { int peer, sy, sn, ry, rn; };
-// rows rank sends to / receives from each band neighbour (both sides of a border move
-// min(rows, the two band heights) rows)
-std::vector<Halo> halo_plan(int H, int world, int rank, int rows) {
+// rows rank sends to / receives from each band neighbour of the partition s (both sides of a
+// border move min(rows, the two band heights) rows)
+std::vector<Halo> halo_plan(const std::vector<int> &s, int rank, int rows) {
     std::vector<Halo> plan;
-    int y0, y1;
-    band_rows(H, world, rank, y0, y1);
+    const int world = (int)s.size() - 1;
+    const int y0 = s[rank], y1 = s[rank + 1];
     if (rank > 0) {
-        int p0, p1;
-        band_rows(H, world, rank - 1, p0, p1);
-        const int n = std::min(rows, std::min(y1 - y0, p1 - p0));
+        const int n = std::min(rows, std::min(y1 - y0, s[rank] - s[rank - 1]));
         plan.push_back({rank - 1, y0, n, y0 - n, n});
     }
     if (rank < world - 1) {
-        int p0, p1;
-        band_rows(H, world, rank + 1, p0, p1);
-        const int n = std::min(rows, std::min(y1 - y0, p1 - p0));
+        const int n = std::min(rows, std::min(y1 - y0, s[rank + 2] - s[rank + 1]));
         plan.push_back({rank + 1, y1 - n, n, y1, n});
     }
     return plan;
+}
+
+// the context's partition: its row_splits, or the equal bands
+std::vector<int> splits_of(const vxpt_ctx *c) {
+    return (int)c->splits.size() == c->nranks + 1 ? c->splits : equal_splits(c->H, c->nranks);
 }
 
 // Halo depths of a banded frame whose camera moved between passes (cur vs prev).  A band's
@@ -1160,8 +1178,9 @@ std::vector<Halo> halo_plan(int H, int world, int rank, int rows) {
 // (nearDepth <= 0) a translated camera is refused; so is a point behind the previous camera or a
 // halo deeper than a neighbouring band (the plan only reaches ranks r +/- 1).  An unmoved camera
 // keeps the static depths (72 / 2).
-bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, int world, int &traceRows, int &histRows,
-                    std::string &err, float nearDepth = 0.0f) {
+bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, const std::vector<int> &splits,
+                    int &traceRows, int &histRows, std::string &err, float nearDepth = 0.0f) {
+    const int world = (int)splits.size() - 1;
     traceRows = kTraceHalo;
     histRows = 2;
     if (world <= 1) return true;
@@ -1178,8 +1197,7 @@ bool band_halo_rows(const CamDev &cam, const CamDev &pc, int W, int H, int world
     int minBand = H;
     float reach = 0.0f;  // rows beyond its band any band pixel reprojects to
     for (int r = 0; r < world; ++r) {
-        int y0, y1;
-        band_rows(H, world, r, y0, y1);
+        const int y0 = splits[r], y1 = splits[r + 1];
         if (y1 <= y0) continue;
         minBand = std::min(minBand, y1 - y0);
         float lo = 1e30f, hi = -1e30f;
@@ -1312,7 +1330,7 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
         if (ncclGroupStart() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupStart");
         ncclResult_t rc = ncclSuccess;
         for (const auto &br : bufRows)
-            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, br.second)) {
+            for (const Halo &h : halo_plan(splits_of(c), c->rank, br.second)) {
                 const int b = br.first;
                 size_t rb;
                 char *send = buffer_rows(c, b, h.sy, rb);
@@ -1336,7 +1354,7 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
     for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
     for (vxpt_ctx *c : cs)
         for (const auto &br : bufRows)
-            for (const Halo &h : halo_plan(c->H, c->nranks, c->rank, br.second)) {
+            for (const Halo &h : halo_plan(splits_of(c), c->rank, br.second)) {
                 const int b = br.first;
                 size_t rb;
                 char *dst = buffer_rows(c, b, h.ry, rb);
@@ -1385,10 +1403,10 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
             if (reused) nearDepth = reuse;
             else search();
         }
-        bool ok = band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err, nearDepth);
+        bool ok = band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, splits_of(c0), traceRows, histRows, err, nearDepth);
         if (!ok && reused) {  // the reused bound is looser than a fresh search: search before refusing
             search();
-            ok = band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, c0->nranks, traceRows, histRows, err, nearDepth);
+            ok = band_halo_rows(c0->cam, c0->prevCam, c0->W, c0->H, splits_of(c0), traceRows, histRows, err, nearDepth);
         }
         if (!ok) return fail(c0, VXPT_ERR_STATE, err.c_str());
     }
@@ -2942,10 +2960,19 @@ int vxpt_band_comm_id(void *id, size_t bytes) {
 }
 
 int vxpt_band_comm_init(vxpt_ctx *c, const void *id, size_t bytes, int nranks, int rank) {
+    return vxpt_band_comm_init_rows(c, id, bytes, nranks, rank, nullptr);
+}
+
+int vxpt_band_comm_init_rows(vxpt_ctx *c, const void *id, size_t bytes, int nranks, int rank, const int32_t *row_splits) {
     if (!c || !id || bytes < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
-    int y0, y1;
-    band_rows(c->H, nranks, rank, y0, y1);
+    std::vector<int> s = equal_splits(c->H, nranks);
+    if (row_splits) {
+        if (!splits_valid(row_splits, nranks, c->H, kTraceHalo))
+            return fail(c, VXPT_ERR_ARG, "row_splits: 0 = s[0] < ... < s[n] = height, 8-aligned, bands >= 72 rows");
+        s.assign(row_splits, row_splits + nranks + 1);
+    }
+    const int y0 = s[rank], y1 = s[rank + 1];
     if (nranks > 1 && (y1 - y0 < kTraceHalo))
         return fail(c, VXPT_ERR_ARG, "bands must be at least 72 rows tall (ReSTIR halo)");
     ncclUniqueId u;
@@ -2958,19 +2985,28 @@ int vxpt_band_comm_init(vxpt_ctx *c, const void *id, size_t bytes, int nranks, i
     if (!c->haloDone) HIPCHK(c, hipEventCreateWithFlags(&c->haloDone, hipEventDisableTiming));
     c->nranks = nranks;
     c->rank = rank;
+    c->splits = s;
     return vxpt_set_band(c, y0, y1);
 }
 
-int vxpt_band_link(vxpt_ctx **cs, int n) {
-    if (!cs || n < 1) return VXPT_ERR_ARG;
+int vxpt_band_link(vxpt_ctx **cs, int n) { return vxpt_band_link_rows(cs, n, nullptr); }
+
+int vxpt_band_link_rows(vxpt_ctx **cs, int n, const int32_t *row_splits) {
+    if (!cs || n < 1 || !cs[0]) return VXPT_ERR_ARG;
+    std::vector<int> s = equal_splits(cs[0]->H, n);
+    if (row_splits) {
+        if (!splits_valid(row_splits, n, cs[0]->H, kTraceHalo))
+            return fail(cs[0], VXPT_ERR_ARG, "row_splits: 0 = s[0] < ... < s[n] = height, 8-aligned, bands >= 72 rows");
+        s.assign(row_splits, row_splits + n + 1);
+    }
     for (int k = 0; k < n; ++k) {
         vxpt_ctx *c = cs[k];
         if (!c || c->W != cs[0]->W || c->H != cs[0]->H) return VXPT_ERR_ARG;
-        int y0, y1;
-        band_rows(c->H, n, k, y0, y1);
+        const int y0 = s[k], y1 = s[k + 1];
         if (n > 1 && (y1 - y0 < kTraceHalo)) return fail(c, VXPT_ERR_ARG, "bands must be at least 72 rows tall");
         c->nranks = n;
         c->rank = k;
+        c->splits = s;
         c->linked.assign(cs, cs + n);
         if (int r = vxpt_set_band(c, y0, y1)) return r;
     }
@@ -2995,9 +3031,9 @@ int band_gather(std::vector<vxpt_ctx *> &cs, int which, int root) {
         if (ncclGroupStart() != ncclSuccess) return fail(c0, VXPT_ERR_HIP, "ncclGroupStart");
         ncclResult_t rc = ncclSuccess;
         if (c0->rank == root) {
+            const std::vector<int> sp = splits_of(c0);
             for (int r = 0; r < world && rc == ncclSuccess; ++r) {
-                int y0, y1;
-                band_rows(c0->H, world, r, y0, y1);
+                const int y0 = sp[r], y1 = sp[r + 1];
                 if (r == root || y1 <= y0) continue;
                 char *dst = buffer_rows(c0, which, y0, rb);
                 rc = ncclRecv(dst, (size_t)(y1 - y0) * rb, ncclUint8, r, c0->comm, c0->stream);
@@ -3064,9 +3100,49 @@ int vxpt_band_rows(int height, int nranks, int rank, int *row_begin, int *row_en
     return VXPT_OK;
 }
 
+// Cost-balanced band boundaries from measured band times.  block_cost holds the frame's cost per
+// 8-row block (ceil(height / 8) entries, carried between calls; a negative first entry = no estimate
+// yet): each band's blocks are scaled so they sum to its measured time (a band without an estimate
+// spreads its time evenly), then the boundaries go where the cumulative cost crosses k / n of the
+// total, on block boundaries, every band keeping >= 72 rows.
+int vxpt_band_balance(int height, int nranks, const int32_t *row_splits, const float *band_ms, float *block_cost,
+                      int32_t *out_splits) {
+    if (height < 1 || nranks < 1 || !row_splits || !band_ms || !block_cost || !out_splits) return VXPT_ERR_ARG;
+    if (!splits_valid(row_splits, nranks, height, nranks > 1 ? kTraceHalo : 1)) return VXPT_ERR_ARG;
+    const int nb = (height + 7) / 8;
+    if (nranks > 1 && (int64_t)nranks * kTraceHalo > height) return VXPT_ERR_ARG;
+    if (block_cost[0] < 0.0f)
+        for (int b = 0; b < nb; ++b) block_cost[b] = 0.0f;
+    for (int k = 0; k < nranks; ++k) {
+        if (!(band_ms[k] >= 0.0f)) return VXPT_ERR_ARG;
+        const int b0 = row_splits[k] / 8, b1 = (row_splits[k + 1] + 7) / 8;
+        double cur = 0.0;
+        for (int b = b0; b < b1; ++b) cur += block_cost[b];
+        for (int b = b0; b < b1; ++b)
+            block_cost[b] = cur > 0.0 ? (float)(block_cost[b] * (band_ms[k] / cur)) : band_ms[k] / (float)(b1 - b0);
+    }
+    std::vector<double> cum(nb + 1, 0.0);
+    for (int b = 0; b < nb; ++b) cum[b + 1] = cum[b] + block_cost[b];
+    const int minBlocks = nranks > 1 ? kTraceHalo / 8 : 1;
+    out_splits[0] = 0;
+    int prev = 0;
+    for (int k = 1; k < nranks; ++k) {
+        const double target = cum[nb] * k / nranks;
+        const int lo = prev + minBlocks;
+        const int hi = (height - (nranks - k) * kTraceHalo) / 8;  // the bands after it keep 72 rows
+        int best = lo;
+        for (int b = lo; b <= hi; ++b)
+            if (std::fabs(cum[b] - target) < std::fabs(cum[best] - target)) best = b;
+        out_splits[k] = best * 8;
+        prev = best;
+    }
+    out_splits[nranks] = height;
+    return VXPT_OK;
+}
+
 int vxpt_halo_plan(int height, int nranks, int rank, int rows, int32_t *out, int *n_entries) {
     if (height < 1 || nranks < 1 || rank < 0 || rank >= nranks || rows < 0 || !out || !n_entries) return VXPT_ERR_ARG;
-    const std::vector<Halo> plan = halo_plan(height, nranks, rank, rows);
+    const std::vector<Halo> plan = halo_plan(equal_splits(height, nranks), rank, rows);
     for (size_t k = 0; k < plan.size(); ++k) {
         const Halo &h = plan[k];
         const int32_t e[5] = {h.peer, h.sy, h.sn, h.ry, h.rn};
@@ -3082,7 +3158,8 @@ int vxpt_band_halo_rows(const vxpt_camera *cur, const vxpt_camera *prev, int wid
     const CamDev c = make_camera(width, height, *cur, nullptr, nullptr);
     const CamDev pc = make_camera(width, height, prev ? *prev : *cur, nullptr, nullptr);
     std::string err;
-    return band_halo_rows(c, pc, width, height, nranks, *trace_rows, *history_rows, err) ? VXPT_OK : VXPT_ERR_STATE;
+    return band_halo_rows(c, pc, width, height, equal_splits(height, nranks), *trace_rows, *history_rows, err)
+               ? VXPT_OK : VXPT_ERR_STATE;
 }
 
 int vxpt_band_halo_rows_near(const vxpt_camera *cur, const vxpt_camera *prev, int width, int height, int nranks,
@@ -3091,8 +3168,8 @@ int vxpt_band_halo_rows_near(const vxpt_camera *cur, const vxpt_camera *prev, in
     const CamDev c = make_camera(width, height, *cur, nullptr, nullptr);
     const CamDev pc = make_camera(width, height, prev ? *prev : *cur, nullptr, nullptr);
     std::string err;
-    return band_halo_rows(c, pc, width, height, nranks, *trace_rows, *history_rows, err, near_depth) ? VXPT_OK
-                                                                                                     : VXPT_ERR_STATE;
+    return band_halo_rows(c, pc, width, height, equal_splits(height, nranks), *trace_rows, *history_rows, err,
+                          near_depth) ? VXPT_OK : VXPT_ERR_STATE;
 }
 
 int vxpt_nearest_surface(vxpt_ctx *c, const float pos[3], float *dist) {

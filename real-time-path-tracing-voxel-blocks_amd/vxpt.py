@@ -183,6 +183,9 @@ def load_library(path=LIB_PATH):
         "vxpt_band_comm_id": (I, [P, ctypes.c_size_t]),
         "vxpt_band_comm_init": (I, [P, P, ctypes.c_size_t, I, I]),
         "vxpt_band_link": (I, [ctypes.POINTER(P), I]),
+        "vxpt_band_comm_init_rows": (I, [P, P, ctypes.c_size_t, I, I, P]),
+        "vxpt_band_link_rows": (I, [ctypes.POINTER(P), I, P]),
+        "vxpt_band_balance": (I, [I, I, P, P, P, P]),
         "vxpt_render_frame_linked": (I, [ctypes.POINTER(P), I, ctypes.POINTER(DenoiseParams), ctypes.c_int32,
                                          ctypes.c_int32]),
         "vxpt_band_rows": (I, [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
@@ -489,11 +492,17 @@ class Renderer:
             mask |= 1 << (BUF[n] if isinstance(n, str) else int(n))
         self._chk(self.lib.vxpt_exchange_halo(self.ctx, mask, rows), "vxpt_exchange_halo")
 
-    def band_comm_init(self, comm_id, nranks, rank):
+    def band_comm_init(self, comm_id, nranks, rank, splits=None):
         """Attach an RCCL communicator (vxpt_band_comm_init): this context renders band `rank`
-        of `nranks` and vxpt_render_frame exchanges the halos itself."""
+        of `nranks` and vxpt_render_frame exchanges the halos itself.  splits: the nranks + 1 row
+        boundaries of an uneven partition (vxpt_band_comm_init_rows), the same on every rank."""
         buf = ctypes.create_string_buffer(bytes(comm_id), len(comm_id))
-        self._chk(self.lib.vxpt_band_comm_init(self.ctx, buf, len(comm_id), nranks, rank), "vxpt_band_comm_init")
+        if splits is None:
+            self._chk(self.lib.vxpt_band_comm_init(self.ctx, buf, len(comm_id), nranks, rank), "vxpt_band_comm_init")
+        else:
+            s = _splits_array(splits, nranks)
+            self._chk(self.lib.vxpt_band_comm_init_rows(self.ctx, buf, len(comm_id), nranks, rank, s.ctypes.data),
+                      "vxpt_band_comm_init_rows")
 
     def denoise(self, frame_num, iteration_index, params=None):
         p = params or DenoiseParams.defaults()
@@ -648,6 +657,36 @@ def bvh_depth(boxes, leaf_max):
     return None if r != 0 else (d.value, n.value)
 
 
+def _splits_array(splits, nranks):
+    s = np.ascontiguousarray(splits, np.int32)
+    if s.shape != (nranks + 1,):
+        raise VxptError("row splits: %d boundaries expected, got %s" % (nranks + 1, s.shape))
+    return s
+
+
+def equal_splits(height, nranks):
+    """The equal bands' nranks + 1 row boundaries (vxpt_band_rows of every rank)."""
+    return [0] + [band_rows(height, nranks, r)[1] for r in range(nranks)]
+
+
+def band_balance(height, splits, band_ms, block_cost=None):
+    """vxpt_band_balance: (new row boundaries, refined per-8-row-block cost) from the measured time
+    of each band of the partition `splits` (pure host function, no GPU).  Pass the returned cost
+    back in to refine the estimate over several measurements."""
+    n = len(splits) - 1
+    s = _splits_array(splits, n)
+    ms = np.ascontiguousarray(band_ms, np.float32)
+    if ms.shape != (n,):
+        raise VxptError("band_ms: %d times expected" % n)
+    cost = np.full((height + 7) // 8, -1.0, np.float32) if block_cost is None else \
+        np.array(block_cost, np.float32).copy()
+    out = np.zeros(n + 1, np.int32)
+    if load_library().vxpt_band_balance(height, n, s.ctypes.data, ms.ctypes.data, cost.ctypes.data,
+                                        out.ctypes.data) != 0:
+        raise VxptError("vxpt_band_balance: bad arguments")
+    return [int(v) for v in out], cost
+
+
 def band_rows(height, nranks, rank):
     """vxpt_band_rows: (row_begin, row_end) of `rank` (pure host function, no GPU)."""
     y0, y1 = ctypes.c_int(0), ctypes.c_int(0)
@@ -690,11 +729,16 @@ class LinkedBands:
     """n contexts of this process rendering the bands of one frame (vxpt_band_link):
     the library's multi-GPU schedule with device copies as the transport."""
 
-    def __init__(self, renderers):
+    def __init__(self, renderers, splits=None):
         self.rs = list(renderers)
         self.lib = load_library()
         self._arr = (ctypes.c_void_p * len(self.rs))(*[r.ctx for r in self.rs])
-        if self.lib.vxpt_band_link(self._arr, len(self.rs)) != 0:
+        if splits is not None:
+            s = _splits_array(splits, len(self.rs))
+            rc = self.lib.vxpt_band_link_rows(self._arr, len(self.rs), s.ctypes.data)
+        else:
+            rc = self.lib.vxpt_band_link(self._arr, len(self.rs))
+        if rc != 0:
             raise VxptError("vxpt_band_link: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
 
     def render_frame(self, frame_num, spp=1, params=None):

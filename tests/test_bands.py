@@ -144,12 +144,16 @@ def test_gpu_bands_match_single_context():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,w,h", [(2, 64, 160), (8, 640, 640)])
-def test_gpu_library_band_schedule_matches_single_context(n, w, h):
+@pytest.mark.parametrize("n,w,h,splits", [(2, 64, 160, None), (8, 640, 640, None),
+                                          (3, 96, 320, [0, 80, 248, 320]),
+                                          (8, 640, 640, [0, 72, 144, 224, 304, 384, 464, 560, 640])])
+def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits):
     """The library's own band schedule (vxpt_band_link / vxpt_render_frame_linked: the one
     vxpt_band_comm_init runs over RCCL, with device copies between the contexts as the
     transport) equals the single-context render bit for bit; 8 bands simulate the 8-GPU
-    partition on one device (bands of 80 rows, wider than the 72-row trace halo)."""
+    partition on one device (bands of 80 rows, wider than the 72-row trace halo).  Uneven
+    partitions (vxpt_band_link_rows, the cost-balanced bands of vxpt_band_balance) too, with
+    bands as short as the halo itself."""
     import vxpt
     spp = 4
     cam = C1_CAMERA
@@ -165,8 +169,8 @@ def test_gpu_library_band_schedule_matches_single_context(n, w, h):
     p = vxpt.DenoiseParams.defaults()
     single = make()
     rs = [make() for _ in range(n)]
-    linked = vxpt.LinkedBands(rs)
-    rows = [bands.band_rows(h, n, k) for k in range(n)]
+    linked = vxpt.LinkedBands(rs, splits)
+    rows = [bands.band_rows(h, n, k) for k in range(n)] if splits is None else list(zip(splits[:-1], splits[1:]))
     for f in range(3):
         single.render_frame(f, spp, p)
         linked.render_frame(f, spp, p)
@@ -222,6 +226,110 @@ def test_library_band_functions_match_bands_py():
                 assert vxpt.band_rows(H, n, r) == rows[r]
                 for depth in (0, 2, 34, 72, 91):
                     assert vxpt.halo_plan(H, n, r, depth) == bands.halo_plan(rows, r, depth), (H, n, r, depth)
+
+
+def _check_splits(s, h, n):
+    assert len(s) == n + 1 and s[0] == 0 and s[-1] == h
+    assert all(b - a >= 72 for a, b in zip(s[:-1], s[1:])), s
+    assert all(v % 8 == 0 for v in s[1:-1]), s
+
+
+def test_band_balance_equalises_a_cost_profile():
+    """vxpt_band_balance: from the band times of a partition, boundaries whose bands cost alike.
+    A synthetic per-row cost (expensive horizon rows above cheap ground rows, as in the C3 view)
+    measured over the equal bands, then over each proposed partition: three rounds bring the
+    slowest band within 6% of the mean (equal bands: 25-60% above it)."""
+    import vxpt
+    for h, n in ((1080, 2), (1080, 4), (1080, 8), (2160, 8)):
+        y = np.arange(h) + 0.5
+        row_cost = 0.4 + np.exp(-((y / h - 0.3) / 0.3) ** 2)
+        measure = lambda s: [float(row_cost[a:b].sum()) for a, b in zip(s[:-1], s[1:])]  # noqa: E731
+        s = vxpt.equal_splits(h, n)
+        t = measure(s)
+        first = max(t) / np.mean(t)
+        cost = None
+        for _ in range(3):
+            s, cost = vxpt.band_balance(h, s, t, cost)
+            _check_splits(s, h, n)
+            t = measure(s)
+        assert first > 1.2 and max(t) / np.mean(t) < 1.06, (h, n, first, max(t) / np.mean(t), s)
+
+
+def test_band_balance_keeps_uniform_costs_and_rejects_bad_partitions():
+    import vxpt
+    s, cost = vxpt.band_balance(1080, vxpt.equal_splits(1080, 4), [1.0] * 4)
+    _check_splits(s, 1080, 4)
+    assert max(abs(a - b) for a, b in zip(s, [0, 272, 544, 816, 1080])) <= 8
+    assert cost.shape == (135,) and np.allclose(cost.sum(), 4.0, rtol=1e-5)
+    # a band that costs nothing still keeps the halo's 72 rows
+    s, _ = vxpt.band_balance(640, vxpt.equal_splits(640, 8), [0.0] * 7 + [10.0])
+    _check_splits(s, 640, 8)
+    for bad in ([0, 100, 200], [0, 64, 200], [8, 100, 200], [0, 100, 208]):
+        with pytest.raises(vxpt.VxptError):
+            vxpt.band_balance(200, bad, [1.0, 1.0])
+    with pytest.raises(vxpt.VxptError):
+        vxpt.band_balance(200, [0, 96, 200], [1.0, -1.0])
+
+
+class _TimedBand:
+    """A stand-in renderer for bench.balance_bands: a frame of band [y0, y1) takes the synthetic
+    cost of its rows in wall time (5 ms for a whole 1080-row frame, rows near the top 3x the rest)."""
+    def __init__(self):
+        self.y0, self.y1 = 0, 1080
+
+    def set_band(self, y0, y1):
+        self.y0, self.y1 = y0, y1
+
+    def render_frames(self, f0, n, spp, params):
+        import time
+        y = np.arange(self.y0, self.y1)
+        time.sleep(n * float(np.where(y < 360, 3.0, 1.0).sum()) * 5e-3 / 1800.0)
+
+    def sync(self):
+        pass
+
+    def close(self):
+        pass
+
+
+def _balance_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        class A:
+            height, spp, primary_only = 1080, 4, False
+        splits, log = bench.balance_bands(A, _TimedBand, None, world, rank, dist)
+        q.put((rank, splits, log))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_band_balance_gloo_two_ranks():
+    """bench.balance_bands over two gloo ranks (the N>1 bench's pre-run step): both ranks time their
+    band, share the times and arrive at the same boundaries, which move the split towards the
+    expensive top rows (cost 3 per row above row 360, 1 below: equal cost at row 300)."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_balance_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (sp, log) for r, sp, log in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    splits, log = res[0]
+    assert log[0]["band_rows"] == [0, 544, 1080] and len(log) == 3
+    assert splits[0] == 0 and splits[2] == 1080 and 280 <= splits[1] <= 336, splits  # 544 -> ~384 -> ~312
 
 
 def _turn(d, yaw_deg, pitch_deg):

@@ -1,7 +1,8 @@
 """One-GPU proxy of the multi-GPU band partition: every rank's band of the C3 frame
 (1920x1080 by default, or 3840x2160 for C4) rendered alone by a single context in band mode
 (vxpt_config row_begin / row_end: the trace and denoiser over the band's rows only, no exchange),
-for N = 1 / 2 / 4 / 8 bands, plus the halo bytes the library's band schedule moves per rank and frame
+for N = 1 / 2 / 4 / 8 bands -- the equal bands, then the cost-balanced ones bench.py runs (two rounds
+of vxpt_band_balance on these same band times) -- plus the halo bytes the library's band schedule moves per rank and frame
 (band_frame in vxpt_host.cpp) and their time on one xGMI link.
 
 python tools/band_proxy.py [WIDTH HEIGHT] [--out profiles/r04_band_proxy.json]
@@ -50,11 +51,13 @@ def band_rows(h, n, k):
     return y0, min(h, y0 + per)
 
 
-def time_band(w, h, rows, frames, warmup, spp):
+def time_band(w, h, rows, frames, warmup, spp, tune):
     pos = tuple(p * 4 for p in (35.6184, 11.8733, 42.0387))
     r = vxpt.Renderer(w, h, rows=rows)
     try:
         r.load_settings()
+        if tune:
+            r.set_tuning(**tune)
         r.generate_terrain((8, 8, 8), height_scale=128.0, freq_den=256.0, global_y=True)
         r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
         r.set_sky()
@@ -78,21 +81,40 @@ def main():
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE")
     a = ap.parse_args()
+    tune = {k: int(v) for k, v in (t.split("=", 1) for t in a.tune)}
     w, h = a.size
     res = {"what": "one-GPU proxy of the band partition: each rank's band of the C3 frame rendered alone "
                    "(single context in band mode, no exchange), and the halo bytes per rank and frame of the "
                    "library's schedule on one xGMI link (%.0f GB/s per direction)" % XGMI_GBS,
-           "width": w, "height": h, "spp": a.spp, "ranks": {}}
+           "width": w, "height": h, "spp": a.spp, "tuning": tune or "defaults (bands: state_sets 3, as bench.py)",
+           "ranks": {}}
     one = None
-    for n in (1, 2, 4, 8):
-        bands = [band_rows(h, n, k) for k in range(n)]
+
+    def measure(n, bands):
         per = []
         for k, rows in enumerate(bands):
-            t = time_band(w, h, rows, a.frames, a.warmup, a.spp)
+            tn = dict(tune)
+            if n > 1:
+                tn.setdefault("state_sets", 3)  # bench.py's banded runs
+            t = time_band(w, h, rows, a.frames, a.warmup, a.spp, tn)
             t.update(rank=k, rows=list(rows))
             per.append(t)
             print(n, k, rows, t, flush=True)
+        return per
+
+    for n in (1, 2, 4, 8):
+        bands = [band_rows(h, n, k) for k in range(n)]
+        per = measure(n, bands)
+        balanced = None
+        if n > 1:
+            splits, cost, eq = [b[0] for b in bands] + [h], None, per
+            for _ in range(2):
+                splits, cost = vxpt.band_balance(h, splits, [t["frame_ms"] for t in per], cost)
+                per = measure(n, list(zip(splits[:-1], splits[1:])))
+            balanced = {"band_rows": splits, "slowest_band_ms": max(t["frame_ms"] for t in per)}
+            per, balanced_per = eq, per
         slow = max(per, key=lambda t: t["frame_ms"])
         min_rows = min(y1 - y0 for y0, y1 in bands)
         ov, od = halo_bytes(w, a.spp, min_rows) if n > 1 else (0, 0)
@@ -102,7 +124,12 @@ def main():
         proj = slow["frame_ms"] + link_ms_ordered
         if n == 1:
             one = slow["frame_ms"]
+        if balanced:
+            balanced["bands"] = balanced_per
+            balanced["projected_frame_ms"] = round(balanced["slowest_band_ms"] + link_ms_ordered, 4)
+            balanced["projected_speedup"] = round(one / balanced["projected_frame_ms"], 3)
         res["ranks"][str(n)] = {
+            "balanced": balanced,
             "bands": per, "slowest_band_ms": slow["frame_ms"], "mean_band_ms": round(sum(t["frame_ms"] for t in per) / n, 4),
             "halo_mb_per_neighbour_per_frame": {"overlapped": round(ov / 1e6, 3), "in_stream_order": round(od / 1e6, 3)},
             "link_ms": {"overlapped": round(link_ms_overlapped, 4), "in_stream_order": round(link_ms_ordered, 4)},
