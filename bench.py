@@ -141,7 +141,20 @@ def cpu_baseline(a, target_s):
     return res
 
 
-def balance_bands(a, make, params, world, rank, dist, rounds=2, frames=6):
+def band_tuning(width, height, world):
+    """Schedule defaults of a rank's band (N>1).  A band is latency bound: a third wavefront state
+    set lets its passes' first halves run further ahead, and below ~0.7 Mpx a third front stream
+    adds overlap (1080p, 8 balanced bands: slowest band 1.52 -> 1.43 ms per frame), while bigger bands
+    lose by it (1080p, 2 bands of 1 Mpx: 3.16 -> 3.22 ms; profiles/r04_band_proxy*.json)."""
+    if world <= 1:
+        return {}
+    t = {"state_sets": 3}
+    if width * height / world < 700e3:
+        t["front_streams"] = 3
+    return t
+
+
+def balance_bands(a, make, params, world, rank, dist, rounds=3, frames=6):
     """Cost-balanced band boundaries (vxpt_band_balance): each round, every rank renders its band
     of the current partition alone in a throwaway context (band mode, no exchange: its compute
     only), the ranks all-gather the per-frame times, and every rank computes the same next
@@ -203,10 +216,8 @@ def main():
     if a.scene is None:
         a.scene = "c1" if a.primary_only else "c3"
     a.tune = {k: int(v) for k, v in (t.split("=", 1) for t in a.tune)}
-    if int(os.environ.get("WORLD_SIZE", 1)) > 1:
-        # a rank's band is latency bound: a third wavefront state set lets its passes' first halves
-        # run further ahead (one 136-row band: 1.63 -> 1.56 ms per frame, profiles/r04_band_proxy.json)
-        a.tune.setdefault("state_sets", 3)
+    for k, v in band_tuning(a.width, a.height, int(os.environ.get("WORLD_SIZE", 1))).items():
+        a.tune.setdefault(k, v)
     assert len(a.bounce_limits) == 2 and a.bounce_limits[0] >= a.bounce_limits[1] >= 1, a.bounces
 
     rank = int(os.environ.get("RANK", 0))

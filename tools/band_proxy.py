@@ -1,7 +1,7 @@
 """One-GPU proxy of the multi-GPU band partition: every rank's band of the C3 frame
 (1920x1080 by default, or 3840x2160 for C4) rendered alone by a single context in band mode
 (vxpt_config row_begin / row_end: the trace and denoiser over the band's rows only, no exchange),
-for N = 1 / 2 / 4 / 8 bands -- the equal bands, then the cost-balanced ones bench.py runs (two rounds
+for N = 1 / 2 / 4 / 8 bands -- the equal bands, then the cost-balanced ones bench.py runs (three rounds
 of vxpt_band_balance on these same band times) -- plus the halo bytes the library's band schedule moves per rank and frame
 (band_frame in vxpt_host.cpp) and their time on one xGMI link.
 
@@ -17,7 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "real-time-path-tracing-voxel-blocks_amd"))
 import vxpt  # noqa: E402
-from bench import C1_DIR  # noqa: E402
+from bench import C1_DIR, band_tuning  # noqa: E402
 
 XGMI_GBS = 153.0   # one xGMI link, one direction (MI355X_MICROARCH.md: 7 links x ~153 GB/s per GPU)
 TRACE_ROWS, HIST_ROWS, PLANE_ROWS = 72, 2, 40   # static camera (vxpt_host.cpp band_frame)
@@ -88,7 +88,7 @@ def main():
     res = {"what": "one-GPU proxy of the band partition: each rank's band of the C3 frame rendered alone "
                    "(single context in band mode, no exchange), and the halo bytes per rank and frame of the "
                    "library's schedule on one xGMI link (%.0f GB/s per direction)" % XGMI_GBS,
-           "width": w, "height": h, "spp": a.spp, "tuning": tune or "defaults (bands: state_sets 3, as bench.py)",
+           "width": w, "height": h, "spp": a.spp, "tuning": tune or "defaults (bands: bench.band_tuning)",
            "ranks": {}}
     one = None
 
@@ -96,8 +96,8 @@ def main():
         per = []
         for k, rows in enumerate(bands):
             tn = dict(tune)
-            if n > 1:
-                tn.setdefault("state_sets", 3)  # bench.py's banded runs
+            for f, v in band_tuning(w, h, n).items():  # bench.py's banded runs
+                tn.setdefault(f, v)
             t = time_band(w, h, rows, a.frames, a.warmup, a.spp, tn)
             t.update(rank=k, rows=list(rows))
             per.append(t)
@@ -110,7 +110,7 @@ def main():
         balanced = None
         if n > 1:
             splits, cost, eq = [b[0] for b in bands] + [h], None, per
-            for _ in range(2):
+            for _ in range(3):
                 splits, cost = vxpt.band_balance(h, splits, [t["frame_ms"] for t in per], cost)
                 per = measure(n, list(zip(splits[:-1], splits[1:])))
             balanced = {"band_rows": splits, "slowest_band_ms": max(t["frame_ms"] for t in per)}
