@@ -974,7 +974,9 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
 }
 
 // The second half of the planned pass, on the context stream, and the ring bookkeeping.
-int trace_back(vxpt_ctx *c, const PassPlan &pl) {
+// mark: record ev[1] behind the pass (vxpt_trace's timing; the frame loops keep their own events --
+// every marker is one more packet between two kernels of the stream)
+int trace_back(vxpt_ctx *c, const PassPlan &pl, bool mark = true) {
     const int set = pl.set;
     if (!pl.a.primaryOnly) {
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[set], 0));
@@ -982,7 +984,7 @@ int trace_back(vxpt_ctx *c, const PassPlan &pl) {
         HIPCHK(c, hipEventRecord(c->backDone[set], c->stream));
     }
     c->haloPending = false;
-    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    if (mark) HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     c->tracePrev2 = c->tracePrev;
     c->tracePrev = c->last;
     c->last = pl.next;
@@ -994,11 +996,11 @@ int trace_back(vxpt_ctx *c, const PassPlan &pl) {
 }
 
 int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
-             bool overlap = false) {
-    HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+             bool overlap = false, bool mark = true) {
+    if (mark) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     PassPlan pl;
     if (int r = trace_front(c, it, flags, accumulate, accumFirst, accumScale, overlap, pl)) return r;
-    return trace_back(c, pl);
+    return trace_back(c, pl, mark);
 }
 
 // history hand-over NormalRough/Depth/Material -> Prev (Denoiser.cu:394-407):
@@ -1432,7 +1434,7 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     }
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
-        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0));
+        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false));
         const int res = ((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN;
         if (s + 1 < spp) {
             // all but the last pass: the next pass's temporal taps' inputs, overlapped with that pass
@@ -2658,11 +2660,8 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
     }
     const int it0 = frameNum * spp;
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
-    for (int s = 0; s < spp; ++s) {
-        int r = do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0);
-        if (r) return r;
-        if (s == 0) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-    }
+    for (int s = 0; s < spp; ++s)
+        if (int r = do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false)) return r;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     c->denoiseInputIsAccum = spp > 1;
     int r = do_denoise(c, p, frameNum, it0 + spp);
@@ -2703,7 +2702,6 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
     bool havePend = false;
     for (int f = 0; f < nFrames; ++f) {
         const int it0 = (frame0 + f) * spp;
-        HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
         for (int s = 0; s < spp; ++s) {
             PassPlan pl;
             if (s == 0 && havePend) {
@@ -2712,9 +2710,8 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             } else if (int r = trace_front(c, it0 + s, 0, spp > 1, s == 0, scale, s > 0, pl)) {
                 return r;
             }
-            if (int r = trace_back(c, pl)) return r;
+            if (int r = trace_back(c, pl, false)) return r;
         }
-        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
         if (f + 1 < nFrames) {
             // The next frame's first pass-half runs beside this frame's last second half.  It writes
             // a G-buffer slot that is neither this frame's (the denoiser's input) nor the history
