@@ -418,6 +418,11 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const 
             return DdaRun;
         }
     } else if constexpr (BOX) {
+#if defined(VX_PREFETCH_BRICKS) && defined(VX_PREFETCH_EMPTY)
+        // a one-brick empty box is left into the same neighbour an occupied brick would be
+        if constexpr (std::is_same_v<F, GlobalBricks>)
+            if ((s.box & 0xFFFFFFu) == 0x010101u) prefetch_next<BOX>(w, s);
+#endif
         skip_box(w, s.r, s.c, (int)(s.box & 0xFFu), (int)((s.box >> 8) & 0xFFu), (int)((s.box >> 16) & 0xFFu));
     } else {
         skip_cube(w, s.r, s.c, s.dist);

@@ -126,20 +126,22 @@ def test_library_walk_on_host_equals_oracle_dda(driver, outside, tmp_path):
     assert 0.05 < got[:, 0].mean() < 0.95
 
 
-@pytest.fixture(scope="module")
-def driver_prefetch(tmp_path_factory):
-    exe = str(tmp_path_factory.mktemp("ddapf") / "dda_box_driver_pf")
+@pytest.fixture(scope="module", params=["occupied", "empty"])
+def driver_prefetch(tmp_path_factory, request):
+    exe = str(tmp_path_factory.mktemp("ddapf") / ("dda_box_driver_pf_" + request.param))
+    flags = ["-DVX_PREFETCH_BRICKS"] + (["-DVX_PREFETCH_EMPTY"] if request.param == "empty" else [])
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-                           "-DVX_PREFETCH_BRICKS", "-I", CSRC, "-x", "hip",
+                           *flags, "-I", CSRC, "-x", "hip",
                            os.path.join(REPO, "tests", "native", "dda_box_driver.hip"), "-o", exe])
     return exe
 
 
 @pytest.mark.parametrize("world", ["c3", "random"])
 def test_brick_prefetch_walk_equals_plain_walk(driver, driver_prefetch, world, tmp_path):
-    """VX_PREFETCH_BRICKS (the walk loads the brick it will leave an occupied brick into while it walks
-    that brick's cells): every closest hit and occlusion answer of the cube and box walks, through
-    save / resume, bit for bit the plain walk's, on random rays from inside and outside the world."""
+    """VX_PREFETCH_BRICKS (the walk loads the brick it will leave an occupied brick -- and, with
+    VX_PREFETCH_EMPTY, a one-brick empty box -- into while it processes this one): every closest hit
+    and occlusion answer of the cube and box walks, through save / resume, bit for bit the plain
+    walk's, on random rays from inside and outside the world."""
     if world == "random":
         chunks = (4, 2, 4)
         ids = _random_world(chunks, 5)
