@@ -239,7 +239,6 @@ __global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int wy0, int wy1
     const int y = wy0 + blockIdx.y * 4 + (l32 >> 3);
     const bool inb = x < W && y < wy1;
     const size_t i = (size_t)y * W + x;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.hfTileCount[0] = 0u;  // k_temporal appends
     const float cd = inb ? a.depth[i] : 0.0f;
     const bool sky = inb && cd > kRange;
     const bool inBand = detect && inb && y >= a.y0 && y < a.y1;
@@ -666,15 +665,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_TA))
     unsigned off = 0;
     for (int k = 0; k < wv; ++k) off += sTot[k];
     if (fix) a.hfList[tile * 256 + off + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)((size_t)y * a.W + x);
-    if (threadIdx.x == 0) {
-        const unsigned n = sTot[0] + sTot[1] + sTot[2] + sTot[3];
-        a.hfCount[tile] = n;
-        if (a.hfCompact && n) {
-            const unsigned tiles = ((a.W + 15) / 16) * ((a.y1 - a.y0 + 15) / 16);
-            const unsigned k = atomicAdd(a.hfTileCount, 1u);
-            if (k < tiles) a.hfTiles[k] = tile;
-        }
-    }
+    if (threadIdx.x == 0) a.hfCount[tile] = sTot[0] + sTot[1] + sTot[2] + sTot[3];
 }
 
 // ---------------------------------------------------------------- HF
@@ -790,17 +781,19 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
     if (lane == 0 && store) a.pong[i] = tf(sum / wsum);
 }
 
-// One tile's list from k_temporal: a sparse list (<= 64 pixels, the steady state) is walked one
-// pixel per wave at a time, a dense one (history just reset) gets one lane per pixel.  zi / zn split
-// a sparse list over zn workgroups (rounds of 8 pixels dealt round-robin): a round is the listed
-// pixel's chain of dependent loads, so a tile's rounds run side by side.
-VX_D void history_fix_tile(const DenoiseArgs &a, unsigned tile, unsigned zi, unsigned zn) {
+// One workgroup per 16x16 tile, over the tile's list from k_temporal: a
+// sparse list (<= 64 pixels, the steady state) is walked one pixel per wave at
+// a time, a dense one (history just reset) gets one lane per pixel.
+// blockIdx.z splits a sparse list over gridDim.z workgroups (rounds of 8 pixels dealt round-robin): a
+// round is the listed pixel's chain of dependent loads, so a tile's rounds run side by side.
+__global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
+    const unsigned tile = blockIdx.y * ((a.W + 15) / 16) + blockIdx.x;
     const unsigned n = a.hfCount[tile];
     const unsigned wv = threadIdx.x >> 6;
     if (n <= 64) {  // sparse (steady state): each half-wave takes every 8th listed pixel, its taps in parallel
         const unsigned half = wv * 2 + ((threadIdx.x >> 5) & 1);
         // wave-uniform trip count; the halves share the readlanes
-        for (unsigned k0 = zi * 8 + wv * 2; k0 < n; k0 += 8 * zn) {
+        for (unsigned k0 = blockIdx.z * 8 + wv * 2; k0 < n; k0 += 8 * gridDim.z) {
             const unsigned k = k0 + (half & 1);
             const bool has = k < n;
             const size_t i = a.hfList[tile * 256 + (has ? k : k0)];
@@ -808,24 +801,9 @@ VX_D void history_fix_tile(const DenoiseArgs &a, unsigned tile, unsigned zi, uns
         }
         return;
     }
-    if (zi != 0 || threadIdx.x >= n) return;
+    if (blockIdx.z != 0 || threadIdx.x >= n) return;
     const size_t i = a.hfList[tile * 256 + threadIdx.x];
     history_fix_px(a, a.W, a.H, (int)(i % (size_t)a.W), (int)(i / (size_t)a.W), i);
-}
-
-// LIST = false: one workgroup per tile of the band (blockIdx.z of gridDim.z per tile), most of them
-// finding an empty list.  LIST = true (the frame's chain): a fixed grid over the tiles k_temporal
-// appended (~960 of 8160 on the C3 bench): 32x fewer workgroups to dispatch.  The frame's k_firefly
-// (the chain's first launch, always run for the world positions) empties the tile list.
-template <bool LIST>
-__global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
-    if (!LIST) {
-        history_fix_tile(a, blockIdx.y * ((a.W + 15) / 16) + blockIdx.x, blockIdx.z, gridDim.z);
-        return;
-    }
-    const unsigned tiles = ((a.W + 15) / 16) * ((a.y1 - a.y0 + 15) / 16);
-    const unsigned nt = min(a.hfTileCount[0], tiles);
-    for (unsigned t = blockIdx.x; t < nt; t += gridDim.x) history_fix_tile(a, a.hfTiles[t], blockIdx.z, gridDim.z);
 }
 
 // HistoryClamping's per-pixel step after the 5x5 moments (m1, m2: the fast history's YCoCg; nm1,
@@ -1276,13 +1254,7 @@ hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st) {
     // (tools/hf_stats.py); tuning hf_split workgroups per tile
     dim3 g = grid16(a);
     g.z = (unsigned)a.tune.hfSplit;
-    if (a.hfCompact) {
-        const unsigned tiles = g.x * g.y;
-        g = dim3(std::min(tiles, 1024u), 1, g.z);
-        hipLaunchKernelGGL(k_history_fix<true>, g, dim3(256), 0, st, a);
-    } else {
-        hipLaunchKernelGGL(k_history_fix<false>, g, dim3(256), 0, st, a);
-    }
+    hipLaunchKernelGGL(k_history_fix, g, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 // tile edge of the LDS-staged 5x5 stencils (history clamping, the first a-trous): 32 stages the

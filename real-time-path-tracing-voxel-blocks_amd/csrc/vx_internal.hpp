@@ -277,10 +277,6 @@ struct DenoiseArgs {
     // history-fix lists (k_temporal -> k_history_fix), per 16x16 tile of the band's
     // grid: up to 256 pixel indices at tile*256, count in hfCount[tile]
     uint32_t *hfList, *hfCount;
-    // the tiles with a non-empty list, appended by k_temporal when hfCompact is set: hfTiles[k] for
-    // k < hfTileCount[0] (emptied by k_firefly)
-    uint32_t *hfTiles, *hfTileCount;
-    int hfCompact;
     // firefly lists per 16x16 tile of the band: ffCount[tile] entries at tile*256 (local pixel
     // index, filtered radiance, replacement reservoir); the consumer resets the count
     uint32_t *ffCount;

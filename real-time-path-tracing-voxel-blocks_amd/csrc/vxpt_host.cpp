@@ -317,7 +317,6 @@ struct vxpt_ctx {
     float *histLen = nullptr, *prevHistLen = nullptr;
     float4 *wpos = nullptr;
     uint32_t *ffCount = nullptr, *ffIndex = nullptr, *hfList = nullptr, *hfCount = nullptr, *ffCandCount = nullptr;
-    uint32_t *hfTiles = nullptr, *hfTileCount = nullptr;
     uint4 *ffCand = nullptr;
     float4 *ffColor = nullptr;
     Reservoir *ffRes = nullptr;
@@ -555,8 +554,6 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.ffCount = c->ffCount; a.ffIndex = c->ffIndex; a.ffColor = c->ffColor; a.ffRes = c->ffRes;
     a.ffCand = c->ffCand; a.ffCandCount = c->ffCandCount;
     a.hfList = c->hfList; a.hfCount = c->hfCount;
-    a.hfTiles = c->hfTiles; a.hfTileCount = c->hfTileCount;
-    a.hfCompact = 0;
     a.wpos = c->wpos;
     a.invW = 1.0f / (float)c->W; a.invH = 1.0f / (float)c->H;
     a.thrB = a.p.disocclusionThreshold + (1.5f / (float)c->H);
@@ -1037,7 +1034,6 @@ int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) 
     if (frameNum == 0) HIPCHK(c, launch_frame0_init(a, st));
     int fin = 0;  // 0 illum, 1 ping, 2 pong, 3 prevIllum
     if (p->enable_temporal_accumulation && frameNum > 0) {
-        a.hfCompact = p->enable_history_fix ? 1 : 0;  // k_temporal lists the tiles k_history_fix visits
         HIPCHK(c, launch_temporal(a, st));
         fin = 1;
         if (p->enable_history_fix) { HIPCHK(c, launch_history_fix(a, st)); fin = 2; }
@@ -1576,8 +1572,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
         dalloc(c, c->wpos, n) || dalloc(c, c->ffCount, tiles16) || dalloc(c, c->ffIndex, tiles16 * 256) ||
         dalloc(c, c->ffColor, tiles16 * 256) || dalloc(c, c->ffRes, tiles16 * 256) ||
         dalloc(c, c->ffCand, tiles16 * 256) || dalloc(c, c->ffCandCount, 1) ||
-        dalloc(c, c->hfList, tiles16 * 256) || dalloc(c, c->hfCount, tiles16) || dalloc(c, c->hfTiles, tiles16) ||
-        dalloc(c, c->hfTileCount, 1))
+        dalloc(c, c->hfList, tiles16 * 256) || dalloc(c, c->hfCount, tiles16))
         return VXPT_ERR_HIP;
     c->illumSet[0] = c->illum;
     c->accumBuf[0] = c->accum;
