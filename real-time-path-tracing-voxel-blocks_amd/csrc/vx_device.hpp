@@ -2,8 +2,6 @@
 // voxel DDA, safe spawn, Disney BSDF, blue-noise sampler, light sampling,
 // reservoirs, sky lookup.  See trace.hip for the pass structure.
 #pragma once
-#include <type_traits>
-
 #include "vx_mesh.hpp"
 
 namespace vx {
@@ -185,11 +183,6 @@ struct Dda {
     uint64_t cm;   // its cube-cell mask (dist == 0)
     int prevId, prevLoc, steps;
     float tmin, tmax;
-#ifdef VX_PREFETCH_BRICKS
-    int pnb;       // the brick after the current occupied one, its data loaded ahead (-1: none)
-    uint32_t pbox;
-    uint64_t pm;
-#endif
 };
 enum { DdaRun = 0, DdaEvent = 1, DdaNone = 2 };
 
@@ -198,17 +191,6 @@ enum { DdaRun = 0, DdaEvent = 1, DdaNone = 2 };
 struct GlobalBricks {
     template <bool BOX>
     VX_HD uint64_t fetch(const WorldDev &w, Dda &s, int nb) const {
-#ifdef VX_PREFETCH_BRICKS
-        if (nb == s.pnb) {  // loaded while the previous brick's cells were walked
-            if constexpr (BOX) {
-                s.box = s.pbox;
-                s.dist = (int)(s.box & 0xFFu);
-            } else {
-                s.dist = (int)s.pbox;
-            }
-            return s.pm;
-        }
-#endif
         // the brick's cube mask is fetched beside its table entry, not behind it: one memory
         // round trip per new brick (8 wasted bytes for an empty one) instead of two
         const uint64_t m = w.cellMask[nb];
@@ -221,31 +203,6 @@ struct GlobalBricks {
         return m;
     }
 };
-
-#ifdef VX_PREFETCH_BRICKS
-// Entering an occupied brick, load the data of the brick the ray leaves it into (the brick face with
-// the smallest crossing, pick3's ties as walk_step's), so that its round trip overlaps the walk of this
-// brick's cells; fetch takes it when the walk does arrive there (a hit inside ends the walk first).
-template <bool BOX>
-VX_HD void prefetch_next(const WorldDev &w, Dda &s) {
-    const Ray3 &r = s.r;
-    const Cell &c = s.c;
-    const int ex = r.sx > 0 ? (c.x | 3) + 1 : (c.x & ~3), ey = r.sy > 0 ? (c.y | 3) + 1 : (c.y & ~3),
-              ez = r.sz > 0 ? (c.z | 3) + 1 : (c.z & ~3);
-    const float tx = r.mx ? ((float)ex - r.ox) * r.ix : INFINITY, ty = r.my ? ((float)ey - r.oy) * r.iy : INFINITY,
-                tz = r.mz ? ((float)ez - r.oz) * r.iz : INFINITY;
-    const int a = pick3(tx, ty, tz);
-    const int nx = a == 0 ? (r.sx > 0 ? ex : ex - 1) : c.x, ny = a == 1 ? (r.sy > 0 ? ey : ey - 1) : c.y,
-              nz = a == 2 ? (r.sz > 0 ? ez : ez - 1) : c.z;
-    if (!((unsigned)nx < (unsigned)w.wx && (unsigned)ny < (unsigned)w.wy && (unsigned)nz < (unsigned)w.wz)) return;
-    const int nb = brick_index(w, nx, ny, nz);
-    if (nb == s.pnb) return;
-    s.pnb = nb;
-    s.pm = w.cellMask[nb];
-    if constexpr (BOX) s.pbox = s.ob[nb];
-    else s.pbox = s.od[nb];
-}
-#endif
 
 // brick data of the walk's current cell (cached per brick); returns the cube bit
 template <bool BOX = false, class F = GlobalBricks>
@@ -359,9 +316,6 @@ VX_HD int dda_begin(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, Dda &
     if constexpr (BOX) s.ob = w.bbox + (size_t)w.nBricks * octant_of(s.r);
     else s.od = w.bdist + (size_t)w.nBricks * octant_of(s.r);
     s.nb = -1;
-#ifdef VX_PREFETCH_BRICKS
-    s.pnb = -1;
-#endif
     const bool solid = locate<BOX>(w, s, f);
     s.prevId = solid ? -1 : 0;
     s.prevLoc = s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z);
@@ -393,9 +347,6 @@ VX_HD void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, con
     if constexpr (BOX) s.ob = w.bbox + (size_t)w.nBricks * octant_of(s.r);
     else s.od = w.bdist + (size_t)w.nBricks * octant_of(s.r);
     s.nb = -1;
-#ifdef VX_PREFETCH_BRICKS
-    s.pnb = -1;
-#endif
     locate<BOX>(w, s);
     s.prevLoc = v.face.x;
     s.prevId = (v.face.y & 0xFFFF) - 1;
@@ -407,9 +358,6 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const 
     if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;
     if (cnt) ++cnt[s.dist == 0 ? 3 : (s.dist == 1 ? 2 : 1)];
     if (s.dist == 0) {
-#ifdef VX_PREFETCH_BRICKS
-        if constexpr (std::is_same_v<F, GlobalBricks>) prefetch_next<BOX>(w, s);
-#endif
         const int rc = brick_walk<OCC>(w, s, h, cnt ? cnt + 4 : nullptr);
         if (rc == 1) return DdaEvent;
         if (rc == 2) return DdaNone;
@@ -418,11 +366,6 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const 
             return DdaRun;
         }
     } else if constexpr (BOX) {
-#if defined(VX_PREFETCH_BRICKS) && defined(VX_PREFETCH_EMPTY)
-        // a one-brick empty box is left into the same neighbour an occupied brick would be
-        if constexpr (std::is_same_v<F, GlobalBricks>)
-            if ((s.box & 0xFFFFFFu) == 0x010101u) prefetch_next<BOX>(w, s);
-#endif
         skip_box(w, s.r, s.c, (int)(s.box & 0xFFu), (int)((s.box >> 8) & 0xFFu), (int)((s.box >> 16) & 0xFFu));
     } else {
         skip_cube(w, s.r, s.c, s.dist);

@@ -124,50 +124,3 @@ def test_library_walk_on_host_equals_oracle_dda(driver, outside, tmp_path):
     np.testing.assert_array_equal(got[:, 14], occ[:, 0])
     np.testing.assert_array_equal(got[:, 15], occ[:, 0])
     assert 0.05 < got[:, 0].mean() < 0.95
-
-
-@pytest.fixture(scope="module", params=["occupied", "empty"])
-def driver_prefetch(tmp_path_factory, request):
-    exe = str(tmp_path_factory.mktemp("ddapf") / ("dda_box_driver_pf_" + request.param))
-    flags = ["-DVX_PREFETCH_BRICKS"] + (["-DVX_PREFETCH_EMPTY"] if request.param == "empty" else [])
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-                           *flags, "-I", CSRC, "-x", "hip",
-                           os.path.join(REPO, "tests", "native", "dda_box_driver.hip"), "-o", exe])
-    return exe
-
-
-@pytest.mark.parametrize("world", ["c3", "random"])
-def test_brick_prefetch_walk_equals_plain_walk(driver, driver_prefetch, world, tmp_path):
-    """VX_PREFETCH_BRICKS (the walk loads the brick it will leave an occupied brick -- and, with
-    VX_PREFETCH_EMPTY, a one-brick empty box -- into while it processes this one): every closest hit
-    and occlusion answer of the cube and box walks, through save / resume, bit for bit the plain
-    walk's, on random rays from inside and outside the world."""
-    if world == "random":
-        chunks = (4, 2, 4)
-        ids = _random_world(chunks, 5)
-    else:
-        chunks = (8, 8, 8)
-        o = oracle.Oracle(8, 8)
-        o.terrain(chunks, height_scale=128.0, freq_den=256.0, global_y=True)
-        ids = o.voxels()
-    path = str(tmp_path / "ids.bin")
-    ids.astype(np.uint8).tofile(path)
-    size = np.array([c * 32 for c in chunks], np.float32)
-    rng = np.random.default_rng(11)
-    n = 40000
-    org = rng.random((n, 3), dtype=np.float32) * size
-    org[::4] = org[::4] * 3.0 - size  # a quarter from outside the world box
-    d = rng.normal(size=(n, 3)).astype(np.float32)
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    d[::7, 1] *= 0.02  # grazing rays, the long walks
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    rays = np.concatenate([org, d, np.full((n, 1), 0.01, np.float32), np.full((n, 1), 1e30, np.float32)], axis=1)
-    rpath = str(tmp_path / "rays.bin")
-    rays.astype(np.float32).tofile(rpath)
-    outs = []
-    for exe in (driver, driver_prefetch):
-        opath = str(tmp_path / (os.path.basename(exe) + ".out"))
-        subprocess.run([exe, path, *map(str, chunks), "--rays", rpath, opath], check=True, timeout=600)
-        outs.append(np.fromfile(opath, np.int32).reshape(n, 16))
-    assert outs[0][:, 0].sum() > n // 10  # enough hits to mean something
-    np.testing.assert_array_equal(outs[1], outs[0])
