@@ -161,6 +161,7 @@ vxpt_tuning tuning_defaults() {
     t.hf_split = 4;           // 16.3 -> 11.8 us history fix (with readlane sums)
     t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
     t.lds_bricks = 0;
+    t.frame_overlap = 1;
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -172,7 +173,7 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.resume_wg_per_cu, 1, 64) && in(t.sort_mode, 0, 2) && in(t.overlap, 0, 1) &&
            in(t.state_sets, 2, kMaxSets) && in(t.firefly_fused, 0, 1) && in(t.ta_supertiles, 0, 1) &&
            in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, kMaxSets) &&
-           in(t.lds_bricks, 0, 1);
+           in(t.lds_bricks, 0, 1) && in(t.frame_overlap, 0, 1);
 }
 
 struct vxpt_ctx {
@@ -182,6 +183,7 @@ struct vxpt_ctx {
     std::string err;
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
+    hipEvent_t runEv[2] = {};  // around a banded vxpt_render_frames run
     vxpt_timing timing{};
     vxpt_tuning tune = tuning_defaults();
 
@@ -1379,7 +1381,22 @@ int atrous_rows(int step) { return step + (step > 4 ? step / 4 : 0); }  // Atrou
     } while (0)
 
 // One banded OfflineBackend::renderFrame over cs (vxpt_render_frame's order).
-int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int frame, int spp) {
+// the last banded frame's timings (its events complete: after a sync of the context streams)
+void band_timings(std::vector<vxpt_ctx *> &cs) {
+    for (vxpt_ctx *c : cs) {
+        float t = 0, d = 0, f = 0;
+        hipEventElapsedTime(&t, c->ev[6], c->ev[1]);
+        hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+        hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
+        c->timing.trace_ms = t;   // the band's trace passes and their halo exchanges
+        c->timing.denoise_ms = d; // the band's denoiser passes and their halo exchanges
+        c->timing.frame_ms = f;
+    }
+}
+
+// sync = false (a run of frames, vxpt_render_frames): enqueue the frame and return, so that the host
+// enqueues the next frame while this one runs; the caller syncs after the last
+int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int frame, int spp, bool sync = true) {
     const int it0 = frame * spp;
     // halo depths for this frame's camera motion; the previous frame exchanged its last pass's
     // rows and the histories for its own camera: top them up before the first pass reads them
@@ -1507,16 +1524,9 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
         HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
     }
-    for (vxpt_ctx *c : cs) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        float t = 0, d = 0, f = 0;
-        hipEventElapsedTime(&t, c->ev[6], c->ev[1]);
-        hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
-        hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
-        c->timing.trace_ms = t;   // the band's trace passes and their halo exchanges
-        c->timing.denoise_ms = d; // the band's denoiser passes and their halo exchanges
-        c->timing.frame_ms = f;
-    }
+    if (!sync) return VXPT_OK;
+    for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
+    band_timings(cs);
     return VXPT_OK;
 }
 
@@ -1616,6 +1626,8 @@ void vxpt_destroy(vxpt_ctx *c) {
         if (fs) hipStreamDestroy(fs);
     for (hipEvent_t e : c->chainEv) hipEventDestroy(e);
     for (auto &e : c->ev)
+        if (e) hipEventDestroy(e);
+    for (auto &e : c->runEv)
         if (e) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -2676,9 +2688,19 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
 int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0, int32_t nFrames, int32_t spp) {
     if (!c || spp < 1 || nFrames < 1 || frame0 < 0) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
-    if (c->comm) {  // banded: frame by frame (the halo exchange orders the passes)
+    if (c->comm) {  // banded: frame after frame (the halo exchanges order the passes), one sync at the end
+        std::vector<vxpt_ctx *> cs{c};
+        if (!c->runEv[0])
+            for (hipEvent_t &e : c->runEv) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+        HIPCHK(c, hipEventRecord(c->runEv[0], c->stream));
         for (int f = 0; f < nFrames; ++f)
-            if (int r = vxpt_render_frame(c, p, frame0 + f, spp)) return r;
+            if (int r = band_frame(cs, p ? p : &c->yamlDenoise, frame0 + f, spp, false)) return r;
+        HIPCHK(c, hipEventRecord(c->runEv[1], c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        band_timings(cs);  // the last frame's trace / denoiser split
+        float f = 0;
+        hipEventElapsedTime(&f, c->runEv[0], c->runEv[1]);
+        c->timing.frame_ms = f / (float)nFrames;
         return VXPT_OK;
     }
     const float scale = 1.0f / (float)spp;
@@ -2707,7 +2729,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             }
             if (int r = trace_back(c, pl, false)) return r;
         }
-        if (f + 1 < nFrames) {
+        if (f + 1 < nFrames && c->tune.frame_overlap) {
             // The next frame's first pass-half runs beside this frame's last second half.  It writes
             // a G-buffer slot that is neither this frame's (the denoiser's input) nor the history
             // the denoiser compares against, the other radiance set, and its own state set; the
@@ -2744,7 +2766,9 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         float a = 0, b = 0, e = 0;
         hipEventElapsedTime(&a, c->ev[6], c->chainEv[3 * k]);
         hipEventElapsedTime(&e, c->ev[6], c->chainEv[3 * k + 1]);
-        if (k + 1 < nFrames && hipEventElapsedTime(&b, c->ev[6], c->chainEv[3 * k + 2]) == hipSuccess) a = std::max(a, b);
+        if (k + 1 < nFrames && c->tune.frame_overlap &&
+            hipEventElapsedTime(&b, c->ev[6], c->chainEv[3 * k + 2]) == hipSuccess)
+            a = std::max(a, b);
         dsum += e - a;
     }
     hipEventElapsedTime(&f, c->ev[6], c->ev[7]);

@@ -716,3 +716,34 @@ def test_gpu_rccl_one_rank_communicator_matches_plain_context():
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_one_rank_render_frames_matches_plain_context():
+    """vxpt_render_frames on a context with a (one-rank) communicator enqueues its banded frames back
+    to back with one sync at the end: the same OUTPUT bit for bit as a plain context's run, and
+    frame / trace / denoiser timings from the run's events."""
+    import vxpt
+    w, h, spp = 96, 80, 4
+    cam = C1_CAMERA
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    a, b = make(), make()
+    try:
+        b.band_comm_init(vxpt.band_comm_id(), 1, 0)
+        a.render_frames(0, 4, spp, p)
+        b.render_frames(0, 4, spp, p)
+        np.testing.assert_array_equal(a.read("OUTPUT").view(np.uint32), b.read("OUTPUT").view(np.uint32))
+        t = b.timings()
+        assert t["frame_ms"] > 0 and t["trace_ms"] > 0 and t["denoise_ms"] > 0, t
+    finally:
+        a.close()
+        b.close()
