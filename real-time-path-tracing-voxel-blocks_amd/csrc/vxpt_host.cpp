@@ -161,7 +161,6 @@ vxpt_tuning tuning_defaults() {
     t.hf_split = 4;           // 16.3 -> 11.8 us history fix (with readlane sums)
     t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
     t.lds_bricks = 0;
-    t.frame_overlap = 1;
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -173,7 +172,7 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.resume_wg_per_cu, 1, 64) && in(t.sort_mode, 0, 2) && in(t.overlap, 0, 1) &&
            in(t.state_sets, 2, kMaxSets) && in(t.firefly_fused, 0, 1) && in(t.ta_supertiles, 0, 1) &&
            in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, kMaxSets) &&
-           in(t.lds_bricks, 0, 1) && in(t.frame_overlap, 0, 1);
+           in(t.lds_bricks, 0, 1);
 }
 
 struct vxpt_ctx {
@@ -2729,7 +2728,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             }
             if (int r = trace_back(c, pl, false)) return r;
         }
-        if (f + 1 < nFrames && c->tune.frame_overlap) {
+        if (f + 1 < nFrames) {
             // The next frame's first pass-half runs beside this frame's last second half.  It writes
             // a G-buffer slot that is neither this frame's (the denoiser's input) nor the history
             // the denoiser compares against, the other radiance set, and its own state set; the
@@ -2766,8 +2765,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         float a = 0, b = 0, e = 0;
         hipEventElapsedTime(&a, c->ev[6], c->chainEv[3 * k]);
         hipEventElapsedTime(&e, c->ev[6], c->chainEv[3 * k + 1]);
-        if (k + 1 < nFrames && c->tune.frame_overlap &&
-            hipEventElapsedTime(&b, c->ev[6], c->chainEv[3 * k + 2]) == hipSuccess)
+        if (k + 1 < nFrames && hipEventElapsedTime(&b, c->ev[6], c->chainEv[3 * k + 2]) == hipSuccess)
             a = std::max(a, b);
         dsum += e - a;
     }
