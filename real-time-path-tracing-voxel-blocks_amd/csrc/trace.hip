@@ -1148,6 +1148,45 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     float tapM0 = 0, tapM1 = 0, tapM2 = 0;
     const V2 jit(bn_rand(a.bn, px, py, a.iterationIndex - 1, 0), bn_rand(a.bn, px, py, a.iterationIndex - 1, 1));
     V3 vd0(0.0f), vd1(0.0f), vd2(0.0f);  // the accepted taps' view directions, for the bias correction
+#ifdef VX_RESTIR_BATCH
+    // the three taps' records fetched together, then their acceptance, then the accepted taps'
+    // reservoirs together: three memory round trips instead of up to nine dependent ones (the
+    // combine below still runs in tap order)
+    float4 rb[3], rn[3];
+    bool rv[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
+        rv[i] = prev_rec_load(a, x, y, rb[i], rn[i]);
+    }
+    unsigned acc = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
+        SurfS ts;
+        V3 vd;
+        if (!rv[i] || !prev_surface_rec(a, jit, ts, x, y, rb[i], rn[i], nullptr, &vd)) continue;
+        if (i == 0) vd0 = vd; else if (i == 1) vd1 = vd; else vd2 = vd;
+        const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
+        const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
+        const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
+        if (nOk && dOk && rOk) acc |= 1u << i;
+    }
+    Reservoir prv[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
+        if (acc & (1u << i)) prv[i] = load_prev_res(a, (size_t)y * a.W + x);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (!(acc & (1u << i))) continue;
+        cached |= (1u << i);
+        Reservoir pr = prv[i];
+#else
     for (int i = 0; i < 3; ++i) {
         const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
         const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
@@ -1161,6 +1200,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         if (!(nOk && dOk && rOk)) continue;
         cached |= (1u << i);
         Reservoir pr = load_prev_res(a, (size_t)y * a.W + x);
+#endif
         if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
         if (pr.M > 20.0f) pr.M = 20.0f;
         if (i == 0) tapM0 = pr.M; else if (i == 1) tapM1 = pr.M; else tapM2 = pr.M;
@@ -1177,6 +1217,15 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     qr.id0 = 4 * s;
     LSample sel = invalid_ls();  // the combined reservoir's light (environment lights: the same for every tap)
     if (rr.lightData != 0) light_from_res(a, sel, rr, sf.pos, hasLocal);
+#ifdef VX_RESTIR_BATCH
+    // the accepted taps' records again (cache hits), fetched together
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
+        if (rr.lightData != 0 && (cached & (1u << i))) prev_rec_load(a, x, y, rb[i], rn[i]);
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (rr.lightData != 0 && (cached & (1u << i))) {
@@ -1184,7 +1233,11 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
             SurfS ts;
             const V3 vdi = i == 0 ? vd0 : (i == 1 ? vd1 : vd2);
+#ifdef VX_RESTIR_BATCH
+            prev_surface_rec(a, jit, ts, x, y, rb[i], rn[i], &vdi, nullptr);
+#else
             prev_surface(a, jit, ts, x, y, &vdi, nullptr);
+#endif
             if (MESH && sel.type == LtLocal) light_from_res(a, sel, rr, ts.pos, hasLocal);  // seen from the tap
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;

@@ -161,6 +161,7 @@ vxpt_tuning tuning_defaults() {
     t.hf_split = 4;           // 16.3 -> 11.8 us history fix (with readlane sums)
     t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
     t.lds_bricks = 0;
+    t.stream_priority = 0;
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -172,7 +173,7 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.resume_wg_per_cu, 1, 64) && in(t.sort_mode, 0, 2) && in(t.overlap, 0, 1) &&
            in(t.state_sets, 2, kMaxSets) && in(t.firefly_fused, 0, 1) && in(t.ta_supertiles, 0, 1) &&
            in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, kMaxSets) &&
-           in(t.lds_bricks, 0, 1);
+           in(t.lds_bricks, 0, 1) && in(t.stream_priority, 0, 2);
 }
 
 struct vxpt_ctx {
@@ -1536,6 +1537,8 @@ extern "C" {
 
 const char *vxpt_last_error(const vxpt_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
+static int make_streams(vxpt_ctx *c);
+
 int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (!cfg || !out) return VXPT_ERR_ARG;
     *out = nullptr;
@@ -1555,8 +1558,7 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     c->yamlDenoise = default_denoise();
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (hipStream_t &fs : c->frontStreams) HIPCHK(c, hipStreamCreateWithFlags(&fs, hipStreamNonBlocking));
+    if (int r = make_streams(c)) return r;
     // tuning state_sets = 3: a third wavefront state set, so a first half may run beside the two
     // previous second halves (C3: 6.40 -> 6.39 ms per frame, within noise: the overlapped halves
     // already fill the chip; two sets are the default)
@@ -3258,6 +3260,18 @@ int vxpt_get_tuning(vxpt_ctx *c, vxpt_tuning *out) {
     return VXPT_OK;
 }
 
+// the context stream and the front streams at the priorities tuning.stream_priority names (lower
+// number = dispatched first by the command processor when both have work)
+static int make_streams(vxpt_ctx *c) {
+    int least = 0, greatest = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const int sp = c->tune.stream_priority;
+    HIPCHK(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, sp == 1 ? greatest : least));
+    for (hipStream_t &fs : c->frontStreams)
+        HIPCHK(c, hipStreamCreateWithPriority(&fs, hipStreamNonBlocking, sp == 2 ? greatest : least));
+    return VXPT_OK;
+}
+
 int vxpt_set_tuning(vxpt_ctx *c, const vxpt_tuning *t) {
     if (!c || !t) return VXPT_ERR_ARG;
     if (!tuning_valid(*t)) return fail(c, VXPT_ERR_ARG, "tuning field out of range");
@@ -3267,7 +3281,13 @@ int vxpt_set_tuning(vxpt_ctx *c, const vxpt_tuning *t) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const bool tables = t->dda_boxes != c->tune.dda_boxes || t->box_cap != c->tune.box_cap ||
                         t->box_cap_up != c->tune.box_cap_up;
+    const bool streams = t->stream_priority != c->tune.stream_priority;
     c->tune = *t;
+    if (streams) {  // (vxpt_stream's handle changes)
+        for (hipStream_t &fs : c->frontStreams) HIPCHK(c, hipStreamDestroy(fs));
+        HIPCHK(c, hipStreamDestroy(c->stream));
+        if (int r = make_streams(c)) return r;
+    }
     c->nSets = t->state_sets;
     c->useBoxes = t->dda_boxes != 0;
     c->boxCap = t->box_cap;
