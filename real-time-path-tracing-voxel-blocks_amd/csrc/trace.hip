@@ -499,6 +499,13 @@ VX_D void store_rec(const TraceArgs &a, size_t pi, V3 n, float rough, bool metal
     a.cur.rec[2 * pi] = make_float4(n.x, n.y, n.z, bits_as_float(float_as_bits(rough) | (metal ? (int)0x80000000u : 0)));
     a.cur.rec[2 * pi + 1] = make_float4(alb.x, alb.y, alb.z, depth);
 }
+VX_D void store_planes_sky(const TraceArgs &a, size_t pi) {  // a seg-0 miss or emitter: the sky's G-buffer
+    a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    a.cur.material[pi] = (float)0xFFFF;
+    a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+    a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+    a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
 VX_D void store_rec_sky(const TraceArgs &a, size_t pi, float depth) {
     store_rec(a, pi, V3(0.0f, -1.0f, 0.0f), 0.0f, false, V3(1.0f), depth);
 }
@@ -506,7 +513,7 @@ VX_D void store_rec_sky(const TraceArgs &a, size_t pi, float depth) {
 VX_D void path_end(const TraceArgs &a, int px, int py, V3 radiance, float primaryDist) {
     if (isnan(radiance.x) || isnan(radiance.y) || isnan(radiance.z)) radiance = V3(0.5f);  // RayGen.cu:175-178
     const size_t pi = (size_t)py * a.W + px;
-    a.cur.depth[pi] = primaryDist;
+    if (a.writePlanes) a.cur.depth[pi] = primaryDist;
     a.illum[pi] = make_float4(radiance.x, radiance.y, radiance.z, primaryDist);
 }
 
@@ -565,17 +572,18 @@ VX_D bool same_bits(V3 a, V3 b) {
     return float_as_bits(a.x) == float_as_bits(b.x) && float_as_bits(a.y) == float_as_bits(b.y) &&
            float_as_bits(a.z) == float_as_bits(b.z);
 }
-// seg 0: the shading normal, roughness and albedo are the G-buffer's (pixel order, the same values;
+// seg 0: the shading normal, roughness and albedo are the pass's tap record's (pixel order, the
+// G-buffer planes' values, written by every pass -- the planes only by a frame's last pass;
 // recomputing the view direction from the camera ray as well was slower); flags = the meta word's SF_*
 VX_D SurfS load_surf(const TraceArgs &a, int s, int px, int py, int seg, int meta, bool &skipAlbedo,
                      SurfX *x = nullptr) {
     const WaveBufs &w = a.wb;
     SurfS sf;
     const size_t pi = (size_t)py * a.W + px;
-    const float4 p = w.sPos[s], n = seg == 0 ? a.cur.normalRough[pi] : w.sNrm[s];
-    const float4 al = seg == 0 ? a.cur.albedo[pi] : w.sAlb[s];
+    const float4 p = w.sPos[s], n = seg == 0 ? a.cur.rec[2 * pi] : w.sNrm[s];
+    const float4 al = seg == 0 ? a.cur.rec[2 * pi + 1] : w.sAlb[s];
     sf.pos = xyz(p); sf.depth = p.w;
-    sf.normal = xyz(n); sf.roughness = n.w;
+    sf.normal = xyz(n); sf.roughness = seg == 0 ? bits_as_float(float_as_bits(n.w) & 0x7FFFFFFF) : n.w;
     const int fl = (meta >> 8) & 0xF;
     sf.geoNormal = (fl & SF_GEO) ? xyz(w.sGeo[s]) : sf.normal;
     sf.translucency = 0.0f;
@@ -709,11 +717,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     if (!h.hit) {  // __miss__radiance (miss.cu:9-82)
         if (seg == 0) {
             meta.x |= F_EMPTY;
-            a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-            a.cur.material[pi] = (float)0xFFFF;
-            a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
-            a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
-            a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (a.writePlanes) store_planes_sky(a, pi);
             store_rec_sky(a, pi, kRayMax);
         }
         seg_end(a, s, px, py, meta, sky_emission(a.sky, rayD), V3(1.0f), 0.0f, true, false, seg == 0, 0.0f, primaryDist);
@@ -732,11 +736,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         if (!(meta.x & F_HFD)) {
             e = V3(m.albedo[0], m.albedo[1], m.albedo[2]);
             if (seg == 0) {
-                a.cur.albedo[pi] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-                a.cur.material[pi] = (float)0xFFFF;
-                a.cur.normalRough[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
-                a.cur.geoNormalThin[pi] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
-                a.cur.matParam[pi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (a.writePlanes) store_planes_sky(a, pi);
                 store_rec_sky(a, pi, h.t);
             }
         }
@@ -775,7 +775,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     if (meta.x & F_HFD) sf.roughness = fminf(sf.roughness * 2.0f + 0.1f, 1.0f);
     const bool isDiffuse = sf.roughness > kRoughThresh;
     sf.translucency = m.translucency;
-    if (seg == 0) {
+    if (seg == 0 && a.writePlanes) {
         a.cur.material[pi] = (float)m.materialId;
         a.cur.normalRough[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, sf.roughness);
         a.cur.geoNormalThin[pi] = make_float4(sf.normal.x, sf.normal.y, sf.normal.z, thin ? 1.0f : 0.0f);
@@ -792,7 +792,7 @@ VX_D void shade_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     bool skipAlbedo = false;
     if (seg == 0) {
         meta.x |= F_HFD;
-        a.cur.albedo[pi] = make_float4(sf.albedo.x, sf.albedo.y, sf.albedo.z, 1.0f);
+        if (a.writePlanes) a.cur.albedo[pi] = make_float4(sf.albedo.x, sf.albedo.y, sf.albedo.z, 1.0f);
         store_rec(a, pi, sf.normal, sf.roughness, sf.metallic, sf.albedo, h.t);  // depth = the primary distance
         skipAlbedo = true;
         primaryDist = h.t;
@@ -1148,45 +1148,6 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     float tapM0 = 0, tapM1 = 0, tapM2 = 0;
     const V2 jit(bn_rand(a.bn, px, py, a.iterationIndex - 1, 0), bn_rand(a.bn, px, py, a.iterationIndex - 1, 1));
     V3 vd0(0.0f), vd1(0.0f), vd2(0.0f);  // the accepted taps' view directions, for the bias correction
-#ifdef VX_RESTIR_BATCH
-    // the three taps' records fetched together, then their acceptance, then the accepted taps'
-    // reservoirs together: three memory round trips instead of up to nine dependent ones (the
-    // combine below still runs in tap order)
-    float4 rb[3], rn[3];
-    bool rv[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
-        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
-        rv[i] = prev_rec_load(a, x, y, rb[i], rn[i]);
-    }
-    unsigned acc = 0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
-        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
-        SurfS ts;
-        V3 vd;
-        if (!rv[i] || !prev_surface_rec(a, jit, ts, x, y, rb[i], rn[i], nullptr, &vd)) continue;
-        if (i == 0) vd0 = vd; else if (i == 1) vd1 = vd; else vd2 = vd;
-        const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
-        const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
-        const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
-        if (nOk && dOk && rOk) acc |= 1u << i;
-    }
-    Reservoir prv[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
-        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
-        if (acc & (1u << i)) prv[i] = load_prev_res(a, (size_t)y * a.W + x);
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        if (!(acc & (1u << i))) continue;
-        cached |= (1u << i);
-        Reservoir pr = prv[i];
-#else
     for (int i = 0; i < 3; ++i) {
         const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
         const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
@@ -1200,7 +1161,6 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         if (!(nOk && dOk && rOk)) continue;
         cached |= (1u << i);
         Reservoir pr = load_prev_res(a, (size_t)y * a.W + x);
-#endif
         if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
         if (pr.M > 20.0f) pr.M = 20.0f;
         if (i == 0) tapM0 = pr.M; else if (i == 1) tapM1 = pr.M; else tapM2 = pr.M;
@@ -1217,15 +1177,6 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
     qr.id0 = 4 * s;
     LSample sel = invalid_ls();  // the combined reservoir's light (environment lights: the same for every tap)
     if (rr.lightData != 0) light_from_res(a, sel, rr, sf.pos, hasLocal);
-#ifdef VX_RESTIR_BATCH
-    // the accepted taps' records again (cache hits), fetched together
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
-        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
-        if (rr.lightData != 0 && (cached & (1u << i))) prev_rec_load(a, x, y, rb[i], rn[i]);
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (rr.lightData != 0 && (cached & (1u << i))) {
@@ -1233,11 +1184,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
             SurfS ts;
             const V3 vdi = i == 0 ? vd0 : (i == 1 ? vd1 : vd2);
-#ifdef VX_RESTIR_BATCH
-            prev_surface_rec(a, jit, ts, x, y, rb[i], rn[i], &vdi, nullptr);
-#else
             prev_surface(a, jit, ts, x, y, &vdi, nullptr);
-#endif
             if (MESH && sel.type == LtLocal) light_from_res(a, sel, rr, ts.pos, hasLocal);  // seen from the tap
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;

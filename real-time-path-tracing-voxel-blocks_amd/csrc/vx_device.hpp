@@ -829,39 +829,6 @@ VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const 
     return true;
 }
 
-// prev_surface split in two: the record's loads (no branch before them: an out-of-frame tap reads
-// pixel 0 and is reported invalid), then the surface from the loaded record
-VX_D bool prev_rec_load(const TraceArgs &a, int x, int y, float4 &b, float4 &nr) {
-    const bool in = !(x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y);
-    const size_t i = in ? (size_t)y * a.W + x : 0;
-    b = a.prev.rec[2 * i + 1];
-    nr = a.prev.rec[2 * i];
-    return in;
-}
-VX_D bool prev_surface_rec(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, float4 b, float4 nr, const V3 *vdIn,
-                           V3 *vdOut) {
-    sf.depth = b.w;
-    if (sf.depth == kRayMax) return false;
-    V3 vd;
-    if (vdIn) {
-        vd = *vdIn;
-    } else {
-        const V2 uv = (V2((float)x, (float)y) + j) * a.prevCam.invRes;
-        vd = a.prevCam.uv_to_dir(uv);
-    }
-    if (vdOut) *vdOut = vd;
-    sf.pos = a.prevCam.pos + vd * sf.depth;
-    sf.wo = -vd;
-    sf.normal = V3(nr.x, nr.y, nr.z);
-    sf.geoNormal = sf.normal;
-    sf.albedo = V3(b.x, b.y, b.z);
-    const int rb = float_as_bits(nr.w);
-    sf.roughness = bits_as_float(rb & 0x7FFFFFFF);
-    sf.metallic = rb < 0;
-    sf.translucency = 0.0f;
-    return true;
-}
-
 VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
     V3 emission(0.0f);
     V2 uv = eq_area_sphere_uv(dir);

@@ -233,6 +233,8 @@ struct TraceArgs {
     int sortMode;       // ray queues grouped by direction class per workgroup (0 off, 1 octant, 2 octant x axis)
     int ldsBricks;      // k_closest reads bricks through a workgroup cache in LDS (trace.hip LdsBricks)
     int writeMotion;    // store the (zero) motion vectors: the plane may hold a host upload
+    int writePlanes;    // store the G-buffer planes (0: a frame's passes before its last -- only their tap
+                        // records are read, by the next pass's temporal reuse)
 };
 
 // kernel launchers (defined in the .hip translation units)

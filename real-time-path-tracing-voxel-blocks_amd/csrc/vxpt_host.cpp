@@ -161,7 +161,6 @@ vxpt_tuning tuning_defaults() {
     t.hf_split = 4;           // 16.3 -> 11.8 us history fix (with readlane sums)
     t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
     t.lds_bricks = 0;
-    t.stream_priority = 0;
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -173,7 +172,7 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.resume_wg_per_cu, 1, 64) && in(t.sort_mode, 0, 2) && in(t.overlap, 0, 1) &&
            in(t.state_sets, 2, kMaxSets) && in(t.firefly_fused, 0, 1) && in(t.ta_supertiles, 0, 1) &&
            in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, kMaxSets) &&
-           in(t.lds_bricks, 0, 1) && in(t.stream_priority, 0, 2);
+           in(t.lds_bricks, 0, 1);
 }
 
 struct vxpt_ctx {
@@ -857,8 +856,10 @@ struct PassPlan {
 // stream here.
 hipStream_t front_stream(const vxpt_ctx *c, int set) { return c->frontStreams[set % c->tune.front_streams]; }
 
+// planes = false: a frame's pass before its last, which writes its tap records but not the G-buffer
+// planes (the frame's planes are its last pass's; nothing reads an earlier pass's)
 int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
-                bool overlap, PassPlan &pl) {
+                bool overlap, PassPlan &pl, bool planes = true) {
     if (!c->voxels.p) return fail(c, VXPT_ERR_STATE, "no voxels uploaded");
     if (!c->skyReady) return fail(c, VXPT_ERR_STATE, "sky not set");
     TraceArgs a{};
@@ -897,11 +898,12 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
         HIPCHK(c, launch_pack_rec(a.prev, (size_t)c->W * c->H, c->stream));
         c->gb[c->last].recStale = false;
     }
-    c->gb[next].recStale = false;  // this pass writes both
+    c->gb[next].recStale = false;  // this pass writes the records (and the planes unless !planes)
     const int set = c->passCount % c->nSets;
     a.illum = c->illumSet[set];
     a.motion = c->motion;
     a.writeMotion = c->motionZero ? 0 : 1;
+    a.writePlanes = (planes || (flags & VXPT_TRACE_PRIMARY_ONLY)) ? 1 : 0;
     const size_t n = (size_t)c->W * c->H;
     a.resCur = c->res + (size_t)(((it % 2) + 2) % 2) * n;
     a.resPrev = c->res + (size_t)((((it + 1) % 2) + 2) % 2) * n;
@@ -995,10 +997,10 @@ int trace_back(vxpt_ctx *c, const PassPlan &pl, bool mark = true) {
 }
 
 int do_trace(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool accumFirst, float accumScale,
-             bool overlap = false, bool mark = true) {
+             bool overlap = false, bool mark = true, bool planes = true) {
     if (mark) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     PassPlan pl;
-    if (int r = trace_front(c, it, flags, accumulate, accumFirst, accumScale, overlap, pl)) return r;
+    if (int r = trace_front(c, it, flags, accumulate, accumFirst, accumScale, overlap, pl, planes)) return r;
     return trace_back(c, pl, mark);
 }
 
@@ -1447,7 +1449,7 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     }
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s) {
-        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false));
+        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false, s + 1 == spp));
         const int res = ((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN;
         if (s + 1 < spp) {
             // all but the last pass: the next pass's temporal taps' inputs, overlapped with that pass
@@ -1537,8 +1539,6 @@ extern "C" {
 
 const char *vxpt_last_error(const vxpt_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
-static int make_streams(vxpt_ctx *c);
-
 int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     if (!cfg || !out) return VXPT_ERR_ARG;
     *out = nullptr;
@@ -1558,7 +1558,8 @@ int vxpt_create(const vxpt_config *cfg, vxpt_ctx **out) {
     c->yamlDenoise = default_denoise();
     *out = c;
     HIPCHK(c, hipSetDevice(c->dev));
-    if (int r = make_streams(c)) return r;
+    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (hipStream_t &fs : c->frontStreams) HIPCHK(c, hipStreamCreateWithFlags(&fs, hipStreamNonBlocking));
     // tuning state_sets = 3: a third wavefront state set, so a first half may run beside the two
     // previous second halves (C3: 6.40 -> 6.39 ms per frame, within noise: the overlapped halves
     // already fill the chip; two sets are the default)
@@ -2669,7 +2670,7 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
     const int it0 = frameNum * spp;
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     for (int s = 0; s < spp; ++s)
-        if (int r = do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false)) return r;
+        if (int r = do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false, s + 1 == spp)) return r;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     c->denoiseInputIsAccum = spp > 1;
     int r = do_denoise(c, p, frameNum, it0 + spp);
@@ -2725,7 +2726,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             if (s == 0 && havePend) {
                 pl = pend;
                 havePend = false;
-            } else if (int r = trace_front(c, it0 + s, 0, spp > 1, s == 0, scale, s > 0, pl)) {
+            } else if (int r = trace_front(c, it0 + s, 0, spp > 1, s == 0, scale, s > 0, pl, s + 1 == spp)) {
                 return r;
             }
             if (int r = trace_back(c, pl, false)) return r;
@@ -2735,7 +2736,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             // a G-buffer slot that is neither this frame's (the denoiser's input) nor the history
             // the denoiser compares against, the other radiance set, and its own state set; the
             // motion plane it stores is all zeros (static world) like the one the denoiser reads.
-            if (int r = trace_front(c, it0 + spp, 0, spp > 1, true, scale, true, pend)) return r;
+            if (int r = trace_front(c, it0 + spp, 0, spp > 1, true, scale, true, pend, spp == 1)) return r;
             havePend = true;
             // the denoiser starts after it, so it runs alone and its timing stays its own.  (Running
             // all of the chain but its firefly stage on a third stream beside the next frame's first
@@ -3260,18 +3261,6 @@ int vxpt_get_tuning(vxpt_ctx *c, vxpt_tuning *out) {
     return VXPT_OK;
 }
 
-// the context stream and the front streams at the priorities tuning.stream_priority names (lower
-// number = dispatched first by the command processor when both have work)
-static int make_streams(vxpt_ctx *c) {
-    int least = 0, greatest = 0;
-    HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
-    const int sp = c->tune.stream_priority;
-    HIPCHK(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, sp == 1 ? greatest : least));
-    for (hipStream_t &fs : c->frontStreams)
-        HIPCHK(c, hipStreamCreateWithPriority(&fs, hipStreamNonBlocking, sp == 2 ? greatest : least));
-    return VXPT_OK;
-}
-
 int vxpt_set_tuning(vxpt_ctx *c, const vxpt_tuning *t) {
     if (!c || !t) return VXPT_ERR_ARG;
     if (!tuning_valid(*t)) return fail(c, VXPT_ERR_ARG, "tuning field out of range");
@@ -3281,13 +3270,7 @@ int vxpt_set_tuning(vxpt_ctx *c, const vxpt_tuning *t) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const bool tables = t->dda_boxes != c->tune.dda_boxes || t->box_cap != c->tune.box_cap ||
                         t->box_cap_up != c->tune.box_cap_up;
-    const bool streams = t->stream_priority != c->tune.stream_priority;
     c->tune = *t;
-    if (streams) {  // (vxpt_stream's handle changes)
-        for (hipStream_t &fs : c->frontStreams) HIPCHK(c, hipStreamDestroy(fs));
-        HIPCHK(c, hipStreamDestroy(c->stream));
-        if (int r = make_streams(c)) return r;
-    }
     c->nSets = t->state_sets;
     c->useBoxes = t->dda_boxes != 0;
     c->boxCap = t->box_cap;
