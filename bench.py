@@ -145,12 +145,19 @@ def band_tuning(width, height, world):
     """Schedule defaults of a rank's band (N>1).  A band is latency bound: a third wavefront state
     set lets its passes' first halves run further ahead, and below ~0.7 Mpx a third front stream
     adds overlap (1080p, 8 balanced bands: slowest band 1.52 -> 1.43 ms per frame), while bigger bands
-    lose by it (1080p, 2 bands of 1 Mpx: 3.16 -> 3.22 ms; profiles/r04_band_proxy*.json)."""
+    lose by it (1080p, 2 bands of 1 Mpx: 3.16 -> 3.22 ms; profiles/r04_band_proxy*.json); below
+    ~0.4 Mpx the longest straggler walks are split across lanes (k_resume_split)."""
     if world <= 1:
         return {}
     t = {"state_sets": 3}
     if width * height / world < 700e3:
         t["front_streams"] = 3
+    if width * height / world < 400e3:
+        # the stragglers still walking after 6 + 8 iterations cut into 16 pieces, one lane each: a
+        # small band's passes wait on their longest walks (136-row 1080p band 1.40-1.42 -> 1.31-1.34
+        # ms per frame; 272 rows even, the whole frame slower: DESIGN.md §4)
+        t["iter_cap2"] = 8
+        t["resume_split"] = 16
     return t
 
 

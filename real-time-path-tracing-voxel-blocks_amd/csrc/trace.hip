@@ -493,6 +493,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESU
     }
 }
 
+// The level-`level` stragglers of queue q with each walk cut into up to G pieces, one lane each
+// (vx_device.hpp seg_plan / dda_seg_start: the pieces together are the walk, its result the first
+// piece's with an event): a wave takes 64 / G stragglers per round, so a long walk's chain of
+// dependent brick loads is G shorter chains side by side.  A piece stops as soon as an earlier piece
+// of its walk has an event.  Level 2 (after iter_cap2 more iterations one lane per walk) holds only
+// the longest walks, where the pieces' setup pays.
+template <bool OCC, bool BOX>
+__global__ __launch_bounds__(256) void k_resume_split(TraceArgs a, int q, int level, int shardCap, int G) {
+    const WaveBufs &w = a.wb;
+    const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
+    const int per = 64 / G, shard = wv % kShards, step = gridDim.x * 256 / kShards / G;
+    const int n = (int)*straggler_count(w, level, q, shard), in = (level - 1) & 1;
+    const int g = lane % G, gbase = lane - g;
+    const unsigned long long below = (1ull << lane) - (1ull << gbase);  // the earlier pieces' lanes
+    const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+    for (int j0 = (wv / kShards) * per; j0 < n; j0 += step) {  // wave-uniform
+        const int j = j0 + lane / G;
+        const bool live = j < n;
+        Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+        Dda st;
+        int rc = DdaNone, id = 0;
+        if (live) {
+            const int k = shard * shardCap + j;
+            const DdaSaved sv{w.sCell[in][k], w.sT[in][k], w.sFace[in][k]};
+            const int e = sv.cell.w;
+            const float4 ro = w.qO[e], rd = w.qD[e];
+            id = w.qId[e];
+            dda_resume<BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, sv, st);
+            int D, cells;
+            const int pieces = seg_plan(a.world, st, G, D, cells);
+            if (g < pieces) {
+                int P0 = 0, P1 = 0;
+                const float T0 = g > 0 ? seg_bound(st, D, g, pieces, cells, P0) : 0.0f;
+                const float T1 = g + 1 < pieces ? seg_bound(st, D, g + 1, pieces, cells, P1) : rd.w;
+                if (g > 0) dda_seg_start<BOX>(a.world, st, D, P0, T0);
+                st.tmax = fminf(T1, rd.w);
+                rc = DdaRun;
+            }
+        }
+        for (;;) {
+            const bool run = rc == DdaRun;
+            if (__ballot(run) == 0ull) break;
+            if (run) rc = dda_iter<OCC, BOX>(a.world, st, h);
+            if (rc == DdaRun && (__ballot(rc == DdaEvent) & below)) rc = DdaNone;  // an earlier piece has it
+        }
+        const unsigned long long ev = __ballot(rc == DdaEvent) & gmask;
+        const int first = ev ? __ffsll((long long)ev) - 1 - gbase : 0;
+        if (live && g == first) store_result<OCC>(w, id, ev ? DdaEvent : DdaNone, h, a.mesh.nInst == 0);
+    }
+}
+
 // ----------------------------------------------------------------- shading
 // the pass's tap record (GBuf::rec) of pixel pi, written wherever the G-buffer planes are
 VX_D void store_rec(const TraceArgs &a, size_t pi, V3 n, float rough, bool metal, V3 alb, float depth) {
@@ -1489,27 +1540,27 @@ struct Launcher {
     // a ray queue's traversal: iteration-capped pass + straggler continuation (+ the mesh pass).  The
     // stragglers' grid: a fixed number of workgroups per CU (their count is on the device; each wave
     // reads it and strides over its shard), vxpt_tuning.resume_wg_per_cu per CU (the sweep in DESIGN.md)
-    void trav(bool occ, int q, int cap) {
+    template <bool OCC, bool BOX>
+    void trav_t(int q, dim3 gq, int shardCap) {
         const dim3 gr(a.numCU * (a.resumeWgPerCU > 0 ? a.resumeWgPerCU : 16));
+        hipLaunchKernelGGL((k_queue<OCC, BOX>), gq, b, 0, st, a, q, a.iterCap, shardCap);
+        if (a.resumeSplit > 1 && a.iterCap2 == 0) {
+            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, 1, shardCap, a.resumeSplit);
+            return;
+        }
+        hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
+        if (a.iterCap2 > 0 && a.resumeSplit > 1)
+            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, a.resumeSplit);
+        else if (a.iterCap2 > 0)
+            hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, 0);
+    }
+    void trav(bool occ, int q, int cap) {
         const dim3 gq((cap + 255) / 256);
         const int shardCap = (int)((gq.x + kShards - 1) / kShards) * 256;
-        if (occ && box) {
-            hipLaunchKernelGGL((k_queue<true, true>), gq, b, 0, st, a, q, a.iterCap, shardCap);
-            hipLaunchKernelGGL((k_resume<true, true>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
-            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<true, true>), gr, b, 0, st, a, q, 2, shardCap, 0);
-        } else if (occ) {
-            hipLaunchKernelGGL((k_queue<true, false>), gq, b, 0, st, a, q, a.iterCap, shardCap);
-            hipLaunchKernelGGL((k_resume<true, false>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
-            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<true, false>), gr, b, 0, st, a, q, 2, shardCap, 0);
-        } else if (box) {
-            hipLaunchKernelGGL((k_queue<false, true>), gq, b, 0, st, a, q, a.iterCap, shardCap);
-            hipLaunchKernelGGL((k_resume<false, true>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
-            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<false, true>), gr, b, 0, st, a, q, 2, shardCap, 0);
-        } else {
-            hipLaunchKernelGGL((k_queue<false, false>), gq, b, 0, st, a, q, a.iterCap, shardCap);
-            hipLaunchKernelGGL((k_resume<false, false>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
-            if (a.iterCap2 > 0) hipLaunchKernelGGL((k_resume<false, false>), gr, b, 0, st, a, q, 2, shardCap, 0);
-        }
+        if (occ && box) trav_t<true, true>(q, gq, shardCap);
+        else if (occ) trav_t<true, false>(q, gq, shardCap);
+        else if (box) trav_t<false, true>(q, gq, shardCap);
+        else trav_t<false, false>(q, gq, shardCap);
         if (mesh) {
             if (occ) hipLaunchKernelGGL(k_mesh_queue<true>, gq, b, 0, st, a, q);
             else hipLaunchKernelGGL(k_mesh_queue<false>, gq, b, 0, st, a, q);

@@ -353,6 +353,64 @@ VX_HD void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, con
     s.steps = v.face.y >> 16;
 }
 
+// Segmented walks (k_resume, tuning resume_split): the rest of a walk cut into G pieces along the
+// ray's dominant axis D, one lane each.  The walk's crossings are the per-axis plane crossings merged
+// in the order `before` (t, then Z before Y before X), so the state after every crossing before D's
+// plane P (t = T) is known without walking: axis D stands in the cell before P, every other axis in
+// the cell skip_axis computes for (T, D).  A piece starts there (its cell's id state as dda_begin
+// sets it: prevId always describes the walk's current cell) and ends at the next piece's T as its
+// tmax, so the pieces together process every crossing of the walk.  A piece's first event is the
+// walk's first event after the piece's start; the walk's result is that of the first piece with an
+// event -- the cell-by-cell walk's, bit for bit.
+//
+// The dominant axis D and the number n of its cells between the walk's cell and where the walk
+// ends (tmax, or the world box's exit); returns the pieces, min(G, n) (at least 1).
+// (per-axis choices as bit blends, as in brick_walk: a select between fields pins the walk in scratch)
+VX_HD int blend_i(int D, int x, int y, int z) { return (x & -(int)(D == 0)) | (y & -(int)(D == 1)) | (z & -(int)(D == 2)); }
+VX_HD float blend_f(int D, float x, float y, float z) {
+    return bits_as_float(blend_i(D, float_as_bits(x), float_as_bits(y), float_as_bits(z)));
+}
+VX_HD int seg_plan(const WorldDev &w, const Dda &s, int G, int &D, int &n) {
+    const Ray3 &r = s.r;
+    const float ax = fabsf(r.dx), ay = fabsf(r.dy), az = fabsf(r.dz);
+    D = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+    float te = s.tmax;
+    if (r.mx) te = fminf(te, ((float)(r.sx > 0 ? w.wx : 0) - r.ox) * r.ix);
+    if (r.my) te = fminf(te, ((float)(r.sy > 0 ? w.wy : 0) - r.oy) * r.iy);
+    if (r.mz) te = fminf(te, ((float)(r.sz > 0 ? w.wz : 0) - r.oz) * r.iz);
+    const int c = blend_i(D, s.c.x, s.c.y, s.c.z), sd = blend_i(D, r.sx, r.sy, r.sz);
+    const float o = blend_f(D, r.ox, r.oy, r.oz), d = blend_f(D, r.dx, r.dy, r.dz);
+    const int wd = blend_i(D, w.wx, w.wy, w.wz);
+    const int e = clampi((int)floorf(o + te * d), 0, wd - 1);
+    n = sd > 0 ? e - c : c - e;
+    return n < 1 ? 1 : (n < G ? n : G);
+}
+// piece k's boundary (1 <= k < pieces): D's plane P entering the piece's first D-cell
+// (k * n / pieces cells ahead of the walk's cell), and its t by next_t's formula
+VX_HD float seg_bound(const Dda &s, int D, int k, int pieces, int n, int &P) {
+    const Ray3 &r = s.r;
+    const int c = blend_i(D, s.c.x, s.c.y, s.c.z), sd = blend_i(D, r.sx, r.sy, r.sz);
+    const float o = blend_f(D, r.ox, r.oy, r.oz), inv = blend_f(D, r.ix, r.iy, r.iz);
+    const int q = c + sd * (k * n / pieces);
+    P = sd > 0 ? q : q + 1;
+    return ((float)P - o) * inv;
+}
+template <bool BOX = false>
+VX_HD void dda_seg_start(const WorldDev &w, Dda &s, int D, int P, float T) {
+    const Ray3 &r = s.r;
+    Cell &c = s.c;
+    if (D == 0) { c.x = r.sx > 0 ? P - 1 : P; c.tx = T; }
+    else if (r.mx) skip_axis(c.x, c.tx, r.sx, r.ox, r.dx, r.ix, 0, w.wx - 1, 0, T, D);
+    if (D == 1) { c.y = r.sy > 0 ? P - 1 : P; c.ty = T; }
+    else if (r.my) skip_axis(c.y, c.ty, r.sy, r.oy, r.dy, r.iy, 0, w.wy - 1, 1, T, D);
+    if (D == 2) { c.z = r.sz > 0 ? P - 1 : P; c.tz = T; }
+    else if (r.mz) skip_axis(c.z, c.tz, r.sz, r.oz, r.dz, r.iz, 0, w.wz - 1, 2, T, D);
+    s.nb = -1;
+    const bool solid = locate<BOX>(w, s);
+    s.prevId = solid ? -1 : 0;
+    s.prevLoc = s.nb * 64 + cell_of(c.x, c.y, c.z);
+}
+
 template <bool OCC, bool BOX = false, class F = GlobalBricks>
 VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const F &f = F()) {
     if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;

@@ -17,6 +17,38 @@
 
 using namespace vx;
 
+// A walk through the straggler hand-over and then cut into up to G pieces (vx_device.hpp seg_plan /
+// seg_bound / dda_seg_start, k_resume's resume_split), the pieces walked one after another: the
+// result of the first piece with an event.  Must equal the whole walk's.
+template <bool OCC>
+static int split_walk(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int cap, int G, Hit &out) {
+    Hit h{0, 0, 0, 0, -1, 0, kRayMax};
+    Dda s;
+    int rc = dda_begin<OCC, true>(w, o, d, tmin, tmax, s, h);
+    for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC, true>(w, s, h);
+    if (rc != DdaRun) { out = h; return rc; }
+    const DdaSaved sv = dda_save(s, 0);
+    Dda s0;
+    dda_resume<true>(w, o, d, tmin, tmax, sv, s0);
+    int D, n;
+    const int pieces = seg_plan(w, s0, G, D, n);
+    for (int k = 0; k < pieces; ++k) {
+        Dda sk;
+        dda_resume<true>(w, o, d, tmin, tmax, sv, sk);
+        int P0 = 0, P1 = 0;
+        const float T0 = k > 0 ? seg_bound(sk, D, k, pieces, n, P0) : 0.0f;
+        const float T1 = k + 1 < pieces ? seg_bound(sk, D, k + 1, pieces, n, P1) : tmax;
+        if (k > 0) dda_seg_start<true>(w, sk, D, P0, T0);
+        sk.tmax = fminf(T1, tmax);
+        Hit hk{0, 0, 0, 0, -1, 0, kRayMax};
+        int r = DdaRun;
+        while (r == DdaRun) r = dda_iter<OCC, true>(w, sk, hk);
+        if (r == DdaEvent) { out = hk; return DdaEvent; }
+    }
+    out = Hit{0, 0, 0, 0, -1, 0, kRayMax};
+    return DdaNone;
+}
+
 int main(int argc, char **argv) {
     if (argc < 7) return 2;
     const int CX = atoi(argv[2]), CY = atoi(argv[3]), CZ = atoi(argv[4]), nrays = atoi(argv[5]);
@@ -135,7 +167,7 @@ int main(int argc, char **argv) {
     }
     std::mt19937 rng(seed);
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
-    long diff = 0, hits = 0, itCube = 0, itBox = 0;
+    long diff = 0, hits = 0, itCube = 0, itBox = 0, splitDiff = 0, splitRuns = 0;
     for (int i = 0; i < nrays; ++i) {
         const bool outside = i % 4 == 0;
         V3 o(U(rng) * wx, U(rng) * wy, U(rng) * wz);
@@ -166,6 +198,22 @@ int main(int argc, char **argv) {
         const bool same = hc.hit == hb.hit && hc.x == hb.x && hc.y == hb.y && hc.z == hb.z && hc.face == hb.face &&
                           hc.id == hb.id && float_as_bits(hc.t) == float_as_bits(hb.t);
         const bool oc = dda_occluded<false>(w, o, d, tmin, tmax), ob = dda_occluded<true>(wb, o, d, tmin, tmax);
+        for (int G : {2, 4, 8}) {
+            const int cap = i % 7;
+            Hit hs;
+            if (split_walk<false>(wb, o, d, 0.0f, tmax, cap, G, hs) != DdaEvent) hs = Hit{0, 0, 0, 0, -1, 0, kRayMax};
+            Hit ho;
+            const bool os = split_walk<true>(wb, o, d, tmin, tmax, cap, G, ho) == DdaEvent;
+            const bool ss = hs.hit == hb.hit && hs.x == hb.x && hs.y == hb.y && hs.z == hb.z && hs.face == hb.face &&
+                            hs.id == hb.id && float_as_bits(hs.t) == float_as_bits(hb.t);
+            ++splitRuns;
+            if (!ss || os != ob) {
+                if (splitDiff < 5)
+                    printf("split diff ray %d G %d cap %d: box hit %d (%d %d %d) f%d t %.9g | split hit %d (%d %d %d) f%d t %.9g | occ %d %d\n",
+                           i, G, cap, hb.hit, hb.x, hb.y, hb.z, hb.face, hb.t, hs.hit, hs.x, hs.y, hs.z, hs.face, hs.t, ob, os);
+                ++splitDiff;
+            }
+        }
         if (!same || oc != ob) {
             if (diff < 5)
                 printf("diff ray %d: cube hit %d (%d %d %d) f%d t %.9g | box hit %d (%d %d %d) f%d t %.9g | occ %d %d\n", i,
@@ -173,7 +221,8 @@ int main(int argc, char **argv) {
             ++diff;
         }
     }
-    printf("rays %d hits %ld diff %ld iters cube %.3f box %.3f empty-entries %ld mean-growth %.3f\n", nrays, hits, diff,
-           (double)itCube / nrays, (double)itBox / nrays, empties, empties ? (double)growX / empties : 0.0);
+    printf("rays %d hits %ld diff %ld split-runs %ld split-diff %ld iters cube %.3f box %.3f empty-entries %ld mean-growth %.3f\n",
+           nrays, hits, diff, splitRuns, splitDiff, (double)itCube / nrays, (double)itBox / nrays, empties,
+           empties ? (double)growX / empties : 0.0);
     return 0;
 }
