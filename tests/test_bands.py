@@ -144,17 +144,20 @@ def test_gpu_bands_match_single_context():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,w,h,splits", [(2, 64, 160, None), (8, 640, 640, None),
-                                          (3, 96, 320, [0, 80, 248, 320]),
-                                          (8, 640, 640, [0, 72, 144, 224, 304, 384, 464, 560, 640])])
-def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits):
+@pytest.mark.parametrize("n,w,h,splits,tune", [(2, 64, 160, None, None), (8, 640, 640, None, None),
+                                               (3, 96, 320, [0, 80, 248, 320], None),
+                                               (8, 640, 640, [0, 72, 144, 224, 304, 384, 464, 560, 640], None),
+                                               (8, 640, 640, None, "bench")])
+def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits, tune):
     """The library's own band schedule (vxpt_band_link / vxpt_render_frame_linked: the one
     vxpt_band_comm_init runs over RCCL, with device copies between the contexts as the
     transport) equals the single-context render bit for bit; 8 bands simulate the 8-GPU
     partition on one device (bands of 80 rows, wider than the 72-row trace halo).  Uneven
     partitions (vxpt_band_link_rows, the cost-balanced bands of vxpt_band_balance) too, with
-    bands as short as the halo itself."""
+    bands as short as the halo itself.  tune "bench": the band contexts run bench.band_tuning's
+    schedule (third state set and front stream, straggler walks in 16 pieces)."""
     import vxpt
+    from bench import band_tuning
     spp = 4
     cam = C1_CAMERA
 
@@ -169,6 +172,11 @@ def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits):
     p = vxpt.DenoiseParams.defaults()
     single = make()
     rs = [make() for _ in range(n)]
+    if tune == "bench":
+        t = band_tuning(1920, 1080, n)
+        assert t.get("resume_split", 1) > 1
+        for r in rs:
+            r.set_tuning(**t)
     linked = vxpt.LinkedBands(rs, splits)
     rows = [bands.band_rows(h, n, k) for k in range(n)] if splits is None else list(zip(splits[:-1], splits[1:]))
     for f in range(3):
