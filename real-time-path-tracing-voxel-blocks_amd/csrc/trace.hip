@@ -522,14 +522,17 @@ __global__ __launch_bounds__(256) void k_resume_split(TraceArgs a, int q, int le
             id = w.qId[e];
             dda_resume<BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, sv, st);
             int D, cells;
-            const int pieces = seg_plan(a.world, st, G, D, cells);
+            float te;
+            const int pieces = seg_plan(a.world, st, G, D, cells, te);
             if (g < pieces) {
                 int P0 = 0, P1 = 0;
                 const float T0 = g > 0 ? seg_bound(st, D, g, pieces, cells, P0) : 0.0f;
                 const float T1 = g + 1 < pieces ? seg_bound(st, D, g + 1, pieces, cells, P1) : rd.w;
-                if (g > 0) dda_seg_start<BOX>(a.world, st, D, P0, T0);
-                st.tmax = fminf(T1, rd.w);
-                rc = DdaRun;
+                if (g == 0 || T0 < te) {
+                    if (g > 0) dda_seg_start<BOX>(a.world, st, D, P0, T0);
+                    st.tmax = fminf(T1, rd.w);
+                    rc = DdaRun;
+                }
             }
         }
         for (;;) {

@@ -364,17 +364,19 @@ VX_HD void dda_resume(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, con
 // event -- the cell-by-cell walk's, bit for bit.
 //
 // The dominant axis D and the number n of its cells between the walk's cell and where the walk
-// ends (tmax, or the world box's exit); returns the pieces, min(G, n) (at least 1).
+// ends (te: tmax, or the world box's exit); returns the pieces, min(G, n) (at least 1).  A piece
+// whose boundary t is not before te (a rounding case at the last cell) is empty: the piece before it
+// walks to the end.
 // (per-axis choices as bit blends, as in brick_walk: a select between fields pins the walk in scratch)
 VX_HD int blend_i(int D, int x, int y, int z) { return (x & -(int)(D == 0)) | (y & -(int)(D == 1)) | (z & -(int)(D == 2)); }
 VX_HD float blend_f(int D, float x, float y, float z) {
     return bits_as_float(blend_i(D, float_as_bits(x), float_as_bits(y), float_as_bits(z)));
 }
-VX_HD int seg_plan(const WorldDev &w, const Dda &s, int G, int &D, int &n) {
+VX_HD int seg_plan(const WorldDev &w, const Dda &s, int G, int &D, int &n, float &te) {
     const Ray3 &r = s.r;
     const float ax = fabsf(r.dx), ay = fabsf(r.dy), az = fabsf(r.dz);
     D = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
-    float te = s.tmax;
+    te = s.tmax;
     if (r.mx) te = fminf(te, ((float)(r.sx > 0 ? w.wx : 0) - r.ox) * r.ix);
     if (r.my) te = fminf(te, ((float)(r.sy > 0 ? w.wy : 0) - r.oy) * r.iy);
     if (r.mz) te = fminf(te, ((float)(r.sz > 0 ? w.wz : 0) - r.oz) * r.iz);

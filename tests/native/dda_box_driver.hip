@@ -31,13 +31,15 @@ static int split_walk(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int
     Dda s0;
     dda_resume<true>(w, o, d, tmin, tmax, sv, s0);
     int D, n;
-    const int pieces = seg_plan(w, s0, G, D, n);
+    float te;
+    const int pieces = seg_plan(w, s0, G, D, n, te);
     for (int k = 0; k < pieces; ++k) {
         Dda sk;
         dda_resume<true>(w, o, d, tmin, tmax, sv, sk);
         int P0 = 0, P1 = 0;
         const float T0 = k > 0 ? seg_bound(sk, D, k, pieces, n, P0) : 0.0f;
         const float T1 = k + 1 < pieces ? seg_bound(sk, D, k + 1, pieces, n, P1) : tmax;
+        if (k > 0 && !(T0 < te)) break;  // past the walk's end: the pieces before covered it
         if (k > 0) dda_seg_start<true>(w, sk, D, P0, T0);
         sk.tmax = fminf(T1, tmax);
         Hit hk{0, 0, 0, 0, -1, 0, kRayMax};
