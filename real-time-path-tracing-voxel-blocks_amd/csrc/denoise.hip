@@ -496,13 +496,6 @@ VX_HD TaHist ta_history(const T &t, int W, int H, const Qt &rot, V3 nIn, V2 prev
         const float pz = t.pz(ox + bcx[k], oy + bcy[k]);
         bicValid *= fabsf(pz - estDepth) > thrv[k >> 1] ? 0.0f : 1.0f;
     }
-#ifdef VX_TA_PH_EARLY
-    // the bilinear history-length taps fetched beside the depth taps (same pixels, edge-clamped, so
-    // always valid reads): one dependent round trip fewer; used only when a tap passes
-    float histTap[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) histTap[k] = t.ph(ox + (k & 1), oy + (k >> 1));
-#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const float pz = t.pz(ox + (k & 1), oy + (k >> 1));
@@ -531,11 +524,9 @@ VX_HD TaHist ta_history(const T &t, int W, int H, const Qt &rot, V3 nIn, V2 prev
     if ((taps[0] * 1.0f + taps[1] * 1.0f + taps[2] * 1.0f + taps[3] * 1.0f) == 0.0f) {
         r.found = 0.0f; r.quality = 0.0f; r.hist = 0.0f;
     } else {
-#ifndef VX_TA_PH_EARLY
         float histTap[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) histTap[k] = t.ph(ox + (k & 1), oy + (k >> 1));
-#endif
         r.hist = bilinear_custom1(histTap, W, H, prevUV, taps);
     }
     r.bicValid = bicValid;

@@ -1547,14 +1547,19 @@ struct Launcher {
     void trav_t(int q, dim3 gq, int shardCap) {
         const dim3 gr(a.numCU * (a.resumeWgPerCU > 0 ? a.resumeWgPerCU : 16));
         hipLaunchKernelGGL((k_queue<OCC, BOX>), gq, b, 0, st, a, q, a.iterCap, shardCap);
-        if (a.resumeSplit > 1 && a.iterCap2 == 0) {
-            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, 1, shardCap, a.resumeSplit);
+        // a path's later segments (queues of segment >= 1) trace what is left of the pass's paths:
+        // few rays, so their traversals wait on the longest walks (tuning later_split: after 8 more
+        // iterations one lane each, the rest in pieces)
+        const bool later = (q >> 2) > 0 && a.laterSplit > 1;
+        const int cap2 = later ? 8 : a.iterCap2, G = later ? a.laterSplit : a.resumeSplit;
+        if (G > 1 && cap2 == 0) {
+            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, 1, shardCap, G);
             return;
         }
-        hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 1, shardCap, a.iterCap2);
-        if (a.iterCap2 > 0 && a.resumeSplit > 1)
-            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, a.resumeSplit);
-        else if (a.iterCap2 > 0)
+        hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 1, shardCap, cap2);
+        if (cap2 > 0 && G > 1)
+            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, G);
+        else if (cap2 > 0)
             hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, 0);
     }
     void trav(bool occ, int q, int cap) {

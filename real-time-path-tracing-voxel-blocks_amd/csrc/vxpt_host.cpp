@@ -162,6 +162,7 @@ vxpt_tuning tuning_defaults() {
     t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
     t.lds_bricks = 0;
     t.resume_split = 1;
+    t.later_split = 1;
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -174,7 +175,8 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.state_sets, 2, kMaxSets) && in(t.firefly_fused, 0, 1) && in(t.ta_supertiles, 0, 1) &&
            in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, kMaxSets) &&
            in(t.lds_bricks, 0, 1) && (t.resume_split == 1 || t.resume_split == 2 || t.resume_split == 4 ||
-                                       t.resume_split == 8 || t.resume_split == 16);
+                                       t.resume_split == 8 || t.resume_split == 16) &&
+           (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16);
 }
 
 struct vxpt_ctx {
@@ -945,6 +947,7 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.sortMode = c->tune.sort_mode;
     a.ldsBricks = c->tune.lds_bricks;
     a.resumeSplit = c->tune.resume_split;
+    a.laterSplit = c->tune.later_split;
     a.prevSceneEmpty = c->prevSceneEmpty;
     // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
     a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;

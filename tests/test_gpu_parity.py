@@ -368,6 +368,30 @@ def test_tuning_changes_no_result(variant):
         b.close()
 
 
+@pytest.mark.parametrize("tune", [dict(later_split=16), dict(later_split=4, resume_split=2)])
+def test_later_segment_pieces_change_no_result(tune):
+    """4/4 bounces (the passes' later segments trace what is left of their paths): the later
+    segments' stragglers in pieces (tuning later_split) render the defaults' frames bit for bit."""
+    def make():
+        r = vxpt.Renderer(100, 70, bounces=(4, 4))
+        r.load_settings()
+        r.generate_terrain((2, 1, 2), height_scale=32.0)
+        r.set_camera(C1_CAMERA[0], C1_CAMERA[1], fov=C1_CAMERA[2], prev=C1_CAMERA)
+        r.set_sky(0.25, 45.0, 0.0, 1.0)
+        return r
+    a, b = make(), make()
+    b.set_tuning(**tune)
+    p = _dn_params()
+    try:
+        a.render_frames(0, 3, 4, p)
+        b.render_frames(0, 3, 4, p)
+        for name in ("ILLUM", "DEPTH", "TAP_RECORD", "RES_EVEN", "RES_ODD", "OUTPUT"):
+            np.testing.assert_array_equal(a.read(name).view(np.uint8), b.read(name).view(np.uint8), err_msg=name)
+    finally:
+        a.close()
+        b.close()
+
+
 def test_tuning_rejects_out_of_range_fields():
     r, _ = _setup(32, 16)
     try:
