@@ -155,7 +155,7 @@ typedef struct vxpt_tuning {
     int32_t front_streams;    /* streams for the passes' first halves (by state set), 1..3: side by side (2) */
     int32_t lds_bricks;       /* 1: camera walks read bricks through a workgroup cache in LDS           (0) */
     int32_t resume_split;     /* straggler walks cut into 1, 2, 4, 8 or 16 pieces walked side by side     (1) */
-    int32_t later_split;      /* the later path segments' stragglers: after 8 more iterations, in 1-16 pieces (1) */
+    int32_t later_split;      /* the later path segments' stragglers: after 8 more iterations, in 1-16 pieces (16) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);

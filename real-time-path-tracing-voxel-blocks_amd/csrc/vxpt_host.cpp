@@ -162,7 +162,7 @@ vxpt_tuning tuning_defaults() {
     t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
     t.lds_bricks = 0;
     t.resume_split = 1;
-    t.later_split = 1;
+    t.later_split = 16;       // 4/4 bounces: 16.39 -> 15.67 ms per frame (3/1 has no later segments)
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
