@@ -539,7 +539,9 @@ __global__ __launch_bounds__(256) void k_resume_split(TraceArgs a, int q, int le
             const bool run = rc == DdaRun;
             if (__ballot(run) == 0ull) break;
             if (run) rc = dda_iter<OCC, BOX>(a.world, st, h);
-            if (rc == DdaRun && (__ballot(rc == DdaEvent) & below)) rc = DdaNone;  // an earlier piece has it
+            // (the ballot outside the condition: every lane's event must be seen)
+            const unsigned long long evNow = __ballot(rc == DdaEvent);
+            if (rc == DdaRun && (evNow & below)) rc = DdaNone;  // an earlier piece has it
         }
         const unsigned long long ev = __ballot(rc == DdaEvent) & gmask;
         const int first = ev ? __ffsll((long long)ev) - 1 - gbase : 0;
