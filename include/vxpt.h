@@ -143,7 +143,7 @@ typedef struct vxpt_tuning {
     int32_t brick_steps;      /* in-brick cell crossings before a queued walk yields, 1..64            (3) */
     int32_t cam_steps;        /* the same for camera / continuing path rays (k_closest), 1..64         (10) */
     int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (6) */
-    int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024      (0) */
+    int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024     (16) */
     int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (16) */
     int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (0) */
     int32_t overlap;          /* 1: pass halves and pipelined frames on two streams; 0: in order        (1) */
@@ -154,7 +154,8 @@ typedef struct vxpt_tuning {
     int32_t stencil_tile;     /* tile edge of the history clamp and the first a-trous, 16 or 32        (16) */
     int32_t front_streams;    /* streams for the passes' first halves (by state set), 1..3: side by side (2) */
     int32_t lds_bricks;       /* 1: camera walks read bricks through a workgroup cache in LDS           (0) */
-    int32_t resume_split;     /* straggler walks cut into 1, 2, 4, 8 or 16 pieces walked side by side     (1) */
+    int32_t resume_split;     /* the last straggler level's walks cut into 1, 2, 4, 8 or 16 pieces walked
+                                 side by side                                                          (16) */
     int32_t later_split;      /* the later path segments' stragglers: after 8 more iterations, in 1-16 pieces (16) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);

@@ -151,7 +151,8 @@ vxpt_tuning tuning_defaults() {
     t.brick_steps = 3;        // in-brick walks yield after 3 crossings: 6.44 -> 6.26 ms
     t.cam_steps = 10;         // camera rays walk whole bricks
     t.iter_cap = 6;           // caps 4 / 6 / 8 / 12: 7.02 / 6.84 / 7.07 / 7.63 ms
-    t.iter_cap2 = 0;          // a second level (6 + 16): 7.59 ms
+    t.iter_cap2 = 16;         // a second level after 16 more iterations, its walks in resume_split pieces:
+                              // 5.74 -> 5.66-5.68 ms (one lane per walk at that level: 7.59 ms, round 2)
     t.resume_wg_per_cu = 16;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms
     t.sort_mode = 0;          // direction-class sort: 1.5 % faster traversal, producers pay it back
     t.overlap = 1;            // pass halves on two streams: 6.84 -> 6.06 ms
@@ -161,7 +162,7 @@ vxpt_tuning tuning_defaults() {
     t.hf_split = 4;           // 16.3 -> 11.8 us history fix (with readlane sums)
     t.stencil_tile = 16;      // 32x32 tiles: 50.0 -> 55.8 / 48.5 -> 52.4 us
     t.lds_bricks = 0;
-    t.resume_split = 1;
+    t.resume_split = 16;      // (with iter_cap2 0: every straggler in pieces, 5.73 -> 6.7-9.2 ms)
     t.later_split = 16;       // 4/4 bounces: 16.39 -> 15.67 ms per frame (3/1 has no later segments)
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
