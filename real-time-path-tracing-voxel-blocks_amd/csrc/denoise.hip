@@ -50,9 +50,12 @@ VX_HD V3 wp(const DenoiseArgs &a, int x, int y) { return xyz4(a.wpos[(size_t)cl(
 // the packed plane's value of a pixel: world position of its primary hit and, in w, its 16-bit
 // material read (Load2DUshort1 quirk, ld_ushort) for the a-trous / history-fix material tests,
 // -1 for sky (no tap weight)
-VX_HD float4 wpos_px(const DenoiseArgs &a, int x, int y, float z) {
+VX_HD float4 wpos_px(const DenoiseArgs &a, int x, int y, float z, float mat16) {
     const V3 p = world_pos(a.cam, x, y, z);
-    return make_float4(p.x, p.y, p.z, z > kRange ? -1.0f : ld_ushort(a.material, a.W, a.H, x, y));
+    return make_float4(p.x, p.y, p.z, z > kRange ? -1.0f : mat16);
+}
+VX_HD float4 wpos_px(const DenoiseArgs &a, int x, int y, float z) {
+    return wpos_px(a, x, y, z, ld_ushort(a.material, a.W, a.H, x, y));
 }
 VX_D float smooth_step10(float x) {  // SmoothStep(1, 0, x)
     // (x - 1) / (0 - 1): dividing by -1 is exact and round-to-nearest is sign
@@ -242,10 +245,12 @@ __global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int wy0, int wy1
     const float cd = inb ? a.depth[i] : 0.0f;
     const bool sky = inb && cd > kRange;
     const bool inBand = detect && inb && y >= a.y0 && y < a.y1;
-    // the reservoir is read beside the depth (not behind the sky test): one memory round trip
+    // the reservoir and the 16-bit material are read beside the depth (not behind the sky test): one
+    // memory round trip
     Reservoir r = Reservoir{0u, 0u, 0.f, 0.f, 0.f};
     if (inBand) r = a.reservoir[i];
-    if (inb) a.wpos[i] = wpos_px(a, x, y, cd);
+    const float mat16 = inb ? ld_ushort(a.material, W, H, x, y) : 0.0f;
+    if (inb) a.wpos[i] = wpos_px(a, x, y, cd, mat16);
     const bool valid = inBand && !sky && r.lightData != 0 && isfinite(r.weightSum) && r.weightSum > 0.0f;
     float v = valid ? r.weightSum : 0.0f;
     unsigned cnt = valid ? 1u : 0u;
@@ -373,10 +378,31 @@ VX_D bool map_tile(const DenoiseArgs &a, int &tx, int &ty) {
 }
 
 // ---------------------------------------------------------------- TA
-// The tap functions read their plane through a loader ld(x, y) (the edge-clamped global plane, or
-// the k_temporal workgroup's LDS window)
-template <bool kQuirk, class L>
-VX_HD V4 bicubic12(const L &ld, int W, int H, V2 uv) {
+// The reprojected history is read from the previous frame's 4x4 tap window whose corner is
+// (ox - 1, oy - 1), corners unused: the bicubic filters read its 12 inner taps, the custom bilinear
+// filters, the smoothstep normal filter and the history length its central 2x2 -- every position is
+// known once the pixel is reprojected.  Tap k of the bicubic order (TemporalAccumulation.h's sample
+// order: (x1, y1 - 1), (x1 + 1, y1 - 1), (x1 - 1, y1), ...) sits at window column kBcC[k], row
+// kBcR[k]; bilinear tap j (x0 + (j & 1), y0 + (j >> 1)) is bicubic tap bl_tap(j).
+struct TaWin {
+    int col[4], row[4];  // edge-clamped window columns, and rows times W
+    VX_HD TaWin(int W, int H, int ox, int oy) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            col[k] = cl(ox - 1 + k, W);
+            row[k] = cl(oy - 1 + k, H) * W;
+        }
+    }
+    VX_HD int bc(int k) const {  // plane index of bicubic tap k
+        const int c[12] = {1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 1, 2}, r[12] = {0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3};
+        return row[r[k]] + col[c[k]];
+    }
+};
+VX_HD int bl_tap(int j) { return j == 0 ? 3 : (j == 1 ? 4 : (j == 2 ? 7 : 8)); }
+
+// The filters take their taps' values from tap(k) (bicubic tap k, bilinear tap j), already fetched
+template <bool kQuirk, class T>
+VX_HD V4 bicubic12(const T &tap, int W, int H, V2 uv) {
     const V2 UV(uv.x * (float)W, uv.y * (float)H);
     const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
     const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
@@ -384,9 +410,6 @@ VX_HD V4 bicubic12(const L &ld, int W, int H, V2 uv) {
     const V2 w1 = 1.5f * f3 - 2.5f * f2 + 1.0f;
     const V2 w3 = 0.5f * (f3 - f2);
     const V2 w2 = 1.0f - w0 - w1 - w3;
-    const int x1 = (int)fx, y1 = (int)fy;
-    const int sx[12] = {x1, x1 + 1, x1 - 1, x1, x1 + 1, x1 + 2, x1 - 1, x1, x1 + 1, x1 + 2, x1, x1 + 1};
-    const int sy[12] = {y1 - 1, y1 - 1, y1, y1, y1, y1, y1 + 1, y1 + 1, y1 + 1, y1 + 1, y1 + 2, y1 + 2};
     const float wt[12] = {w1.x * w0.y, w2.x * w0.y, w0.x * w1.y, w1.x * w1.y, w2.x * w1.y, w3.x * w1.y,
                           w0.x * w2.y, w1.x * w2.y, w2.x * w2.y, w3.x * w2.y, w1.x * w3.y, w2.x * w3.y};
     V4 out;
@@ -395,7 +418,7 @@ VX_HD V4 bicubic12(const L &ld, int W, int H, V2 uv) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         sum += wt[k];
-        const V4 v = ld(sx[k], sy[k]);
+        const V4 v = tap(k);
         if (kQuirk) out += v * wt[k];
         else out3 += v.xyz() * wt[k];
     }
@@ -412,8 +435,8 @@ VX_HD void bilinear_taps(int W, int H, V2 uv, int &x0, int &y0, float w[4]) {
     y0 = (int)fy;
     w[0] = w0.x * w0.y; w[1] = w1.x * w0.y; w[2] = w0.x * w1.y; w[3] = w1.x * w1.y;
 }
-template <class L>
-VX_HD V4 bilinear_custom4(const L &ld, int W, int H, V2 uv, const float cw[4]) {
+template <class T>
+VX_HD V4 bilinear_custom4(const T &tap, int W, int H, V2 uv, const float cw[4]) {
     int x0, y0;
     float w[4];
     bilinear_taps(W, H, uv, x0, y0, w);
@@ -424,7 +447,7 @@ VX_HD V4 bilinear_custom4(const L &ld, int W, int H, V2 uv, const float cw[4]) {
         const float wt = w[k] * cw[k];
         const float weight = (wt < 1e-6f) ? 1e-6f : wt;
         sum += weight;
-        out += ld(x0 + (k & 1), y0 + (k >> 1)) * weight;
+        out += tap(k) * weight;
     }
     out /= sum;
     return out;
@@ -444,76 +467,132 @@ VX_HD float bilinear_custom1(const float v[4], int W, int H, V2 uv, const float 
     }
     return out / sum;
 }
-template <class L>
-VX_HD V3 bicubic_smoothstep3(const L &ld, int W, int H, V2 uv) {
+template <class T>
+VX_HD V3 bicubic_smoothstep3(const T &tap, int W, int H, V2 uv) {
     const V2 UV(uv.x * (float)W, uv.y * (float)H);
     const float fx = floorf(UV.x - 0.5f), fy = floorf(UV.y - 0.5f);
     const V2 fr = UV - V2(fx + 0.5f, fy + 0.5f), f2 = fr * fr, f3 = f2 * fr;
     const V2 w1 = -2.0f * f3 + 3.0f * f2;
     const V2 w0 = 1.0f - w1;
-    const int x0 = (int)fx, y0 = (int)fy;
     const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
     V3 out(0.0f);
     float sum = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 4; ++k) {  // tap k at (x0 + (k & 1), y0 + (k >> 1))
         sum += wt[k];
-        out += ld(x0 + (k & 1), y0 + (k >> 1)).xyz() * wt[k];
+        out += tap(k) * wt[k];
     }
     out /= sum;
     return out;
 }
 
-// The planes temporal_px reads around a pixel: edge-clamped global loads.  (A workgroup window of
-// them staged in LDS was measured slower -- 95 -> 109 us, 137 VGPRs -- and removed)
-struct TaGlobal {
-    const DenoiseArgs *a;
-    VX_HD V4 n(int x, int y) const { return ld4(a->normalRough, a->W, a->H, x, y); }
-    VX_HD float pz(int x, int y) const { return ld1(a->prevDepth, a->W, a->H, x, y); }
-    VX_HD V4 pn(int x, int y) const { return ld4(a->prevNormalRough, a->W, a->H, x, y); }
-    VX_HD V4 pi(int x, int y) const { return ld4(a->prevIllum, a->W, a->H, x, y); }
-    VX_HD V4 pf(int x, int y) const { return ld4(a->prevFast, a->W, a->H, x, y); }
-    VX_HD float ph(int x, int y) const { return ld1(a->prevHistLen, a->W, a->H, x, y); }
-};
-
 // The reprojected history of a pixel (TemporalAccumulation.h loadSurfaceMotionBasedPrevData):
 // the 12 depth taps' validity, the previous normal's test, the bicubic / custom-bilinear history
-// and fast history, and the bilinear history length.
+// and fast history, and the bilinear history length.  Three round trips, none behind a branch: the
+// window's depth, normal and history-length taps; its radiance taps; its fast-history taps (the
+// filter the validity chooses reads a subset of the same 12 positions).  The last two stay apart
+// (VX_TA_FENCE) so that only one set of 12 taps is in flight in registers.  (A workgroup window of
+// the planes staged in LDS was measured slower -- 95 -> 109 us, 137 VGPRs -- and removed, DESIGN.md
+// Appendix A.)
+#ifndef VX_TA_SPLIT
+#define VX_TA_SPLIT 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define VX_TA_FENCE() do { if (VX_TA_SPLIT) __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define VX_TA_FENCE() do { } while (0)
+#endif
+// The previous frame's planes at a plane index: plain loads (host tests) or, in the kernel, buffer
+// loads with a 32-bit offset (one VGPR per tap address instead of a 64-bit pointer)
+struct TaPlanesH {
+    const DenoiseArgs *a;
+    VX_HD float pz(int i) const { return a->prevDepth[i]; }
+    VX_HD V3 pn(int i) const { return xyz4(a->prevNormalRough[i]); }
+    VX_HD float ph(int i) const { return a->prevHistLen[i]; }
+    VX_HD V3 pi(int i) const { return xyz4(a->prevIllum[i]); }
+    VX_HD V3 pf(int i) const { return xyz4(a->prevFast[i]); }
+};
+VX_D __amdgpu_buffer_rsrc_t rsrc(const void *p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, bytes, 0x00020000);
+}
+VX_D float ldb1(__amdgpu_buffer_rsrc_t r, int i) { return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, i * 4, 0, 0)); }
+VX_D V3 ldb3(__amdgpu_buffer_rsrc_t r, int i) {  // xyz of a float4 plane
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, i * 16, 0, 0);
+    return V3(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]));
+}
+VX_D V4 ldb4(__amdgpu_buffer_rsrc_t r, int i) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16, 0, 0);
+    return V4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
+}
+struct TaPlanesD {
+    __amdgpu_buffer_rsrc_t z, n, h, i, f;
+    VX_D explicit TaPlanesD(const DenoiseArgs &a)
+        : z(rsrc(a.prevDepth, a.W * a.H * 4)), n(rsrc(a.prevNormalRough, a.W * a.H * 16)),
+          h(rsrc(a.prevHistLen, a.W * a.H * 4)), i(rsrc(a.prevIllum, a.W * a.H * 16)), f(rsrc(a.prevFast, a.W * a.H * 16)) {}
+    VX_D float pz(int k) const { return ldb1(z, k); }
+    VX_D V3 pn(int k) const { return ldb3(n, k); }
+    VX_D float ph(int k) const { return ldb1(h, k); }
+    VX_D V3 pi(int k) const { return ldb3(i, k); }
+    VX_D V3 pf(int k) const { return ldb3(f, k); }
+};
 struct TaHist {
     V4 prevI;
     V3 prevF;
     float bicValid, found, quality, hist;
 };
-template <class T>
-VX_HD TaHist ta_history(const T &t, int W, int H, const Qt &rot, V3 nIn, V2 prevUV, int ox, int oy, float estDepth,
+template <class P>
+VX_HD TaHist ta_history(const P &pl, int W, int H, const Qt &rot, V3 nIn, V2 prevUV, int ox, int oy, float estDepth,
                         const float thrv[4]) {
-    const int bcx[8] = {0, -1, 1, 2, -1, 0, 2, 1}, bcy[8] = {-1, 0, -1, 0, 1, 2, 1, 2};
+    const TaWin win(W, H, ox, oy);
+    float pz[12], ph[4];
+    V3 pn[4];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) pz[k] = pl.pz(win.bc(k));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int t = win.bc(bl_tap(j));
+        pn[j] = pl.pn(t);
+        ph[j] = pl.ph(t);
+    }
     TaHist r;
     float bicValid = 1.0f;
     float taps[4];
+    // the 8 outer taps in the reference's order ((0,-1), (-1,0), (1,-1), (2,0), (-1,1), (0,2), (2,1),
+    // (1,2) from (ox, oy)), then the central 2x2
+    const int outer[8] = {0, 2, 1, 5, 6, 10, 9, 11};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const float pz = t.pz(ox + bcx[k], oy + bcy[k]);
-        bicValid *= fabsf(pz - estDepth) > thrv[k >> 1] ? 0.0f : 1.0f;
-    }
+    for (int k = 0; k < 8; ++k) bicValid *= fabsf(pz[outer[k]] - estDepth) > thrv[k >> 1] ? 0.0f : 1.0f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float pz = t.pz(ox + (k & 1), oy + (k >> 1));
-        const float v = fabsf(pz - estDepth) > thrv[k] ? 0.0f : 1.0f;
+        const float v = fabsf(pz[bl_tap(k)] - estDepth) > thrv[k] ? 0.0f : 1.0f;
         bicValid *= v;
         taps[k] = v;
     }
-    const V3 pnf = normalize(bicubic_smoothstep3([&](int x, int y) { return t.pn(x, y); }, W, H, prevUV));
+    const V3 pnf = normalize(bicubic_smoothstep3([&](int j) { return pn[j]; }, W, H, prevUV));
     const V3 pnr = normalize(q_rotate(rot, pnf));
     if (dot(nIn, pnr) < 0.0f) {
         taps[0] = taps[1] = taps[2] = taps[3] = 0.0f;
         bicValid = 0.0f;
     }
     const bool useBic = bicValid > 0;
-    const auto li = [&](int x, int y) { return t.pi(x, y); };
-    const auto lf = [&](int x, int y) { return t.pf(x, y); };
-    V4 prevI = useBic ? bicubic12<true>(li, W, H, prevUV) : bilinear_custom4(li, W, H, prevUV, taps);
-    V3 prevF = useBic ? bicubic12<false>(lf, W, H, prevUV).xyz() : bilinear_custom4(lf, W, H, prevUV, taps).xyz();
+    // the radiance taps: only xyz is read (Float4 * scalar takes w from z, LinearMath.h:866-874)
+    V3 pi[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) pi[k] = pl.pi(win.bc(k));
+    const auto li = [&](int k) { return V4(pi[k], 0.0f); };
+    const auto lib = [&](int j) { return V4(pi[bl_tap(j)], 0.0f); };
+    // both filters evaluated and one selected: a branch between them would take the taps' fetches
+    // into it (one dependent fetch after another on a wave whose lanes disagree)
+    const V4 bicI = bicubic12<true>(li, W, H, prevUV), bilI = bilinear_custom4(lib, W, H, prevUV, taps);
+    const V4 prevI = useBic ? bicI : bilI;
+    VX_TA_FENCE();
+    V3 pf[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) pf[k] = pl.pf(win.bc(k));
+    const auto lf = [&](int k) { return V4(pf[k], 0.0f); };
+    const auto lfb = [&](int j) { return V4(pf[bl_tap(j)], 0.0f); };
+    const V3 bicF = bicubic12<false>(lf, W, H, prevUV).xyz(), bilF = bilinear_custom4(lfb, W, H, prevUV, taps).xyz();
+    const V3 prevF = useBic ? bicF : bilF;
     r.prevI = V4(fmaxf(prevI.x, 0.0f), fmaxf(prevI.y, 0.0f), fmaxf(prevI.z, 0.0f), fmaxf(prevI.w, 0.0f));
     r.prevF = max3(prevF, V3(0.0f));
     r.found = (bicValid > 0.0f) ? 2.0f : 1.0f;
@@ -524,41 +603,61 @@ VX_HD TaHist ta_history(const T &t, int W, int H, const Qt &rot, V3 nIn, V2 prev
     if ((taps[0] * 1.0f + taps[1] * 1.0f + taps[2] * 1.0f + taps[3] * 1.0f) == 0.0f) {
         r.found = 0.0f; r.quality = 0.0f; r.hist = 0.0f;
     } else {
-        float histTap[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) histTap[k] = t.ph(ox + (k & 1), oy + (k >> 1));
-        r.hist = bilinear_custom1(histTap, W, H, prevUV, taps);
+        r.hist = bilinear_custom1(ph, W, H, prevUV, taps);
     }
     r.bicValid = bicValid;
     return r;
 }
 
-// Returns whether the history fix must filter the pixel (HistoryFix.h:20-22:
-// non-sky and history <= 4; pixels past the denoising range keep last frame's length).
-VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol) {
+// The pixel's own inputs and its 3x3 normals: the temporal pass's first memory round trip, fetched
+// before anything else (k_temporal issues it ahead of the firefly-list hand-over, the normals staged
+// in LDS for the workgroup's tile)
+struct TaPix {
+    float z;
+    V3 cN, avgN, motion, illum;
+};
+VX_HD TaPix ta_pixel(const DenoiseArgs &a, int x, int y) {
     const int W = a.W, H = a.H;
     const size_t i = (size_t)y * W + x;
-    const float z = a.depth[i];
-    if (z > a.p.denoisingRange) return z <= kRange && a.histLen[i] <= 4.0f;
-    const CamDev &cam = a.cam, &pc = a.prevCam;
-    const TaGlobal g{&a};
-    const V3 cN = f4(a.normalRough[i]).xyz();
-    V3 avgN = cN;
+    TaPix p;
+    p.z = a.depth[i];
+    p.cN = f4(a.normalRough[i]).xyz();
+    V3 avgN = p.cN;
     for (int ax = -1; ax <= 1; ++ax)
         for (int by = -1; by <= 1; ++by) {
             if (ax == 0 && by == 0) continue;
-            avgN += g.n(x + ax, y + by).xyz();
+            avgN += ld4(a.normalRough, W, H, x + ax, y + by).xyz();
         }
+    p.avgN = avgN;
+    p.motion = f4(a.motion[i]).xyz();
+    p.illum = f4(a.illum[i]).xyz();
+    return p;
+}
+
+// Returns whether the history fix must filter the pixel (HistoryFix.h:20-22:
+// non-sky and history <= 4; pixels past the denoising range keep last frame's length).
+// p: the pixel's inputs (ta_pixel); ffCol: its firefly-filtered radiance, if any; pl: the previous
+// frame's planes (TaPlanesH / TaPlanesD)
+template <class P>
+VX_HD bool temporal_px(const DenoiseArgs &a, const P &pl, const Qt &rot, int x, int y, const TaPix &p,
+                       const float4 *ffCol) {
+    const int W = a.W, H = a.H;
+    const size_t i = (size_t)y * W + x;
+    const float z = p.z;
+    if (z > a.p.denoisingRange) return z <= kRange && a.histLen[i] <= 4.0f;
+    const CamDev &cam = a.cam, &pc = a.prevCam;
+    const V3 cN = p.cN;
+    V3 avgN = p.avgN;
     avgN /= 9.0f;
     const V2 pixelUv = (V2((float)x, (float)y) + 0.5f) * V2(a.invW, a.invH);
     const V2 curUV = (V2((float)x, (float)y) + 0.5f) * cam.invRes;
     const V3 view = cam.uv_to_dir(curUV);
-    const V3 cWP = wp(a, x, y);
+    const V3 cWP = cam.pos + view * z;  // world_pos(cam, x, y, z) term for term: the packed plane's value
     const V3 Vv = -normalize(view);
     const float NoV = fabsf(dot(cN, Vv));
-    const V3 prevWP = cWP + f4(a.motion[i]).xyz();
+    const V3 prevWP = cWP + p.motion;
     const V2 prevUV = pc.dir_to_uv(normalize(prevWP - pc.pos));
-    const V3 illum = f4(ffCol ? *ffCol : a.illum[i]).xyz();
+    const V3 illum = ffCol ? xyz4(*ffCol) : p.illum;
     const float m1 = luminance(illum), m2 = m1 * m1;
     const V3 camDelta = pc.pos - cam.pos;
     float par1, par2;
@@ -591,18 +690,24 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
     }
     thr4 -= 1e-6f;
     const float thrv[4] = {thr4.x, thr4.y, thr4.z, thr4.w};
-    const TaHist hh = ta_history(g, W, H, rot, nIn, prevUV, ox, oy, estDepth, thrv);
+    // the quality factor needs no history: computed before the history's round trips, so that
+    // none of its inputs stays live across them
+    float qf;
+    {
+        const V3 Vp = normalize(prevWP - pc.pos);
+        const float NoVp = fabsf(dot(cN, Vp));
+        float sq = (NoVp + 1e-3f) / (NoV + 1e-3f);
+        sq *= sq;
+        sq *= sq;
+        qf = lerpf(0.1f, 1.0f, saturate(sq));
+    }
+    const TaHist hh = ta_history(pl, W, H, rot, nIn, prevUV, ox, oy, estDepth, thrv);
     const V4 prevI = hh.prevI;
     const V3 prevF = hh.prevF;
     const float found = hh.found;
     float quality = hh.quality, hist = hh.hist;
     hist = hist + 1.0f;
-    const V3 Vp = normalize(prevWP - pc.pos);
-    const float NoVp = fabsf(dot(cN, Vp));
-    float sq = (NoVp + 1e-3f) / (NoV + 1e-3f);
-    sq *= sq;
-    sq *= sq;
-    quality *= lerpf(0.1f, 1.0f, saturate(sq));
+    quality *= qf;
     if (quality < 1.0f) {
         hist *= sqrtf(quality);
         hist = fmaxf(hist, 1.0f);
@@ -617,17 +722,22 @@ VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const 
     a.histLen[i] = hist;
     return hist <= 4.0f;
 }
+// the whole temporal step of one pixel with plain loads (tests/native/denoise_driver.hip)
+VX_HD bool temporal_px(const DenoiseArgs &a, const Qt &rot, int x, int y, const float4 *ffCol) {
+    return temporal_px(a, TaPlanesH{&a}, rot, x, y, ta_pixel(a, x, y), ffCol);
+}
 
 // The pixels the history fix must filter (rare once history has built up)
 // are listed per 16x16 tile: hfList[tile*256 + k] = pixel index, hfCount[tile]
 // = k's; no atomics, and the history-fix launch only works on listed pixels.
 // The tile's firefly list (k_firefly) is applied first: its entries go back to the radiance and
 // reservoir planes, and the filtered values of the tile's own pixels are handed over in LDS.
-// 123 VGPRs (4 waves/SIMD); bounding it to 5 waves spills 80-116 B/lane and was slower (89 -> 105 us),
-// and fetching the pixel's inputs before the depth test or the history taps with the depth taps
-// raised it to 130 (3 waves: 100-103 us)
+// The pixel's own inputs are fetched first, before the tile's firefly-list hand-over (a clamped
+// pixel for the grid's padding lanes, so every lane loads unconditionally): the list's round trip and
+// the pixel's overlap, and the history taps follow in two more (ta_history).
+// 4 waves/SIMD (128 VGPRs, 12 B/lane of spill): 94.3 -> 88.8 us against the compiler's 130 VGPRs at 3
 #ifndef VX_WPE_TA
-#define VX_WPE_TA 1  // occupancy bound of k_temporal (waves per SIMD; 1 = the compiler's choice)
+#define VX_WPE_TA 4  // occupancy bound of k_temporal (waves per SIMD; 1 = the compiler's choice)
 #endif
 template <bool ST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_TA))) void k_temporal(DenoiseArgs a, Qt rot) {
@@ -636,6 +746,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_TA))
     int tx, ty;  // supertiles (default) or raster tiles (vxpt_tuning.ta_supertiles = 0)
     if (!map_tile<ST>(a, tx, ty)) return;
     const unsigned tile = ty * ((a.W + 15) / 16) + tx;
+    const int W = a.W, H = a.H;
+    const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);
+    // the pixel's inputs (a clamped pixel for the padding lanes) and the tile's normals with a 1-pixel
+    // apron (18x18, edge-clamped like ld4; one slot more for the staging lanes past it), fetched
+    // before the firefly-list hand-over below
+    constexpr int NT = 18 * 18;
+    __shared__ float sN[3][NT + 1];
+    const size_t i = (size_t)min(y, a.y1 - 1) * W + min(x, W - 1);
+    TaPix px;
+    px.z = a.depth[i];
+    px.motion = xyz4(a.motion[i]);
+    px.illum = xyz4(a.illum[i]);
+    V3 nv[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int k = min((int)threadIdx.x + r * 256, NT - 1);
+        nv[r] = xyz4(a.normalRough[(size_t)cl(a.y0 + ty * 16 - 1 + k / 18, H) * W + cl(tx * 16 - 1 + k % 18, W)]);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int k = min((int)threadIdx.x + r * 256, NT);
+        sN[0][k] = nv[r].x; sN[1][k] = nv[r].y; sN[2][k] = nv[r].z;
+    }
     if (threadIdx.x == 0) {
         const unsigned n = a.ffCount[tile];
         sFFn = n;
@@ -656,8 +789,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_TA))
         __syncthreads();
     }
     const bool own = nff && ((sFFmask[threadIdx.x >> 5] >> (threadIdx.x & 31)) & 1u);
-    const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);
-    const bool fix = x < a.W && y < a.y1 && temporal_px(a, rot, x, y, own ? &sFF[threadIdx.x] : nullptr);
+    {  // the centre normal and the 3x3 sum in ta_pixel's order
+        const auto nrm = [&](int dx, int dy) {
+            const int k = ((int)(threadIdx.x >> 4) + 1 + dy) * 18 + (int)(threadIdx.x & 15) + 1 + dx;
+            return V3(sN[0][k], sN[1][k], sN[2][k]);
+        };
+        px.cN = nrm(0, 0);
+        V3 avgN = px.cN;
+        for (int ax = -1; ax <= 1; ++ax)
+            for (int by = -1; by <= 1; ++by) {
+                if (ax == 0 && by == 0) continue;
+                avgN += nrm(ax, by);
+            }
+        px.avgN = avgN;
+    }
+    const bool fix = x < a.W && y < a.y1 &&
+                     temporal_px(a, TaPlanesD(a), rot, x, y, px, own ? &sFF[threadIdx.x] : nullptr);
     const unsigned long long m = __ballot(fix);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0) sTot[wv] = (unsigned)__popcll(m);
@@ -808,18 +955,18 @@ __global__ __launch_bounds__(256) void k_history_fix(DenoiseArgs a) {
 
 // HistoryClamping's per-pixel step after the 5x5 moments (m1, m2: the fast history's YCoCg; nm1,
 // nm2: the radiance), shared by k_history_clamp (moments from its LDS tile) and the host tests
-VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V3 m2, V3 nm1, float nm2) {
+// center: the fast history's YCoCg at the pixel; pi: its temporal history (ping); noisyC: its radiance
+VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V3 m2, V3 nm1, float nm2, V3 center,
+                            V4 pi, V3 noisyC) {
     m1 /= 25.0f; m2 /= 25.0f; nm1 /= 25.0f; nm2 /= 25.0f;
     const V3 sigma(sqrtf(fmaxf(0.0f, m2.x - m1.x * m1.x)), sqrtf(fmaxf(0.0f, m2.y - m1.y * m1.y)),
                    sqrtf(fmaxf(0.0f, m2.z - m1.z * m1.z)));
     V3 cmin = m1 - 2.0f * sigma, cmax = m1 + 2.0f * sigma;
-    const V3 center = rgb_to_ycocg(f4(a.pong[i]).xyz());
     // LinearMath.h template min / max on Float3 (x-compare), as component selects (a select of whole
     // vectors went through scratch memory)
     const bool useMin = cmin.x < center.x, useMax = cmax.x > center.x;
     cmin = V3(useMin ? cmin.x : center.x, useMin ? cmin.y : center.y, useMin ? cmin.z : center.z);
     cmax = V3(useMax ? cmax.x : center.x, useMax ? cmax.y : center.y, useMax ? cmax.z : center.z);
-    const V4 pi = f4(a.ping[i]);
     const V3 dY = rgb_to_ycocg(pi.xyz());
     const V3 cY(clampf(dY.x, cmin.x, cmax.x), clampf(dY.y, cmin.y, cmax.y), clampf(dY.z, cmin.z, cmax.z));
     V4 outD(ycocg_to_rgb(cY), pi.w);
@@ -845,7 +992,6 @@ VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V
     const float sSig = 4.5f * sigma.x;
     float reset = 0.5f * fmaxf(0.0f, fabsf(dL - nL) - sSig - tSig) / (1.0e-6f + fmaxf(dL, nL) + sSig + tSig);
     reset = saturate(reset);
-    const V3 noisyC = f4(a.illum[i]).xyz();
     outD.set_xyz(lerp3(outD.xyz(), noisyC, reset));
     outR.set_xyz(lerp3(outR.xyz(), noisyC, reset));
     const float oL = luminance(outD.xyz());
@@ -863,27 +1009,41 @@ VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V
 // frame, time 49.7 -> 49.3 us against raster tiles; XCD strips were slower, 51 -> 57 us).
 template <int TS, bool ST>
 __global__ __launch_bounds__(TS * TS) void k_history_clamp(DenoiseArgs a) {
-    constexpr int T = TS + 4, N = T * T;
+    constexpr int T = TS + 4, N = T * T, NT = TS * TS, R = (N + NT - 1) / NT;
     const int W = a.W, H = a.H;
     const int tx = threadIdx.x % TS, ty = threadIdx.x / TS;
     int btx, bty;
     if (!map_tile<ST, TS>(a, btx, bty)) return;
     const int x0 = btx * TS, y0 = a.y0 + bty * TS;
     const int x = x0 + tx, y = y0 + ty;
-    __shared__ float sY[3][N], sR[3][N];
-    for (int k = threadIdx.x; k < N; k += TS * TS) {
-        const int gx = cl(x0 + k % T - 2, W), gy = cl(y0 + k / T - 2, H);
-        const size_t j = (size_t)gy * W + gx;
-        const V3 yc = rgb_to_ycocg(f4(a.pong[j]).xyz());
-        const float4 n = a.illum[j];
+    // one slot more than the tile: the staging rounds' lanes past the tile all store into it, so
+    // that every staging store is unconditional (a store behind a condition takes its fetch into the
+    // branch, behind the other rounds' stores)
+    __shared__ float sY[3][N + 1], sR[3][N + 1];
+    // one memory round trip: the pixel's own inputs (a clamped pixel for the padding lanes) and every
+    // staged tap are fetched before the first is used (the tile's fast history and radiance at the
+    // centre come from the staged tile: the same values)
+    const size_t i = (size_t)min(y, a.y1 - 1) * W + min(x, W - 1);
+    const float z = a.depth[i], hist = a.histLen[i];
+    const V4 pi = f4(a.ping[i]);
+    float4 pg[R], il[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int k = min((int)threadIdx.x + r * NT, N - 1);
+        const size_t j = (size_t)cl(y0 + k / T - 2, H) * W + cl(x0 + k % T - 2, W);
+        pg[r] = a.pong[j];
+        il[r] = a.illum[j];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int k = min((int)threadIdx.x + r * NT, N);
+        const V3 yc = rgb_to_ycocg(xyz4(pg[r]));
         sY[0][k] = yc.x; sY[1][k] = yc.y; sY[2][k] = yc.z;
-        sR[0][k] = n.x; sR[1][k] = n.y; sR[2][k] = n.z;
+        sR[0][k] = il[r].x; sR[1][k] = il[r].y; sR[2][k] = il[r].z;
     }
     __syncthreads();
     if (x >= W || y >= a.y1) return;
-    const size_t i = (size_t)y * W + x;
-    if (a.depth[i] > kRange) return;
-    const float hist = a.histLen[i];
+    if (z > kRange) return;
     V3 m1(0.0f), m2(0.0f), nm1(0.0f);
     float nm2 = 0.0f;
     // one column of taps per iteration: fully unrolled, the 25 taps' LDS values were all held in
@@ -903,7 +1063,9 @@ __global__ __launch_bounds__(TS * TS) void k_history_clamp(DenoiseArgs a) {
             nm1 += nz;
             nm2 += nl * nl;
         }
-    history_clamp_px(a, i, hist, m1, m2, nm1, nm2);
+    const int kc = (ty + 2) * T + tx + 2;
+    history_clamp_px(a, i, hist, m1, m2, nm1, nm2, V3(sY[0][kc], sY[1][kc], sY[2][kc]), pi,
+                     V3(sR[0][kc], sR[1][kc], sR[2][kc]));
 }
 
 // host restatement of the kernel's moments (the same taps in the same order, read from the planes
@@ -925,7 +1087,7 @@ VX_HD void history_clamp_host(const DenoiseArgs &a, int x, int y) {
             nm1 += nz;
             nm2 += nl * nl;
         }
-    history_clamp_px(a, i, hist, m1, m2, nm1, nm2);
+    history_clamp_px(a, i, hist, m1, m2, nm1, nm2, rgb_to_ycocg(f4(a.pong[i]).xyz()), f4(a.ping[i]), f4(a.illum[i]).xyz());
 }
 
 // ---------------------------------------------------------------- A-trous (LDS variant)
@@ -943,28 +1105,42 @@ __global__ __launch_bounds__(TS * TS) void k_atrous_smem(DenoiseArgs a) {
     if (!map_tile<ST, TS>(a, btx, bty)) return;
     const int x0 = btx * TS, y0 = a.y0 + bty * TS;
     const int x = x0 + tx, y = y0 + ty;
-    __shared__ float4 sI[N];
-    __shared__ float sNx[N], sNy[N], sNz[N], sM[N], sPx[N], sPy[N], sPz[N];
-    for (int k = threadIdx.x; k < N; k += TS * TS) {
-        const int gx = cl(x0 + k % T - 2, W), gy = cl(y0 + k / T - 2, H);
-        const size_t j = (size_t)gy * W + gx;
-        sI[k] = a.prevIllum[j];
-        const float4 n = a.normalRough[j], p = a.wpos[j];
-        sNx[k] = n.x; sNy[k] = n.y; sNz[k] = n.z;
-        sM[k] = a.material[j];
-        sPx[k] = p.x; sPy[k] = p.y; sPz[k] = p.z;
+    constexpr int NT = TS * TS, R = (N + NT - 1) / NT, NP = N + 1;
+    // one slot more than the tile: every staging store is unconditional (k_history_clamp)
+    __shared__ float4 sI[NP];
+    __shared__ float sNx[NP], sNy[NP], sNz[NP], sM[NP], sPx[NP], sPy[NP], sPz[NP];
+    // one memory round trip: the pixel's depth and history length (a clamped pixel for the padding
+    // lanes) and every staged tap, fetched before the first is used
+    const size_t i = (size_t)min(y, a.y1 - 1) * W + min(x, W - 1);
+    const float z = a.depth[i], hist = a.histLen[i];
+    float4 vI[R];
+    V3 vN[R], vP[R];
+    float vM[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int k = min((int)threadIdx.x + r * NT, N - 1);
+        const size_t j = (size_t)cl(y0 + k / T - 2, H) * W + cl(x0 + k % T - 2, W);
+        vI[r] = a.prevIllum[j];
+        vN[r] = xyz4(a.normalRough[j]);
+        vM[r] = a.material[j];
+        vP[r] = xyz4(a.wpos[j]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int k = min((int)threadIdx.x + r * NT, N);
+        sI[k] = vI[r];
+        sNx[k] = vN[r].x; sNy[k] = vN[r].y; sNz[k] = vN[r].z;
+        sM[k] = vM[r];
+        sPx[k] = vP[r].x; sPy[k] = vP[r].y; sPz[k] = vP[r].z;
     }
     __syncthreads();
     if (x >= W || y >= a.y1) return;
-    const size_t i = (size_t)y * W + x;
-    const float z = a.depth[i];
     if (z > 500000.0f) return;
     // the centre's normal, position and material come from the staged tile
     const int kc = (ty + 2) * T + tx + 2;
     const V3 cN(sNx[kc], sNy[kc], sNz[kc]);
     const V3 cWP(sPx[kc], sPy[kc], sPz[kc]);
     const float cMat = sM[kc];
-    const float hist = a.histLen[i];
     const float k3[2] = {0.44198f, 0.27901f};
     if (hist >= 3.0f) {
         V4 vs;
@@ -1062,16 +1238,18 @@ struct TileTaps {  // the TSxTS tile at (x0, y0) with an R-pixel apron, zeros ou
     VX_D V4 val(int px, int py, int) const { return f4(sI[k(px, py)]); }
 };
 
+// z, hist: the pixel's depth and history length, fetched by the caller in its first round trip
 template <class Src>
-VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, float4 *out, unsigned step,
-                    unsigned frameIndex, int final, int x, int y) {
+VX_D void atrous_px(const DenoiseArgs &a, const Src &src, float4 *out, unsigned step, unsigned frameIndex, int final,
+                    int x, int y, float z, float hist) {
     const int W = a.W, H = a.H;
     const size_t i = (size_t)y * W + x;
-    const float z = a.depth[i];
     if (z > 500000.0f) {
         if (final) a.output[i] = a.illum[i];  // BufferCopySky
         return;
     }
+    // the output's albedo is fetched beside the taps, not behind the result
+    const float4 al = final ? a.albedo[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     int ofx = 0, ofy = 0;
     if (step > 4) {
         const uint32_t lin = explode((uint32_t)x) | (explode((uint32_t)y) << 1);
@@ -1106,7 +1284,6 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
     const float cMat = cP.w;
     const V3 cN = src.nrm(x, y, W);
     const V3 cWP = cP.xyz();
-    const float hist = a.histLen[i];
     float lobe = a.p.lobeAngleFraction / sqrtf((float)step);
     lobe = lerpf(0.99f, lobe, saturate(hist / 5.0f));
     const V4 c = src.val(x, y, W);
@@ -1145,10 +1322,7 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, const float4 *in, floa
     }
     const V4 res = sum / V4(V3(sumW), sumW * sumW);
     out[i] = tf(res);
-    if (final) {
-        const float4 al = a.albedo[i];
-        a.output[i] = make_float4(res.x * al.x, res.y * al.y, res.z * al.z, 0.0f);
-    }
+    if (final) a.output[i] = make_float4(res.x * al.x, res.y * al.y, res.z * al.z, 0.0f);
 }
 
 __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
@@ -1158,38 +1332,54 @@ __global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in,
     const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.y1) return;
     const GlobalTaps src{Plane4(a.wpos, a.W * a.H), Plane4(a.normalRough, a.W * a.H), Plane4(in, a.W * a.H)};
-    atrous_px(a, src, in, out, step, frameIndex, final, x, y);
+    const size_t i = (size_t)y * a.W + x;
+    atrous_px(a, src, out, step, frameIndex, final, x, y, a.depth[i], a.histLen[i]);
 }
 
 // the tile and its apron staged once in LDS (steps 2 and 4, R = step: 49 -> 36 and 46 -> 36 us)
 template <int R, int TS>
 __global__ __launch_bounds__(TS * TS) void k_atrous_tile(DenoiseArgs a, const float4 *in, float4 *out,
                                                          unsigned step, unsigned frameIndex, int final) {
-    constexpr int T = TileTaps<R, TS>::T;
-    __shared__ float4 sP[T * T], sI[T * T];
-    __shared__ float sNx[T * T], sNy[T * T], sNz[T * T];
+    constexpr int T = TileTaps<R, TS>::T, N = T * T, NT = TS * TS, NR = (N + NT - 1) / NT, NP = N + 1;
+    // one slot more than the tile: every staging store is unconditional (k_history_clamp)
+    __shared__ float4 sP[NP], sI[NP];
+    __shared__ float sNx[NP], sNy[NP], sNz[NP];
     int tx, ty;
     if (!xcd_tile<TS>(a, tx, ty)) return;
     const int W = a.W, H = a.H;
     const int x0 = tx * TS, y0 = a.y0 + ty * TS;
-    for (int k = threadIdx.x; k < T * T; k += TS * TS) {
+    const int x = x0 + (int)(threadIdx.x % TS), y = y0 + (int)(threadIdx.x / TS);
+    // one memory round trip: the pixel's depth and history length (a clamped pixel for the padding
+    // lanes) and every staged tap (from a clamped position; zero outside the frame), fetched before
+    // the first is used
+    const size_t i = (size_t)min(y, a.y1 - 1) * W + min(x, W - 1);
+    const float z = a.depth[i], hist = a.histLen[i];
+    float4 vP[NR], vN[NR], vI[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int k = min((int)threadIdx.x + r * NT, N - 1);
+        const size_t j = (size_t)cl(y0 - R + k / T, H) * W + cl(x0 - R + k % T, W);
+        vP[r] = a.wpos[j];
+        vN[r] = a.normalRough[j];
+        vI[r] = in[j];
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int k = min((int)threadIdx.x + r * NT, N);
         const int gx = x0 - R + k % T, gy = y0 - R + k / T;
-        float4 p = make_float4(0.f, 0.f, 0.f, 0.f), n = p, v = p;
-        if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
-            const size_t j = (size_t)gy * W + gx;
-            p = a.wpos[j];
-            n = a.normalRough[j];
-            v = in[j];
-        }
-        sP[k] = p;
-        sI[k] = v;
-        sNx[k] = n.x; sNy[k] = n.y; sNz[k] = n.z;
+        const float m = (gx >= 0 && gy >= 0 && gx < W && gy < H) ? 1.0f : 0.0f;
+        // zero outside the frame, component by component (a select of whole float4s went through
+        // scratch memory); x * 1 and x * 0 are exact for the finite planes
+        const auto z4 = [&](float4 v) { return make_float4(m != 0.0f ? v.x : 0.0f, m != 0.0f ? v.y : 0.0f,
+                                                            m != 0.0f ? v.z : 0.0f, m != 0.0f ? v.w : 0.0f); };
+        sP[k] = z4(vP[r]);
+        sI[k] = z4(vI[r]);
+        sNx[k] = m != 0.0f ? vN[r].x : 0.0f; sNy[k] = m != 0.0f ? vN[r].y : 0.0f; sNz[k] = m != 0.0f ? vN[r].z : 0.0f;
     }
     __syncthreads();
-    const int x = x0 + (int)(threadIdx.x % TS), y = y0 + (int)(threadIdx.x / TS);
     if (x >= W || y >= a.y1) return;
     const TileTaps<R, TS> src{sP, sI, sNx, sNy, sNz, x0, y0};
-    atrous_px(a, src, in, out, step, frameIndex, final, x, y);
+    atrous_px(a, src, out, step, frameIndex, final, x, y, z, hist);
 }
 
 __global__ __launch_bounds__(256) void k_copy_output(DenoiseArgs a, const float4 *in) {
