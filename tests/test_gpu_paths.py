@@ -173,7 +173,7 @@ def test_firefly_outlier_branch_fires():
     r.trace(0)
     p = _dn_params()
     rng = np.random.default_rng(17)
-    for f in range(2):
+    for f in range(3):
         r.trace(f)
         o.trace(f)
         o.post_trace()
@@ -209,4 +209,7 @@ def test_firefly_outlier_branch_fires():
         for name in ("OUTPUT", "PREV_ILLUM"):
             rel = _rel(r.read(name), o.read(vxpt.BUF[name]))
             assert rel.max() < 1e-4, (f, name, rel.max())
+        # the filtered radiance written back to the plane
+        rel = _rel(r.read("ILLUM"), o.read(0))
+        assert rel.max() < 1e-5, (f, "ILLUM", rel.max())
     r.close()
