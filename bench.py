@@ -325,6 +325,33 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    # bands: after the timed region, 4 more frames with the library's band instrumentation on
+    # (vxpt_band_stats: every frame's trace / denoiser spans, the halo groups' HIP-event time, count and
+    # bytes per neighbour) -- what the first multi-GPU run needs to explain its own scaling
+    band_diag, timing_src = None, "vxpt_timings (the pipelined run's chains)" if pipelined else "vxpt_timings per frame"
+    if world > 1 and not a.primary_only:
+        r.band_stats_enable(True)
+        r.render_frames(frame, 4, a.spp, params)
+        frame += 4
+        st = r.band_stats()
+        r.band_stats_enable(False)
+        nf = max(st["frames"], 1)
+        mine = {"rank": rank, "rows": [st["row_begin"], st["row_end"]], "frames": st["frames"],
+                "trace_ms": round(st["trace_ms"] / nf, 4), "denoise_ms": round(st["denoise_ms"] / nf, 4),
+                "halo_ordered_ms": round(st["exchange_ms"] / nf, 4),
+                "halo_overlapped_ms": round(st["exchange_overlap_ms"] / nf, 4),
+                "halo_groups": round(st["groups"] / nf, 2), "halo_groups_ordered": round(st["groups_ordered"] / nf, 2),
+                "halo_mb_up": round(st["bytes_up"] / nf / 1e6, 3), "halo_mb_down": round(st["bytes_down"] / nf / 1e6, 3)}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        band_diag = {"frames": nf, "what": "per rank and frame, 4 banded frames after the timed region with "
+                     "vxpt_band_stats on: trace / denoiser spans (with their exchanges), HIP-event time inside the "
+                     "ordered and the overlapped halo groups, groups per frame, MB sent up / down",
+                     "ranks": ranks}
+        # every frame's spans (vxpt_timings of a banded run holds its last frame's)
+        trace_ms, denoise_ms = [mine["trace_ms"]], [mine["denoise_ms"]]
+        timing_src = "vxpt_band_stats over the 4 diagnostic frames (every frame's spans)"
+
     band_px = a.width * a.height
     if band is not None:
         band_px = a.width * (band[1] - band[0])
@@ -419,7 +446,8 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "avg_duration_ms": round(dur_ms, 4)},
-            "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4), "primary_hit_frac": round(hit_frac, 4),
+            "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4), "timing_source": timing_src,
+            "band_diag": band_diag, "primary_hit_frac": round(hit_frac, 4),
             # the trace passes over this rank's rows (bands: with their halo exchanges)
             "trace_mpaths_s": round(band_px * spp / (avg_trace * 1e-3) / 1e6, 3),
             "trace_valu_util": valu, "trace_valu_util_source": valu_src,

@@ -403,6 +403,30 @@ int vxpt_band_balance(int height, int nranks, const int32_t *row_splits, const f
 int vxpt_render_frame_linked(vxpt_ctx **ctxs, int n, const vxpt_denoise_params *p, int32_t frame_num,
                              int32_t spp);
 
+/* Halo-exchange instrumentation of a banded context (no reference counterpart; the first multi-GPU
+ * run explains itself with it).  With collection on, every exchange group of a banded
+ * vxpt_render_frame(s) / vxpt_render_frame_linked is bracketed by HIP events on the stream it runs on
+ * (ordered groups on the context stream, overlapped ones on the exchange stream beside the next pass)
+ * and its bytes are counted per neighbour, and each banded frame's trace span (its passes with their
+ * exchanges) and denoiser span are timed.  Totals since the last enable; vxpt_band_stats syncs the
+ * context's streams first.  (vxpt_timings of a banded vxpt_render_frames run holds the last frame's
+ * trace / denoiser split and the run's mean frame time; these spans are every frame's.) */
+typedef struct vxpt_band_stat {
+    int32_t frames;            /* banded frames rendered while collecting */
+    int32_t groups;            /* exchange groups: one RCCL group, or one context's set of linked copies */
+    int32_t groups_ordered;    /* of them, on the context stream (in stream order with the kernels) */
+    float exchange_ms;         /* HIP-event time inside the ordered groups, summed */
+    float exchange_overlap_ms; /* the same for the overlapped groups (exchange stream) */
+    float trace_ms;            /* the frames' trace spans, summed */
+    float denoise_ms;          /* the frames' denoiser spans, summed */
+    double bytes_up;           /* bytes sent to the band above (rank - 1) */
+    double bytes_down;         /* bytes sent to the band below (rank + 1) */
+    int32_t row_begin, row_end;
+} vxpt_band_stat;
+/* on != 0: collection on, totals reset; 0: off */
+int vxpt_band_stats_enable(vxpt_ctx *ctx, int on);
+int vxpt_band_stats(vxpt_ctx *ctx, vxpt_band_stat *out);
+
 /* copy any logical buffer to/from host memory (parity hooks, PNG output).  Uploads of G-buffer planes
  * mark the slots' ReSTIR tap records stale; the next trace rebuilds them from NORMAL_ROUGH, ALBEDO,
  * MAT_PARAM.x and DEPTH (k_pack_rec).  The taps take their geometric normal from NORMAL_ROUGH: the trace

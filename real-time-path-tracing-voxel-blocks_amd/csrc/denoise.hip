@@ -231,8 +231,14 @@ VX_D void firefly_filter_wave(const DenoiseArgs &a, int lane, int x, int y, floa
     a.ffRes[slot] = dst;
 }
 
+// 6 waves/SIMD (80 VGPRs, 12 B/lane of spill in the rare filter): 26.2 -> 23.9 us against the compiler's
+// 84 VGPRs at 5; at 8 (64 VGPRs) the spills reach the detection path: 31.9 us
+#ifndef VX_WPE_FF
+#define VX_WPE_FF 6  // occupancy bound of k_firefly (waves per SIMD; 1 = the compiler's choice)
+#endif
 template <bool FUSED>
-__global__ __launch_bounds__(256) void k_firefly(DenoiseArgs a, int wy0, int wy1, int detect) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_FF))) void k_firefly(DenoiseArgs a, int wy0,
+                                                                                                 int wy1, int detect) {
     const int W = a.W, H = a.H;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int l32 = lane & 31;
@@ -1215,8 +1221,11 @@ __global__ __launch_bounds__(TS * TS) void k_atrous_smem(DenoiseArgs a) {
 // One pixel of an a-trous pass (Atrous.h); taps come from Src: global planes through buffer
 // descriptors (any step, jitter) or an LDS tile with a step-wide apron (steps 2 and 4).  The
 // arithmetic is the same code for both.
+#ifndef VX_A8_BATCH
+#define VX_A8_BATCH 8
+#endif
 struct GlobalTaps {
-    static constexpr bool kBatch = true;  // every tap fetched up front (one round trip)
+    static constexpr int kBatch = VX_A8_BATCH;  // taps fetched together (8: one round trip for all)
     Plane4 pW, pN, pI;
     VX_D V4 wpos(int px, int py, int W) const { return pW[py * W + px]; }
     VX_D V3 nrm(int px, int py, int W) const { return pN[py * W + px].xyz(); }
@@ -1225,7 +1234,7 @@ struct GlobalTaps {
 template <int R, int TS = 16>
 struct TileTaps {  // the TSxTS tile at (x0, y0) with an R-pixel apron, zeros outside the frame
     static constexpr int T = TS + 2 * R;
-    static constexpr bool kBatch = false;  // LDS taps: read where used
+    static constexpr int kBatch = 0;  // LDS taps: read where used
     const float4 *sP, *sI;
     const float *sNx, *sNy, *sNz;
     int x0, y0;
@@ -1270,16 +1279,17 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, float4 *out, unsigned 
     // depth test; out-of-frame taps read 0 and get weight 0 below)
     V4 tP[8], tV[8];
     V3 tN[8];
-    if (Src::kBatch) {
+    const auto fetch = [&](int k0) {  // taps k0 .. k0 + kBatch - 1
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = k0; k < k0 + Src::kBatch; ++k) {
             const int t = k < 4 ? k : k + 1, xx = t % 3 - 1, yy = t / 3 - 1;
             const int px = x + ofx + xx * (int)step, py = y + ofy + yy * (int)step;
             tP[k] = src.wpos(px, py, W);
             tN[k] = src.nrm(px, py, W);
             tV[k] = src.val(px, py, W);
         }
-    }
+    };
+    if (Src::kBatch) fetch(0);
     const V4 cP = src.wpos(x, y, W);
     const float cMat = cP.w;
     const V3 cN = src.nrm(x, y, W);
@@ -1300,6 +1310,7 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, float4 *out, unsigned 
         const int px = x + ofx + xx * (int)step, py = y + ofy + yy * (int)step;
         const bool inside = px >= 0 && py >= 0 && px < W && py < H;
         const float kernel = k3[abs(xx)] * k3[abs(yy)];
+        if (Src::kBatch && k > 0 && k % Src::kBatch == 0) fetch(k);
         if (!Src::kBatch) {
             tP[k] = src.wpos(px, py, W);
             tN[k] = src.nrm(px, py, W);
@@ -1325,8 +1336,11 @@ VX_D void atrous_px(const DenoiseArgs &a, const Src &src, float4 *out, unsigned 
     if (final) a.output[i] = make_float4(res.x * al.x, res.y * al.y, res.z * al.z, 0.0f);
 }
 
-__global__ __launch_bounds__(256) void k_atrous(DenoiseArgs a, const float4 *in, float4 *out, unsigned step,
-                                      unsigned frameIndex, int final) {
+#ifndef VX_WPE_A8
+#define VX_WPE_A8 1  // occupancy bound of k_atrous (waves per SIMD; 1 = the compiler's choice)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_A8))) void k_atrous(
+    DenoiseArgs a, const float4 *in, float4 *out, unsigned step, unsigned frameIndex, int final) {
     int tx, ty;
     if (!xcd_tile(a, tx, ty)) return;
     const int x = tx * 16 + (threadIdx.x & 15), y = a.y0 + ty * 16 + (threadIdx.x >> 4);

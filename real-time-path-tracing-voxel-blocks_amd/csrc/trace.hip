@@ -172,7 +172,8 @@ struct LdsBricks {
         static_assert(BOX, "the LDS brick cache holds box-table entries");
         const int key = nb * 8 + octant_of(s.r);
         const int slot = key & (kLdsBrickSlots - 1);
-        const int k = __hip_atomic_load(&c->key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // acquire: pairs with the filler's release below, so the entry's data is read after its key
+        const int k = __hip_atomic_load(&c->key[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         uint64_t m;
         if (k == key) {
             s.box = c->box[slot];
@@ -183,8 +184,7 @@ struct LdsBricks {
             if (k == -1 && atomicCAS(&c->key[slot], -1, -2) == -1) {
                 c->box[slot] = s.box;
                 c->cm[slot] = m;
-                __threadfence_block();
-                atomicExch(&c->key[slot], key);
+                __hip_atomic_store(&c->key[slot], key, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
         s.dist = (int)(s.box & 0xFFu);
@@ -446,7 +446,9 @@ template <bool OCC, bool BOX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESUME))) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
     const WaveBufs &w = a.wb;
     const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
-    const int shard = wv % kShards, step = gridDim.x * 256 / kShards;
+    // the shard's own wave count (any grid size: shards differ by one wave when 4 x gridDim.x is not a
+    // multiple of kShards)
+    const int shard = wv % kShards, step = ((int)gridDim.x * 4 - shard + kShards - 1) / kShards * 64;
     const int n = (int)*straggler_count(w, level, q, shard);
     const int in = (level - 1) & 1, out = level & 1;
     for (int j = (wv / kShards) * 64 + lane; j - lane < n; j += step) {
@@ -503,7 +505,8 @@ template <bool OCC, bool BOX>
 __global__ __launch_bounds__(256) void k_resume_split(TraceArgs a, int q, int level, int shardCap, int G) {
     const WaveBufs &w = a.wb;
     const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
-    const int per = 64 / G, shard = wv % kShards, step = gridDim.x * 256 / kShards / G;
+    const int per = 64 / G, shard = wv % kShards;
+    const int step = ((int)gridDim.x * 4 - shard + kShards - 1) / kShards * per;  // the shard's waves (k_resume)
     const int n = (int)*straggler_count(w, level, q, shard), in = (level - 1) & 1;
     const int g = lane % G, gbase = lane - g;
     const unsigned long long below = (1ull << lane) - (1ull << gbase);  // the earlier pieces' lanes

@@ -369,6 +369,18 @@ struct vxpt_ctx {
     // pass up to its temporal-reuse kernel (haloDone: recorded after the exchange)
     hipStream_t commStream = nullptr;
     hipEvent_t haloReady = nullptr, haloDone = nullptr;
+    // vxpt_band_stats collection: timing events from a pool (reused after a reset) bracketing each
+    // exchange group (kind 0 on the context stream, 1 on the exchange stream) and each banded frame's
+    // trace (2) and denoiser (3) spans, and the bytes sent to each neighbour
+    struct BandStat {
+        bool on = false;
+        std::vector<hipEvent_t> pool;
+        size_t used = 0;
+        struct Span { size_t e0, e1; int kind; };
+        std::vector<Span> spans;
+        int frames = 0, groups = 0, groupsOrdered = 0;
+        double up = 0.0, down = 0.0;
+    } bst;
     // halo depths the last banded frame exchanged: tap records + reservoirs, histories, G-buffer planes
     int haloTraceRows = 72, haloHistRows = 2, haloPlaneRows = 40;
     bool haloPending = false;
@@ -1331,6 +1343,27 @@ int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows
     return exchange_set(cs, br, overlap);
 }
 
+#define BANDCHK_(expr)                  \
+    do {                                \
+        if (int r_ = (expr)) return r_; \
+    } while (0)
+// a vxpt_band_stats timing event recorded on st (collection on), its pool index
+int stat_mark(vxpt_ctx *c, hipStream_t st, size_t &idx) {
+    auto &b = c->bst;
+    if (b.used == b.pool.size()) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        b.pool.push_back(e);
+    }
+    idx = b.used++;
+    HIPCHK(c, hipEventRecord(b.pool[idx], st));
+    return 0;
+}
+// the bytes a halo plan entry sends, to the neighbour above (peer < rank) or below
+void stat_bytes(vxpt_ctx *c, const Halo &h, size_t rowBytes) {
+    (h.peer < c->rank ? c->bst.up : c->bst.down) += (double)h.sn * (double)rowBytes;
+}
+
 int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, int>> &bufRows, bool overlap) {
     if (cs.size() == 1 && cs[0]->comm) {
         vxpt_ctx *c = cs[0];
@@ -1340,6 +1373,8 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
             HIPCHK(c, hipStreamWaitEvent(c->commStream, c->haloReady, 0));
             st = c->commStream;
         }
+        size_t m0 = 0, m1 = 0;
+        if (c->bst.on) BANDCHK_(stat_mark(c, st, m0));
         if (ncclGroupStart() != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclGroupStart");
         ncclResult_t rc = ncclSuccess;
         for (const auto &br : bufRows)
@@ -1350,12 +1385,19 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
                 char *recv = buffer_rows(c, b, h.ry, rb);
                 if (rc == ncclSuccess) rc = ncclSend(send, (size_t)h.sn * rb, ncclUint8, h.peer, c->comm, st);
                 if (rc == ncclSuccess) rc = ncclRecv(recv, (size_t)h.rn * rb, ncclUint8, h.peer, c->comm, st);
+                if (c->bst.on) stat_bytes(c, h, rb);
             }
         const ncclResult_t re = ncclGroupEnd();  // closes the group whatever failed inside it
         if (rc != ncclSuccess)
             return fail(c, VXPT_ERR_HIP, std::string("ncclSend/ncclRecv (halo exchange): ") + ncclGetErrorString(rc));
         if (re != ncclSuccess)
             return fail(c, VXPT_ERR_HIP, std::string("ncclGroupEnd (halo exchange): ") + ncclGetErrorString(re));
+        if (c->bst.on) {
+            BANDCHK_(stat_mark(c, st, m1));
+            c->bst.spans.push_back({m0, m1, overlap ? 1 : 0});
+            ++c->bst.groups;
+            if (!overlap) ++c->bst.groupsOrdered;
+        }
         if (overlap) {
             HIPCHK(c, hipEventRecord(c->haloDone, c->commStream));
             c->haloPending = true;
@@ -1365,7 +1407,9 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
     // linked contexts of one process: device copies from each neighbour's own rows
     // (never written by an exchange), after every band finished the producing pass
     for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (vxpt_ctx *c : cs)
+    for (vxpt_ctx *c : cs) {
+        size_t m0 = 0, m1 = 0;
+        if (c->bst.on) BANDCHK_(stat_mark(c, c->stream, m0));
         for (const auto &br : bufRows)
             for (const Halo &h : halo_plan(splits_of(c), c->rank, br.second)) {
                 const int b = br.first;
@@ -1373,7 +1417,16 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
                 char *dst = buffer_rows(c, b, h.ry, rb);
                 const char *src = buffer_rows(cs[h.peer], b, h.ry, rb);
                 HIPCHK(c, hipMemcpyAsync(dst, src, (size_t)h.rn * rb, hipMemcpyDeviceToDevice, c->stream));
+                // this band's rows the neighbour copies: what an RCCL rank sends
+                if (c->bst.on) stat_bytes(c, h, rb);
             }
+        if (c->bst.on) {
+            BANDCHK_(stat_mark(c, c->stream, m1));
+            c->bst.spans.push_back({m0, m1, 0});
+            ++c->bst.groups;
+            ++c->bst.groupsOrdered;
+        }
+    }
     for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
     return VXPT_OK;
 }
@@ -1455,6 +1508,9 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         c->haloPlaneRows = planeRows;
     }
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+    std::vector<size_t> mk(cs.size() * 3, 0);  // vxpt_band_stats: trace start, trace end, denoiser end
+    for (size_t k = 0; k < cs.size(); ++k)
+        if (cs[k]->bst.on) BANDCHK(stat_mark(cs[k], cs[k]->stream, mk[3 * k]));
     for (int s = 0; s < spp; ++s) {
         FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false, s + 1 == spp));
         const int res = ((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN;
@@ -1478,6 +1534,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
         HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     }
+    for (size_t k = 0; k < cs.size(); ++k)
+        if (cs[k]->bst.on) BANDCHK(stat_mark(cs[k], cs[k]->stream, mk[3 * k + 1]));
     const int it = it0 + spp, used = it > 0 ? it - 1 : 0;
     if (!p->enable_firefly_filter) FOR_BANDS(run_pass(c, p, 11, 0, 0));
     if (p->enable_firefly_filter) {  // + world positions
@@ -1532,6 +1590,14 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     for (vxpt_ctx *c : cs) {
         HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
         HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+    }
+    for (size_t k = 0; k < cs.size(); ++k) {
+        vxpt_ctx *c = cs[k];
+        if (!c->bst.on) continue;
+        BANDCHK(stat_mark(c, c->stream, mk[3 * k + 2]));
+        c->bst.spans.push_back({mk[3 * k], mk[3 * k + 1], 2});
+        c->bst.spans.push_back({mk[3 * k + 1], mk[3 * k + 2], 3});
+        ++c->bst.frames;
     }
     if (!sync) return VXPT_OK;
     for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1634,6 +1700,7 @@ void vxpt_destroy(vxpt_ctx *c) {
     for (hipStream_t fs : c->frontStreams)
         if (fs) hipStreamDestroy(fs);
     for (hipEvent_t e : c->chainEv) hipEventDestroy(e);
+    for (hipEvent_t e : c->bst.pool) hipEventDestroy(e);
     for (auto &e : c->ev)
         if (e) hipEventDestroy(e);
     for (auto &e : c->runEv)
@@ -3019,6 +3086,43 @@ int vxpt_band_comm_init_rows(vxpt_ctx *c, const void *id, size_t bytes, int nran
 }
 
 int vxpt_band_link(vxpt_ctx **cs, int n) { return vxpt_band_link_rows(cs, n, nullptr); }
+
+int vxpt_band_stats_enable(vxpt_ctx *c, int on) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // no recorded event of the last collection pending
+    if (c->commStream) HIPCHK(c, hipStreamSynchronize(c->commStream));
+    auto &b = c->bst;
+    b.on = on != 0;
+    b.used = 0;
+    b.spans.clear();
+    b.frames = b.groups = b.groupsOrdered = 0;
+    b.up = b.down = 0.0;
+    return VXPT_OK;
+}
+
+int vxpt_band_stats(vxpt_ctx *c, vxpt_band_stat *out) {
+    if (!c || !out) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->commStream) HIPCHK(c, hipStreamSynchronize(c->commStream));
+    const auto &b = c->bst;
+    vxpt_band_stat s{};
+    s.frames = b.frames;
+    s.groups = b.groups;
+    s.groups_ordered = b.groupsOrdered;
+    s.bytes_up = b.up;
+    s.bytes_down = b.down;
+    s.row_begin = c->rowBegin;
+    s.row_end = c->rowEnd;
+    for (const auto &sp : b.spans) {
+        float ms = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&ms, b.pool[sp.e0], b.pool[sp.e1]));
+        (sp.kind == 0 ? s.exchange_ms : sp.kind == 1 ? s.exchange_overlap_ms : sp.kind == 2 ? s.trace_ms : s.denoise_ms) += ms;
+    }
+    *out = s;
+    return VXPT_OK;
+}
 
 int vxpt_band_link_rows(vxpt_ctx **cs, int n, const int32_t *row_splits) {
     if (!cs || n < 1 || !cs[0]) return VXPT_ERR_ARG;

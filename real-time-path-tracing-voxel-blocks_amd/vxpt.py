@@ -108,6 +108,14 @@ class Timing(ctypes.Structure):
                 ("frame_ms", ctypes.c_float)]
 
 
+class BandStat(ctypes.Structure):  # vxpt_band_stat
+    _fields_ = [("frames", ctypes.c_int32), ("groups", ctypes.c_int32), ("groups_ordered", ctypes.c_int32),
+                ("exchange_ms", ctypes.c_float), ("exchange_overlap_ms", ctypes.c_float),
+                ("trace_ms", ctypes.c_float), ("denoise_ms", ctypes.c_float),
+                ("bytes_up", ctypes.c_double), ("bytes_down", ctypes.c_double),
+                ("row_begin", ctypes.c_int32), ("row_end", ctypes.c_int32)]
+
+
 _lib = None
 
 
@@ -159,6 +167,8 @@ def load_library(path=LIB_PATH):
         "vxpt_upload": (I, [P, I, P, ctypes.c_size_t]),
         "vxpt_get_sky_alias": (I, [P, P, P, P, P]),
         "vxpt_timings": (I, [P, ctypes.POINTER(Timing)]),
+        "vxpt_band_stats_enable": (I, [P, I]),
+        "vxpt_band_stats": (I, [P, ctypes.POINTER(BandStat)]),
         "vxpt_tuning_defaults": (I, [ctypes.POINTER(Tuning)]),
         "vxpt_get_tuning": (I, [P, ctypes.POINTER(Tuning)]),
         "vxpt_set_tuning": (I, [P, ctypes.POINTER(Tuning)]),
@@ -541,6 +551,16 @@ class Renderer:
         t = Timing()
         self._chk(self.lib.vxpt_timings(self.ctx, ctypes.byref(t)), "vxpt_timings")
         return dict(trace_ms=t.trace_ms, denoise_ms=t.denoise_ms, sky_ms=t.sky_ms, frame_ms=t.frame_ms)
+
+    def band_stats_enable(self, on=True):
+        """vxpt_band_stats_enable: halo-exchange / band-span collection on (totals reset) or off."""
+        self._chk(self.lib.vxpt_band_stats_enable(self.ctx, 1 if on else 0), "vxpt_band_stats_enable")
+
+    def band_stats(self):
+        """vxpt_band_stats: the totals since the last enable, as a dict."""
+        s = BandStat()
+        self._chk(self.lib.vxpt_band_stats(self.ctx, ctypes.byref(s)), "vxpt_band_stats")
+        return {f: getattr(s, f) for f, _ in s._fields_}
 
     def sync(self):
         self._chk(self.lib.vxpt_sync(self.ctx), "vxpt_sync")

@@ -200,7 +200,7 @@ int main(int argc, char **argv) {
         const bool same = hc.hit == hb.hit && hc.x == hb.x && hc.y == hb.y && hc.z == hb.z && hc.face == hb.face &&
                           hc.id == hb.id && float_as_bits(hc.t) == float_as_bits(hb.t);
         const bool oc = dda_occluded<false>(w, o, d, tmin, tmax), ob = dda_occluded<true>(wb, o, d, tmin, tmax);
-        for (int G : {2, 4, 8}) {
+        for (int G : {2, 4, 8, 16}) {
             const int cap = i % 7;
             Hit hs;
             if (split_walk<false>(wb, o, d, 0.0f, tmax, cap, G, hs) != DdaEvent) hs = Hit{0, 0, 0, 0, -1, 0, kRayMax};

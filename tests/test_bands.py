@@ -752,6 +752,59 @@ def test_gpu_rccl_one_rank_render_frames_matches_plain_context():
         np.testing.assert_array_equal(a.read("OUTPUT").view(np.uint32), b.read("OUTPUT").view(np.uint32))
         t = b.timings()
         assert t["frame_ms"] > 0 and t["trace_ms"] > 0 and t["denoise_ms"] > 0, t
+        # the band instrumentation of the same run: every frame's spans, its exchange groups (a single
+        # rank has no neighbour: nothing sent), results unchanged
+        b.band_stats_enable(True)
+        a.render_frames(4, 3, spp, p)
+        b.render_frames(4, 3, spp, p)
+        st = b.band_stats()
+        np.testing.assert_array_equal(a.read("OUTPUT").view(np.uint32), b.read("OUTPUT").view(np.uint32))
+        assert st["frames"] == 3 and st["groups"] >= 3 * 5 and st["groups_ordered"] < st["groups"], st
+        assert st["bytes_up"] == 0 and st["bytes_down"] == 0, st
+        assert st["trace_ms"] > 0 and st["denoise_ms"] > 0 and st["exchange_ms"] >= 0, st
+        assert (st["row_begin"], st["row_end"]) == (0, h), st
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_band_stats_linked_bands():
+    """vxpt_band_stats over linked contexts (the multi-GPU run's self-description): every frame's
+    trace and denoiser spans, the exchange groups, and the bytes each band sends a neighbour -- the
+    halo plan's rows of every exchanged buffer, the same both ways across a border; results unchanged."""
+    import vxpt
+    w, h, spp, n = 96, 240, 4, 3
+    cam = C1_CAMERA
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    single = make()
+    rs = [make() for _ in range(n)]
+    linked = vxpt.LinkedBands(rs)
+    rows = [bands.band_rows(h, n, k) for k in range(n)]
+    for r in rs:
+        r.band_stats_enable(True)
+    for f in range(3):
+        single.render_frame(f, spp, p)
+        linked.render_frame(f, spp, p)
+    out = np.concatenate([r.read("OUTPUT")[y0:y1] for r, (y0, y1) in zip(rs, rows)])
+    np.testing.assert_array_equal(out.view(np.uint32), single.read("OUTPUT").view(np.uint32))
+    st = [r.band_stats() for r in rs]
+    for k, s in enumerate(st):
+        assert s["frames"] == 3 and s["groups"] >= 3 * 10, s
+        assert s["trace_ms"] > 0 and s["denoise_ms"] > 0 and s["exchange_ms"] > 0, s
+        assert (s["row_begin"], s["row_end"]) == rows[k], s
+    assert st[0]["bytes_up"] == 0 and st[-1]["bytes_down"] == 0
+    for k in range(n - 1):  # a border's rows move the same way both ways (equal band heights)
+        assert st[k]["bytes_down"] > 0 and st[k]["bytes_down"] == st[k + 1]["bytes_up"], (k, st)
+    for r in rs:
+        r.close()
+    single.close()

@@ -66,9 +66,9 @@ def test_box_tables_walk_equals_cube_walk(driver, world, tmp_path):
     import re
     vals = dict(re.findall(r"([a-z-]+) ([0-9.]+)", out.strip().splitlines()[-1]))
     assert int(vals["diff"]) == 0, out
-    # the straggler walks cut into 2 / 4 / 8 pieces (k_resume, vxpt_tuning.resume_split) end as the
+    # the straggler walks cut into 2 / 4 / 8 / 16 pieces (k_resume, vxpt_tuning.resume_split) end as the
     # whole walk, closest hits and occlusion alike
-    assert int(vals["split-runs"]) == 3 * n and int(vals["split-diff"]) == 0, out
+    assert int(vals["split-runs"]) == 4 * n and int(vals["split-diff"]) == 0, out
     assert int(vals["hits"]) > n // 10
     # the box walk also yields every 3 in-brick crossings (more outer iterations), so its count is
     # not compared with the cube walk's; the hits are (above)
