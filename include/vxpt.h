@@ -62,8 +62,15 @@ enum vxpt_buffer {
     VXPT_BUF_TAP_RECORD = 47,    /* read-only: the last pass's ReSTIR tap records, 32 B per pixel (normal xyz,
                                   * roughness with the metallic flag in its sign bit; albedo xyz, depth) --
                                   * the G-buffer planes GetPrevSurface reads (Restir.h:348-381), packed */
-    VXPT_BUF_BOX_TABLES = 48     /* read-only: 8 x nBricks u32, the walk's empty-box extents per brick and ray
+    VXPT_BUF_BOX_TABLES = 48,    /* read-only: 8 x nBricks u32, the walk's empty-box extents per brick and ray
                                   * octant (x | y << 8 | z << 16 bricks; 0 = occupied), box_tables.hpp */
+    VXPT_BUF_CLAMP_DECISION = 49 /* read-only parity hook (vxpt_debug_clamp_decisions): per pixel, a float
+                                  * holding the last denoise's history-clamp decision bits -- 1: the x-only
+                                  * Float3 compare cmin.x < centre.x (HistoryClamping.h:124), 2: cmax.x >
+                                  * centre.x (:125), 4: the pixel's history exceeds 4 frames, so the clamp
+                                  * uses them, 8: its anti-lag factor's quotient (:131) is ill-conditioned
+                                  * (denominator within 1e-3 of the luma, quotient inside (0, 1)); 0 where
+                                  * the clamp did not run */
 };
 
 typedef struct vxpt_config {
@@ -426,6 +433,10 @@ typedef struct vxpt_band_stat {
 /* on != 0: collection on, totals reset; 0: off */
 int vxpt_band_stats_enable(vxpt_ctx *ctx, int on);
 int vxpt_band_stats(vxpt_ctx *ctx, vxpt_band_stat *out);
+
+/* on != 0: the history clamp records its decisions in VXPT_BUF_CLAMP_DECISION (parity hook; one more
+ * plane store per pixel while on) */
+int vxpt_debug_clamp_decisions(vxpt_ctx *ctx, int on);
 
 /* copy any logical buffer to/from host memory (parity hooks, PNG output).  Uploads of G-buffer planes
  * mark the slots' ReSTIR tap records stale; the next trace rebuilds them from NORMAL_ROUGH, ALBEDO,

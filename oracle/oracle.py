@@ -28,7 +28,7 @@ TABLES = os.path.join(REPO, "data", "tables")
 
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
-FLOAT1 = {1, 5, 12, 13, 19, 20}
+FLOAT1 = {1, 5, 12, 13, 19, 20, 49}
 # default cube materials (data/assets/materials.yaml order): (block id, roughness, material id)
 TERRAIN_ROUGHNESS = [0.8, 0.9, 0.85, 0.9, 0.8, 0.7, 0.85, 0.6, 0.7, 0.65, 0.75, 0.75]
 

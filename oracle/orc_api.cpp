@@ -41,6 +41,7 @@ std::vector<float> *f1_buf(Frame &f, int id) {
         case 13: return &f.prevMaterial;
         case 19: return &f.histLen;
         case 20: return &f.prevHistLen;
+        case 49: return &f.clampBits;
         default: return nullptr;
     }
 }

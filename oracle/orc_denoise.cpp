@@ -455,6 +455,7 @@ void pass_history_clamp(Frame &f) {
     for (int y = f.by0(); y < f.by1(); ++y)
         for (int x = 0; x < W; ++x) {
             const size_t i = (size_t)y * W + x;
+            f.clampBits[i] = 0.0f;
             if (f.depth[i] > kRange) continue;
             const float hist = f.histLen[i];
             F3 m1(0.0f), m2(0.0f), nm1(0.0f);
@@ -474,6 +475,7 @@ void pass_history_clamp(Frame &f) {
             F3 cmin = m1 - 2.0f * sigma, cmax = m1 + 2.0f * sigma;
             F3 center = rgb_to_ycocg(f.pong[i].xyz());
             // LinearMath.h:69-72 templates: Float3 operator< / > compare .x only
+            f.clampBits[i] = (float)((cmin.x < center.x ? 1 : 0) | (cmax.x > center.x ? 2 : 0) | (hist > 4.0f ? 4 : 0));
             cmin = (cmin.x < center.x) ? cmin : center;
             cmax = (cmax.x > center.x) ? cmax : center;
             F4 pi = f.ping[i];
@@ -485,6 +487,10 @@ void pass_history_clamp(Frame &f) {
             F4 outR(respC, 0.0f);
             if (hist <= 4.0f) outD.set_xyz(outR.xyz());
             float factor = (cY.x - dY.x) == 0.0f ? 0.0f : saturate((cY.x - dY.x) / (center.x - dY.x));
+            // test diagnostic bit 8: the factor's quotient ill-conditioned (see denoise.hip)
+            if (hist > 4.0f && factor > 0.0f && factor < 1.0f &&
+                std::fabs(center.x - dY.x) <= 1e-3f * std::fmax(std::fabs(center.x), std::fabs(dY.x)))
+                f.clampBits[i] += 8.0f;
             if (hist <= 4.0f) factor = 1.0f;
             float hdl = 10.0f * 0.3f * luminance(abs3(respC - pi.xyz()));
             hdl *= factor;

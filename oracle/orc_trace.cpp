@@ -15,7 +15,7 @@ void Frame::alloc(int w, int h) {
     for (auto *v : {&illum, &normalRough, &geoNormalThin, &albedo, &matParam, &motion, &prevNormalRough,
                     &prevGeoNormalThin, &prevAlbedo, &prevMatParam, &ping, &pong, &prevIllum, &prevFast, &output})
         v->assign(n, F4(0.0f));
-    for (auto *v : {&depth, &material, &prevDepth, &prevMaterial, &histLen, &prevHistLen}) v->assign(n, 0.0f);
+    for (auto *v : {&depth, &material, &prevDepth, &prevMaterial, &histLen, &prevHistLen, &clampBits}) v->assign(n, 0.0f);
     reservoir.assign(2 * n, Reservoir{});
 }
 

@@ -55,6 +55,10 @@ struct Frame {
     std::vector<Reservoir> reservoir;  // 2*W*H, ping-pong on iterationIndex parity
     std::vector<F4> ping, pong, prevIllum, prevFast, output;
     std::vector<float> histLen, prevHistLen;
+    // test diagnostic (buffer 49): the history clamp's decision bits of the last denoise -- 1: the
+    // x-only compare cmin.x < centre.x, 2: cmax.x > centre.x, 4: history > 4 (the clamp uses them),
+    // 8: the clamp's factor quotient ill-conditioned
+    std::vector<float> clampBits;
     void alloc(int w, int h);
 };
 

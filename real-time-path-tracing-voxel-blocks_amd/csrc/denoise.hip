@@ -971,6 +971,7 @@ VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V
     // LinearMath.h template min / max on Float3 (x-compare), as component selects (a select of whole
     // vectors went through scratch memory)
     const bool useMin = cmin.x < center.x, useMax = cmax.x > center.x;
+    if (a.clampDbg) a.clampDbg[i] = (float)((useMin ? 1 : 0) | (useMax ? 2 : 0) | (hist > 4.0f ? 4 : 0));
     cmin = V3(useMin ? cmin.x : center.x, useMin ? cmin.y : center.y, useMin ? cmin.z : center.z);
     cmax = V3(useMax ? cmax.x : center.x, useMax ? cmax.y : center.y, useMax ? cmax.z : center.z);
     const V3 dY = rgb_to_ycocg(pi.xyz());
@@ -980,6 +981,11 @@ VX_HD void history_clamp_px(const DenoiseArgs &a, size_t i, float hist, V3 m1, V
     V4 outR(respC, 0.0f);
     if (hist <= 4.0f) outD.set_xyz(outR.xyz());
     float factor = (cY.x - dY.x) == 0.0f ? 0.0f : saturate((cY.x - dY.x) / (center.x - dY.x));
+    // parity hook: bit 8 -- the factor's quotient is ill-conditioned (its denominator within 1e-3 of
+    // the fast history's luma, the quotient inside (0, 1)): rounding-level input differences move it
+    if (a.clampDbg && hist > 4.0f && factor > 0.0f && factor < 1.0f &&
+        fabsf(center.x - dY.x) <= 1e-3f * fmaxf(fabsf(center.x), fabsf(dY.x)))
+        a.clampDbg[i] += 8.0f;
     if (hist <= 4.0f) factor = 1.0f;
     float hdl = 10.0f * 0.3f * luminance(abs3(respC - pi.xyz()));
     hdl *= factor;
@@ -1049,7 +1055,10 @@ __global__ __launch_bounds__(TS * TS) void k_history_clamp(DenoiseArgs a) {
     }
     __syncthreads();
     if (x >= W || y >= a.y1) return;
-    if (z > kRange) return;
+    if (z > kRange) {
+        if (a.clampDbg) a.clampDbg[i] = 0.0f;
+        return;
+    }
     V3 m1(0.0f), m2(0.0f), nm1(0.0f);
     float nm2 = 0.0f;
     // one column of taps per iteration: fully unrolled, the 25 taps' LDS values were all held in
@@ -1079,7 +1088,10 @@ __global__ __launch_bounds__(TS * TS) void k_history_clamp(DenoiseArgs a) {
 VX_HD void history_clamp_host(const DenoiseArgs &a, int x, int y) {
     const int W = a.W, H = a.H;
     const size_t i = (size_t)y * W + x;
-    if (a.depth[i] > kRange) return;
+    if (a.depth[i] > kRange) {
+        if (a.clampDbg) a.clampDbg[i] = 0.0f;
+        return;
+    }
     const float hist = a.histLen[i];
     V3 m1(0.0f), m2(0.0f), nm1(0.0f);
     float nm2 = 0.0f;
@@ -1433,6 +1445,13 @@ hipError_t launch_firefly(const DenoiseArgs &a, int wy0, int wy1, bool detect, b
     else hipLaunchKernelGGL(k_firefly<false>, g, dim3(256), 0, st, a, wy0, wy1, detect ? 1 : 0);
     if (detect && !fused) hipLaunchKernelGGL(k_firefly_filter, dim3(1024), dim3(64), 0, st, a);
     if (detect && apply) hipLaunchKernelGGL(k_firefly_apply, grid16(a), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+// an empty one-wave kernel: a timing event recorded behind it is stamped once the stream has passed
+// every wait before it (vxpt_render_frames' chain start after the cross-stream hand-off)
+__global__ __launch_bounds__(64) void k_stream_mark() {}
+hipError_t launch_stream_mark(hipStream_t st) {
+    hipLaunchKernelGGL(k_stream_mark, dim3(1), dim3(64), 0, st);
     return hipGetLastError();
 }
 hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st) {

@@ -1152,8 +1152,13 @@ VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) {
     return r;
 }
 
+// stash: an LDS home for the accepted taps' records ([tap][half][thread], k_restir's workgroup), so
+// the bias correction reads them there instead of fetching them again (VX_RESTIR_STASH)
+#ifndef VX_RESTIR_STASH
+#define VX_RESTIR_STASH 1
+#endif
 template <bool MESH>
-VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
+VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*stash)[2][256]) {
     int px, py;
     if (!slot_pixel(a, s, px, py)) return;
     const WaveBufs &w = a.wb;
@@ -1212,13 +1217,18 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
         const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
         SurfS ts;
         V3 vd;
-        if (!prev_surface(a, jit, ts, x, y, nullptr, &vd)) continue;
+        float4 rec[2];
+        if (!prev_surface(a, jit, ts, x, y, nullptr, &vd, rec)) continue;
         if (i == 0) vd0 = vd; else if (i == 1) vd1 = vd; else vd2 = vd;
         const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
         const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
         const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
         if (!(nOk && dOk && rOk)) continue;
         cached |= (1u << i);
+        if (VX_RESTIR_STASH) {
+            stash[i][0][threadIdx.x] = rec[0];
+            stash[i][1][threadIdx.x] = rec[1];
+        }
         Reservoir pr = load_prev_res(a, (size_t)y * a.W + x);
         if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
         if (pr.M > 20.0f) pr.M = 20.0f;
@@ -1243,7 +1253,8 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
             const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
             SurfS ts;
             const V3 vdi = i == 0 ? vd0 : (i == 1 ? vd1 : vd2);
-            prev_surface(a, jit, ts, x, y, &vdi, nullptr);
+            if (VX_RESTIR_STASH) rec_surface(a, stash[i][0][threadIdx.x], stash[i][1][threadIdx.x], vdi, ts);
+            else prev_surface(a, jit, ts, x, y, &vdi, nullptr);
             if (MESH && sel.type == LtLocal) light_from_res(a, sel, rr, ts.pos, hasLocal);  // seen from the tap
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;
@@ -1285,9 +1296,10 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr) {
 
 template <bool MESH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESTIR))) void k_restir(TraceArgs a, int seg) {
+    __shared__ float4 stash[VX_RESTIR_STASH ? 3 : 1][2][256];
     QRays qr;
     qr.mask = 0u;
-    restir_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr);
+    restir_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr, stash);
     block_enqueue(a, 4 * seg + 3, qr);
 }
 

@@ -860,7 +860,22 @@ VX_D int reflect_view(int p, int n) {
 // GetPrevSurface (Restir.h): the previous pass's G-buffer at (x, y).  j = the previous pass's
 // camera jitter of the shading pixel (bn_rand(px, py, iterationIndex - 1, 0 / 1): the same for
 // every tap); vd = the tap's view direction, computed when vdIn is null and returned in vdOut.
-VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const V3 *vdIn, V3 *vdOut) {
+// the surface of a tap record (nr, b) seen along vd
+VX_D void rec_surface(const TraceArgs &a, float4 nr, float4 b, V3 vd, SurfS &sf) {
+    sf.depth = b.w;
+    sf.pos = a.prevCam.pos + vd * sf.depth;
+    sf.wo = -vd;
+    sf.normal = V3(nr.x, nr.y, nr.z);
+    sf.geoNormal = sf.normal;
+    sf.albedo = V3(b.x, b.y, b.z);
+    const int rb = float_as_bits(nr.w);
+    sf.roughness = bits_as_float(rb & 0x7FFFFFFF);
+    sf.metallic = rb < 0;
+    sf.translucency = 0.0f;  // not read by the taps' target pdf (disney_eval)
+}
+// rec: the tap's record, returned when not null (k_restir keeps it for the bias correction)
+VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const V3 *vdIn, V3 *vdOut,
+                       float4 *rec = nullptr) {
     if (x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y) return false;
     const size_t i = (size_t)y * a.W + x;
     // the previous pass's tap record (GBuf::rec): the planes' depth, normal (normalRough and
@@ -869,6 +884,10 @@ VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const 
     sf.depth = b.w;
     if (sf.depth == kRayMax) return false;
     const float4 nr = a.prev.rec[2 * i];
+    if (rec) {
+        rec[0] = nr;
+        rec[1] = b;
+    }
     V3 vd;
     if (vdIn) {
         vd = *vdIn;

@@ -296,6 +296,8 @@ struct DenoiseArgs {
     // thresholds, the frustum scale tanHalfFov.x / (res.x / 2), 1/(maxAcc+1),
     // 1/(maxFast+1)
     float invW, invH, thrB, thrA, frustumK, invAcc1, invFast1;
+    // parity hook (vxpt_debug_clamp_decisions): the history clamp's decision bits per pixel, or null
+    float *clampDbg;
     // launch shapes (vxpt_tuning; host side only: read by the launch functions)
     struct {
         int ffFused, taSupertiles, hfSplit, stencilTile;
@@ -357,6 +359,7 @@ hipError_t launch_tri_lights(const float *tri, int nTri, const int *inst, int nI
 
 hipError_t launch_firefly(const DenoiseArgs &a, int wy0, int wy1, bool detect, bool apply, hipStream_t st);
 hipError_t launch_frame0_init(const DenoiseArgs &a, hipStream_t st);
+hipError_t launch_stream_mark(hipStream_t st);
 hipError_t launch_temporal(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_history_fix(const DenoiseArgs &a, hipStream_t st);
 hipError_t launch_history_clamp(const DenoiseArgs &a, hipStream_t st);

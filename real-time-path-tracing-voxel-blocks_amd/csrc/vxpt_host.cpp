@@ -320,6 +320,8 @@ struct vxpt_ctx {
     bool motionZero = true;
     Reservoir *res = nullptr;  // 2*W*H
     float4 *ping = nullptr, *pong = nullptr, *prevIllum = nullptr, *prevFast = nullptr, *output = nullptr;
+    float *clampDbg = nullptr;  // vxpt_debug_clamp_decisions (written while clampDbgOn)
+    bool clampDbgOn = false;
     float *histLen = nullptr, *prevHistLen = nullptr;
     float4 *wpos = nullptr;
     uint32_t *ffCount = nullptr, *ffIndex = nullptr, *hfList = nullptr, *hfCount = nullptr, *ffCandCount = nullptr;
@@ -573,6 +575,7 @@ void fill_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, DenoiseArgs &a, int
     a.ffCand = c->ffCand; a.ffCandCount = c->ffCandCount;
     a.hfList = c->hfList; a.hfCount = c->hfCount;
     a.wpos = c->wpos;
+    a.clampDbg = c->clampDbgOn ? c->clampDbg : nullptr;
     a.invW = 1.0f / (float)c->W; a.invH = 1.0f / (float)c->H;
     a.thrB = a.p.disocclusionThreshold + (1.5f / (float)c->H);
     a.thrA = a.p.disocclusionThresholdAlternate + (1.5f / (float)c->H);
@@ -655,6 +658,7 @@ bool buffer_ptr(vxpt_ctx *c, int which, void *&p, size_t &bytes, bool forWrite, 
         case VXPT_BUF_BLOOM: p = c->bloomB; bytes = n * 16; return c->bloomB != nullptr;
         case VXPT_BUF_LIGHTS: p = c->lights.p; bytes = (size_t)c->nLights * sizeof(LightInfo); return !forWrite && c->nLights;
         case VXPT_BUF_TAP_RECORD: p = g.rec; bytes = n * 32; return !forWrite;
+        case VXPT_BUF_CLAMP_DECISION: p = c->clampDbg; bytes = n * 4; return !forWrite && p;
         case VXPT_BUF_BOX_TABLES: p = c->bbox.p; bytes = (size_t)8 * c->nBricks * 4; return !forWrite && c->bbox.p;
         case VXPT_BUF_LIGHT_ALIAS:
             p = c->lightAlias.p; bytes = (size_t)c->nLights * sizeof(AliasBin); return !forWrite && c->nLights;
@@ -2782,9 +2786,12 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
     const float scale = 1.0f / (float)spp;
     // events around every denoiser chain: the chains run alone (below), so the frames' trace time is
     // the whole minus their sum.  A chain starts when both the frame's last second half (context
-    // stream) and the next frame's first half (its front stream) have finished: a marker behind each,
-    // the later of the two is its start (a marker behind a cross-stream wait is not reliably stamped
-    // after the wait: measured 10-40 us early)
+    // stream) and the next frame's first half (its front stream) have finished.  A marker right behind
+    // the cross-stream wait is not reliably stamped after the wait (measured 10-40 us early), so an
+    // empty one-wave kernel follows the wait and the chain's start marker follows that kernel: the
+    // chain is timed from its first kernel's launch, as in a frame call -- the hand-off's own latency
+    // (~12 us in a kernel trace: the context stream's first launch after the front stream's last
+    // kernel) stays in the frame time, not in the chain's.
     while (c->chainEv.size() < (size_t)3 * nFrames) {
         hipEvent_t e;
         HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -2821,8 +2828,9 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             // before the chain changed nothing -- the frame is still 0.14 ms shorter this way)
             if (!pend.a.primaryOnly) {
                 HIPCHK(c, hipEventRecord(c->chainEv[3 * f + 2], front_stream(c, pend.set)));
-                HIPCHK(c, hipEventRecord(c->chainEv[3 * f], c->stream));
                 HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
+                HIPCHK(c, launch_stream_mark(c->stream));
+                HIPCHK(c, hipEventRecord(c->chainEv[3 * f], c->stream));
             }
         }
         c->denoiseInputIsAccum = spp > 1;
@@ -3086,6 +3094,16 @@ int vxpt_band_comm_init_rows(vxpt_ctx *c, const void *id, size_t bytes, int nran
 }
 
 int vxpt_band_link(vxpt_ctx **cs, int n) { return vxpt_band_link_rows(cs, n, nullptr); }
+
+int vxpt_debug_clamp_decisions(vxpt_ctx *c, int on) {
+    if (!c) return VXPT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (on && !c->clampDbg)  // kept until the context goes (zero-filled)
+        if (int r = dalloc(c, c->clampDbg, (size_t)c->W * c->H)) return r;
+    c->clampDbgOn = on != 0;
+    return VXPT_OK;
+}
 
 int vxpt_band_stats_enable(vxpt_ctx *c, int on) {
     if (!c) return VXPT_ERR_ARG;

@@ -24,8 +24,8 @@ BUF = dict(ILLUM=0, DEPTH=1, NORMAL_ROUGH=2, GEO_NORMAL_THIN=3, ALBEDO=4, MATERI
            PREV_MATERIAL=13, RESERVOIRS=14, PING=15, PONG=16, PREV_ILLUM=17, PREV_FAST=18, HIST_LEN=19,
            PREV_HIST_LEN=20, OUTPUT=21, SKY=32, SUN=33, VOXELS=34, RES_EVEN=35, RES_ODD=36, WPOS=37, FRAME=38,
            OCTANT_TABLES=39, CELL_MASKS=40, BRICK_IDS=41, MACRO_MASKS=42, TEXELS=43, LIGHTS=44,
-           LIGHT_ALIAS=45, BLOOM=46, TAP_RECORD=47, BOX_TABLES=48)
-FLOAT1_BUFS = {1, 5, 12, 13, 19, 20}
+           LIGHT_ALIAS=45, BLOOM=46, TAP_RECORD=47, BOX_TABLES=48, CLAMP_DECISION=49)
+FLOAT1_BUFS = {1, 5, 12, 13, 19, 20, 49}
 RESERVOIR_DTYPE = np.dtype([("lightData", "<u4"), ("uvData", "<u4"), ("weightSum", "<f4"), ("targetPdf", "<f4"),
                             ("M", "<f4")])
 ALIAS_DTYPE = np.dtype([("q", "<f4"), ("p", "<f4"), ("alias", "<i4")])
@@ -168,6 +168,7 @@ def load_library(path=LIB_PATH):
         "vxpt_get_sky_alias": (I, [P, P, P, P, P]),
         "vxpt_timings": (I, [P, ctypes.POINTER(Timing)]),
         "vxpt_band_stats_enable": (I, [P, I]),
+        "vxpt_debug_clamp_decisions": (I, [P, I]),
         "vxpt_band_stats": (I, [P, ctypes.POINTER(BandStat)]),
         "vxpt_tuning_defaults": (I, [ctypes.POINTER(Tuning)]),
         "vxpt_get_tuning": (I, [P, ctypes.POINTER(Tuning)]),
@@ -551,6 +552,10 @@ class Renderer:
         t = Timing()
         self._chk(self.lib.vxpt_timings(self.ctx, ctypes.byref(t)), "vxpt_timings")
         return dict(trace_ms=t.trace_ms, denoise_ms=t.denoise_ms, sky_ms=t.sky_ms, frame_ms=t.frame_ms)
+
+    def debug_clamp_decisions(self, on=True):
+        """vxpt_debug_clamp_decisions: the history clamp records its decision bits (CLAMP_DECISION)."""
+        self._chk(self.lib.vxpt_debug_clamp_decisions(self.ctx, 1 if on else 0), "vxpt_debug_clamp_decisions")
 
     def band_stats_enable(self, on=True):
         """vxpt_band_stats_enable: halo-exchange / band-span collection on (totals reset) or off."""

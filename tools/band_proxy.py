@@ -5,7 +5,7 @@ for N = 1 / 2 / 4 / 8 bands -- the equal bands, then the cost-balanced ones benc
 of vxpt_band_balance on these same band times) -- plus the halo bytes the library's band schedule moves per rank and frame
 (band_frame in vxpt_host.cpp) and their time on one xGMI link.
 
-python tools/band_proxy.py [WIDTH HEIGHT] [--out profiles/r04_band_proxy.json]
+python tools/band_proxy.py [WIDTH HEIGHT] [--out profiles/r05_band_proxy.json]
 """
 import argparse
 import json
@@ -20,6 +20,7 @@ import vxpt  # noqa: E402
 from bench import C1_DIR, band_tuning  # noqa: E402
 
 XGMI_GBS = 153.0   # one xGMI link, one direction (MI355X_MICROARCH.md: 7 links x ~153 GB/s per GPU)
+GROUP_US = 15.0    # latency charged per ordered RCCL group (send/recv to the neighbours), not measurable here
 TRACE_ROWS, HIST_ROWS, PLANE_ROWS = 72, 2, 40   # static camera (vxpt_host.cpp band_frame)
 PLANE_B = 16 + 16 + 16 + 16 + 4 + 4             # depth, normalRough, geoNormalThin, albedo, material, matParam
 
@@ -74,6 +75,35 @@ def time_band(w, h, rows, frames, warmup, spp, tune):
         r.close()
 
 
+def ordered_groups(w, h, spp, frames=3):
+    """Exchange groups per frame of the library's band schedule, counted by vxpt_band_stats over two
+    linked contexts (the same band_frame code as the RCCL path): (ordered, overlapped)."""
+    pos = tuple(p * 4 for p in (35.6184, 11.8733, 42.0387))
+    rs = []
+    try:
+        for _ in range(2):
+            r = vxpt.Renderer(w, h)
+            r.load_settings()
+            r.generate_terrain((8, 8, 8), height_scale=128.0, freq_den=256.0, global_y=True)
+            r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
+            r.set_sky()
+            rs.append(r)
+        linked = vxpt.LinkedBands(rs)
+        p = vxpt.DenoiseParams.defaults()
+        linked.render_frame(0, spp, p)  # frame 0 has its own extra exchange (the history seed)
+        for r in rs:
+            r.band_stats_enable(True)
+        for f in range(1, 1 + frames):
+            linked.render_frame(f, spp, p)
+        st = rs[0].band_stats()
+        # linked contexts exchange every group in stream order; the RCCL path overlaps spp - 1 of them
+        per = st["groups"] / st["frames"]
+        return per - (spp - 1), spp - 1
+    finally:
+        for r in rs:
+            r.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("size", nargs="*", type=int, default=[1920, 1080])
@@ -85,10 +115,15 @@ def main():
     a = ap.parse_args()
     tune = {k: int(v) for k, v in (t.split("=", 1) for t in a.tune)}
     w, h = a.size
+    g_ord, g_ov = ordered_groups(w, h, a.spp)
+    group_ms = g_ord * GROUP_US * 1e-3
     res = {"what": "one-GPU proxy of the band partition: each rank's band of the C3 frame rendered alone "
                    "(single context in band mode, no exchange), and the halo bytes per rank and frame of the "
-                   "library's schedule on one xGMI link (%.0f GB/s per direction)" % XGMI_GBS,
+                   "library's schedule on one xGMI link (%.0f GB/s per direction), plus %.0f us per ordered "
+                   "exchange group (RCCL group latency, charged, not measured)" % (XGMI_GBS, GROUP_US),
            "width": w, "height": h, "spp": a.spp, "tuning": tune or "defaults (bands: bench.band_tuning)",
+           "groups_per_frame": {"ordered": g_ord, "overlapped": g_ov, "counted_by": "vxpt_band_stats, 2 linked contexts"},
+           "group_latency_ms_per_frame": round(group_ms, 4),
            "ranks": {}}
     one = None
 
@@ -121,12 +156,12 @@ def main():
         # an interior rank talks to two neighbours over two links at once: the time of one link's bytes
         link_ms_ordered = od / (XGMI_GBS * 1e9) * 1e3
         link_ms_overlapped = ov / (XGMI_GBS * 1e9) * 1e3
-        proj = slow["frame_ms"] + link_ms_ordered
+        proj = slow["frame_ms"] + link_ms_ordered + (group_ms if n > 1 else 0.0)
         if n == 1:
             one = slow["frame_ms"]
         if balanced:
             balanced["bands"] = balanced_per
-            balanced["projected_frame_ms"] = round(balanced["slowest_band_ms"] + link_ms_ordered, 4)
+            balanced["projected_frame_ms"] = round(balanced["slowest_band_ms"] + link_ms_ordered + group_ms, 4)
             balanced["projected_speedup"] = round(one / balanced["projected_frame_ms"], 3)
         res["ranks"][str(n)] = {
             "balanced": balanced,
@@ -135,7 +170,8 @@ def main():
             "link_ms": {"overlapped": round(link_ms_overlapped, 4), "in_stream_order": round(link_ms_ordered, 4)},
             "projected_frame_ms": round(proj, 4),
             "projected_speedup": round(one / proj, 3) if one else None,
-            "balanced_speedup_bound": round(one / (sum(t["frame_ms"] for t in per) / n + link_ms_ordered), 3)
+            "balanced_speedup_bound": round(one / (sum(t["frame_ms"] for t in per) / n + link_ms_ordered +
+                                                   (group_ms if n > 1 else 0.0)), 3)
             if one else None,
         }
     print(json.dumps(res, indent=1))
