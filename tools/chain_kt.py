@@ -4,7 +4,7 @@ import sqlite3
 import sys
 
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-CHAIN = ("k_firefly", "k_temporal", "k_history_fix", "k_history_clamp", "k_atrous_smem", "k_atrous_tile",
+CHAIN = ("k_firefly", "k_temporal", "k_history_fix", "k_history_clamp", "k_atrous_smem", "k_atrous_tile", "k_atrous_24",
          "k_atrous", "k_firefly_apply")
 db = sqlite3.connect(sys.argv[1])
 rows = list(db.execute("select name, duration from kernels order by start"))
