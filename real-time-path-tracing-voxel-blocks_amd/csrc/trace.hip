@@ -1141,8 +1141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MESH ? 1 : 
 // LoadDIReservoir (Restir.h:48-79): the previous pass's reservoir, its local-light index remapped
 // in the pass after a light update (a light that is gone empties it).  Taken literally: an empty
 // reservoir (lightData 0) reads as index 0 and is remapped as well.
-VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) {
-    Reservoir r = a.resPrev[i];
+VX_D Reservoir remap_prev_res(const TraceArgs &a, Reservoir r) {
     if (!a.lightsDirty) return r;
     const uint32_t li = r.lightData & 0x7FFFFFFFu;
     if (li >= 0x7FFFFFFDu || li >= (uint32_t)a.prevNumLights) return r;  // sun / sky, or not a previous light
@@ -1151,11 +1150,33 @@ VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) {
     r.lightData = (r.lightData & 0x80000000u) | (uint32_t)cur;
     return r;
 }
+VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) { return remap_prev_res(a, a.resPrev[i]); }
+
+// an empty asm that takes and returns the value in VGPRs: the reads producing it complete before this
+// point (restir_slot: several taps' reads in flight together instead of one per branch)
+VX_D void vx_pin(float &v) { asm volatile("" : "+v"(v)); }
+VX_D void vx_pin(int &v) { asm volatile("" : "+v"(v)); }
+VX_D void vx_pin(V3 &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z)); }
+VX_D void vx_pin(float4 &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+VX_D void vx_pin(Reservoir &r) {
+    asm volatile("" : "+v"(r.lightData), "+v"(r.uvData), "+v"(r.weightSum), "+v"(r.targetPdf), "+v"(r.M));
+}
+
+// a, b, c for k = 0, 1, 2, else d -- component by component (a select of whole float4s from an
+// array goes through scratch memory)
+VX_D float pick1(int k, float a, float b, float c, float d) { return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d)); }
+VX_D float4 pick4(int k, float4 a, float4 b, float4 c, float4 d) {
+    return make_float4(pick1(k, a.x, b.x, c.x, d.x), pick1(k, a.y, b.y, c.y, d.y), pick1(k, a.z, b.z, c.z, d.z),
+                       pick1(k, a.w, b.w, c.w, d.w));
+}
 
 // stash: an LDS home for the accepted taps' records ([tap][half][thread], k_restir's workgroup), so
 // the bias correction reads them there instead of fetching them again (VX_RESTIR_STASH)
 #ifndef VX_RESTIR_STASH
 #define VX_RESTIR_STASH 1
+#endif
+#ifndef VX_RESTIR_BATCH
+#define VX_RESTIR_BATCH 1
 #endif
 template <bool MESH>
 VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*stash)[2][256]) {
@@ -1164,16 +1185,40 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     const WaveBufs &w = a.wb;
     int4 meta = load_meta(w, s);
     if (!(meta.x & F_NEE)) return;
+#if VX_RESTIR_BATCH
+    // read ahead with the surface below (functions of the pixel and meta.y only): the temporal disks'
+    // four random numbers, the previous pass's jitter and the RIS sample's visibility
+    float rd0 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y), rd1 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 1),
+          rd2 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 2), rd3 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 3);
+    float jx = bn_rand(a.bn, px, py, a.iterationIndex - 1, 0), jy = bn_rand(a.bn, px, py, a.iterationIndex - 1, 1);
+    // and the next three, for the temporal taps' combine chain
+    float rq0 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 4), rq1 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 5),
+          rq2 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 6);
+    int hit0 = w.oHit[4 * s];
+#endif
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(a, s, px, py, seg, meta.x, skipAlbedo, &sp);
+    SurfS sf = load_surf(a, s, px, py, seg, meta.x, skipAlbedo, &sp);
     const bool hasLocal = MESH && a.numLights > 0;
-    const float4 ris4 = w.rRis[s];
-    Reservoir ris{(uint32_t)float_as_bits(ris4.x), (uint32_t)float_as_bits(ris4.y), ris4.z, ris4.w, 1.0f};
+    float4 ris4 = w.rRis[s];
     LSample ls = load_ls(a, s);
+#if VX_RESTIR_BATCH
+    // every read above completes here (unpinned, the compiler sinks them into the branches below,
+    // where they follow one another)
+    vx_pin(rd0); vx_pin(rd1); vx_pin(rd2); vx_pin(rd3); vx_pin(jx); vx_pin(jy); vx_pin(hit0);
+    vx_pin(rq0); vx_pin(rq1); vx_pin(rq2);
+    vx_pin(sf.pos); vx_pin(sf.normal); vx_pin(sf.geoNormal); vx_pin(sf.albedo); vx_pin(sf.wo);
+    vx_pin(sf.depth); vx_pin(sf.roughness); vx_pin(sp.back); vx_pin(ris4);
+    vx_pin(ls.position); vx_pin(ls.radiance); vx_pin(ls.solidAnglePdf);
+#endif
+    Reservoir ris{(uint32_t)float_as_bits(ris4.x), (uint32_t)float_as_bits(ris4.y), ris4.z, ris4.w, 1.0f};
     bool visible = false;
     if (ls.type != LtInvalid && ris.lightData != 0) {
+#if VX_RESTIR_BATCH
+        visible = !hit0;
+#else
         visible = !w.oHit[4 * s];
+#endif
         if (!visible) { ris.lightData = 0; ris.weightSum = 0; }
     }
     if (!(meta.x & F_RESTIR)) {
@@ -1197,6 +1242,18 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     // three temporal taps (scalars, not arrays: no runtime-indexed private memory)
     const int ox0 = ppx - px, oy0 = ppy - py;
     int ox1, oy1, ox2, oy2;
+#if VX_RESTIR_BATCH
+    {
+        const V2 dsk = restir_disk(rd0, rd1);
+        ox1 = ppx - px + (int)dsk.x; oy1 = ppy - py + (int)dsk.y;
+    }
+    {
+        const V2 dsk = restir_disk(rd2, rd3);
+        ox2 = (int)dsk.x; oy2 = (int)dsk.y;
+    }
+    rng.idx += 4;
+    const V2 jit(jx, jy);
+#else
     {
         const float r0 = rng.next(), r1 = rng.next();
         const V2 dsk = restir_disk(r0, r1);
@@ -1207,11 +1264,85 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
         const V2 dsk = restir_disk(r0, r1);
         ox2 = (int)dsk.x; oy2 = (int)dsk.y;
     }
+    const V2 jit(bn_rand(a.bn, px, py, a.iterationIndex - 1, 0), bn_rand(a.bn, px, py, a.iterationIndex - 1, 1));
+#endif
     unsigned cached = 0;
     int selLoop = -1;
     float tapM0 = 0, tapM1 = 0, tapM2 = 0;
-    const V2 jit(bn_rand(a.bn, px, py, a.iterationIndex - 1, 0), bn_rand(a.bn, px, py, a.iterationIndex - 1, 1));
     V3 vd0(0.0f), vd1(0.0f), vd2(0.0f);  // the accepted taps' view directions, for the bias correction
+#if VX_RESTIR_BATCH
+    // the taps' memory reads go out together instead of tap after tap: every tap's record and previous
+    // reservoir (a rejected tap's reservoir is read and dropped), then the acceptance tests, then every
+    // tap's environment-light entry, then the combine chain in tap order (the same operations on the
+    // same values as the loop below)
+    float4 tb[3], tn[3];
+    Reservoir tr[3];
+    bool tin[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
+        tin[i] = x >= 0 && y >= 0 && x < (int)a.prevCam.res.x && y < (int)a.prevCam.res.y;
+        const size_t ti = tin[i] ? (size_t)y * a.W + x : 0;
+        tb[i] = a.prev.rec[2 * ti + 1];
+        tn[i] = a.prev.rec[2 * ti];
+        tr[i] = a.resPrev[ti];
+    }
+    // (held here: without the pins the compiler sinks each tap's reads into its own branch below,
+    // one memory round trip per tap again)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        vx_pin(tb[i]);
+        vx_pin(tn[i]);
+        vx_pin(tr[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (!tin[i] || tb[i].w == kRayMax) continue;  // prev_surface: off screen or sky
+        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
+        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
+        const V3 vd = a.prevCam.uv_to_dir((V2((float)x, (float)y) + jit) * a.prevCam.invRes);
+        SurfS ts;
+        rec_surface(a, tn[i], tb[i], vd, ts);
+        if (i == 0) vd0 = vd; else if (i == 1) vd1 = vd; else vd2 = vd;
+        const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
+        const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
+        const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
+        if (!(nOk && dOk && rOk)) continue;
+        cached |= (1u << i);
+        if (VX_RESTIR_STASH) {
+            stash[i][0][threadIdx.x] = tn[i];
+            stash[i][1][threadIdx.x] = tb[i];
+        }
+    }
+    float4 te[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        Reservoir pr = remap_prev_res(a, tr[i]);
+        if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
+        if (pr.M > 20.0f) pr.M = 20.0f;
+        tr[i] = pr;
+        te[i] = env_entry(a.sky, pr);
+    }
+    const float4 teRis = env_entry(a.sky, ris);  // the combined reservoir's light when no tap is selected
+    int nDraw = 0;  // the k-th accepted tap draws rng's k-th next value (rq0..2, read ahead)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (!(cached & (1u << i))) continue;
+        Reservoir pr = tr[i];
+        if (i == 0) tapM0 = pr.M; else if (i == 1) tapM1 = pr.M; else tapM2 = pr.M;
+        float nw = 0.0f;
+        LSample cand = invalid_ls();
+        if (pr.lightData != 0) {
+            if (!light_from_entry(a, cand, pr, sf.pos, hasLocal, te[i])) pr = empty_res();
+            nw = target_pdf(cand, sf);
+        }
+        const float rnd = nDraw == 0 ? rq0 : (nDraw == 1 ? rq1 : rq2);
+        ++nDraw;
+        if (combine(rr, pr, rnd, nw)) { ls = cand; selLoop = i; }
+    }
+    rng.idx += nDraw;
+#else
     for (int i = 0; i < 3; ++i) {
         const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
         const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
@@ -1241,11 +1372,18 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
         }
         if (combine(rr, pr, rng.next(), nw)) { ls = cand; selLoop = i; }
     }
+#endif
     // bias-correction rays: the selected light seen from each accepted tap's surface
     float psv0 = 0, psv1 = 0, psv2 = 0;
     qr.id0 = 4 * s;
     LSample sel = invalid_ls();  // the combined reservoir's light (environment lights: the same for every tap)
+#if VX_RESTIR_BATCH
+    if (rr.lightData != 0)
+        light_from_entry(a, sel, rr, sf.pos, hasLocal,
+                         pick4(selLoop, te[0], te[1], te[2], teRis));
+#else
     if (rr.lightData != 0) light_from_res(a, sel, rr, sf.pos, hasLocal);
+#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (rr.lightData != 0 && (cached & (1u << i))) {

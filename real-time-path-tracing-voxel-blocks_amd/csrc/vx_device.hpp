@@ -850,6 +850,39 @@ VX_D bool light_from_res(const TraceArgs &a, LSample &ls, const Reservoir &r, V3
     }
     return li < kInvalidLight;
 }
+// light_from_res in two steps, so that several reservoirs' table reads are in flight together:
+// env_entry issues the environment light's radiance read (the sky or sun table entry; for any other
+// light sky entry 0, unused), light_from_entry finishes with it -- light_from_res's values exactly
+VX_D float4 env_entry(const SkyDev &k, const Reservoir &r) {
+    const uint32_t li = r.lightData & kIndexMask;
+    const float ux = (float)(r.uvData & 0xffff) / float(0xffff), uy = (float)(r.uvData >> 16) / float(0xffff);
+    const bool sun = li == kSunLight;
+    const int w = sun ? k.sunW : k.skyW, h = sun ? k.sunH : k.skyH;
+    const int x = clampi(int(ux * w), 0, w - 1), y = clampi(int(uy * h), 0, h - 1);
+    return (sun ? k.sun : k.sky)[(sun || li == kSkyLight) ? (size_t)y * w + x : 0];
+}
+VX_D bool light_from_entry(const TraceArgs &a, LSample &ls, const Reservoir &r, V3 pos, bool hasLocal, float4 e) {
+    const SkyDev &k = a.sky;
+    const uint32_t li = r.lightData & kIndexMask;
+    const float ux = (float)(r.uvData & 0xffff) / float(0xffff), uy = (float)(r.uvData >> 16) / float(0xffff);
+    if (li == kSkyLight) {
+        const int x = clampi(int(ux * k.skyW), 0, k.skyW - 1), y = clampi(int(uy * k.skyH), 0, k.skyH - 1);
+        ls.solidAnglePdf = (k.skyW * k.skyH) / (4.0f * kPi);  // sky_ls at y * skyW + x
+        ls.position = eq_area_sphere_dir((x + 0.5f) / float(k.skyW), (y + 0.5f) / float(k.skyH));
+        ls.radiance = V3(e.x, e.y, e.z);
+        ls.type = LtSky;
+    } else if (li == kSunLight) {
+        const int x = clampi(int(ux * k.sunW), 0, k.sunW - 1), y = clampi(int(uy * k.sunH), 0, k.sunH - 1);
+        ls.solidAnglePdf = (k.sunW * k.sunH) / (kTwoPi * (1.0f - k.sunCosMax));  // sun_ls at y * sunW + x
+        ls.position = eq_area_cone_dir(k.sunDir, (x + 0.5f) / float(k.sunW), (y + 0.5f) / float(k.sunH), k.sunCosMax);
+        ls.radiance = V3(e.x, e.y, e.z);
+        ls.type = LtSun;
+    } else if (hasLocal && li < (uint32_t)a.numLights) {
+        ls = tri_sample(tri_light(a.lights[li]), V2(ux, uy), pos);
+        return true;
+    }
+    return li < kInvalidLight;
+}
 
 VX_D int reflect_view(int p, int n) {
     if (p < 0) p = -p;
