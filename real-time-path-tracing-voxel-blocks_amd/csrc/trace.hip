@@ -86,6 +86,25 @@ VX_D Hit unpack_hit(int4 v, float t) {
 VX_D V3 xyz(float4 v) { return V3(v.x, v.y, v.z); }
 VX_D float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
+// an empty asm that takes and returns the value in VGPRs: the reads producing it complete before this
+// point -- several reads in flight together instead of one per branch (unpinned, the compiler sinks
+// each read into the branch that uses it; k_restir, k_finish)
+VX_D void vx_pin(float &v) { asm volatile("" : "+v"(v)); }
+VX_D void vx_pin(int &v) { asm volatile("" : "+v"(v)); }
+VX_D void vx_pin(V3 &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z)); }
+VX_D void vx_pin(float4 &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+VX_D void vx_pin(Reservoir &r) {
+    asm volatile("" : "+v"(r.lightData), "+v"(r.uvData), "+v"(r.weightSum), "+v"(r.targetPdf), "+v"(r.M));
+}
+
+// a, b, c for k = 0, 1, 2, else d -- component by component (a select of whole float4s from an
+// array goes through scratch memory)
+VX_D float pick1(int k, float a, float b, float c, float d) { return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d)); }
+VX_D float4 pick4(int k, float4 a, float4 b, float4 c, float4 d) {
+    return make_float4(pick1(k, a.x, b.x, c.x, d.x), pick1(k, a.y, b.y, c.y, d.y), pick1(k, a.z, b.z, c.z, d.z),
+                       pick1(k, a.w, b.w, c.w, d.w));
+}
+
 // temporal-reuse disk offset (Restir.h: concentric square-to-disk, radius 64)
 VX_D V2 restir_disk(float r0, float r1) {
     const V2 u = V2(r0 * 2.0f - 1.0f, r1 * 2.0f - 1.0f);
@@ -682,6 +701,28 @@ VX_D void store_ls(const WaveBufs &w, int s, const LSample &ls, int tex) {
     w.ls0[s] = f4(ls.position, bits_as_float((ls.type << 24) | (tex & 0xFFFFFF)));
     if (ls.type == LtLocal) w.ls1[s] = f4(ls.radiance, ls.solidAnglePdf);
 }
+// load_ls in two steps (k_finish): the sun / sky map entry of a stored sample (sky entry 0 for other
+// types, unused), then the sample -- load_ls's values
+VX_D float4 ls_entry(const SkyDev &k, float4 p) {
+    const int tb = float_as_bits(p.w), type = (tb >> 24) & 0xFF, tex = tb & 0xFFFFFF;
+    if (type == LtSun) {
+        const int sx = tex % k.sunW, sy = tex / k.sunW;
+        return k.sun[(size_t)clampi(sy, 0, k.sunH - 1) * k.sunW + clampi(sx, 0, k.sunW - 1)];  // sun_ls_at
+    }
+    return k.sky[(type == LtLocal || type == LtInvalid) ? 0 : (size_t)tex];  // sky_ls_at
+}
+VX_D LSample load_ls_entry(const TraceArgs &a, int s, float4 p, float4 e) {
+    const int type = (float_as_bits(p.w) >> 24) & 0xFF;
+    if (type == LtLocal) {
+        const float4 b = a.wb.ls1[s];
+        return LSample{xyz(p), xyz(b), b.w, LtLocal};
+    }
+    if (type == LtInvalid) return invalid_ls();
+    const SkyDev &k = a.sky;
+    if (type == LtSun)
+        return LSample{xyz(p), V3(e.x, e.y, e.z), (k.sunW * k.sunH) / (kTwoPi * (1.0f - k.sunCosMax)), LtSun};
+    return LSample{xyz(p), V3(e.x, e.y, e.z), (k.skyW * k.skyH) / (4.0f * kPi), LtSky};
+}
 VX_D LSample load_ls(const TraceArgs &a, int s) {
     const WaveBufs &w = a.wb;
     const float4 p = w.ls0[s];
@@ -1152,24 +1193,6 @@ VX_D Reservoir remap_prev_res(const TraceArgs &a, Reservoir r) {
 }
 VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) { return remap_prev_res(a, a.resPrev[i]); }
 
-// an empty asm that takes and returns the value in VGPRs: the reads producing it complete before this
-// point (restir_slot: several taps' reads in flight together instead of one per branch)
-VX_D void vx_pin(float &v) { asm volatile("" : "+v"(v)); }
-VX_D void vx_pin(int &v) { asm volatile("" : "+v"(v)); }
-VX_D void vx_pin(V3 &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z)); }
-VX_D void vx_pin(float4 &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
-VX_D void vx_pin(Reservoir &r) {
-    asm volatile("" : "+v"(r.lightData), "+v"(r.uvData), "+v"(r.weightSum), "+v"(r.targetPdf), "+v"(r.M));
-}
-
-// a, b, c for k = 0, 1, 2, else d -- component by component (a select of whole float4s from an
-// array goes through scratch memory)
-VX_D float pick1(int k, float a, float b, float c, float d) { return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d)); }
-VX_D float4 pick4(int k, float4 a, float4 b, float4 c, float4 d) {
-    return make_float4(pick1(k, a.x, b.x, c.x, d.x), pick1(k, a.y, b.y, c.y, d.y), pick1(k, a.z, b.z, c.z, d.z),
-                       pick1(k, a.w, b.w, c.w, d.w));
-}
-
 // stash: an LDS home for the accepted taps' records ([tap][half][thread], k_restir's workgroup), so
 // the bias correction reads them there instead of fetching them again (VX_RESTIR_STASH)
 #ifndef VX_RESTIR_STASH
@@ -1451,23 +1474,37 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
         return;
     }
     if (!(meta.x & F_NEE) || !(meta.x & F_RESTIR)) return;
+    // every read of the slot's state at once: the surface, the combined reservoir, the taps' record,
+    // the four visibility results (one word), the stored light sample and the continuation (pinned
+    // below: unpinned, the compiler sinks each read into the branch that uses it)
+    const bool one = a.segments == 1;
+    Reservoir rr = w.rRR[s];
+    float4 psv4 = w.tapPsv[s], m4 = w.tapM[s], ls0 = w.ls0[s];
+    int hits = (int)reinterpret_cast<const uint32_t *>(w.oHit)[s];  // oHit[4s .. 4s + 3], low byte first
+    // segment 0 (the only one with temporal reuse); travelled and the primary distance: its hit
+    // distance (sPos.w).  A one-segment pass ends the path here (k_shade stored no continuation).
+    float4 b = one ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : w.pBop[s];
+    float pdf = one ? 1.0f : w.pDir[s].w;
     bool skipAlbedo;
     SurfX sp;
-    const SurfS sf = load_surf(a, s, px, py, 0, meta.x, skipAlbedo, &sp);
-    Reservoir rr = w.rRR[s];
-    const float4 psv4 = w.tapPsv[s], m4 = w.tapM[s];
+    SurfS sf = load_surf(a, s, px, py, 0, meta.x, skipAlbedo, &sp);
+    vx_pin(rr); vx_pin(psv4); vx_pin(m4); vx_pin(ls0); vx_pin(hits); vx_pin(b); vx_pin(pdf);
+    vx_pin(sf.pos); vx_pin(sf.normal); vx_pin(sf.geoNormal); vx_pin(sf.albedo); vx_pin(sf.wo);
+    vx_pin(sf.depth); vx_pin(sf.roughness); vx_pin(sp.back);
     const int selLoop = float_as_bits(m4.z);
     const unsigned cached = (unsigned)float_as_bits(m4.w);
-    LSample ls = invalid_ls();  // restir_slot's selection: a tap's light (from rr) or the RIS sample
-    if (selLoop >= 0) light_from_res(a, ls, rr, sf.pos, a.mesh.nInst > 0 && a.numLights > 0);
-    else ls = load_ls(a, s);
+    // restir_slot's selection: a tap's light (from rr) or the RIS sample; both map entries read together
+    const float4 eR = env_entry(a.sky, rr), eS = ls_entry(a.sky, ls0);
+    LSample ls = invalid_ls();
+    if (selLoop >= 0) light_from_entry(a, ls, rr, sf.pos, a.mesh.nInst > 0 && a.numLights > 0, eR);
+    else ls = load_ls_entry(a, s, ls0, eS);
     if (rr.lightData != 0) {
         float piv = rr.targetPdf, piSum = rr.targetPdf * 1;
         for (int i = 0; i < 3; ++i) {
             if ((cached & (1u << i)) == 0) continue;
             float psv = i == 0 ? psv4.x : (i == 1 ? psv4.y : psv4.z);
             const float M = i == 0 ? psv4.w : (i == 1 ? m4.x : m4.y);
-            if (w.oHit[4 * s + 1 + i]) psv = 0.0f;
+            if ((hits >> (8 * (1 + i))) & 0xFF) psv = 0.0f;  // oHit[4s + 1 + i]
             if (selLoop == i) piv = psv;
             piSum += psv * M;
         }
@@ -1475,18 +1512,13 @@ VX_D void finish_slot(const TraceArgs &a, int s, int px, int py) {
     }
     bool visible = false;
     if (ls.type != LtInvalid) {
-        visible = !w.oHit[4 * s];
+        visible = !(hits & 0xFF);  // oHit[4s]
         if (!visible) { rr.lightData = 0; rr.weightSum = 0; }
     }
     V3 segRad(0.0f);
     if (ls.type != LtInvalid && rr.lightData != 0 && visible) segRad = shade_light(sf, skipAlbedo, ls, rr);
     a.resCur[pi] = rr;
-    // segment 0 (the only one with temporal reuse); travelled and the primary distance: its hit
-    // distance (sPos.w).  A one-segment pass ends the path here (k_shade stored no continuation).
-    const bool one = a.segments == 1;
-    const float4 b = one ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : w.pBop[s];
-    seg_end(a, s, px, py, meta, segRad, xyz(b), one ? 1.0f : w.pDir[s].w, b.w != 0.0f, true, true,
-            a.texEnabled ? sf.depth : 0.0f, sf.depth);
+    seg_end(a, s, px, py, meta, segRad, xyz(b), pdf, b.w != 0.0f, true, true, a.texEnabled ? sf.depth : 0.0f, sf.depth);
     store_meta(w, s, meta);
 }
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_FINISH))) void k_finish(TraceArgs a) {
