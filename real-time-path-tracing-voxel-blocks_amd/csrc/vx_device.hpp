@@ -695,6 +695,7 @@ VX_D unsigned alias_sample(const AliasBin *b, int len, float u, float &pmf) {
     pmf = b[e.alias].p;
     return e.alias;
 }
+
 struct LSample { V3 position, radiance; float solidAnglePdf; int type; };
 
 VX_D V3 ld3(const float4 *p, size_t i) { const float4 v = p[i]; return V3(v.x, v.y, v.z); }
@@ -976,26 +977,17 @@ VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
 }
 
 // ---------------------------------------------------------------- textures
-// VX_TEX_BATCH (apply_textures below): 0 map by map, each map's reads one after another; 1 the four
-// maps' infos, level offsets and every texel each in flight together; 2 the infos and offsets
-// together, then each map's texels together
-#ifndef VX_TEX_BATCH
-#define VX_TEX_BATCH 0
-#endif
 // tex2DLod on an RGBA8 mip chain (TextureManager.cu:228-246: wrap addressing, linear filter,
 // linear mip filter, normalized coordinates, unorm reads, lod clamped to [0, maxLod]).  The
 // hardware's 8-bit fixed-point filter weights are float weights here (the oracle does the same).
-#if VX_TEX_BATCH == 0
 VX_D float4 texel_f(const uchar4 *t, unsigned off, int S, int x, int y) {
     const uchar4 v = t[off + (unsigned)(y * S + x)];
     return make_float4(v.x / 255.0f, v.y / 255.0f, v.z / 255.0f, v.w / 255.0f);
 }
-#endif
 VX_D int wrap_i(int i, int S) {
     const int m = i % S;
     return m < 0 ? m + S : m;
 }
-#if VX_TEX_BATCH == 0
 VX_D V4 tex_bilinear(const uchar4 *t, const TexInfo &ti, int l, float u, float v) {
     const int S = ti.size >> l;
     const float x = u * (float)S - 0.5f, y = v * (float)S - 0.5f;
@@ -1020,7 +1012,6 @@ VX_D V4 tex_lod(const uchar4 *t, const TexInfo &ti, float u, float v, float lod)
     return c0 * (1.0f - fl) + c1 * fl;
 }
 
-#endif
 // Camera::getRayConeWidth (Camera.h:133-149): the angle one pixel subtends
 VX_D float ray_cone_spread(const CamDev &cam, int px, int py) {
     const V2 pc = (V2((float)px, (float)py) + 0.5f) - cam.res / 2.0f;
@@ -1030,162 +1021,6 @@ VX_D float ray_cone_spread(const CamDev &cam, int px, int py) {
     return atanf(sqrtf(pF.x * pF.x + pF.y * pF.y)) - atanf(sqrtf(pN.x * pN.x + pN.y * pN.y));
 }
 
-#if VX_TEX_BATCH != 0
-// One mip level's bilinear tap, its reads split from its arithmetic so that several maps' reads are
-// in flight together: tex_taps gives the level's 4 texel indices (wrap addressing) and weights,
-// tex_mix the filtered value from the 4 texel words
-VX_D void tex_taps(int size, int l, unsigned o, float u, float v, unsigned idx[4], float &ax, float &ay) {
-    const int S = size >> l;
-    const float x = u * (float)S - 0.5f, y = v * (float)S - 0.5f;
-    const float fx = floorf(x), fy = floorf(y);
-    ax = x - fx;
-    ay = y - fy;
-    const int x0 = wrap_i((int)fx, S), x1 = wrap_i((int)fx + 1, S);
-    const int y0 = wrap_i((int)fy, S), y1 = wrap_i((int)fy + 1, S);
-    idx[0] = o + (unsigned)(y0 * S + x0);
-    idx[1] = o + (unsigned)(y0 * S + x1);
-    idx[2] = o + (unsigned)(y1 * S + x0);
-    idx[3] = o + (unsigned)(y1 * S + x1);
-}
-VX_D float4 texel_word(unsigned w) {  // the unorm RGBA8 texel held in w (x in the low byte)
-    return make_float4((float)(w & 255u) / 255.0f, (float)((w >> 8) & 255u) / 255.0f, (float)((w >> 16) & 255u) / 255.0f,
-                       (float)(w >> 24) / 255.0f);
-}
-VX_D V4 tex_mix(unsigned wa, unsigned wb, unsigned wc, unsigned wd, float ax, float ay) {
-    const float4 a = texel_word(wa), b = texel_word(wb), c = texel_word(wc), d = texel_word(wd);
-    const float w00 = (1.0f - ax) * (1.0f - ay), w10 = ax * (1.0f - ay), w01 = (1.0f - ax) * ay, w11 = ax * ay;
-    return V4(a.x * w00 + b.x * w10 + c.x * w01 + d.x * w11, a.y * w00 + b.y * w10 + c.y * w01 + d.y * w11,
-              a.z * w00 + b.z * w10 + c.z * w01 + d.z * w11, a.w * w00 + b.w * w10 + c.w * w01 + d.w * w11);
-}
-VX_D void pin_u(unsigned &v) { asm volatile("" : "+v"(v)); }
-VX_D void pin_i(int &v) { asm volatile("" : "+v"(v)); }
-
-// Textured MaterialState (closesthit.cu:167-254): world-grid uv of the front position, ray-cone
-// lod, albedo x texture, roughness / metallic from textures, tangent-space normal map aligned to
-// the face and blended at strength 0.2.  coneWidth = the ray cone's width at this hit.
-// vertexTc: the mesh triangle's interpolated texcoords (closesthit.cu:189; useVertexTc = a mesh hit)
-// tex2DLod per map: lod clamped to [0, maxLod], levels floor(lod) and the next (clamped), blended by
-// the fraction.  The four maps' reads go out together, step by step (their infos, their levels'
-// offsets, every texel of both levels -- the second level's read even when the lod has no
-// fraction, unused then).
-VX_D void apply_textures(const uchar4 *texels, const TexInfo *tex, const MatDev &m, V3 pos, V3 ng, V3 wo,
-                         float coneWidth, V3 &albedo, float &roughness, bool &metallic, V3 &normal,
-                         bool useVertexTc = false, V2 vertexTc = V2(0.0f, 0.0f)) {
-    V2 tc(0.0f, 0.0f);
-    if (m.worldGridUV) {
-        if (fabsf(ng.x) > 0.9f) tc = V2(fmodf(pos.z, m.uvScale), fmodf(pos.y, m.uvScale));
-        else if (fabsf(ng.y) > 0.9f) tc = V2(fmodf(pos.x, m.uvScale), fmodf(pos.z, m.uvScale));
-        else if (fabsf(ng.z) > 0.9f) tc = V2(fmodf(pos.x, m.uvScale), fmodf(pos.y, m.uvScale));
-    } else if (useVertexTc) {
-        tc = vertexTc;
-    }
-    tc = tc / m.uvScale;
-    const float mip0 = sqrtf(1024.0f * 1024.0f + 1024.0f * 1024.0f);  // MaterialParameter::texSize (1024, 1024)
-    const float lod = log2f(coneWidth / fmaxf(dot(ng, wo), 0.2f) / m.uvScale * 2.0f * mip0) - 3.0f;
-    const unsigned *words = reinterpret_cast<const unsigned *>(texels);
-    int id[4], size[4], maxLod[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        id[t] = m.tex[t];
-        size[t] = 0;
-        maxLod[t] = 0;
-        if (id[t] >= 0) {
-            size[t] = tex[id[t]].size;
-            maxLod[t] = tex[id[t]].maxLod;
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        pin_i(size[t]);
-        pin_i(maxLod[t]);
-    }
-    float fl[4];
-    int l0[4], l1[4];
-    unsigned o0[4], o1[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const float ld = fminf(fmaxf(lod, 0.0f), (float)maxLod[t]);
-        l0[t] = (int)floorf(ld);
-        fl[t] = ld - (float)l0[t];
-        l1[t] = min(l0[t] + 1, maxLod[t]);
-        o0[t] = o1[t] = 0u;
-        if (id[t] >= 0) {
-            o0[t] = tex[id[t]].off[l0[t]];
-            o1[t] = tex[id[t]].off[l1[t]];
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        pin_u(o0[t]);
-        pin_u(o1[t]);
-    }
-#if VX_TEX_BATCH == 2
-    // then map by map: both levels' texels together (the second level only when blended)
-    auto value = [&](int t) -> V4 {  // map t's tex2DLod value
-        unsigned i0[4], i1[4], w[8];
-        float ax0, ay0, ax1, ay1;
-        tex_taps(size[t], l0[t], o0[t], tc.x, tc.y, i0, ax0, ay0);
-        tex_taps(size[t], l1[t], o1[t], tc.x, tc.y, i1, ax1, ay1);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w[k] = words[i0[k]];
-            w[4 + k] = 0u;
-            if (fl[t] > 0.0f) w[4 + k] = words[i1[k]];
-        }
-        const V4 c0 = tex_mix(w[0], w[1], w[2], w[3], ax0, ay0);
-        if (!(fl[t] > 0.0f)) return c0;
-        const V4 c1 = tex_mix(w[4], w[5], w[6], w[7], ax1, ay1);
-        return c0 * (1.0f - fl[t]) + c1 * fl[t];
-    };
-#else
-    unsigned w[4][8];
-    float ax0[4], ay0[4], ax1[4], ay1[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        unsigned i0[4], i1[4];
-        tex_taps(size[t], l0[t], o0[t], tc.x, tc.y, i0, ax0[t], ay0[t]);
-        tex_taps(size[t], l1[t], o1[t], tc.x, tc.y, i1, ax1[t], ay1[t]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w[t][k] = 0u;
-            w[t][4 + k] = 0u;
-            if (id[t] >= 0) {
-                w[t][k] = words[i0[k]];
-                if (fl[t] > 0.0f) w[t][4 + k] = words[i1[k]];  // the second level only when blended
-            }
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pin_u(w[t][k]);
-    auto value = [&](int t) -> V4 {  // map t's tex2DLod value
-        const V4 c0 = tex_mix(w[t][0], w[t][1], w[t][2], w[t][3], ax0[t], ay0[t]);
-        if (!(fl[t] > 0.0f)) return c0;
-        const V4 c1 = tex_mix(w[t][4], w[t][5], w[t][6], w[t][7], ax1[t], ay1[t]);
-        return c0 * (1.0f - fl[t]) + c1 * fl[t];
-    };
-#endif
-    if (id[0] >= 0) {
-        const V4 c = value(0);
-        albedo = albedo * V3(c.x, c.y, c.z);
-    }
-    albedo = max3(albedo, V3(0.001f));
-    if (id[2] >= 0) roughness = value(2).x;
-    if (id[3] >= 0) metallic = value(3).x > 0.5f;
-    if (id[1] >= 0) {
-        const V4 c = value(1);
-        V3 n = normalize(V3(c.x - 0.5f, c.y - 0.5f, c.z - 0.5f));
-        n.x = -n.x;
-        n.y = -n.y;
-        align_vector(ng, n);
-        normal = n;
-    } else {
-        normal = ng;
-    }
-    normal = lerp3(ng, normal, 0.2f);
-}
-#else
 // Textured MaterialState (closesthit.cu:167-254): world-grid uv of the front position, ray-cone
 // lod, albedo x texture, roughness / metallic from textures, tangent-space normal map aligned to
 // the face and blended at strength 0.2.  coneWidth = the ray cone's width at this hit.
@@ -1223,7 +1058,6 @@ VX_D void apply_textures(const uchar4 *texels, const TexInfo *tex, const MatDev 
     }
     normal = lerp3(ng, normal, 0.2f);
 }
-#endif
 
 }  // namespace
 }  // namespace vx
