@@ -164,6 +164,8 @@ typedef struct vxpt_tuning {
     int32_t resume_split;     /* the last straggler level's walks cut into 1, 2, 4, 8 or 16 pieces walked
                                  side by side                                                          (16) */
     int32_t later_split;      /* the later path segments' stragglers: after 8 more iterations, in 1-16 pieces (16) */
+    int32_t restir_waves;     /* k_restir's occupancy: 0 the compiler's register budget (3 waves/SIMD), 4: bounded
+                                 to 4 waves (spills; a small band's launch fits one generation of waves)   (0) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);

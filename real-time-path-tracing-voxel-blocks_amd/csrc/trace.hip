@@ -1455,8 +1455,9 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     store_meta(w, s, meta);
 }
 
-template <bool MESH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESTIR))) void k_restir(TraceArgs a, int seg) {
+// WPE: the occupancy bound (1: the compiler's register budget; 4 for small bands, tuning restir_waves)
+template <bool MESH, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_restir(TraceArgs a, int seg) {
     __shared__ float4 stash[VX_RESTIR_STASH ? 3 : 1][2][256];
     QRays qr;
     qr.mask = 0u;
@@ -1772,8 +1773,9 @@ struct Launcher {
         trav(true, 4 * seg + 2, a.nSlots);
     }
     void restir(int seg) {
-        if (mesh) hipLaunchKernelGGL(k_restir<true>, g, b, 0, st, a, seg);
-        else hipLaunchKernelGGL(k_restir<false>, g, b, 0, st, a, seg);
+        const bool w4 = a.restirWaves == 4;
+        if (mesh) hipLaunchKernelGGL((w4 ? k_restir<true, 4> : k_restir<true, VX_WPE_RESTIR>), g, b, 0, st, a, seg);
+        else hipLaunchKernelGGL((w4 ? k_restir<false, 4> : k_restir<false, VX_WPE_RESTIR>), g, b, 0, st, a, seg);
     }
 };
 }  // namespace

@@ -233,6 +233,7 @@ struct TraceArgs {
     int sortMode;       // ray queues grouped by direction class per workgroup (0 off, 1 octant, 2 octant x axis)
     int ldsBricks;      // k_closest reads bricks through a workgroup cache in LDS (trace.hip LdsBricks)
     int resumeSplit;    // straggler walks cut into this many pieces, one lane each (trace.hip k_resume_split)
+    int restirWaves;    // k_restir's occupancy bound (0: the compiler's, 4: 4 waves/SIMD)
     int laterSplit;     // the same for the queues of a path's later segments, after 8 more iterations
     int writeMotion;    // store the (zero) motion vectors: the plane may hold a host upload
     int writePlanes;    // store the G-buffer planes (0: a frame's passes before its last -- only their tap

@@ -164,6 +164,7 @@ vxpt_tuning tuning_defaults() {
     t.lds_bricks = 0;
     t.resume_split = 16;      // (with iter_cap2 0: every straggler in pieces, 5.73 -> 6.7-9.2 ms)
     t.later_split = 16;       // 4/4 bounces: 16.39 -> 15.67 ms per frame (3/1 has no later segments)
+    t.restir_waves = 0;       // 4 waves: whole frames slower (Appendix A); see bench.band_tuning for bands
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -177,7 +178,8 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.hf_split, 1, 16) && (t.stencil_tile == 16 || t.stencil_tile == 32) && in(t.front_streams, 1, kMaxSets) &&
            in(t.lds_bricks, 0, 1) && (t.resume_split == 1 || t.resume_split == 2 || t.resume_split == 4 ||
                                        t.resume_split == 8 || t.resume_split == 16) &&
-           (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16);
+           (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16) &&
+           (t.restir_waves == 0 || t.restir_waves == 4);
 }
 
 struct vxpt_ctx {
@@ -965,6 +967,7 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.ldsBricks = c->tune.lds_bricks;
     a.resumeSplit = c->tune.resume_split;
     a.laterSplit = c->tune.later_split;
+    a.restirWaves = c->tune.restir_waves;
     a.prevSceneEmpty = c->prevSceneEmpty;
     // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
     a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;
