@@ -186,6 +186,10 @@ bool tuning_valid(const vxpt_tuning &t) {
 #ifndef VX_CHAIN_HOST_GATE
 #define VX_CHAIN_HOST_GATE 1
 #endif
+// banded vxpt_render_frames: 1 = frames pipelined (band_frame's pipe), 0 = frame after frame
+#ifndef VX_BAND_PIPE
+#define VX_BAND_PIPE 1
+#endif
 
 struct vxpt_ctx {
     int W = 0, H = 0, dev = 0, rowBegin = 0, rowEnd = 0;
@@ -1347,7 +1351,10 @@ char *buffer_rows(vxpt_ctx *c, int which, int y, size_t &rowBytes) {
 // received ones before that kernel (they write the other G-buffer slot and
 // reservoir parity).
 // several buffers with their own halo depths in one group (one RCCL launch, one sync point)
-int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, int>> &bufRows, bool overlap = false);
+// after (RCCL, overlap): the exchange starts once that event has completed instead of behind the
+// context stream's work so far (the tap records: after the producing pass's first half)
+int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, int>> &bufRows, bool overlap = false,
+                 hipEvent_t after = nullptr);
 
 int exchange(std::vector<vxpt_ctx *> &cs, const std::vector<int> &bufs, int rows, bool overlap = false) {
     std::vector<std::pair<int, int>> br;
@@ -1376,13 +1383,17 @@ void stat_bytes(vxpt_ctx *c, const Halo &h, size_t rowBytes) {
     (h.peer < c->rank ? c->bst.up : c->bst.down) += (double)h.sn * (double)rowBytes;
 }
 
-int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, int>> &bufRows, bool overlap) {
+int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, int>> &bufRows, bool overlap,
+                 hipEvent_t after) {
     if (cs.size() == 1 && cs[0]->comm) {
         vxpt_ctx *c = cs[0];
         hipStream_t st = c->stream;
         if (overlap) {
-            HIPCHK(c, hipEventRecord(c->haloReady, c->stream));
-            HIPCHK(c, hipStreamWaitEvent(c->commStream, c->haloReady, 0));
+            if (!after) {
+                HIPCHK(c, hipEventRecord(c->haloReady, c->stream));
+                after = c->haloReady;
+            }
+            HIPCHK(c, hipStreamWaitEvent(c->commStream, after, 0));
             st = c->commStream;
         }
         size_t m0 = 0, m1 = 0;
@@ -1469,8 +1480,15 @@ void band_timings(std::vector<vxpt_ctx *> &cs) {
 }
 
 // sync = false (a run of frames, vxpt_render_frames): enqueue the frame and return, so that the host
-// enqueues the next frame while this one runs; the caller syncs after the last
-int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int frame, int spp, bool sync = true) {
+// enqueues the next frame while this one runs; the caller syncs after the last.
+// pipe (the pipelined run, vxpt_render_frames' order for bands): when it holds plans, they are this
+// frame's first pass-halves, enqueued by the previous frame's call beside its last second half, and
+// this call opens with their second halves; with pipeNext this call leaves the next frame's first
+// pass-halves in it (their first halves run beside this frame's last second half and its exchange,
+// the denoiser chain after them), and the next call gates its later first halves on the host behind
+// this frame's chain (vxpt_render_frames' host gate: no front stream parked behind a wait for it).
+int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int frame, int spp, bool sync = true,
+               std::vector<PassPlan> *pipe = nullptr, bool pipeNext = false) {
     const int it0 = frame * spp;
     // halo depths for this frame's camera motion; the previous frame exchanged its last pass's
     // rows and the histories for its own camera: top them up before the first pass reads them
@@ -1523,13 +1541,32 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     std::vector<size_t> mk(cs.size() * 3, 0);  // vxpt_band_stats: trace start, trace end, denoiser end
     for (size_t k = 0; k < cs.size(); ++k)
         if (cs[k]->bst.on) BANDCHK(stat_mark(cs[k], cs[k]->stream, mk[3 * k]));
+    const bool piped = pipe && pipe->size() == cs.size();
     for (int s = 0; s < spp; ++s) {
-        FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false, s + 1 == spp));
+        if (s == 0 && piped) {
+            for (size_t k = 0; k < cs.size(); ++k) BANDCHK(trace_back(cs[k], (*pipe)[k], false));
+            pipe->clear();
+            // the previous frame's denoiser chain reads the old history slot: the later first halves
+            // are enqueued once it has finished
+            for (vxpt_ctx *c : cs) HIPCHK(c, hipEventSynchronize(c->ev[7]));
+        } else {
+            FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false, s + 1 == spp));
+        }
+        if (s + 1 == spp && pipe && pipeNext) {  // the next frame's first pass-halves
+            pipe->resize(cs.size());
+            for (size_t k = 0; k < cs.size(); ++k)
+                BANDCHK(trace_front(cs[k], it0 + spp, 0, spp > 1, true, 1.0f / (float)spp, true, (*pipe)[k], spp == 1));
+        }
         const int res = ((it0 + s) & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN;
         if (s + 1 < spp) {
-            // all but the last pass: the next pass's temporal taps' inputs, overlapped with that pass
-            // up to its temporal reuse
-            BANDCHK(exchange_set(cs, {{VXPT_BUF_TAP_RECORD, traceRows}, {res, traceRows}}, true));
+            // all but the last pass: the next pass's temporal taps' inputs -- the tap records on the
+            // exchange stream once the pass's first half wrote them (beside its second half; the next
+            // pass's k_restir waits for them), the reservoirs in stream order after its second half
+            // (the next second half opens with k_restir: nothing to overlap them with; round 4 sent
+            // both after the second half on the exchange stream)
+            hipEvent_t recDone = cs.size() == 1 && cs[0]->comm ? cs[0]->frontDone[cs[0]->lastSet] : nullptr;
+            BANDCHK(exchange_set(cs, {{VXPT_BUF_TAP_RECORD, traceRows}}, true, recDone));
+            BANDCHK(exchange_set(cs, {{res, traceRows}}, false));
         } else {
             // the last pass: its planes for the denoiser, and the denoiser input (radiance, or the spp
             // average) for the firefly filter's 3x3 neighbours.  Its reservoirs go out at the trace
@@ -1541,8 +1578,12 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
             BANDCHK(exchange_set(cs, br, false));
         }
     }
-    for (vxpt_ctx *c : cs) {
+    for (size_t k = 0; k < cs.size(); ++k) {
+        vxpt_ctx *c = cs[k];
         c->denoiseInputIsAccum = spp > 1;
+        // the chain after the next frame's first pass-half (pipelined), so it runs alone
+        if (pipe && pipeNext && pipe->size() == cs.size())
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[(*pipe)[k].set], 0));
         HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
         HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     }
@@ -2776,13 +2817,15 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
 int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0, int32_t nFrames, int32_t spp) {
     if (!c || spp < 1 || nFrames < 1 || frame0 < 0) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
-    if (c->comm) {  // banded: frame after frame (the halo exchanges order the passes), one sync at the end
+    if (c->comm) {  // banded: pipelined like the single-context loop below (band_frame), one sync at the end
         std::vector<vxpt_ctx *> cs{c};
         if (!c->runEv[0])
             for (hipEvent_t &e : c->runEv) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         HIPCHK(c, hipEventRecord(c->runEv[0], c->stream));
+        std::vector<PassPlan> pipe;  // the next frame's first pass-halves (band_frame)
         for (int f = 0; f < nFrames; ++f)
-            if (int r = band_frame(cs, p ? p : &c->yamlDenoise, frame0 + f, spp, false)) return r;
+            if (int r = band_frame(cs, p ? p : &c->yamlDenoise, frame0 + f, spp, false, &pipe, VX_BAND_PIPE && f + 1 < nFrames))
+                return r;
         HIPCHK(c, hipEventRecord(c->runEv[1], c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         band_timings(cs);  // the last frame's trace / denoiser split

@@ -34,15 +34,16 @@ def halo_bytes(width, spp, rows_avail):
     library's schedule: (overlapped, in stream order).  rows_avail caps every depth at the bands'
     height (vxpt_halo_plan moves min(rows, both band heights))."""
     r = lambda n: min(n, rows_avail)  # noqa: E731
-    per_pass = (32 + 20) * r(TRACE_ROWS)                         # tap records + reservoirs
-    overlapped = (spp - 1) * per_pass * width
+    # each non-last pass: its tap records beside its second half, its reservoirs after it (in order)
+    overlapped = (spp - 1) * 32 * r(TRACE_ROWS) * width
+    res_in_order = (spp - 1) * 20 * r(TRACE_ROWS)
     last = 32 * r(TRACE_ROWS) + 16 * r(2) + 20 * r(2) + PLANE_B * r(PLANE_ROWS)
     ff = 20 * r(TRACE_ROWS) + 16 * r(2)                           # filtered reservoirs + radiance
     ta = 16 * r(34) + 16 * r(2)                                   # ping for the history fix, pong
     hf = 16 * r(2)
     hc = (16 + 16 + 4) * r(HIST_ROWS)
     at = 16 * r(atrous_rows(2)) + 16 * r(atrous_rows(4)) + 16 * r(atrous_rows(8))
-    ordered = (last + ff + ta + hf + hc + at) * width
+    ordered = (res_in_order + last + ff + ta + hf + hc + at) * width
     return overlapped, ordered
 
 
@@ -52,9 +53,13 @@ def band_rows(h, n, k):
     return y0, min(h, y0 + per)
 
 
-def time_band(w, h, rows, frames, warmup, spp, tune):
+def time_band(w, h, rows, frames, warmup, spp, tune, rccl=True):
+    """One band's frames alone.  rccl: through a one-rank RCCL communicator on the band's rows --
+    band_frame's schedule, the one every rank of a multi-GPU run executes (its exchange groups with
+    no neighbour: the stream structure without the bytes); otherwise a plain context in band mode
+    (the single-context pipelined loop, what round 4 measured)."""
     pos = tuple(p * 4 for p in (35.6184, 11.8733, 42.0387))
-    r = vxpt.Renderer(w, h, rows=rows)
+    r = vxpt.Renderer(w, h) if rccl else vxpt.Renderer(w, h, rows=rows)
     try:
         r.load_settings()
         if tune:
@@ -62,6 +67,9 @@ def time_band(w, h, rows, frames, warmup, spp, tune):
         r.generate_terrain((8, 8, 8), height_scale=128.0, freq_den=256.0, global_y=True)
         r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
         r.set_sky()
+        if rccl:
+            r.band_comm_init(vxpt.band_comm_id(), 1, 0)
+            r.set_band(*rows)
         p = vxpt.DenoiseParams.defaults()
         r.render_frames(0, warmup, spp, p)
         r.sync()
@@ -96,7 +104,9 @@ def ordered_groups(w, h, spp, frames=3):
         for f in range(1, 1 + frames):
             linked.render_frame(f, spp, p)
         st = rs[0].band_stats()
-        # linked contexts exchange every group in stream order; the RCCL path overlaps spp - 1 of them
+        # linked contexts exchange every group in stream order; on the RCCL path each non-last pass's
+        # tap records go beside its second half (spp - 1 groups off the critical path) and every other
+        # group -- those passes' reservoirs included -- sits between two dependent kernels
         per = st["groups"] / st["frames"]
         return per - (spp - 1), spp - 1
     finally:
@@ -112,13 +122,17 @@ def main():
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--out", default=None)
     ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE")
+    ap.add_argument("--plain", action="store_true",
+                    help="time every band through a plain band-mode context (the single-context loop) instead of "
+                         "a one-rank RCCL communicator's band_frame schedule")
     a = ap.parse_args()
     tune = {k: int(v) for k, v in (t.split("=", 1) for t in a.tune)}
     w, h = a.size
     g_ord, g_ov = ordered_groups(w, h, a.spp)
     group_ms = g_ord * GROUP_US * 1e-3
     res = {"what": "one-GPU proxy of the band partition: each rank's band of the C3 frame rendered alone "
-                   "(single context in band mode, no exchange), and the halo bytes per rank and frame of the "
+                   "(N > 1: through a one-rank RCCL communicator, band_frame's schedule with no neighbour; N = 1: "
+                   "the single-context loop), and the halo bytes per rank and frame of the "
                    "library's schedule on one xGMI link (%.0f GB/s per direction), plus %.0f us per ordered "
                    "exchange group (RCCL group latency, charged, not measured)" % (XGMI_GBS, GROUP_US),
            "width": w, "height": h, "spp": a.spp, "tuning": tune or "defaults (bands: bench.band_tuning)",
@@ -133,7 +147,7 @@ def main():
             tn = dict(tune)
             for f, v in band_tuning(w, h, n).items():  # bench.py's banded runs
                 tn.setdefault(f, v)
-            t = time_band(w, h, rows, a.frames, a.warmup, a.spp, tn)
+            t = time_band(w, h, rows, a.frames, a.warmup, a.spp, tn, rccl=n > 1 and not a.plain)
             t.update(rank=k, rows=list(rows))
             per.append(t)
             print(n, k, rows, t, flush=True)
