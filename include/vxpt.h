@@ -301,7 +301,9 @@ int vxpt_render_frame(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame
 /* n_frames consecutive vxpt_render_frame calls (frames frame0 .. frame0+n_frames-1) with the
  * camera, world and lights left as they are: mainOffline's frame loop for a static camera.  The
  * buffers afterwards equal those calls' bit for bit; each frame's first trace pass is enqueued
- * beside the previous frame's last one, so the sequence takes less time.  Timing (HIP events):
+ * beside the previous frame's last one, so the sequence takes less time (banded contexts too); the
+ * host waits for each denoiser chain before it enqueues the next frame's later passes, so the call
+ * returns only after the last frame's chain has been enqueued and the others have run.  Timing (HIP events):
  * frame_ms is the mean per frame, denoise_ms the mean of the frames' denoiser chains (each timed on
  * its own; they run alone), trace_ms the mean per frame without them. */
 int vxpt_render_frames(vxpt_ctx *ctx, const vxpt_denoise_params *p, int32_t frame0, int32_t n_frames,
