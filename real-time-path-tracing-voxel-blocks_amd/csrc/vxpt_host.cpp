@@ -156,7 +156,7 @@ vxpt_tuning tuning_defaults() {
     t.resume_wg_per_cu = 16;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms
     t.sort_mode = 0;          // direction-class sort: 1.5 % faster traversal, producers pay it back
     t.overlap = 1;            // pass halves on two streams: 6.84 -> 6.06 ms
-    t.state_sets = 2;         // 3 sets: 6.40 -> 6.39 ms
+    t.state_sets = 3;         // 3 sets: 5.409 -> 5.394 ms (four interleaved runs each, every run faster; round 5)
     t.firefly_fused = 1;      // -4 us per chain
     t.ta_supertiles = 1;      // temporal pass traffic 351 -> 266 MB per frame
     t.hf_split = 4;           // 16.3 -> 11.8 us history fix (with readlane sums)
@@ -1590,54 +1590,68 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     for (size_t k = 0; k < cs.size(); ++k)
         if (cs[k]->bst.on) BANDCHK(stat_mark(cs[k], cs[k]->stream, mk[3 * k + 1]));
     const int it = it0 + spp, used = it > 0 ? it - 1 : 0;
+    std::vector<std::pair<int, int>> deferred;  // halo rows no pass reads before the next group
+    auto exg = [&](std::vector<std::pair<int, int>> br) {
+        br.insert(br.end(), deferred.begin(), deferred.end());
+        deferred.clear();
+        return exchange_set(cs, br);
+    };
+    auto to_rows = [](const std::vector<int> &bufs, int rows) {
+        std::vector<std::pair<int, int>> br;
+        for (int bf : bufs) br.emplace_back(bf, rows);
+        return br;
+    };
     if (!p->enable_firefly_filter) FOR_BANDS(run_pass(c, p, 11, 0, 0));
     if (p->enable_firefly_filter) {  // + world positions
         FOR_BANDS(run_pass(c, p, 0, used & 1, 0));
-        // the filtered reservoirs: the next frame's first temporal taps read them at the trace depth
-        BANDCHK(exchange_set(cs, {{(used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows}, {VXPT_BUF_ILLUM, 2}}));
+        // the filtered reservoirs (read by the next frame's first temporal taps) and radiance (read by
+        // the history clamp's neighbourhood) ride along with the next group instead of one of their own
+        deferred.emplace_back((used & 1) ? VXPT_BUF_RES_ODD : VXPT_BUF_RES_EVEN, traceRows);
+        deferred.emplace_back(VXPT_BUF_ILLUM, 2);
     }
     const std::vector<int> hist(std::begin(kHistoryBufs), std::end(kHistoryBufs));
     if (frame == 0) {
         FOR_BANDS(run_pass(c, p, 12, 0, 0));
-        BANDCHK(exchange(cs, hist, histRows));
+        BANDCHK(exg(to_rows(hist, histRows)));
     }
     int fin = 0;
     if (p->enable_temporal_accumulation && frame > 0) {
         FOR_BANDS(run_pass(c, p, 2, 0, 0));
         // HistoryFix taps: 2 x (2^3 + 1) rows of ping; pong for its 2-row stencils
-        BANDCHK(exchange_set(cs, {{VXPT_BUF_PING, 34}, {VXPT_BUF_PONG, 2}}));
+        BANDCHK(exg({{VXPT_BUF_PING, 34}, {VXPT_BUF_PONG, 2}}));
         fin = 1;
         if (p->enable_history_fix) {
             FOR_BANDS(run_pass(c, p, 3, 0, 0));
-            BANDCHK(exchange(cs, {VXPT_BUF_PONG}, 2));
+            BANDCHK(exg({{VXPT_BUF_PONG, 2}}));
             fin = 2;
         }
         if (p->enable_history_clamping) {
             FOR_BANDS(run_pass(c, p, 4, 0, 0));
-            BANDCHK(exchange(cs, hist, histRows));
+            BANDCHK(exg(to_rows(hist, histRows)));
             fin = 3;
         }
     }
     bool outDone = false;
     if (p->enable_spatial_filtering) {
         FOR_BANDS(run_pass(c, p, 5, 0, 0));
-        BANDCHK(exchange(cs, {VXPT_BUF_PING}, atrous_rows(2)));
+        BANDCHK(exg({{VXPT_BUF_PING, atrous_rows(2)}}));
         fin = 1;
         if (p->atrous_iteration_num > 0) {
             int idx = 1, step = 2;
             while (idx < 2 * p->atrous_iteration_num) {
                 FOR_BANDS(run_pass(c, p, 6, step, it));
                 step = 1 << ++idx;
-                BANDCHK(exchange(cs, {VXPT_BUF_PONG}, atrous_rows(step)));
+                BANDCHK(exg({{VXPT_BUF_PONG, atrous_rows(step)}}));
                 FOR_BANDS(run_pass(c, p, 7, step, it));
                 step = 1 << ++idx;
-                BANDCHK(exchange(cs, {VXPT_BUF_PING}, atrous_rows(step)));
+                BANDCHK(exg({{VXPT_BUF_PING, atrous_rows(step)}}));
             }
             FOR_BANDS(run_pass(c, p, 10, step, it));
             fin = 2;
             outDone = true;
         }
     }
+    if (!deferred.empty()) BANDCHK(exg({}));  // nothing after the firefly pass exchanged (chain switches)
     if (!outDone) FOR_BANDS(run_pass(c, p, 13, fin, 0));
     FOR_BANDS(run_pass(c, p, 14, 0, 0));
     for (vxpt_ctx *c : cs) {

@@ -333,11 +333,11 @@ def test_denoiser_history_fix_after_camera_move():
     r.close()
 
 
-TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=3), dict(sort_mode=1), dict(sort_mode=2),
+TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=2), dict(sort_mode=1), dict(sort_mode=2),
                    dict(iter_cap=2, iter_cap2=3, resume_wg_per_cu=3), dict(brick_steps=1, cam_steps=2),
                    dict(dda_boxes=0), dict(box_cap=2, box_cap_up=40), dict(firefly_fused=0), dict(ta_supertiles=0),
                    dict(hf_split=1), dict(stencil_tile=32), dict(front_streams=1),
-                   dict(front_streams=1, state_sets=3), dict(state_sets=3), dict(front_streams=3, state_sets=3),
+                   dict(front_streams=1, state_sets=3), dict(state_sets=2, front_streams=1), dict(front_streams=3, state_sets=3),
                    dict(lds_bricks=1), dict(iter_cap2=0, resume_split=1), dict(iter_cap2=0, resume_split=4),
                    dict(iter_cap2=8, resume_split=16), dict(iter_cap2=2, resume_split=2), dict(restir_waves=4)]
 
