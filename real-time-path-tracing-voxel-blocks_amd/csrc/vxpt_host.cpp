@@ -382,6 +382,11 @@ struct vxpt_ctx {
     // pass up to its temporal-reuse kernel (haloDone: recorded after the exchange)
     hipStream_t commStream = nullptr;
     hipEvent_t haloReady = nullptr, haloDone = nullptr;
+    // exDone: after the last exchange in stream order; the exchange stream's next group waits for it,
+    // and an exchange in stream order waits for an exchange-stream group still pending (haloDone):
+    // the communicator's groups run one after another, in the order every rank issues them
+    hipEvent_t exDone = nullptr;
+    bool exDoneRec = false;
     // vxpt_band_stats collection: timing events from a pool (reused after a reset) bracketing each
     // exchange group (kind 0 on the context stream, 1 on the exchange stream) and each banded frame's
     // trace (2) and denoiser (3) spans, and the bytes sent to each neighbour
@@ -1394,7 +1399,10 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
                 after = c->haloReady;
             }
             HIPCHK(c, hipStreamWaitEvent(c->commStream, after, 0));
+            if (c->exDoneRec) HIPCHK(c, hipStreamWaitEvent(c->commStream, c->exDone, 0));
             st = c->commStream;
+        } else if (c->haloPending) {
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->haloDone, 0));
         }
         size_t m0 = 0, m1 = 0;
         if (c->bst.on) BANDCHK_(stat_mark(c, st, m0));
@@ -1424,6 +1432,9 @@ int exchange_set(std::vector<vxpt_ctx *> &cs, const std::vector<std::pair<int, i
         if (overlap) {
             HIPCHK(c, hipEventRecord(c->haloDone, c->commStream));
             c->haloPending = true;
+        } else {
+            HIPCHK(c, hipEventRecord(c->exDone, c->stream));
+            c->exDoneRec = true;
         }
         return VXPT_OK;
     }
@@ -1777,6 +1788,7 @@ void vxpt_destroy(vxpt_ctx *c) {
     if (c->commStream) hipStreamDestroy(c->commStream);
     if (c->haloReady) hipEventDestroy(c->haloReady);
     if (c->haloDone) hipEventDestroy(c->haloDone);
+    if (c->exDone) hipEventDestroy(c->exDone);
     delete c;
 }
 
@@ -3163,10 +3175,12 @@ int vxpt_band_comm_init_rows(vxpt_ctx *c, const void *id, size_t bytes, int nran
     std::memcpy(&u, id, sizeof(u));
     if (c->comm) ncclCommDestroy(c->comm);
     c->comm = nullptr;
+    c->exDoneRec = false;
     if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclCommInitRank");
     if (!c->commStream) HIPCHK(c, hipStreamCreateWithFlags(&c->commStream, hipStreamNonBlocking));
     if (!c->haloReady) HIPCHK(c, hipEventCreateWithFlags(&c->haloReady, hipEventDisableTiming));
     if (!c->haloDone) HIPCHK(c, hipEventCreateWithFlags(&c->haloDone, hipEventDisableTiming));
+    if (!c->exDone) HIPCHK(c, hipEventCreateWithFlags(&c->exDone, hipEventDisableTiming | hipEventDisableSystemFence));
     c->nranks = nranks;
     c->rank = rank;
     c->splits = s;
