@@ -29,7 +29,7 @@
 // occupancy bounds (waves per SIMD) of the traversal and shading kernels; the defaults are the
 // measured best, the macros let experiment builds try others
 #ifndef VX_WPE_QUEUE
-#define VX_WPE_QUEUE 8
+#define VX_WPE_QUEUE 7  // round 5: 8 -> 7 waves (66-71 VGPRs, no spill): 1530.0 -> 1533.1 Mpaths/s, three runs each
 #endif
 #ifndef VX_WPE_RESUME
 #define VX_WPE_RESUME 6
