@@ -34,6 +34,9 @@
 #ifndef VX_WPE_RESUME
 #define VX_WPE_RESUME 6
 #endif
+#ifndef VX_WPE_RESUME_CL  // the closest-hit resume (k_resume<false, *>)
+#define VX_WPE_RESUME_CL 6
+#endif
 #ifndef VX_WPE_SHADE
 #define VX_WPE_SHADE 5
 #endif
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_QUEU
 // stop after cap more iterations and the unfinished ones move on to the next
 // level, same shard, one atomic per wave.
 template <bool OCC, bool BOX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_RESUME))) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC ? VX_WPE_RESUME : VX_WPE_RESUME_CL))) void k_resume(TraceArgs a, int q, int level, int shardCap, int cap) {
     const WaveBufs &w = a.wb;
     const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = t >> 6;
     // the shard's own wave count (any grid size: shards differ by one wave when 4 x gridDim.x is not a
