@@ -30,6 +30,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -141,6 +142,67 @@ def cpu_baseline(a, target_s):
     return res
 
 
+FRAME_LIMIT_S = 10.0  # watchdog: a frame (any rank) that takes longer ends the run (one takes ~6 ms)
+SETUP_LIMIT_S = 300.0  # watchdog: context creation, world generation, rendezvous, the balancing renders
+
+
+class Watchdog:
+    """Host watchdog over the run's GPU syncs and collectives (no re-exec, no retry): a section armed
+    with a limit that has not been disarmed when the limit expires prints what it was doing and ends
+    the process with status 5 -- a hung halo exchange or kernel on one rank ends the driver's
+    multi-GPU bench with a message instead of a hang."""
+
+    def __init__(self, rank=0):
+        self.rank, self._t = rank, None
+
+    def arm(self, seconds, what):
+        self.disarm()
+        self._t = threading.Timer(seconds, self._fire, (seconds, what))
+        self._t.daemon = True
+        self._t.start()
+
+    def frames(self, n, what):
+        self.arm(FRAME_LIMIT_S * n + 30.0, "%s (%d frames, %.0f s per frame)" % (what, n, FRAME_LIMIT_S))
+
+    def disarm(self):
+        if self._t is not None:
+            self._t.cancel()
+            self._t = None
+
+    def _fire(self, seconds, what):
+        print("bench watchdog: rank %d: %s did not finish within %.0f s; exiting" % (self.rank, what, seconds),
+              file=sys.stderr, flush=True)
+        os._exit(5)
+
+
+def band_parity(out, ref):
+    """The banded run's frame gathered at the root against the single-context render of the same frame
+    sequence: bit-exact per pixel (every channel's bits).  Returns the JSON fields of the check."""
+    import numpy as np
+    a = np.ascontiguousarray(out).view(np.uint32).reshape(out.shape[0], out.shape[1], -1)
+    b = np.ascontiguousarray(ref).view(np.uint32).reshape(ref.shape[0], ref.shape[1], -1)
+    if a.shape != b.shape:
+        return {"band_parity": False, "mismatched_px": None, "why": "shapes %s vs %s" % (a.shape, b.shape)}
+    bad = (a != b).any(axis=-1)
+    res = {"band_parity": not bool(bad.any()), "mismatched_px": int(bad.sum())}
+    if bad.any():
+        rows = np.nonzero(bad.any(axis=1))[0]
+        res["mismatched_rows"] = [int(rows[0]), int(rows[-1])]
+    return res
+
+
+def single_context_frames(make, frames, spp, params, primary_only=False):
+    """The frame sequence a banded context rendered (frames 0 .. frames-1), in one whole-frame context:
+    the reference image of band_parity.  Returns the context (the caller reads and closes it)."""
+    s = make()
+    if primary_only:
+        s.trace(frames - 1, primary_only=True)  # primary rays: no state carried between frames
+    else:
+        s.render_frames(0, frames, spp, params)
+    s.sync()
+    return s
+
+
 def band_tuning(width, height, world):
     """Schedule defaults of a rank's band (N>1).  A band is latency bound: a third wavefront state
     set lets its passes' first halves run further ahead, and below ~0.7 Mpx a third front stream
@@ -218,6 +280,11 @@ def main():
                     help="N>1: keep the equal row bands instead of balancing the boundaries on measured band times")
     ap.add_argument("--frame-calls", action="store_true",
                     help="time K vxpt_render_frame calls instead of one pipelined vxpt_render_frames(K)")
+    ap.add_argument("--bands", action="store_true",
+                    help="N=1: run the banded path through a one-rank RCCL communicator (the N>1 schedule, "
+                         "its instrumentation and its band_parity check, with no neighbour)")
+    ap.add_argument("--no-band-parity", action="store_true",
+                    help="banded runs: skip the check of the gathered frame against a single-context render")
     a = ap.parse_args()
     a.bounce_limits = tuple(int(v) for v in a.bounces.split("/"))
     if a.scene is None:
@@ -230,6 +297,9 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    banded = world > 1 or a.bands
+    wd = Watchdog(rank)
+    wd.arm(SETUP_LIMIT_S, "setup (rendezvous, contexts, world, band balancing)")
     dist = None
     if world > 1:
         import torch
@@ -259,27 +329,32 @@ def main():
         splits, balance_log = balance_bands(a, make, params, world, rank, dist)
     r = make()
     band = None
-    if world > 1:
+    if banded:
         # the library renders this rank's band and enqueues the halo exchanges itself
         # (RCCL over xGMI on the context stream); the host only hands out the unique id
         obj = [vxpt.band_comm_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
+        if dist is not None:
+            dist.broadcast_object_list(obj, src=0)
         err = ""
         try:
             r.band_comm_init(obj[0], world, rank, splits)
         except vxpt.VxptError as e:
             err = str(e)
-        errs = [None] * world
-        dist.all_gather_object(errs, err)
+        errs = [err]
+        if dist is not None:
+            errs = [None] * world
+            dist.all_gather_object(errs, err)
         if any(errs):
             # no band communicator on some rank: no banded frame can be rendered, and N independent
             # whole frames would not be the banded workload -- fail instead of reporting them
             bad = next(e for e in errs if e)
             print("band exchange unavailable (vxpt_band_comm_init): %s" % bad, file=sys.stderr, flush=True)
             r.close()
-            dist.destroy_process_group()
+            if dist is not None:
+                dist.destroy_process_group()
             sys.exit(3)
         band = bands.band_rows(a.height, world, rank) if splits is None else (splits[rank], splits[rank + 1])
+    wd.disarm()
 
     def step(frame):
         if a.primary_only:
@@ -289,9 +364,11 @@ def main():
             r.render_frame(frame, a.spp, params)
 
     frame = 0
+    wd.frames(a.warmup, "warmup")
     for _ in range(a.warmup):
         step(frame)
         frame += 1
+    wd.disarm()
 
     def barrier():
         torch.cuda.synchronize(local)
@@ -301,6 +378,7 @@ def main():
 
     trace_ms, denoise_ms = [], []
     pipelined = not a.primary_only and not a.frame_calls
+    wd.frames(a.steps + 2, "timed region")
     barrier()
     t0 = time.perf_counter()
     if pipelined:
@@ -324,17 +402,20 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    wd.disarm()
 
     # bands: after the timed region, 4 more frames with the library's band instrumentation on
     # (vxpt_band_stats: every frame's trace / denoiser spans, the halo groups' HIP-event time, count and
     # bytes per neighbour) -- what the first multi-GPU run needs to explain its own scaling
     band_diag, timing_src = None, "vxpt_timings (the pipelined run's chains)" if pipelined else "vxpt_timings per frame"
-    if world > 1 and not a.primary_only:
+    if banded and not a.primary_only:
+        wd.frames(4, "band instrumentation frames")
         r.band_stats_enable(True)
         r.render_frames(frame, 4, a.spp, params)
         frame += 4
         st = r.band_stats()
         r.band_stats_enable(False)
+        wd.disarm()
         nf = max(st["frames"], 1)
         mine = {"rank": rank, "rows": [st["row_begin"], st["row_end"]], "frames": st["frames"],
                 "trace_ms": round(st["trace_ms"] / nf, 4), "denoise_ms": round(st["denoise_ms"] / nf, 4),
@@ -342,8 +423,10 @@ def main():
                 "halo_overlapped_ms": round(st["exchange_overlap_ms"] / nf, 4),
                 "halo_groups": round(st["groups"] / nf, 2), "halo_groups_ordered": round(st["groups_ordered"] / nf, 2),
                 "halo_mb_up": round(st["bytes_up"] / nf / 1e6, 3), "halo_mb_down": round(st["bytes_down"] / nf / 1e6, 3)}
-        ranks = [None] * world
-        dist.all_gather_object(ranks, mine)
+        ranks = [mine]
+        if dist is not None:
+            ranks = [None] * world
+            dist.all_gather_object(ranks, mine)
         band_diag = {"frames": nf, "what": "per rank and frame, 4 banded frames after the timed region with "
                      "vxpt_band_stats on: trace / denoiser spans (with their exchanges), HIP-event time inside the "
                      "ordered and the overlapped halo groups, groups per frame, MB sent up / down",
@@ -351,6 +434,31 @@ def main():
         # every frame's spans (vxpt_timings of a banded run holds its last frame's)
         trace_ms, denoise_ms = [mine["trace_ms"]], [mine["denoise_ms"]]
         timing_src = "vxpt_band_stats over the 4 diagnostic frames (every frame's spans)"
+
+    # banded runs check themselves: every band's rows of the last frame gathered at rank 0 (RCCL,
+    # vxpt_band_gather) against one whole-frame context rendering the same frame sequence on rank 0
+    # (tools/rccl_bands_check.py's check, on the benchmarked workload); a mismatch fails the run
+    parity = None
+    if banded and not a.no_band_parity:
+        name = "DEPTH" if a.primary_only else "OUTPUT"
+        wd.frames(frame + 2, "band parity (gather + single-context render of %d frames)" % frame)
+        r.band_gather(name, 0)
+        if rank == 0:
+            s = single_context_frames(make, frame, a.spp, params, a.primary_only)
+            try:
+                parity = band_parity(r.read(name), s.read(name))
+            finally:
+                s.close()
+            parity.update({"buffer": name, "frames": frame,
+                           "what": "rank 0: the banded run's last frame gathered from every band (vxpt_band_gather) "
+                                   "vs one whole-frame context rendering the same %d frames, bit for bit" % frame})
+        if dist is not None:
+            obj = [parity]
+            dist.broadcast_object_list(obj, src=0)
+            parity = obj[0]
+        wd.disarm()
+        if not parity["band_parity"]:
+            print("band parity FAILED: %s" % json.dumps(parity), file=sys.stderr, flush=True)
 
     band_px = a.width * a.height
     if band is not None:
@@ -372,7 +480,7 @@ def main():
     # profiles/*_pmc_denoise.json) of this same mode only; PMC cannot run inside this timed process
     mode = run_mode(a, 1 if a.primary_only else a.spp)
     traffic, traffic_src, valu, valu_src = None, None, None, None
-    if not a.primary_only and world == 1:
+    if not a.primary_only and not banded:
         d, traffic_src = matching_profile("*_pmc_denoise.json", mode)
         traffic = d["traffic_bytes_per_frame"] if d else None
         # VALU issue utilisation of the trace kernels (tools/valu_util.py -> profiles/*_valu_util.json)
@@ -381,7 +489,7 @@ def main():
     # after the timed region: the same denoiser chain timed over frame-by-frame calls (nothing of the
     # next frame beside or just before it), a labelled extra beside the contract's roofline above
     chain_alone = None
-    if pipelined and world == 1:
+    if pipelined and not banded:
         ds = []
         for _ in range(4):
             r.render_frame(frame, a.spp, params)
@@ -416,14 +524,14 @@ def main():
     depth = r.read("DEPTH")
     hit_frac = float((depth < 1e26).mean())  # scene sanity: fraction of primary rays that hit voxels
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not banded and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, a.cpu_seconds)
     if rank == 0:
         line = {
             "metric": "Mpaths/s @1080p 4spp (+ms/frame, denoiser HBM GB/s vs roofline)",
             "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "strong" if world > 1 else "weak",
+            "scaling": "strong" if banded else "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": ("C2: %dx%d primary-only DDA + sky + G-buffer" % (a.width, a.height) if
                                     a.primary_only else "C3: %dx%d, %d spp full path + ReLAX denoiser" % (
@@ -436,8 +544,8 @@ def main():
                            a.bounce_limits + ((" (the reference's RayGen.cu:146-147 limits)",) if a.bounce_limits == (3, 1)
                                               else (" (BASELINE.json's '4 bounces' reading; the reference renders 3/1)",)
                                               if a.bounce_limits == (4, 4) else ("",))),
-                       "parallelism": ("bands%d (RCCL halo exchange)" % world) if world > 1 else "single GPU",
-                       "band_rows": (splits or vxpt.equal_splits(a.height, world)) if world > 1 else None,
+                       "parallelism": ("bands%d (RCCL halo exchange)" % world) if banded else "single GPU",
+                       "band_rows": (splits or vxpt.equal_splits(a.height, world)) if banded else None,
                        "band_balance": balance_log,
                        "frame_loop": "vxpt_render_frames (pipelined)" if pipelined else "vxpt_render_frame per step",
                        "tuning": a.tune or "defaults"},
@@ -447,7 +555,8 @@ def main():
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "avg_duration_ms": round(dur_ms, 4)},
             "trace_ms": round(avg_trace, 4), "denoise_ms": round(avg_dn, 4), "timing_source": timing_src,
-            "band_diag": band_diag, "primary_hit_frac": round(hit_frac, 4),
+            "band_diag": band_diag, "band_parity": parity["band_parity"] if parity else None,
+            "band_parity_detail": parity, "primary_hit_frac": round(hit_frac, 4),
             # the trace passes over this rank's rows (bands: with their halo exchanges)
             "trace_mpaths_s": round(band_px * spp / (avg_trace * 1e-3) / 1e6, 3),
             "trace_valu_util": valu, "trace_valu_util_source": valu_src,
@@ -459,6 +568,8 @@ def main():
     r.close()
     if dist is not None:
         dist.destroy_process_group()
+    if parity is not None and not parity["band_parity"]:
+        sys.exit(4)
 
 
 if __name__ == "__main__":

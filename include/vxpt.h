@@ -166,6 +166,9 @@ typedef struct vxpt_tuning {
     int32_t later_split;      /* the later path segments' stragglers: after 8 more iterations, in 1-16 pieces (16) */
     int32_t restir_waves;     /* k_restir's occupancy: 0 the compiler's register budget (3 waves/SIMD), 4: bounded
                                  to 4 waves (spills; a small band's launch fits one generation of waves)   (0) */
+    int32_t ghost_rows;       /* banded frames: 1: the history clamp and the a-trous steps compute the rows they
+                                 read outside the band (2 exchanges in the chain instead of 6); 0: exchange
+                                 after every pass                                                          (1) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);
@@ -413,6 +416,12 @@ int vxpt_band_balance(int height, int nranks, const int32_t *row_splits, const f
                       int32_t *out_splits);
 int vxpt_render_frame_linked(vxpt_ctx **ctxs, int n, const vxpt_denoise_params *p, int32_t frame_num,
                              int32_t spp);
+/* n_frames banded frames over linked contexts with the RCCL run's own pipelined schedule (a banded
+ * vxpt_render_frames: the next frame's first pass-halves enqueued beside the last second half and its
+ * exchange, the denoiser chain after them, the later first halves gated on the host behind the chain),
+ * device copies as the transport; results equal n_frames vxpt_render_frame_linked calls bit for bit. */
+int vxpt_render_frames_linked(vxpt_ctx **ctxs, int n, const vxpt_denoise_params *p, int32_t frame0,
+                              int32_t n_frames, int32_t spp);
 
 /* Halo-exchange instrumentation of a banded context (no reference counterpart; the first multi-GPU
  * run explains itself with it).  With collection on, every exchange group of a banded

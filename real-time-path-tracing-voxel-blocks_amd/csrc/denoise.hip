@@ -500,11 +500,8 @@ VX_HD V3 bicubic_smoothstep3(const T &tap, int W, int H, V2 uv) {
 // (VX_TA_FENCE) so that only one set of 12 taps is in flight in registers.  (A workgroup window of
 // the planes staged in LDS was measured slower -- 95 -> 109 us, 137 VGPRs -- and removed, DESIGN.md
 // Appendix A.)
-#ifndef VX_TA_SPLIT
-#define VX_TA_SPLIT 1
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
-#define VX_TA_FENCE() do { if (VX_TA_SPLIT) __builtin_amdgcn_sched_barrier(0); } while (0)
+#define VX_TA_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define VX_TA_FENCE() do { } while (0)
 #endif
@@ -879,23 +876,17 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
             const V3 sWP = wp(a, sx, sy);
             // the tap's value is fetched beside its weight's inputs (edge-clamped, so always a valid
             // read): one dependent round trip fewer; used only when the weight passes
-#ifndef VX_HF_LATE_VALUE
             const V4 sv = ld4(a.ping, W, H, sx, sy);
-#endif
             float w = plane_w(cWP, cN, sWP, dthr);
             w *= powf(fmaxf(0.01f, dot(cN, sN)), 8.0f);
             w = inside ? w : 0;
             w *= (float)(sMat == cMat);
             if (w > 1e-4f) {
-#ifdef VX_HF_LATE_VALUE
-                const V4 sv = ld4(a.ping, W, H, sx, sy);
-#endif
                 c = sv * w;
                 cw = w;
             }
         }
     }
-#ifndef VX_HF_BPERMUTE
     // the taps' values reach every lane of the half through v_readlane (constant lane indices, both
     // halves read, each keeps its own): no LDS-crossbar round trip per tap
     const bool hi = (threadIdx.x & 32u) != 0;
@@ -916,21 +907,6 @@ VX_D void history_fix_wave(const DenoiseArgs &a, int W, int H, int x, int y, siz
             wsum += tw;
         }
     }
-#else
-    const int base = (int)(threadIdx.x & 32u);  // the half's first lane in the wave
-    V4 sum(__shfl(c.x, base + 12), __shfl(c.y, base + 12), __shfl(c.z, base + 12), __shfl(c.w, base + 12));
-    float wsum = 1.0f;
-#pragma unroll 1
-    for (int t = 0; t < 25; ++t) {
-        if (t == 12) continue;
-        const float tw = __shfl(cw, base + t);
-        const V4 tc(__shfl(c.x, base + t), __shfl(c.y, base + t), __shfl(c.z, base + t), __shfl(c.w, base + t));
-        if (tw > 0.0f) {
-            sum += tc;
-            wsum += tw;
-        }
-    }
-#endif
     if (lane == 0 && store) a.pong[i] = tf(sum / wsum);
 }
 
@@ -1236,6 +1212,8 @@ __global__ __launch_bounds__(TS * TS) void k_atrous_smem(DenoiseArgs a) {
 #ifndef VX_A8_BATCH
 #define VX_A8_BATCH 8
 #endif
+// fetch(k0) fills tP/tN/tV[k0 .. k0 + kBatch - 1] of the 8-tap arrays at every k0 % kBatch == 0
+static_assert(VX_A8_BATCH == 0 || (VX_A8_BATCH > 0 && 8 % VX_A8_BATCH == 0), "VX_A8_BATCH must divide 8");
 struct GlobalTaps {
     static constexpr int kBatch = VX_A8_BATCH;  // taps fetched together (8: one round trip for all)
     Plane4 pW, pN, pI;

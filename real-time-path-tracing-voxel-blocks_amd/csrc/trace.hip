@@ -126,7 +126,7 @@ VX_D V2 restir_disk(float r0, float r1) {
 // traversal statistics (experiment builds only), per kind 8 counters:
 // rays, waves, sum of per-wave max outer iterations, outer iterations by level
 // (64^3 skip, 16^3 skip, 4^3 skip, brick walk), in-brick cell steps
-__device__ unsigned long long g_stats[8 * 8];  // kinds 0-4 as tools/trace_stats.py, 5 = stragglers
+__device__ unsigned long long g_stats[8 * 8];  // kinds 0-4 as tools/trace_stats.py, 5 = stragglers, 6 = straggler pieces
 VX_D int wsum(int v) { for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o); return v; }
 VX_D void stat_wave(int kind, bool active, const int *it) {
     const unsigned long long m = __ballot(active);
@@ -539,6 +539,9 @@ __global__ __launch_bounds__(256) void k_resume_split(TraceArgs a, int q, int le
         Hit h{0, 0, 0, 0, -1, 0, kRayMax};
         Dda st;
         int rc = DdaNone, id = 0;
+#ifdef VX_STATS
+        int iters[5] = {0, 0, 0, 0, 0};
+#endif
         if (live) {
             const int k = shard * shardCap + j;
             const DdaSaved sv{w.sCell[in][k], w.sT[in][k], w.sFace[in][k]};
@@ -563,11 +566,14 @@ __global__ __launch_bounds__(256) void k_resume_split(TraceArgs a, int q, int le
         for (;;) {
             const bool run = rc == DdaRun;
             if (__ballot(run) == 0ull) break;
-            if (run) rc = dda_iter<OCC, BOX>(a.world, st, h);
+            if (run) rc = dda_iter<OCC, BOX>(a.world, st, h VX_IT);
             // (the ballot outside the condition: every lane's event must be seen)
             const unsigned long long evNow = __ballot(rc == DdaEvent);
             if (rc == DdaRun && (evNow & below)) rc = DdaNone;  // an earlier piece has it
         }
+#ifdef VX_STATS
+        stat_wave(6, iters[1] + iters[2] + iters[3] > 0, iters);  // the pieces that walked
+#endif
         const unsigned long long ev = __ballot(rc == DdaEvent) & gmask;
         const int first = ev ? __ffsll((long long)ev) - 1 - gbase : 0;
         if (live && g == first) store_result<OCC>(w, id, ev ? DdaEvent : DdaNone, h, a.mesh.nInst == 0);
@@ -1194,16 +1200,9 @@ VX_D Reservoir remap_prev_res(const TraceArgs &a, Reservoir r) {
     r.lightData = (r.lightData & 0x80000000u) | (uint32_t)cur;
     return r;
 }
-VX_D Reservoir load_prev_res(const TraceArgs &a, size_t i) { return remap_prev_res(a, a.resPrev[i]); }
 
 // stash: an LDS home for the accepted taps' records ([tap][half][thread], k_restir's workgroup), so
-// the bias correction reads them there instead of fetching them again (VX_RESTIR_STASH)
-#ifndef VX_RESTIR_STASH
-#define VX_RESTIR_STASH 1
-#endif
-#ifndef VX_RESTIR_BATCH
-#define VX_RESTIR_BATCH 1
-#endif
+// the bias correction reads them there instead of fetching them again
 template <bool MESH>
 VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*stash)[2][256]) {
     int px, py;
@@ -1211,7 +1210,6 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     const WaveBufs &w = a.wb;
     int4 meta = load_meta(w, s);
     if (!(meta.x & F_NEE)) return;
-#if VX_RESTIR_BATCH
     // read ahead with the surface below (functions of the pixel and meta.y only): the temporal disks'
     // four random numbers, the previous pass's jitter and the RIS sample's visibility
     float rd0 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y), rd1 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 1),
@@ -1221,14 +1219,12 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     float rq0 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 4), rq1 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 5),
           rq2 = bn_rand(a.bn, px, py, a.iterationIndex, meta.y + 6);
     int hit0 = w.oHit[4 * s];
-#endif
     bool skipAlbedo;
     SurfX sp;
     SurfS sf = load_surf(a, s, px, py, seg, meta.x, skipAlbedo, &sp);
     const bool hasLocal = MESH && a.numLights > 0;
     float4 ris4 = w.rRis[s];
     LSample ls = load_ls(a, s);
-#if VX_RESTIR_BATCH
     // every read above completes here (unpinned, the compiler sinks them into the branches below,
     // where they follow one another)
     vx_pin(rd0); vx_pin(rd1); vx_pin(rd2); vx_pin(rd3); vx_pin(jx); vx_pin(jy); vx_pin(hit0);
@@ -1236,15 +1232,10 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     vx_pin(sf.pos); vx_pin(sf.normal); vx_pin(sf.geoNormal); vx_pin(sf.albedo); vx_pin(sf.wo);
     vx_pin(sf.depth); vx_pin(sf.roughness); vx_pin(sp.back); vx_pin(ris4);
     vx_pin(ls.position); vx_pin(ls.radiance); vx_pin(ls.solidAnglePdf);
-#endif
     Reservoir ris{(uint32_t)float_as_bits(ris4.x), (uint32_t)float_as_bits(ris4.y), ris4.z, ris4.w, 1.0f};
     bool visible = false;
     if (ls.type != LtInvalid && ris.lightData != 0) {
-#if VX_RESTIR_BATCH
         visible = !hit0;
-#else
-        visible = !w.oHit[4 * s];
-#endif
         if (!visible) { ris.lightData = 0; ris.weightSum = 0; }
     }
     if (!(meta.x & F_RESTIR)) {
@@ -1268,7 +1259,6 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     // three temporal taps (scalars, not arrays: no runtime-indexed private memory)
     const int ox0 = ppx - px, oy0 = ppy - py;
     int ox1, oy1, ox2, oy2;
-#if VX_RESTIR_BATCH
     {
         const V2 dsk = restir_disk(rd0, rd1);
         ox1 = ppx - px + (int)dsk.x; oy1 = ppy - py + (int)dsk.y;
@@ -1279,24 +1269,10 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     }
     rng.idx += 4;
     const V2 jit(jx, jy);
-#else
-    {
-        const float r0 = rng.next(), r1 = rng.next();
-        const V2 dsk = restir_disk(r0, r1);
-        ox1 = ppx - px + (int)dsk.x; oy1 = ppy - py + (int)dsk.y;
-    }
-    {
-        const float r0 = rng.next(), r1 = rng.next();
-        const V2 dsk = restir_disk(r0, r1);
-        ox2 = (int)dsk.x; oy2 = (int)dsk.y;
-    }
-    const V2 jit(bn_rand(a.bn, px, py, a.iterationIndex - 1, 0), bn_rand(a.bn, px, py, a.iterationIndex - 1, 1));
-#endif
     unsigned cached = 0;
     int selLoop = -1;
     float tapM0 = 0, tapM1 = 0, tapM2 = 0;
     V3 vd0(0.0f), vd1(0.0f), vd2(0.0f);  // the accepted taps' view directions, for the bias correction
-#if VX_RESTIR_BATCH
     // the taps' memory reads go out together instead of tap after tap: every tap's record and previous
     // reservoir (a rejected tap's reservoir is read and dropped), then the acceptance tests, then every
     // tap's environment-light entry, then the combine chain in tap order (the same operations on the
@@ -1324,7 +1300,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        if (!tin[i] || tb[i].w == kRayMax) continue;  // prev_surface: off screen or sky
+        if (!tin[i] || tb[i].w == kRayMax) continue;  // the tap is off screen or sky
         const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
         const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
         const V3 vd = a.prevCam.uv_to_dir((V2((float)x, (float)y) + jit) * a.prevCam.invRes);
@@ -1336,10 +1312,8 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
         const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
         if (!(nOk && dOk && rOk)) continue;
         cached |= (1u << i);
-        if (VX_RESTIR_STASH) {
-            stash[i][0][threadIdx.x] = tn[i];
-            stash[i][1][threadIdx.x] = tb[i];
-        }
+        stash[i][0][threadIdx.x] = tn[i];
+        stash[i][1][threadIdx.x] = tb[i];
     }
     float4 te[3];
 #pragma unroll
@@ -1368,57 +1342,19 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
         if (combine(rr, pr, rnd, nw)) { ls = cand; selLoop = i; }
     }
     rng.idx += nDraw;
-#else
-    for (int i = 0; i < 3; ++i) {
-        const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
-        const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
-        SurfS ts;
-        V3 vd;
-        float4 rec[2];
-        if (!prev_surface(a, jit, ts, x, y, nullptr, &vd, rec)) continue;
-        if (i == 0) vd0 = vd; else if (i == 1) vd1 = vd; else vd2 = vd;
-        const bool nOk = dot(sf.normal, ts.geoNormal) >= 0.5f;
-        const bool dOk = fabsf(expDepth - ts.depth) <= 0.1f * fmaxf(expDepth, ts.depth);
-        const bool rOk = fabsf(sf.roughness - ts.roughness) <= 0.5f * fmaxf(sf.roughness, ts.roughness);
-        if (!(nOk && dOk && rOk)) continue;
-        cached |= (1u << i);
-        if (VX_RESTIR_STASH) {
-            stash[i][0][threadIdx.x] = rec[0];
-            stash[i][1][threadIdx.x] = rec[1];
-        }
-        Reservoir pr = load_prev_res(a, (size_t)y * a.W + x);
-        if (isnan(pr.weightSum) || isinf(pr.weightSum)) pr = empty_res();
-        if (pr.M > 20.0f) pr.M = 20.0f;
-        if (i == 0) tapM0 = pr.M; else if (i == 1) tapM1 = pr.M; else tapM2 = pr.M;
-        float nw = 0.0f;
-        LSample cand = invalid_ls();
-        if (pr.lightData != 0) {
-            if (!light_from_res(a, cand, pr, sf.pos, hasLocal)) pr = empty_res();
-            nw = target_pdf(cand, sf);
-        }
-        if (combine(rr, pr, rng.next(), nw)) { ls = cand; selLoop = i; }
-    }
-#endif
     // bias-correction rays: the selected light seen from each accepted tap's surface
     float psv0 = 0, psv1 = 0, psv2 = 0;
     qr.id0 = 4 * s;
     LSample sel = invalid_ls();  // the combined reservoir's light (environment lights: the same for every tap)
-#if VX_RESTIR_BATCH
     if (rr.lightData != 0)
         light_from_entry(a, sel, rr, sf.pos, hasLocal,
                          pick4(selLoop, te[0], te[1], te[2], teRis));
-#else
-    if (rr.lightData != 0) light_from_res(a, sel, rr, sf.pos, hasLocal);
-#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (rr.lightData != 0 && (cached & (1u << i))) {
-            const int oxi = i == 0 ? ox0 : (i == 1 ? ox1 : ox2), oyi = i == 0 ? oy0 : (i == 1 ? oy1 : oy2);
-            const int x = reflect_view(px + oxi, a.W), y = reflect_view(py + oyi, a.H);
             SurfS ts;
             const V3 vdi = i == 0 ? vd0 : (i == 1 ? vd1 : vd2);
-            if (VX_RESTIR_STASH) rec_surface(a, stash[i][0][threadIdx.x], stash[i][1][threadIdx.x], vdi, ts);
-            else prev_surface(a, jit, ts, x, y, &vdi, nullptr);
+            rec_surface(a, stash[i][0][threadIdx.x], stash[i][1][threadIdx.x], vdi, ts);
             if (MESH && sel.type == LtLocal) light_from_res(a, sel, rr, ts.pos, hasLocal);  // seen from the tap
             const float psv = target_pdf(sel, ts);
             if (i == 0) psv0 = psv; else if (i == 1) psv1 = psv; else psv2 = psv;
@@ -1461,7 +1397,7 @@ VX_D void restir_slot(const TraceArgs &a, int seg, int s, QRays &qr, float4 (*st
 // WPE: the occupancy bound (1: the compiler's register budget; 4 for small bands, tuning restir_waves)
 template <bool MESH, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_restir(TraceArgs a, int seg) {
-    __shared__ float4 stash[VX_RESTIR_STASH ? 3 : 1][2][256];
+    __shared__ float4 stash[3][2][256];
     QRays qr;
     qr.mask = 0u;
     restir_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr, stash);

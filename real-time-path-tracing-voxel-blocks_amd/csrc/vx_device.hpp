@@ -906,40 +906,6 @@ VX_D void rec_surface(const TraceArgs &a, float4 nr, float4 b, V3 vd, SurfS &sf)
     sf.metallic = rb < 0;
     sf.translucency = 0.0f;  // not read by the taps' target pdf (disney_eval)
 }
-// rec: the tap's record, returned when not null (k_restir keeps it for the bias correction)
-VX_D bool prev_surface(const TraceArgs &a, V2 j, SurfS &sf, int x, int y, const V3 *vdIn, V3 *vdOut,
-                       float4 *rec = nullptr) {
-    if (x < 0 || y < 0 || x >= (int)a.prevCam.res.x || y >= (int)a.prevCam.res.y) return false;
-    const size_t i = (size_t)y * a.W + x;
-    // the previous pass's tap record (GBuf::rec): the planes' depth, normal (normalRough and
-    // geoNormalThin hold the same one), roughness, metallic flag and albedo
-    const float4 b = a.prev.rec[2 * i + 1];
-    sf.depth = b.w;
-    if (sf.depth == kRayMax) return false;
-    const float4 nr = a.prev.rec[2 * i];
-    if (rec) {
-        rec[0] = nr;
-        rec[1] = b;
-    }
-    V3 vd;
-    if (vdIn) {
-        vd = *vdIn;
-    } else {
-        const V2 uv = (V2((float)x, (float)y) + j) * a.prevCam.invRes;
-        vd = a.prevCam.uv_to_dir(uv);
-    }
-    if (vdOut) *vdOut = vd;
-    sf.pos = a.prevCam.pos + vd * sf.depth;
-    sf.wo = -vd;
-    sf.normal = V3(nr.x, nr.y, nr.z);
-    sf.geoNormal = sf.normal;
-    sf.albedo = V3(b.x, b.y, b.z);
-    const int rb = float_as_bits(nr.w);
-    sf.roughness = bits_as_float(rb & 0x7FFFFFFF);
-    sf.metallic = rb < 0;
-    sf.translucency = 0.0f;  // not read by the taps' target pdf (disney_eval)
-    return true;
-}
 
 VX_D V3 sky_emission(const SkyDev &k, V3 dir) {  // miss.cu:53-77
     V3 emission(0.0f);

@@ -165,6 +165,7 @@ vxpt_tuning tuning_defaults() {
     t.resume_split = 16;      // (with iter_cap2 0: every straggler in pieces, 5.73 -> 6.7-9.2 ms)
     t.later_split = 16;       // 4/4 bounces: 16.39 -> 15.67 ms per frame (3/1 has no later segments)
     t.restir_waves = 0;       // 4 waves: whole frames slower (Appendix A); see bench.band_tuning for bands
+    t.ghost_rows = 1;         // bands: the chain's ordered exchange groups 7 -> 3 per frame
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -179,17 +180,9 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.lds_bricks, 0, 1) && (t.resume_split == 1 || t.resume_split == 2 || t.resume_split == 4 ||
                                        t.resume_split == 8 || t.resume_split == 16) &&
            (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16) &&
-           (t.restir_waves == 0 || t.restir_waves == 4);
+           (t.restir_waves == 0 || t.restir_waves == 4) && in(t.ghost_rows, 0, 1);
 }
 
-// vxpt_render_frames: 1 = the host gates the first halves behind each denoiser chain (below)
-#ifndef VX_CHAIN_HOST_GATE
-#define VX_CHAIN_HOST_GATE 1
-#endif
-// banded vxpt_render_frames: 1 = frames pipelined (band_frame's pipe), 0 = frame after frame
-#ifndef VX_BAND_PIPE
-#define VX_BAND_PIPE 1
-#endif
 
 struct vxpt_ctx {
     int W = 0, H = 0, dev = 0, rowBegin = 0, rowEnd = 0;
@@ -387,15 +380,18 @@ struct vxpt_ctx {
     // the communicator's groups run one after another, in the order every rank issues them
     hipEvent_t exDone = nullptr;
     bool exDoneRec = false;
-    // vxpt_band_stats collection: timing events from a pool (reused after a reset) bracketing each
-    // exchange group (kind 0 on the context stream, 1 on the exchange stream) and each banded frame's
-    // trace (2) and denoiser (3) spans, and the bytes sent to each neighbour
+    // vxpt_band_stats collection: timing events from a pool bracketing each exchange group (kind 0 on
+    // the context stream, 1 on the exchange stream) and each banded frame's trace (2) and denoiser (3)
+    // spans, and the bytes sent to each neighbour.  Completed spans are folded into `ms` and their
+    // events reused (stat_fold: at every sync of a banded run, and before a frame once the pool holds
+    // kStatPoolFold events), so a long collection keeps a bounded pool.
     struct BandStat {
         bool on = false;
         std::vector<hipEvent_t> pool;
         size_t used = 0;
         struct Span { size_t e0, e1; int kind; };
         std::vector<Span> spans;
+        double ms[4] = {};
         int frames = 0, groups = 0, groupsOrdered = 0;
         double up = 0.0, down = 0.0;
     } bst;
@@ -1112,9 +1108,14 @@ int do_denoise(vxpt_ctx *c, const vxpt_denoise_params *p, int frameNum, int it) 
 }
 
 // one denoiser pass on the context's band, enqueued on its stream (vxpt_denoise_pass ids)
-int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int arg2) {
+// margin (banded chains, band_frame's ghost rows): the pass also computes `margin` rows either side of
+// the context's rows (8-aligned, clipped to the frame) -- the rows a later pass of the chain reads there,
+// computed here from the same inputs as the neighbour computes them instead of received from it
+int run_pass(vxpt_ctx *c, const vxpt_denoise_params *p, int pass, int arg, int arg2, int margin = 0) {
     DenoiseArgs a{};
     fill_denoise(c, p, a, pass == 0 ? (arg & 1) : 0);
+    a.y0 = std::max(0, a.y0 - margin);
+    a.y1 = std::min(a.H, a.y1 + margin);
     switch (pass) {
         case 0: HIPCHK(c, firefly_band(a, true, true, c->stream)); break;  // + world positions
         case 2: HIPCHK(c, launch_temporal(a, c->stream)); break;
@@ -1383,6 +1384,25 @@ int stat_mark(vxpt_ctx *c, hipStream_t st, size_t &idx) {
     HIPCHK(c, hipEventRecord(b.pool[idx], st));
     return 0;
 }
+// the collected spans' times into the running totals, their events back to the pool (every span's
+// events have completed: the caller synchronised the context and exchange streams)
+constexpr size_t kStatPoolFold = 512;
+int stat_fold(vxpt_ctx *c) {
+    auto &b = c->bst;
+    for (const auto &sp : b.spans) {
+        float ms = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&ms, b.pool[sp.e0], b.pool[sp.e1]));
+        b.ms[sp.kind] += ms;
+    }
+    b.spans.clear();
+    b.used = 0;
+    return VXPT_OK;
+}
+int stat_sync_fold(vxpt_ctx *c) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->commStream) HIPCHK(c, hipStreamSynchronize(c->commStream));
+    return stat_fold(c);
+}
 // the bytes a halo plan entry sends, to the neighbour above (peer < rank) or below
 void stat_bytes(vxpt_ctx *c, const Halo &h, size_t rowBytes) {
     (h.peer < c->rank ? c->bst.up : c->bst.down) += (double)h.sn * (double)rowBytes;
@@ -1548,6 +1568,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         c->haloHistRows = histRows;
         c->haloPlaneRows = planeRows;
     }
+    for (vxpt_ctx *c : cs)  // no span of this frame is open yet: a full pool is folded here
+        if (c->bst.on && c->bst.used >= kStatPoolFold) BANDCHK(stat_sync_fold(c));
     for (vxpt_ctx *c : cs) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     std::vector<size_t> mk(cs.size() * 3, 0);  // vxpt_band_stats: trace start, trace end, denoiser end
     for (size_t k = 0; k < cs.size(); ++k)
@@ -1625,8 +1647,59 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         FOR_BANDS(run_pass(c, p, 12, 0, 0));
         BANDCHK(exg(to_rows(hist, histRows)));
     }
+    // Ghost rows (the default chain, frames > 0): the history clamp and the a-trous steps compute the
+    // rows the later steps read outside the band themselves (run_pass margins), so the chain exchanges
+    // twice -- after the temporal pass and after the history fix -- instead of after every pass.  The
+    // margins, backwards from the output (margin 0): a step at margin m reads its input at m + its reach
+    // (a-trous rows of the step; 2 for the LDS a-trous and the clamp's 5x5), 8-aligned.  The history fix
+    // (its taps 34 rows away) stays at margin 0: ghost rows for it would cost 34 more rows of every pass
+    // before it.  Its inputs at the clamp's margin + 2 come in the two groups; the clamp's histories at
+    // its margin serve the next frame's temporal pass (histRows <= that margin: no exchange).
+    std::vector<int> atrousSteps;  // steps 2, 4, ..., 2^(2n+1): the last one (pass 10) writes the output
+    for (int idx = 1; idx <= 2 * p->atrous_iteration_num + 1; ++idx) atrousSteps.push_back(1 << idx);
+    std::vector<int> stepMargin(atrousSteps.size(), 0);
+    int smemMargin = 0, clampMargin = 0;
+    {
+        int m = 0;
+        for (int k = (int)atrousSteps.size() - 1; k >= 0; --k) {
+            stepMargin[k] = m;
+            m = (m + atrous_rows(atrousSteps[k]) + 7) / 8 * 8;
+        }
+        smemMargin = m;
+        clampMargin = (smemMargin + 2 + 7) / 8 * 8;
+    }
+    const bool ghost = cs.size() > 0 && cs[0]->tune.ghost_rows && frame > 0 && p->enable_temporal_accumulation &&
+                       p->enable_history_fix && p->enable_history_clamping && p->enable_spatial_filtering &&
+                       p->atrous_iteration_num > 0 &&
+                       // the clamp's pixel planes and the a-trous taps' world positions / normals, read at
+                       // up to the LDS a-trous margin + 2, are there already (the last pass's planes, the
+                       // firefly pass's positions)
+                       clampMargin <= planeRows && smemMargin + 2 <= kWposHalo;
     int fin = 0;
-    if (p->enable_temporal_accumulation && frame > 0) {
+    if (ghost) {
+        FOR_BANDS(run_pass(c, p, 2, 0, 0));
+        // the history fix's ping taps (34 rows) and the clamp's inputs at its margin: ping and the history
+        // length at the pixel, the radiance in its 5x5 (the firefly-filtered values; the deferred 2-row
+        // radiance entry is this one)
+        std::vector<std::pair<int, int>> br{{VXPT_BUF_PING, std::max(34, clampMargin)}, {VXPT_BUF_PONG, 2},
+                                            {VXPT_BUF_HIST_LEN, clampMargin}, {VXPT_BUF_ILLUM, clampMargin + 2}};
+        for (const auto &d : deferred)
+            if (d.first != VXPT_BUF_ILLUM) br.push_back(d);
+        deferred.clear();
+        BANDCHK(exchange_set(cs, br));
+        FOR_BANDS(run_pass(c, p, 3, 0, 0));
+        BANDCHK(exchange_set(cs, {{VXPT_BUF_PONG, clampMargin + 2}}));  // the clamp's 5x5 of the fixed history
+        FOR_BANDS(run_pass(c, p, 4, 0, 0, clampMargin));
+        if (histRows > clampMargin) BANDCHK(exchange_set(cs, to_rows(hist, histRows)));
+        FOR_BANDS(run_pass(c, p, 5, 0, 0, smemMargin));
+        for (size_t k = 0; k < atrousSteps.size(); ++k) {
+            const int pass = k + 1 == atrousSteps.size() ? 10 : (k % 2 == 0 ? 6 : 7);
+            FOR_BANDS(run_pass(c, p, pass, atrousSteps[k], it, stepMargin[k]));
+        }
+        for (vxpt_ctx *c : cs) c->haloHistRows = std::max(histRows, clampMargin);
+        FOR_BANDS(run_pass(c, p, 14, 0, 0));
+    }
+    if (p->enable_temporal_accumulation && frame > 0 && !ghost) {
         FOR_BANDS(run_pass(c, p, 2, 0, 0));
         // HistoryFix taps: 2 x (2^3 + 1) rows of ping; pong for its 2-row stencils
         BANDCHK(exg({{VXPT_BUF_PING, 34}, {VXPT_BUF_PONG, 2}}));
@@ -1642,8 +1715,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
             fin = 3;
         }
     }
-    bool outDone = false;
-    if (p->enable_spatial_filtering) {
+    bool outDone = ghost;
+    if (p->enable_spatial_filtering && !ghost) {
         FOR_BANDS(run_pass(c, p, 5, 0, 0));
         BANDCHK(exg({{VXPT_BUF_PING, atrous_rows(2)}}));
         fin = 1;
@@ -1664,7 +1737,7 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     }
     if (!deferred.empty()) BANDCHK(exg({}));  // nothing after the firefly pass exchanged (chain switches)
     if (!outDone) FOR_BANDS(run_pass(c, p, 13, fin, 0));
-    FOR_BANDS(run_pass(c, p, 14, 0, 0));
+    if (!ghost) FOR_BANDS(run_pass(c, p, 14, 0, 0));
     for (vxpt_ctx *c : cs) {
         HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
         HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
@@ -1680,6 +1753,8 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     if (!sync) return VXPT_OK;
     for (vxpt_ctx *c : cs) HIPCHK(c, hipStreamSynchronize(c->stream));
     band_timings(cs);
+    for (vxpt_ctx *c : cs)
+        if (c->bst.on) BANDCHK(stat_sync_fold(c));
     return VXPT_OK;
 }
 
@@ -2850,11 +2925,13 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         HIPCHK(c, hipEventRecord(c->runEv[0], c->stream));
         std::vector<PassPlan> pipe;  // the next frame's first pass-halves (band_frame)
         for (int f = 0; f < nFrames; ++f)
-            if (int r = band_frame(cs, p ? p : &c->yamlDenoise, frame0 + f, spp, false, &pipe, VX_BAND_PIPE && f + 1 < nFrames))
+            if (int r = band_frame(cs, p ? p : &c->yamlDenoise, frame0 + f, spp, false, &pipe, f + 1 < nFrames))
                 return r;
         HIPCHK(c, hipEventRecord(c->runEv[1], c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         band_timings(cs);  // the last frame's trace / denoiser split
+        if (c->bst.on)
+            if (int r = stat_sync_fold(c)) return r;
         float f = 0;
         hipEventElapsedTime(&f, c->runEv[0], c->runEv[1]);
         c->timing.frame_ms = f / (float)nFrames;
@@ -2920,7 +2997,6 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         if (int r = do_denoise(c, p, frame0 + f, it0 + spp)) return r;
         HIPCHK(c, hipEventRecord(c->chainEv[3 * f + 1], c->stream));
         if (havePend) {  // later first halves wait for the denoiser (it reads the old history slot)
-#if VX_CHAIN_HOST_GATE
             // on the host: the next frame's first second half goes behind the chain on the context
             // stream, then the host waits for the chain before it enqueues any later first half.  A
             // first half parked on a front stream behind a wait for the chain (the device-side gate)
@@ -2929,10 +3005,6 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             if (int r = trace_back(c, pend, false)) return r;
             pendBackQueued = true;
             HIPCHK(c, hipEventSynchronize(c->chainEv[3 * f + 1]));
-#else
-            HIPCHK(c, hipEventRecord(c->frontGate, c->stream));
-            for (hipStream_t fs : c->frontStreams) HIPCHK(c, hipStreamWaitEvent(fs, c->frontGate, 0));
-#endif
         }
     }
     HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
@@ -3208,6 +3280,7 @@ int vxpt_band_stats_enable(vxpt_ctx *c, int on) {
     b.on = on != 0;
     b.used = 0;
     b.spans.clear();
+    for (double &m : b.ms) m = 0.0;
     b.frames = b.groups = b.groupsOrdered = 0;
     b.up = b.down = 0.0;
     return VXPT_OK;
@@ -3216,8 +3289,7 @@ int vxpt_band_stats_enable(vxpt_ctx *c, int on) {
 int vxpt_band_stats(vxpt_ctx *c, vxpt_band_stat *out) {
     if (!c || !out) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->commStream) HIPCHK(c, hipStreamSynchronize(c->commStream));
+    if (int r = stat_sync_fold(c)) return r;
     const auto &b = c->bst;
     vxpt_band_stat s{};
     s.frames = b.frames;
@@ -3227,11 +3299,10 @@ int vxpt_band_stats(vxpt_ctx *c, vxpt_band_stat *out) {
     s.bytes_down = b.down;
     s.row_begin = c->rowBegin;
     s.row_end = c->rowEnd;
-    for (const auto &sp : b.spans) {
-        float ms = 0.0f;
-        HIPCHK(c, hipEventElapsedTime(&ms, b.pool[sp.e0], b.pool[sp.e1]));
-        (sp.kind == 0 ? s.exchange_ms : sp.kind == 1 ? s.exchange_overlap_ms : sp.kind == 2 ? s.trace_ms : s.denoise_ms) += ms;
-    }
+    s.exchange_ms = (float)b.ms[0];
+    s.exchange_overlap_ms = (float)b.ms[1];
+    s.trace_ms = (float)b.ms[2];
+    s.denoise_ms = (float)b.ms[3];
     *out = s;
     return VXPT_OK;
 }
@@ -3430,6 +3501,24 @@ int vxpt_render_frame_linked(vxpt_ctx **cs, int n, const vxpt_denoise_params *p,
         if (!cs[k] || cs[k]->rank != k || cs[k]->nranks != n) return VXPT_ERR_STATE;
     HIPCHK(cs[0], hipSetDevice(cs[0]->dev));
     return band_frame(v, p ? p : &v[0]->yamlDenoise, frameNum, spp);
+}
+
+// the banded vxpt_render_frames' pipelined schedule (band_frame's pipe) over linked contexts
+int vxpt_render_frames_linked(vxpt_ctx **cs, int n, const vxpt_denoise_params *p, int32_t frame0, int32_t nFrames,
+                              int32_t spp) {
+    if (!cs || n < 1 || spp < 1 || nFrames < 1 || frame0 < 0) return VXPT_ERR_ARG;
+    std::vector<vxpt_ctx *> v(cs, cs + n);
+    for (int k = 0; k < n; ++k)
+        if (!cs[k] || cs[k]->rank != k || cs[k]->nranks != n) return VXPT_ERR_STATE;
+    HIPCHK(cs[0], hipSetDevice(cs[0]->dev));
+    std::vector<PassPlan> pipe;  // every band's next-frame first pass-halves
+    for (int f = 0; f < nFrames; ++f)
+        if (int r = band_frame(v, p ? p : &v[0]->yamlDenoise, frame0 + f, spp, false, &pipe, f + 1 < nFrames)) return r;
+    for (vxpt_ctx *c : v) HIPCHK(c, hipStreamSynchronize(c->stream));
+    band_timings(v);
+    for (vxpt_ctx *c : v)
+        if (c->bst.on) BANDCHK(stat_sync_fold(c));
+    return VXPT_OK;
 }
 
 

@@ -93,7 +93,7 @@ class ImageDiffResult(ctypes.Structure):
 TUNING_FIELDS = ("dda_boxes", "box_cap", "box_cap_up", "brick_steps", "cam_steps", "iter_cap", "iter_cap2",
                  "resume_wg_per_cu", "sort_mode", "overlap", "state_sets", "firefly_fused", "ta_supertiles",
                  "hf_split", "stencil_tile", "front_streams", "lds_bricks", "resume_split", "later_split",
-                 "restir_waves")
+                 "restir_waves", "ghost_rows")
 
 
 class Tuning(ctypes.Structure):
@@ -200,6 +200,8 @@ def load_library(path=LIB_PATH):
         "vxpt_band_balance": (I, [I, I, P, P, P, P]),
         "vxpt_render_frame_linked": (I, [ctypes.POINTER(P), I, ctypes.POINTER(DenoiseParams), ctypes.c_int32,
                                          ctypes.c_int32]),
+        "vxpt_render_frames_linked": (I, [ctypes.POINTER(P), I, ctypes.POINTER(DenoiseParams), ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32]),
         "vxpt_band_rows": (I, [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
         "vxpt_bvh_depth": (I, [P, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
         "vxpt_halo_plan": (I, [I, I, I, I, P, ctypes.POINTER(I)]),
@@ -771,6 +773,12 @@ class LinkedBands:
         p = params or DenoiseParams.defaults()
         if self.lib.vxpt_render_frame_linked(self._arr, len(self.rs), ctypes.byref(p), frame_num, spp) != 0:
             raise VxptError("vxpt_render_frame_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
+
+    def render_frames(self, frame0, n_frames, spp=1, params=None):
+        """vxpt_render_frames_linked: the banded run's pipelined schedule over the linked bands."""
+        p = params or DenoiseParams.defaults()
+        if self.lib.vxpt_render_frames_linked(self._arr, len(self.rs), ctypes.byref(p), frame0, n_frames, spp) != 0:
+            raise VxptError("vxpt_render_frames_linked: " + self.lib.vxpt_last_error(self.rs[0].ctx).decode())
 
     def gather(self, name, root=0):
         """vxpt_band_gather_linked: every band's rows of `name` into band `root`'s buffer."""

@@ -147,7 +147,8 @@ def test_gpu_bands_match_single_context():
 @pytest.mark.parametrize("n,w,h,splits,tune", [(2, 64, 160, None, None), (8, 640, 640, None, None),
                                                (3, 96, 320, [0, 80, 248, 320], None),
                                                (8, 640, 640, [0, 72, 144, 224, 304, 384, 464, 560, 640], None),
-                                               (8, 640, 640, None, "bench")])
+                                               (8, 640, 640, None, "bench"),
+                                               (3, 96, 320, [0, 80, 248, 320], "noghost")])
 def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits, tune):
     """The library's own band schedule (vxpt_band_link / vxpt_render_frame_linked: the one
     vxpt_band_comm_init runs over RCCL, with device copies between the contexts as the
@@ -155,7 +156,8 @@ def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits, tune)
     partition on one device (bands of 80 rows, wider than the 72-row trace halo).  Uneven
     partitions (vxpt_band_link_rows, the cost-balanced bands of vxpt_band_balance) too, with
     bands as short as the halo itself.  tune "bench": the band contexts run bench.band_tuning's
-    schedule (third state set and front stream, straggler walks in 16 pieces)."""
+    schedule (third state set and front stream, straggler walks in 16 pieces); "noghost": the chain
+    exchanges after every pass (ghost_rows 0) instead of computing its ghost rows."""
     import vxpt
     from bench import band_tuning
     spp = 4
@@ -177,6 +179,9 @@ def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits, tune)
         assert t.get("resume_split", 1) > 1
         for r in rs:
             r.set_tuning(**t)
+    if tune == "noghost":
+        for r in rs:
+            r.set_tuning(ghost_rows=0)
     linked = vxpt.LinkedBands(rs, splits)
     rows = [bands.band_rows(h, n, k) for k in range(n)] if splits is None else list(zip(splits[:-1], splits[1:]))
     for f in range(3):
@@ -799,7 +804,7 @@ def test_gpu_band_stats_linked_bands():
     np.testing.assert_array_equal(out.view(np.uint32), single.read("OUTPUT").view(np.uint32))
     st = [r.band_stats() for r in rs]
     for k, s in enumerate(st):
-        assert s["frames"] == 3 and s["groups"] >= 3 * 10, s
+        assert s["frames"] == 3 and s["groups"] >= 3 * 8, s
         assert s["trace_ms"] > 0 and s["denoise_ms"] > 0 and s["exchange_ms"] > 0, s
         assert (s["row_begin"], s["row_end"]) == rows[k], s
     assert st[0]["bytes_up"] == 0 and st[-1]["bytes_down"] == 0
@@ -808,3 +813,80 @@ def test_gpu_band_stats_linked_bands():
     for r in rs:
         r.close()
     single.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,spp", [(2, 160, 1), (2, 160, 4), (3, 240, 4)])
+def test_gpu_linked_render_frames_pipelined_matches_frame_calls(n, h, spp):
+    """The banded vxpt_render_frames schedule (band_frame's pipe: the next frame's first pass-halves
+    enqueued beside the last second half and its exchange, the chain after them, the later first halves
+    gated on the host) run with neighbours: vxpt_render_frames_linked over n linked bands x 4 frames
+    equals n x 4 vxpt_render_frame_linked calls and one whole-frame context, bit for bit.  Then bench.py's
+    own self-check of a banded run (band_parity): the OUTPUT gathered at the root band against
+    bench.single_context_frames of the same frame sequence -- true, and false with the rows named when
+    one band's row is disturbed."""
+    import vxpt
+    from bench import band_parity, single_context_frames
+    w, frames = 96, 4
+    cam = C1_CAMERA
+
+    def make():
+        r = vxpt.Renderer(w, h)
+        r.load_settings()
+        r.generate_terrain((2, 1, 2))
+        r.set_camera(*cam[:2], fov=cam[2], prev=cam)
+        r.set_sky()
+        return r
+
+    p = vxpt.DenoiseParams.defaults()
+    rows = [bands.band_rows(h, n, k) for k in range(n)]
+    piped = [make() for _ in range(n)]
+    calls = [make() for _ in range(n)]
+    try:
+        lp, lc = vxpt.LinkedBands(piped), vxpt.LinkedBands(calls)
+        lp.render_frames(0, frames, spp, p)
+        for f in range(frames):
+            lc.render_frame(f, spp, p)
+        for name in ("OUTPUT", "ILLUM", "PREV_ILLUM", "HIST_LEN"):
+            for k, (y0, y1) in enumerate(rows):
+                np.testing.assert_array_equal(piped[k].read(name)[y0:y1].view(np.uint32),
+                                              calls[k].read(name)[y0:y1].view(np.uint32),
+                                              err_msg="%s band %d" % (name, k))
+        lp.gather("OUTPUT", 0)
+        single = single_context_frames(make, frames, spp, p)
+        try:
+            ref = single.read("OUTPUT")
+        finally:
+            single.close()
+        res = band_parity(piped[0].read("OUTPUT"), ref)
+        assert res == {"band_parity": True, "mismatched_px": 0}, res
+        bad = piped[0].read("OUTPUT")
+        y = rows[-1][0] + 3  # a row of the last band, as gathered at the root
+        bad[y, 5, 0] = np.nextafter(bad[y, 5, 0], np.float32(np.inf))
+        res = band_parity(bad, ref)
+        assert not res["band_parity"] and res["mismatched_px"] == 1 and res["mismatched_rows"] == [y, y], res
+    finally:
+        for r in piped + calls:
+            r.close()
+
+
+def test_band_parity_helper_and_watchdog():
+    """bench.band_parity on host arrays (bit-exact per pixel, every channel; -0.0 vs 0.0 differs), and the
+    bench watchdog ending a process whose armed section outlives its limit with status 5."""
+    import subprocess
+    import sys
+    from bench import REPO, band_parity
+    a = np.random.default_rng(3).random((16, 8, 4), dtype=np.float32)
+    assert band_parity(a, a.copy()) == {"band_parity": True, "mismatched_px": 0}
+    b = a.copy()
+    b[2, 1, 3] = -0.0 if a[2, 1, 3] == 0 else np.float32(0.0)
+    b[9, 7, :] = np.float32(-0.0)
+    r = band_parity(a, b)
+    assert not r["band_parity"] and r["mismatched_px"] == 2 and r["mismatched_rows"] == [2, 9], r
+    z = np.zeros((4, 4, 4), np.float32)
+    assert not band_parity(z, -z)["band_parity"]
+    assert band_parity(a, a[:8])["band_parity"] is False
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; w = bench.Watchdog(1); "
+            "w.arm(0.5, 'a stuck frame'); time.sleep(30)") % REPO
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 5 and "a stuck frame" in p.stderr, (p.returncode, p.stderr)

@@ -29,13 +29,18 @@ def atrous_rows(step):
     return step + (step // 4 if step > 4 else 0)
 
 
-def halo_bytes(width, spp, rows_avail):
+def halo_bytes(width, spp, rows_avail, measured=None):
     """Bytes one rank sends to ONE neighbour per frame (it receives as many), static camera, the
-    library's schedule: (overlapped, in stream order).  rows_avail caps every depth at the bands'
-    height (vxpt_halo_plan moves min(rows, both band heights))."""
+    library's schedule: (overlapped, in stream order).  measured: the bytes per frame vxpt_band_stats
+    counted over linked contexts (ordered_groups) -- the overlapped ones are each non-last pass's tap
+    records, the rest is in stream order.  Without it, the round-5 schedule's table (every chain pass
+    exchanging).  rows_avail caps every depth at the bands' height (vxpt_halo_plan moves
+    min(rows, both band heights))."""
     r = lambda n: min(n, rows_avail)  # noqa: E731
     # each non-last pass: its tap records beside its second half, its reservoirs after it (in order)
     overlapped = (spp - 1) * 32 * r(TRACE_ROWS) * width
+    if measured is not None and rows_avail >= 72:
+        return overlapped, measured - overlapped
     res_in_order = (spp - 1) * 20 * r(TRACE_ROWS)
     last = 32 * r(TRACE_ROWS) + 16 * r(2) + 20 * r(2) + PLANE_B * r(PLANE_ROWS)
     ff = 20 * r(TRACE_ROWS) + 16 * r(2)                           # filtered reservoirs + radiance
@@ -83,15 +88,18 @@ def time_band(w, h, rows, frames, warmup, spp, tune, rccl=True):
         r.close()
 
 
-def ordered_groups(w, h, spp, frames=3):
+def ordered_groups(w, h, spp, frames=3, tune=None):
     """Exchange groups per frame of the library's band schedule, counted by vxpt_band_stats over two
-    linked contexts (the same band_frame code as the RCCL path): (ordered, overlapped)."""
+    linked contexts (the same band_frame code as the RCCL path): (ordered, overlapped, bytes one band
+    sends its neighbour per frame)."""
     pos = tuple(p * 4 for p in (35.6184, 11.8733, 42.0387))
     rs = []
     try:
         for _ in range(2):
             r = vxpt.Renderer(w, h)
             r.load_settings()
+            if tune:
+                r.set_tuning(**tune)
             r.generate_terrain((8, 8, 8), height_scale=128.0, freq_den=256.0, global_y=True)
             r.set_camera(pos, C1_DIR, 90.0, prev=(pos, C1_DIR, 90.0))
             r.set_sky()
@@ -108,7 +116,7 @@ def ordered_groups(w, h, spp, frames=3):
         # tap records go beside its second half (spp - 1 groups off the critical path) and every other
         # group -- those passes' reservoirs included -- sits between two dependent kernels
         per = st["groups"] / st["frames"]
-        return per - (spp - 1), spp - 1
+        return per - (spp - 1), spp - 1, st["bytes_down"] / st["frames"]
     finally:
         for r in rs:
             r.close()
@@ -128,7 +136,7 @@ def main():
     a = ap.parse_args()
     tune = {k: int(v) for k, v in (t.split("=", 1) for t in a.tune)}
     w, h = a.size
-    g_ord, g_ov = ordered_groups(w, h, a.spp)
+    g_ord, g_ov, sent = ordered_groups(w, h, a.spp, tune=tune)
     group_ms = g_ord * GROUP_US * 1e-3
     res = {"what": "one-GPU proxy of the band partition: each rank's band of the C3 frame rendered alone "
                    "(N > 1: through a one-rank RCCL communicator, band_frame's schedule with no neighbour; N = 1: "
@@ -137,6 +145,7 @@ def main():
                    "exchange group (RCCL group latency, charged, not measured)" % (XGMI_GBS, GROUP_US),
            "width": w, "height": h, "spp": a.spp, "tuning": tune or "defaults (bands: bench.band_tuning)",
            "groups_per_frame": {"ordered": g_ord, "overlapped": g_ov, "counted_by": "vxpt_band_stats, 2 linked contexts"},
+           "bytes_per_neighbour_per_frame": round(sent), "bytes_counted_by": "vxpt_band_stats, 2 linked contexts",
            "group_latency_ms_per_frame": round(group_ms, 4),
            "ranks": {}}
     one = None
@@ -166,7 +175,7 @@ def main():
             per, balanced_per = eq, per
         slow = max(per, key=lambda t: t["frame_ms"])
         min_rows = min(y1 - y0 for y0, y1 in bands)
-        ov, od = halo_bytes(w, a.spp, min_rows) if n > 1 else (0, 0)
+        ov, od = halo_bytes(w, a.spp, min_rows, sent) if n > 1 else (0, 0)
         # an interior rank talks to two neighbours over two links at once: the time of one link's bytes
         link_ms_ordered = od / (XGMI_GBS * 1e9) * 1e3
         link_ms_overlapped = ov / (XGMI_GBS * 1e9) * 1e3

@@ -6,6 +6,7 @@
 #   full     bench.py (defaults, CPU baseline on)                          -> gpurun_out/b_full.json
 #   c2       bench.py --primary-only                                       -> gpurun_out/b_c2.json
 #   b44      bench.py --bounces 4/4 --no-cpu-baseline                      -> gpurun_out/b_44.json
+#   bands1   bench.py --bands (the banded path over a one-rank communicator, band_parity) -> gpurun_out/b_bands1.json
 #   counters rocprofv3 -L                                                  -> gpurun_out/counters.txt
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -26,6 +27,7 @@ for step in "$@"; do
     full) run full 400 python -u bench.py > gpurun_out/b_full.json 2> gpurun_out/b_full.err || exit $? ;;
     c2) run c2 300 python -u bench.py --primary-only --cpu-seconds 8 > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || exit $? ;;
     b44) run b44 200 python -u bench.py --bounces 4/4 --steps 10 --warmup 4 --no-cpu-baseline > gpurun_out/b_44.json 2> gpurun_out/b_44.err || exit $? ;;
+    bands1) run bands1 300 python -u bench.py --bands --steps 10 --warmup 4 --no-cpu-baseline > gpurun_out/b_bands1.json 2> gpurun_out/b_bands1.err || exit $? ;;
     counters) (cd /tmp && TMPDIR=/tmp timeout -k 5 60 rocprofv3 -L > "$GRAFT_REPO_ROOT/gpurun_out/counters.txt" 2>&1); true ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
