@@ -73,6 +73,28 @@ def matching_profile(pattern, mode):
     return None, None
 
 
+def trace_roofline_profile(mode):
+    """The trace's roofline (tools/trace_roofline.py -> profiles/*_trace_roofline.json) measured on this
+    run's workload: its mode equals the run's but for the kernels-one-at-a-time schedule it is measured
+    with (tune overlap = 0, a schedule knob that changes no result) and its frame count."""
+    want = dict(mode, tune={k: v for k, v in mode["tune"].items() if k != "overlap"})
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_trace_roofline.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        m = dict(d.get("mode", {}))
+        m.pop("frames", None)
+        m["tune"] = {k: v for k, v in m.get("tune", {}).items() if k != "overlap"}
+        if m == want:
+            keep = ("bound", "unit", "achieved", "peak", "frac", "lane_util", "peak_converged", "frac_converged",
+                    "steps_per_frame", "insts_per_step", "traversal_ms_per_frame", "per_path")
+            out = {k: d[k] for k in keep if k in d}
+            out["source"] = os.path.relpath(path, REPO)
+            out["what"] = ("the traversal kernels (k_closest, k_queue, k_resume, k_resume_split), kernels one at a "
+                           "time: lane DDA steps per s against the VALU-issue-bound peak (DESIGN.md §6)")
+            return out
+    return None
+
+
 def native_oracle():
     """Build the oracle for this host with -march=native (the CPU baseline's
     flags) into oracle/_native/ -- the prebuilt liboracle.so targets x86-64-v3 because it is
@@ -479,8 +501,9 @@ def main():
     # measured HBM bytes of the chain per frame: committed rocprofv3 PMC passes (tools/gpu_pmc.sh ->
     # profiles/*_pmc_denoise.json) of this same mode only; PMC cannot run inside this timed process
     mode = run_mode(a, 1 if a.primary_only else a.spp)
-    traffic, traffic_src, valu, valu_src = None, None, None, None
+    traffic, traffic_src, valu, valu_src, trace_roof = None, None, None, None, None
     if not a.primary_only and not banded:
+        trace_roof = trace_roofline_profile(mode)
         d, traffic_src = matching_profile("*_pmc_denoise.json", mode)
         traffic = d["traffic_bytes_per_frame"] if d else None
         # VALU issue utilisation of the trace kernels (tools/valu_util.py -> profiles/*_valu_util.json)
@@ -559,7 +582,7 @@ def main():
             "band_parity_detail": parity, "primary_hit_frac": round(hit_frac, 4),
             # the trace passes over this rank's rows (bands: with their halo exchanges)
             "trace_mpaths_s": round(band_px * spp / (avg_trace * 1e-3) / 1e6, 3),
-            "trace_valu_util": valu, "trace_valu_util_source": valu_src,
+            "trace_valu_util": valu, "trace_valu_util_source": valu_src, "trace_roofline": trace_roof,
             "roofline_chain_alone": chain_alone,
             "hbm_copy_gbs": copy_gbs,
             "cpu_baseline": cpu,

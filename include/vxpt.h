@@ -169,6 +169,10 @@ typedef struct vxpt_tuning {
     int32_t ghost_rows;       /* banded frames: 1: the history clamp and the a-trous steps compute the rows they
                                  read outside the band (2 exchanges in the chain instead of 6); 0: exchange
                                  after every pass                                                          (1) */
+    int32_t chain_gate;       /* pipelined frames (vxpt_render_frames, banded frames): 1: a frame's later passes'
+                                 first halves are enqueued once the previous frame's denoiser chain has
+                                 finished (the chain runs alone); 0: as soon as their state set is free
+                                 (spp >= 2 and no uploaded motion plane; otherwise the gate stays)       (1) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);

@@ -23,7 +23,10 @@ xGMI on GPUs, gloo on CPU) or LocalExchange (bands of one process; tests).
 Bands must be at least TRACE_HALO rows tall.  A camera that turns between
 frames needs deeper halos: pass run_frame the depths vxpt.band_halo_rows gives
 for the frame's camera pair (and the previous frame's), as the library's own
-schedule (vxpt_render_frame with a communicator, vxpt_render_frame_linked) does.
+schedule (vxpt_render_frame with a communicator, vxpt_render_frame_linked) does.  (The library's
+own chain computes the history clamp's and the a-trous steps' out-of-band rows itself -- its ghost
+rows, tuning ghost_rows -- instead of exchanging after each of those passes; this host-driven schedule
+keeps one exchange per pass.  Both are the single-GPU render bit for bit.)
 """
 import numpy as np
 

@@ -166,6 +166,7 @@ vxpt_tuning tuning_defaults() {
     t.later_split = 16;       // 4/4 bounces: 16.39 -> 15.67 ms per frame (3/1 has no later segments)
     t.restir_waves = 0;       // 4 waves: whole frames slower (Appendix A); see bench.band_tuning for bands
     t.ghost_rows = 1;         // bands: the chain's ordered exchange groups 7 -> 3 per frame
+    t.chain_gate = 1;         // the chain alone on the GPU (its roofline); bench.band_tuning: 0 for bands
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -180,7 +181,8 @@ bool tuning_valid(const vxpt_tuning &t) {
            in(t.lds_bricks, 0, 1) && (t.resume_split == 1 || t.resume_split == 2 || t.resume_split == 4 ||
                                        t.resume_split == 8 || t.resume_split == 16) &&
            (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16) &&
-           (t.restir_waves == 0 || t.restir_waves == 4) && in(t.ghost_rows, 0, 1);
+           (t.restir_waves == 0 || t.restir_waves == 4) && in(t.ghost_rows, 0, 1) &&
+           in(t.chain_gate, 0, 1);
 }
 
 
@@ -1010,6 +1012,13 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     return 0;
 }
 
+// Pipelined frames: whether a frame's later first halves wait (on the host) for the previous frame's
+// denoiser chain.  Nothing requires it when spp >= 2 and the motion plane is the static world's: a
+// first half writes a G-buffer slot that excludes the two the chain reads (hist, histOld), its own state
+// set and radiance plane (the chain reads the spp average), and the motion plane only after an upload
+// of it.  Otherwise (tuning chain_gate, the default) the gate keeps the chain alone on the GPU.
+bool chain_gate(const vxpt_ctx *c, int spp) { return c->tune.chain_gate || spp < 2 || !c->motionZero; }
+
 // The second half of the planned pass, on the context stream, and the ring bookkeeping.
 // mark: record ev[1] behind the pass (vxpt_trace's timing; the frame loops keep their own events --
 // every marker is one more packet between two kernels of the stream)
@@ -1579,9 +1588,9 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
         if (s == 0 && piped) {
             for (size_t k = 0; k < cs.size(); ++k) BANDCHK(trace_back(cs[k], (*pipe)[k], false));
             pipe->clear();
-            // the previous frame's denoiser chain reads the old history slot: the later first halves
-            // are enqueued once it has finished
-            for (vxpt_ctx *c : cs) HIPCHK(c, hipEventSynchronize(c->ev[7]));
+            // the later first halves are enqueued once the previous frame's chain has finished (chain_gate)
+            for (vxpt_ctx *c : cs)
+                if (chain_gate(c, spp)) HIPCHK(c, hipEventSynchronize(c->ev[7]));
         } else {
             FOR_BANDS(do_trace(c, it0 + s, 0, spp > 1, s == 0, 1.0f / (float)spp, s > 0, false, s + 1 == spp));
         }
@@ -3004,7 +3013,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             // streams sharing the context stream's hardware queue).
             if (int r = trace_back(c, pend, false)) return r;
             pendBackQueued = true;
-            HIPCHK(c, hipEventSynchronize(c->chainEv[3 * f + 1]));
+            if (chain_gate(c, spp)) HIPCHK(c, hipEventSynchronize(c->chainEv[3 * f + 1]));
         }
     }
     HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
@@ -3250,8 +3259,12 @@ int vxpt_band_comm_init_rows(vxpt_ctx *c, const void *id, size_t bytes, int nran
     c->exDoneRec = false;
     if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclCommInitRank");
     if (!c->commStream) HIPCHK(c, hipStreamCreateWithFlags(&c->commStream, hipStreamNonBlocking));
-    if (!c->haloReady) HIPCHK(c, hipEventCreateWithFlags(&c->haloReady, hipEventDisableTiming));
-    if (!c->haloDone) HIPCHK(c, hipEventCreateWithFlags(&c->haloDone, hipEventDisableTiming));
+#ifndef VX_HALO_SYSFENCE
+#define VX_HALO_SYSFENCE 1
+#endif
+    const unsigned haloFlags = hipEventDisableTiming | (VX_HALO_SYSFENCE ? 0u : (unsigned)hipEventDisableSystemFence);
+    if (!c->haloReady) HIPCHK(c, hipEventCreateWithFlags(&c->haloReady, haloFlags));
+    if (!c->haloDone) HIPCHK(c, hipEventCreateWithFlags(&c->haloDone, haloFlags));
     if (!c->exDone) HIPCHK(c, hipEventCreateWithFlags(&c->exDone, hipEventDisableTiming | hipEventDisableSystemFence));
     c->nranks = nranks;
     c->rank = rank;

@@ -816,15 +816,17 @@ def test_gpu_band_stats_linked_bands():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,h,spp", [(2, 160, 1), (2, 160, 4), (3, 240, 4)])
-def test_gpu_linked_render_frames_pipelined_matches_frame_calls(n, h, spp):
+@pytest.mark.parametrize("n,h,spp,tune", [(2, 160, 1, None), (2, 160, 4, None), (3, 240, 4, None),
+                                          (3, 240, 4, dict(chain_gate=0)), (2, 160, 1, dict(chain_gate=0))])
+def test_gpu_linked_render_frames_pipelined_matches_frame_calls(n, h, spp, tune):
     """The banded vxpt_render_frames schedule (band_frame's pipe: the next frame's first pass-halves
     enqueued beside the last second half and its exchange, the chain after them, the later first halves
     gated on the host) run with neighbours: vxpt_render_frames_linked over n linked bands x 4 frames
     equals n x 4 vxpt_render_frame_linked calls and one whole-frame context, bit for bit.  Then bench.py's
     own self-check of a banded run (band_parity): the OUTPUT gathered at the root band against
     bench.single_context_frames of the same frame sequence -- true, and false with the rows named when
-    one band's row is disturbed."""
+    one band's row is disturbed.  tune chain_gate 0: the later first halves not gated behind the previous
+    frame's chain (bench.band_tuning's schedule; at spp 1 the library keeps the gate)."""
     import vxpt
     from bench import band_parity, single_context_frames
     w, frames = 96, 4
@@ -842,6 +844,9 @@ def test_gpu_linked_render_frames_pipelined_matches_frame_calls(n, h, spp):
     rows = [bands.band_rows(h, n, k) for k in range(n)]
     piped = [make() for _ in range(n)]
     calls = [make() for _ in range(n)]
+    if tune:
+        for r in piped:
+            r.set_tuning(**tune)
     try:
         lp, lc = vxpt.LinkedBands(piped), vxpt.LinkedBands(calls)
         lp.render_frames(0, frames, spp, p)

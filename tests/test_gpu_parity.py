@@ -339,7 +339,8 @@ TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=2), dict(sort_mode=1), dict(
                    dict(hf_split=1), dict(stencil_tile=32), dict(front_streams=1),
                    dict(front_streams=1, state_sets=3), dict(state_sets=2, front_streams=1), dict(front_streams=3, state_sets=3),
                    dict(lds_bricks=1), dict(iter_cap2=0, resume_split=1), dict(iter_cap2=0, resume_split=4),
-                   dict(iter_cap2=8, resume_split=16), dict(iter_cap2=2, resume_split=2), dict(restir_waves=4)]
+                   dict(iter_cap2=8, resume_split=16), dict(iter_cap2=2, resume_split=2), dict(restir_waves=4),
+                   dict(chain_gate=0), dict(chain_gate=0, state_sets=2, front_streams=1)]
 
 
 @pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
