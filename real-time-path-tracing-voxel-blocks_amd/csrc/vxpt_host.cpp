@@ -3259,12 +3259,11 @@ int vxpt_band_comm_init_rows(vxpt_ctx *c, const void *id, size_t bytes, int nran
     c->exDoneRec = false;
     if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) return fail(c, VXPT_ERR_HIP, "ncclCommInitRank");
     if (!c->commStream) HIPCHK(c, hipStreamCreateWithFlags(&c->commStream, hipStreamNonBlocking));
-#ifndef VX_HALO_SYSFENCE
-#define VX_HALO_SYSFENCE 1
-#endif
-    const unsigned haloFlags = hipEventDisableTiming | (VX_HALO_SYSFENCE ? 0u : (unsigned)hipEventDisableSystemFence);
-    if (!c->haloReady) HIPCHK(c, hipEventCreateWithFlags(&c->haloReady, haloFlags));
-    if (!c->haloDone) HIPCHK(c, hipEventCreateWithFlags(&c->haloDone, haloFlags));
+    // the exchange stream's events keep the system-scope fence: the rows a peer GPU wrote over xGMI must
+    // be visible to the kernel that waits for them (without it one band measured ~1 % faster, within the
+    // run-to-run spread: not worth a stale-cache risk)
+    if (!c->haloReady) HIPCHK(c, hipEventCreateWithFlags(&c->haloReady, hipEventDisableTiming));
+    if (!c->haloDone) HIPCHK(c, hipEventCreateWithFlags(&c->haloDone, hipEventDisableTiming));
     if (!c->exDone) HIPCHK(c, hipEventCreateWithFlags(&c->exDone, hipEventDisableTiming | hipEventDisableSystemFence));
     c->nranks = nranks;
     c->rank = rank;

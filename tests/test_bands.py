@@ -477,6 +477,8 @@ def test_oracle_bands_follow_a_translating_camera():
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,w,h,turns", [
     (2, 96, 320, [(0, 0), (2, 0.8), (0, 3), (0, 2), (1, 1)]),
+    # a 10-degree pitch: history halo 53 rows, deeper than the ghost rows' 40 (the clamp's histories exchanged)
+    (2, 96, 320, [(0, 0), (0, 10), (0, 2)]),
     (8, 640, 640, [(0, 0), (1, 0.3), (0.5, 0.5), (1.5, 0.4), (0, 1.0)])])
 def test_gpu_linked_bands_follow_a_turning_camera(n, w, h, turns):
     """A camera that yaws / pitches between frames: the banded frame deepens its halos
