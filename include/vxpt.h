@@ -154,7 +154,8 @@ typedef struct vxpt_tuning {
     int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (16) */
     int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (0) */
     int32_t overlap;          /* 1: pass halves and pipelined frames on two streams; 0: in order        (1) */
-    int32_t state_sets;       /* wavefront state sets, 2..3                                             (3) */
+    int32_t state_sets;       /* wavefront state sets, 2..3: a pass's first half waits for the second half
+                                 state_sets passes back                                                (3) */
     int32_t firefly_fused;    /* 1: the detecting wave filters its fireflies; 0: a second launch        (1) */
     int32_t ta_supertiles;    /* 1: temporal accumulation on XCD supertiles; 0: raster tiles            (1) */
     int32_t hf_split;         /* history-fix workgroups per tile, 1..16                                 (4) */

@@ -140,7 +140,7 @@ bool as_bool(const std::string &s) { return s == "true" || s == "1" || s == "Tru
 
 constexpr int kBlockTypes = 30;  // BlockTypeNum (generated/voxelengine/BlockType.h:39)
 constexpr int kPostHist = 257;   // 256 luminance bins + the lens flare's sun flag
-constexpr int kMaxSets = 3;      // wavefront state sets (vxpt_ctx::nSets)
+constexpr int kMaxSets = 3;      // wavefront state sets (vxpt_ctx::nSets; 4 measured slower on bands)
 
 // the measured best schedule; vxpt_set_tuning changes it per context
 vxpt_tuning tuning_defaults() {
@@ -1623,8 +1623,9 @@ int band_frame(std::vector<vxpt_ctx *> &cs, const vxpt_denoise_params *p, int fr
     for (size_t k = 0; k < cs.size(); ++k) {
         vxpt_ctx *c = cs[k];
         c->denoiseInputIsAccum = spp > 1;
-        // the chain after the next frame's first pass-half (pipelined), so it runs alone
-        if (pipe && pipeNext && pipe->size() == cs.size())
+        // the chain after the next frame's first pass-half (pipelined), so it runs alone -- with the
+        // chain gate (without it the later first halves run beside the chain anyway: no wait)
+        if (pipe && pipeNext && pipe->size() == cs.size() && chain_gate(c, spp))
             HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[(*pipe)[k].set], 0));
         HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
         HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
@@ -2963,6 +2964,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
     HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
     PassPlan pend;
     bool havePend = false, pendBackQueued = false;
+    std::vector<char> frontMarked(nFrames, 0);  // chainEv[3f + 2] recorded in this run
     for (int f = 0; f < nFrames; ++f) {
         const int it0 = (frame0 + f) * spp;
         for (int s = 0; s < spp; ++s) {
@@ -2993,7 +2995,8 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             // (chains after such a first half measure 0.40 instead of 0.36 ms, every chain kernel 5-10 %
             // slower with the GPU idle beside them; an L2 write-back of the first half's dirty lines
             // before the chain changed nothing -- the frame is still 0.14 ms shorter this way)
-            if (!pend.a.primaryOnly) {
+            if (!pend.a.primaryOnly && chain_gate(c, spp)) {
+                frontMarked[f] = 1;
                 HIPCHK(c, hipEventRecord(c->chainEv[3 * f + 2], front_stream(c, pend.set)));
                 HIPCHK(c, hipStreamWaitEvent(c->stream, c->frontDone[pend.set], 0));
                 HIPCHK(c, launch_stream_mark(c->stream));
@@ -3001,7 +3004,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             }
         }
         c->denoiseInputIsAccum = spp > 1;
-        const bool waited = havePend && !pend.a.primaryOnly;
+        const bool waited = havePend && !pend.a.primaryOnly && chain_gate(c, spp);
         if (!waited) HIPCHK(c, hipEventRecord(c->chainEv[3 * f], c->stream));
         if (int r = do_denoise(c, p, frame0 + f, it0 + spp)) return r;
         HIPCHK(c, hipEventRecord(c->chainEv[3 * f + 1], c->stream));
@@ -3023,11 +3026,12 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         float a = 0, b = 0, e = 0;
         hipEventElapsedTime(&a, c->ev[6], c->chainEv[3 * k]);
         hipEventElapsedTime(&e, c->ev[6], c->chainEv[3 * k + 1]);
-        if (k + 1 < nFrames && hipEventElapsedTime(&b, c->ev[6], c->chainEv[3 * k + 2]) == hipSuccess)
+        if (frontMarked[k] && hipEventElapsedTime(&b, c->ev[6], c->chainEv[3 * k + 2]) == hipSuccess)
             a = std::max(a, b);
         dsum += e - a;
     }
     hipEventElapsedTime(&f, c->ev[6], c->ev[7]);
+    (void)hipGetLastError();  // a failed timing read must not surface as a later launch's error
     c->timing.trace_ms = (f - dsum) / (float)nFrames;  // per frame, the chains excluded
     c->timing.denoise_ms = dsum / (float)nFrames;        // the mean chain
     c->timing.frame_ms = f / (float)nFrames;

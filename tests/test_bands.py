@@ -819,7 +819,8 @@ def test_gpu_band_stats_linked_bands():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,h,spp,tune", [(2, 160, 1, None), (2, 160, 4, None), (3, 240, 4, None),
-                                          (3, 240, 4, dict(chain_gate=0)), (2, 160, 1, dict(chain_gate=0))])
+                                          (3, 240, 4, dict(chain_gate=0)), (2, 160, 1, dict(chain_gate=0)),
+                                          (3, 240, 4, dict(chain_gate=0, state_sets=3, front_streams=3))])
 def test_gpu_linked_render_frames_pipelined_matches_frame_calls(n, h, spp, tune):
     """The banded vxpt_render_frames schedule (band_frame's pipe: the next frame's first pass-halves
     enqueued beside the last second half and its exchange, the chain after them, the later first halves

@@ -340,7 +340,8 @@ TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=2), dict(sort_mode=1), dict(
                    dict(front_streams=1, state_sets=3), dict(state_sets=2, front_streams=1), dict(front_streams=3, state_sets=3),
                    dict(lds_bricks=1), dict(iter_cap2=0, resume_split=1), dict(iter_cap2=0, resume_split=4),
                    dict(iter_cap2=8, resume_split=16), dict(iter_cap2=2, resume_split=2), dict(restir_waves=4),
-                   dict(chain_gate=0), dict(chain_gate=0, state_sets=2, front_streams=1)]
+                   dict(chain_gate=0), dict(chain_gate=0, state_sets=2, front_streams=1),
+                   dict(chain_gate=0, state_sets=3, front_streams=3)]
 
 
 @pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
@@ -398,7 +399,8 @@ def test_tuning_rejects_out_of_range_fields():
     r, _ = _setup(32, 16)
     try:
         before = r.tuning()
-        for bad in (dict(state_sets=4), dict(stencil_tile=24), dict(iter_cap=0), dict(sort_mode=3)):
+        for bad in (dict(state_sets=4), dict(front_streams=4), dict(stencil_tile=24), dict(iter_cap=0), dict(sort_mode=3),
+                    dict(ghost_rows=2), dict(chain_gate=-1)):
             with pytest.raises(vxpt.VxptError):
                 r.set_tuning(**bad)
             assert r.tuning() == before
