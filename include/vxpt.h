@@ -137,6 +137,8 @@ typedef struct vxpt_timing {  /* HIP-event times of the last frame, ms (replaces
     float denoise_ms;
     float sky_ms;
     float frame_ms;
+    float host_ms;  /* host time per frame to enqueue the last vxpt_render_frames run (before its final sync):
+                       close to frame_ms means the GPU waited for the host */
 } vxpt_timing;
 
 /* Schedule and traversal tuning of a context (no reference counterpart: the reference's OptiX

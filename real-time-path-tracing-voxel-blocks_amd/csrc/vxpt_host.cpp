@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
@@ -2928,6 +2929,11 @@ int vxpt_render_frame(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frameNu
 int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0, int32_t nFrames, int32_t spp) {
     if (!c || spp < 1 || nFrames < 1 || frame0 < 0) return VXPT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->dev));
+    const auto hostT0 = std::chrono::steady_clock::now();
+    auto hostMs = [&]() {
+        return (float)(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - hostT0).count() /
+                       nFrames);
+    };
     if (c->comm) {  // banded: pipelined like the single-context loop below (band_frame), one sync at the end
         std::vector<vxpt_ctx *> cs{c};
         if (!c->runEv[0])
@@ -2938,8 +2944,10 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
             if (int r = band_frame(cs, p ? p : &c->yamlDenoise, frame0 + f, spp, false, &pipe, f + 1 < nFrames))
                 return r;
         HIPCHK(c, hipEventRecord(c->runEv[1], c->stream));
+        const float host = hostMs();
         HIPCHK(c, hipStreamSynchronize(c->stream));
         band_timings(cs);  // the last frame's trace / denoiser split
+        c->timing.host_ms = host;
         if (c->bst.on)
             if (int r = stat_sync_fold(c)) return r;
         float f = 0;
@@ -3020,6 +3028,7 @@ int vxpt_render_frames(vxpt_ctx *c, const vxpt_denoise_params *p, int32_t frame0
         }
     }
     HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+    c->timing.host_ms = hostMs();
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float dsum = 0, f = 0;
     for (int k = 0; k < nFrames; ++k) {

@@ -106,7 +106,7 @@ class Tuning(ctypes.Structure):
 
 class Timing(ctypes.Structure):
     _fields_ = [("trace_ms", ctypes.c_float), ("denoise_ms", ctypes.c_float), ("sky_ms", ctypes.c_float),
-                ("frame_ms", ctypes.c_float)]
+                ("frame_ms", ctypes.c_float), ("host_ms", ctypes.c_float)]
 
 
 class BandStat(ctypes.Structure):  # vxpt_band_stat
@@ -554,7 +554,8 @@ class Renderer:
     def timings(self):
         t = Timing()
         self._chk(self.lib.vxpt_timings(self.ctx, ctypes.byref(t)), "vxpt_timings")
-        return dict(trace_ms=t.trace_ms, denoise_ms=t.denoise_ms, sky_ms=t.sky_ms, frame_ms=t.frame_ms)
+        return dict(trace_ms=t.trace_ms, denoise_ms=t.denoise_ms, sky_ms=t.sky_ms, frame_ms=t.frame_ms,
+                    host_ms=t.host_ms)
 
     def debug_clamp_decisions(self, on=True):
         """vxpt_debug_clamp_decisions: the history clamp records its decision bits (CLAMP_DECISION)."""
