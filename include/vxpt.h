@@ -176,6 +176,8 @@ typedef struct vxpt_tuning {
                                  first halves are enqueued once the previous frame's denoiser chain has
                                  finished (the chain runs alone); 0: as soon as their state set is free
                                  (spp >= 2 and no uploaded motion plane; otherwise the gate stays)       (1) */
+    int32_t sky_exit;         /* 1: a walk that leaves an empty box above the world's highest cube cell without
+                                 heading down ends there (nothing ahead can be hit)                      (0) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);

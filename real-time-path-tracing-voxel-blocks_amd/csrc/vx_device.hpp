@@ -425,10 +425,14 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const 
             --s.steps;
             return DdaRun;
         }
-    } else if constexpr (BOX) {
-        skip_box(w, s.r, s.c, (int)(s.box & 0xFFu), (int)((s.box >> 8) & 0xFFu), (int)((s.box >> 16) & 0xFFu));
     } else {
-        skip_cube(w, s.r, s.c, s.dist);
+        if constexpr (BOX) skip_box(w, s.r, s.c, (int)(s.box & 0xFFu), (int)((s.box >> 8) & 0xFFu), (int)((s.box >> 16) & 0xFFu));
+        else skip_cube(w, s.r, s.c, s.dist);
+        // sky exit: the walk stands in an empty cell above every cube cell and does not head down, so no
+        // crossing ahead joins or leaves a cube -- the cell-by-cell walk would reach the world's edge
+        // without an event (prevId is 0 in an empty cell reached without one).  Checked once per empty
+        // box, not per cell step.
+        if (s.c.y > w.topY && !(s.r.dy < 0.0f)) return DdaNone;
     }
     // the next crossing leaves the brick (or the skipped box)
     float t;

@@ -70,6 +70,8 @@ struct WorldDev {
                               // (0 = 10: a whole brick); vxpt_tuning.brick_steps
     uint64_t top;
     int topValid;
+    int topY;                 // sky exit (vxpt_tuning.sky_exit): a walk that leaves an empty box above this cell
+                              // row without heading down meets no cube again (-1: never; INT_MAX: off)
     int cx, cy, cz;       // chunks
     int wx, wy, wz;       // cells
     int mx, my, mz;       // 16^3 macro cells

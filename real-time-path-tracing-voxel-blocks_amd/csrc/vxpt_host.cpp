@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <climits>
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
@@ -168,6 +169,7 @@ vxpt_tuning tuning_defaults() {
     t.restir_waves = 0;       // 4 waves: whole frames slower (Appendix A); see bench.band_tuning for bands
     t.ghost_rows = 1;         // bands: the chain's ordered exchange groups 7 -> 3 per frame
     t.chain_gate = 1;         // the chain alone on the GPU (its roofline); bench.band_tuning: 0 for bands
+    t.sky_exit = 0;
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -183,7 +185,7 @@ bool tuning_valid(const vxpt_tuning &t) {
                                        t.resume_split == 8 || t.resume_split == 16) &&
            (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16) &&
            (t.restir_waves == 0 || t.restir_waves == 4) && in(t.ghost_rows, 0, 1) &&
-           in(t.chain_gate, 0, 1);
+           in(t.chain_gate, 0, 1) && in(t.sky_exit, 0, 1);
 }
 
 
@@ -213,6 +215,7 @@ struct vxpt_ctx {
     int nBricks = 0;
     uint64_t top = 0;
     int topValid = 0;
+    int topY = -1;  // the highest cube cell row of the world (edits raise it, never lower it: a bound)
     // host mirrors of the world: picking, incremental edits, chunk files (the device copies are
     // updated from them in place)
     std::vector<uint8_t> hIds, hBricks, hOd;
@@ -548,6 +551,7 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.brickStepsCam = c->tune.cam_steps;
     w.top = c->top;
     w.topValid = c->topValid;
+    w.topY = c->tune.sky_exit ? c->topY : INT_MAX;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
     w.wx = c->cx * 32; w.wy = c->cy * 32; w.wz = c->cz * 32;
     w.mx = w.wx / 16; w.my = w.wy / 16; w.mz = w.wz / 16;
@@ -758,6 +762,7 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     const int tx = (wx + 63) / 64, ty = (wy + 63) / 64, tz = (wz + 63) / 64;
     c->topCount.assign((size_t)tx * ty * tz, 0);
     c->hNonAir.assign((size_t)mx * my * mz * 64, 0);
+    c->topY = -1;
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -773,6 +778,7 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
                     c->hMacro[b / 64] |= 1ull << (b % 64);
                     c->hCell[b] |= 1ull << lc;
                     c->topCount[top_block(c, x, y, z)]++;
+                    c->topY = std::max(c->topY, y);
                 }
             }
     c->topValid = (tx * ty * tz <= 64) ? 1 : 0;
@@ -823,6 +829,7 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
         HIPCHK(c, hipMemcpyAsync(c->cellMask.p + b, &c->hCell[b], 8, hipMemcpyHostToDevice, st));
         c->topCount[top_block(c, x, y, z)] += is_cube(id) ? 1 : -1;
         refresh_top(c);
+        if (is_cube(id)) c->topY = std::max(c->topY, y);
         if ((before != 0) != (c->hCell[b] != 0)) {
             const size_t m = b / 64;
             c->hMacro[m] = c->hCell[b] ? (c->hMacro[m] | (1ull << (b % 64))) : (c->hMacro[m] & ~(1ull << (b % 64)));

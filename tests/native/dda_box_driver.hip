@@ -6,6 +6,7 @@
 //        dda_box_driver ids.bin CX CY CZ --rays rays.bin out.bin   (rays: 8 f32 each, o d tmin tmax;
 //        out per ray: 16 i32 = cube closest (hit x y z face id, t bits), box closest (same, through
 //        save / resume), cube occluded, box occluded -- the probe kernels' modes 0 and 2)
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -67,6 +68,7 @@ int main(int argc, char **argv) {
     };
     std::vector<uint8_t> bricks(nB * 64, 0);
     std::vector<uint64_t> cellMask(nB, 0);
+    int topY = -1;  // the highest cube cell row (the box walks' sky exit)
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -76,7 +78,10 @@ int main(int argc, char **argv) {
                 const size_t b = blin(x >> 2, y >> 2, z >> 2);
                 const int lc = (x & 3) + 4 * ((z & 3) + 4 * (y & 3));
                 bricks[b * 64 + lc] = id;
-                if (id >= 1 && id <= 12) cellMask[b] |= 1ull << lc;
+                if (id >= 1 && id <= 12) {
+                    cellMask[b] |= 1ull << lc;
+                    topY = std::max(topY, y);
+                }
             }
     // the default cube tables (vxpt_host.cpp octant_fill's recurrence, whole grid)
     std::vector<uint8_t> od(8 * nB, 0);
@@ -129,8 +134,10 @@ int main(int argc, char **argv) {
     w.mx = wx / 16; w.my = wy / 16; w.mz = wz / 16;
     // the box-table walks also yield every 3 cell crossings inside a brick (WorldDev::brickSteps; the
     // cube-table walks take whole bricks): the same hits prove the yield and its save / resume exact
+    w.topY = INT_MAX;  // the cube-table walks: no sky exit (the reference walk)
     WorldDev wb = w;
     wb.brickSteps = 3;
+    wb.topY = topY;  // the box walks end above the highest cube when not heading down (vxpt_tuning.sky_exit)
     if (std::string(argv[5]) == "--rays") {
         FILE *fr = fopen(argv[6], "rb");
         if (!fr) return 1;

@@ -11,6 +11,7 @@
 // waves mixing hits and misses (sky), their minority lanes, and the distinct block ids of a wave's
 // hits.
 // Usage: tile_working_set ids.bin CX CY CZ cam.bin W H   (cam.bin: the oracle's camera_info, 32 f32)
+#include <climits>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -105,6 +106,7 @@ int main(int argc, char **argv) {
                 }
     }
     WorldDev w{};
+    w.topY = INT_MAX;  // no sky exit
     w.bricks = bricks.data();
     w.cellMask = cellMask.data();
     w.bdist = od.data();
