@@ -422,7 +422,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_QUEU
         const float4 ro = w.qO[i], rd = w.qD[i];
         id = w.qId[i];
         rc = dda_begin<OCC, BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
-        for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC, BOX>(a.world, st, h, itp);
+        // visibility walks may end above the cubes they can still reach (the sky exit, vx_device.hpp):
+        // the rays toward the sun and sky that leave the terrain (closest-hit walks measured slower with it)
+        for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC, BOX, GlobalBricks, OCC>(a.world, st, h, itp);
     }
 #ifdef VX_STATS
     stat_wave((q & 3) == 1 ? 1 : ((q & 3) == 2 ? 4 : 3), live, iters);
@@ -492,7 +494,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC ? VX_WP
             id = w.qId[e];
             dda_resume<BOX>(a.world, xyz(ro), xyz(rd), ro.w, rd.w, sv, st);
             rc = DdaRun;
-            for (int it = 0; rc == DdaRun && (cap <= 0 || it < cap); ++it) rc = dda_iter<OCC, BOX>(a.world, st, h, itp);
+            for (int it = 0; rc == DdaRun && (cap <= 0 || it < cap); ++it)
+                rc = dda_iter<OCC, BOX, GlobalBricks, OCC>(a.world, st, h, itp);  // sky exit: k_queue
         }
 #ifdef VX_STATS
         stat_wave(5, live, iters);
@@ -566,7 +569,7 @@ __global__ __launch_bounds__(256) void k_resume_split(TraceArgs a, int q, int le
         for (;;) {
             const bool run = rc == DdaRun;
             if (__ballot(run) == 0ull) break;
-            if (run) rc = dda_iter<OCC, BOX>(a.world, st, h VX_IT);
+            if (run) rc = dda_iter<OCC, BOX, GlobalBricks, OCC>(a.world, st, h VX_IT);
             // (the ballot outside the condition: every lane's event must be seen)
             const unsigned long long evNow = __ballot(rc == DdaEvent);
             if (rc == DdaRun && (evNow & below)) rc = DdaNone;  // an earlier piece has it
@@ -1583,7 +1586,7 @@ __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *r
         while (rc == DdaRun) {
             const DdaSaved sv = dda_save(st, i);
             dda_resume<BOX>(w, o, d, tmin, r[7], sv, st);
-            rc = occ ? dda_iter<true, BOX>(w, st, h) : dda_iter<false, BOX>(w, st, h);
+            rc = occ ? dda_iter<true, BOX, GlobalBricks, true>(w, st, h) : dda_iter<false, BOX, GlobalBricks, true>(w, st, h);
         }
         if (occ) {
             q[0] = rc == DdaEvent ? 1 : 0;
@@ -1597,12 +1600,12 @@ __global__ __launch_bounds__(256) void k_probe(WorldDev w, int n, const float *r
         return;
     }
     if (mode == 2) {
-        q[0] = dda_occluded<BOX>(w, o, d, r[6], r[7]) ? 1 : 0;
+        q[0] = dda_occluded<BOX, true>(w, o, d, r[6], r[7]) ? 1 : 0;
         q[1] = q[2] = q[3] = q[4] = q[5] = 0;
         t[i] = 0.0f;
         return;
     }
-    const Hit h = dda_closest<BOX>(w, o, d, r[7]);
+    const Hit h = dda_closest<BOX, GlobalBricks, true>(w, o, d, r[7]);
     q[0] = h.hit; q[1] = h.x; q[2] = h.y; q[3] = h.z; q[4] = h.face; q[5] = h.id;
     t[i] = h.t;
 }

@@ -2,6 +2,7 @@
 // voxel DDA, safe spawn, Disney BSDF, blue-noise sampler, light sampling,
 // reservoirs, sky lookup.  See trace.hip for the pass structure.
 #pragma once
+#include <climits>
 #include "vx_mesh.hpp"
 
 namespace vx {
@@ -413,7 +414,9 @@ VX_HD void dda_seg_start(const WorldDev &w, Dda &s, int D, int P, float T) {
     s.prevLoc = s.nb * 64 + cell_of(c.x, c.y, c.z);
 }
 
-template <bool OCC, bool BOX = false, class F = GlobalBricks>
+// SKY: the walk may end above the cubes it can still reach (WorldDev::skyTop, below); a compile-time
+// switch so that the walks without it (camera rays, a queue's first iterations) keep their code
+template <bool OCC, bool BOX = false, class F = GlobalBricks, bool SKY = false>
 VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const F &f = F()) {
     if (++s.steps > w.wx + w.wy + w.wz + 3) return DdaNone;
     if (cnt) ++cnt[s.dist == 0 ? 3 : (s.dist == 1 ? 2 : 1)];
@@ -428,12 +431,9 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const 
     } else {
         if constexpr (BOX) skip_box(w, s.r, s.c, (int)(s.box & 0xFFu), (int)((s.box >> 8) & 0xFFu), (int)((s.box >> 16) & 0xFFu));
         else skip_cube(w, s.r, s.c, s.dist);
-        // sky exit: the walk stands in an empty cell above every cube cell and does not head down, so no
-        // crossing ahead joins or leaves a cube -- the cell-by-cell walk would reach the world's edge
-        // without an event (prevId is 0 in an empty cell reached without one).  Checked once per empty
-        // box, not per cell step.
-        if (s.c.y > w.topY && !(s.r.dy < 0.0f)) return DdaNone;
     }
+    // sky exit, after an empty box (not per cell step): see below
+    const bool skyCheck = SKY && s.dist != 0 && w.skyTop && !(s.r.dy < 0.0f);
     // the next crossing leaves the brick (or the skipped box)
     float t;
     int planeCoord, face;
@@ -445,7 +445,18 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const 
         // leaving the world: only a visibility ray leaving a cube cell sees a face
         return (OCC && t >= s.tmin && s.prevId != 0) ? DdaEvent : DdaNone;
     }
+    // sky exit: the walk left an empty box (prevId 0: no cube left behind) into a cell at or above every
+    // cube cell of the brick columns it can still reach (x and z only move with the ray, y does not
+    // fall), so this cell is empty and no crossing ahead joins or leaves a cube -- the cell-by-cell walk
+    // would reach the world's edge without an event.  The table entry is fetched beside the brick's.
+    int top = INT_MAX;
+    if constexpr (SKY)
+        if (skyCheck)
+            top = (int)w.skyTop[((size_t)((s.r.sx > 0 ? 1 : 0) | (s.r.sz > 0 ? 2 : 0)) * (w.wz >> 2) + (s.c.z >> 2)) *
+                                    (w.wx >> 2) + (s.c.x >> 2)];
     const bool solid = locate<BOX>(w, s, f);
+    if constexpr (SKY)
+        if (s.c.y >= top) return DdaNone;
     if (solid || s.prevId != 0) {
         if (cross<OCC>(w, s, solid, s.nb * 64 + cell_of(s.c.x, s.c.y, s.c.z), chunkPlane, t, face, h))
             return DdaEvent;
@@ -453,22 +464,22 @@ VX_HD int dda_iter(const WorldDev &w, Dda &s, Hit &h, int *cnt = nullptr, const 
     return DdaRun;
 }
 
-template <bool BOX = false, class F = GlobalBricks>
+template <bool BOX = false, class F = GlobalBricks, bool SKY = false>
 VX_HD Hit dda_closest(const WorldDev &w, V3 o, V3 d, float tmax, int *iters = nullptr, const F &f = F()) {
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
     Dda s;
     int rc = dda_begin<false, BOX>(w, o, d, 0.0f, tmax, s, h, f);
-    while (rc == DdaRun) rc = dda_iter<false, BOX>(w, s, h, iters, f);
+    while (rc == DdaRun) rc = dda_iter<false, BOX, F, SKY>(w, s, h, iters, f);
     if (rc != DdaEvent) h = Hit{0, 0, 0, 0, -1, 0, kRayMax};
     return h;
 }
 
-template <bool BOX = false>
+template <bool BOX = false, bool SKY = false>
 VX_HD bool dda_occluded(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int *iters = nullptr) {
     Hit h;
     Dda s;
     int rc = dda_begin<true, BOX>(w, o, d, tmin, tmax, s, h);
-    while (rc == DdaRun) rc = dda_iter<true, BOX>(w, s, h, iters);
+    while (rc == DdaRun) rc = dda_iter<true, BOX, GlobalBricks, SKY>(w, s, h, iters);
     return rc == DdaEvent;
 }
 

@@ -70,8 +70,10 @@ struct WorldDev {
                               // (0 = 10: a whole brick); vxpt_tuning.brick_steps
     uint64_t top;
     int topValid;
-    int topY;                 // sky exit (vxpt_tuning.sky_exit): a walk that leaves an empty box above this cell
-                              // row without heading down meets no cube again (-1: never; INT_MAX: off)
+    const uint16_t *skyTop;   // sky exit (vxpt_tuning.sky_exit; null: off): per x / z direction quadrant q =
+                              // (dx > 0) | (dz > 0) << 1 and brick column (bx, bz), 1 + the highest cube cell
+                              // row of the columns the quadrant can still reach from it ([q][bz][bx], 0 =
+                              // none): a walk not heading down whose cell row is at least that meets no cube
     int cx, cy, cz;       // chunks
     int wx, wy, wz;       // cells
     int mx, my, mz;       // 16^3 macro cells

@@ -169,7 +169,7 @@ vxpt_tuning tuning_defaults() {
     t.restir_waves = 0;       // 4 waves: whole frames slower (Appendix A); see bench.band_tuning for bands
     t.ghost_rows = 1;         // bands: the chain's ordered exchange groups 7 -> 3 per frame
     t.chain_gate = 1;         // the chain alone on the GPU (its roofline); bench.band_tuning: 0 for bands
-    t.sky_exit = 0;
+    t.sky_exit = 1;           // C3 frame 5.443 -> 5.419 ms (two runs each, both faster); one band 1-2 %
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -215,7 +215,10 @@ struct vxpt_ctx {
     int nBricks = 0;
     uint64_t top = 0;
     int topValid = 0;
-    int topY = -1;  // the highest cube cell row of the world (edits raise it, never lower it: a bound)
+    // sky exit (WorldDev::skyTop): per brick column 1 + its highest cube cell row (edits raise it, never
+    // lower it: a bound), and its suffix maxima per x / z direction quadrant (the device table)
+    std::vector<uint16_t> colTop, hSkyTop;
+    DBuf<uint16_t> skyTop;
     // host mirrors of the world: picking, incremental edits, chunk files (the device copies are
     // updated from them in place)
     std::vector<uint8_t> hIds, hBricks, hOd;
@@ -551,7 +554,7 @@ void fill_world(vxpt_ctx *c, WorldDev &w) {
     w.brickStepsCam = c->tune.cam_steps;
     w.top = c->top;
     w.topValid = c->topValid;
-    w.topY = c->tune.sky_exit ? c->topY : INT_MAX;
+    w.skyTop = c->tune.sky_exit ? c->skyTop.p : nullptr;
     w.cx = c->cx; w.cy = c->cy; w.cz = c->cz;
     w.wx = c->cx * 32; w.wy = c->cy * 32; w.wz = c->cz * 32;
     w.mx = w.wx / 16; w.my = w.wy / 16; w.mz = w.wz / 16;
@@ -753,6 +756,29 @@ void refresh_top(vxpt_ctx *c) {
 }
 
 // DDA acceleration layout (WorldDev) from chunk-major ids, built in the host mirrors and uploaded
+// the sky exit's table: for each x / z direction quadrant q ((dx > 0) | (dz > 0) << 1) and brick column,
+// the highest 1 + cube row over the columns a walk in that quadrant can still reach (x, z not moving
+// against the ray: a suffix maximum along each axis), uploaded on the context stream
+int upload_sky_top(vxpt_ctx *c) {
+    const int nbx = c->cx * 8, nbz = c->cz * 8;
+    c->hSkyTop.assign((size_t)4 * nbx * nbz, 0);
+    for (int q = 0; q < 4; ++q) {
+        const bool px = q & 1, pz = q & 2;
+        uint16_t *t = c->hSkyTop.data() + (size_t)q * nbx * nbz;
+        for (int kz = 0; kz < nbz; ++kz)
+            for (int kx = 0; kx < nbx; ++kx) {
+                // walk the columns from the far corner of the quadrant towards its origin
+                const int bz = pz ? nbz - 1 - kz : kz, bx = px ? nbx - 1 - kx : kx;
+                const int fz = pz ? bz + 1 : bz - 1, fx = px ? bx + 1 : bx - 1;  // the next column along z / x
+                uint16_t m = c->colTop[(size_t)bz * nbx + bx];
+                if (fz >= 0 && fz < nbz) m = std::max(m, t[(size_t)fz * nbx + bx]);
+                if (fx >= 0 && fx < nbx) m = std::max(m, t[(size_t)bz * nbx + fx]);
+                t[(size_t)bz * nbx + bx] = m;
+            }
+    }
+    return upload_vec(c, c->skyTop, c->hSkyTop.data(), c->hSkyTop.size());
+}
+
 int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     const int wx = c->cx * 32, wy = c->cy * 32, wz = c->cz * 32;
     const int mx = wx / 16, my = wy / 16, mz = wz / 16;
@@ -762,7 +788,7 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
     const int tx = (wx + 63) / 64, ty = (wy + 63) / 64, tz = (wz + 63) / 64;
     c->topCount.assign((size_t)tx * ty * tz, 0);
     c->hNonAir.assign((size_t)mx * my * mz * 64, 0);
-    c->topY = -1;
+    c->colTop.assign((size_t)(wx >> 2) * (wz >> 2), 0);
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -778,11 +804,13 @@ int build_occupancy(vxpt_ctx *c, const uint8_t *ids) {
                     c->hMacro[b / 64] |= 1ull << (b % 64);
                     c->hCell[b] |= 1ull << lc;
                     c->topCount[top_block(c, x, y, z)]++;
-                    c->topY = std::max(c->topY, y);
+                    uint16_t &ct = c->colTop[(size_t)(z >> 2) * (wx >> 2) + (x >> 2)];
+                    ct = std::max<uint16_t>(ct, (uint16_t)(y + 1));
                 }
             }
     c->topValid = (tx * ty * tz <= 64) ? 1 : 0;
     refresh_top(c);
+    if (int r = upload_sky_top(c)) return r;
     const int BX = wx / 4, BY = wy / 4, BZ = wz / 4;
     const size_t nB = (size_t)BX * BY * BZ;
     c->hOd.assign(8 * nB, 0);
@@ -829,7 +857,10 @@ int set_block(vxpt_ctx *c, int x, int y, int z, int id) {
         HIPCHK(c, hipMemcpyAsync(c->cellMask.p + b, &c->hCell[b], 8, hipMemcpyHostToDevice, st));
         c->topCount[top_block(c, x, y, z)] += is_cube(id) ? 1 : -1;
         refresh_top(c);
-        if (is_cube(id)) c->topY = std::max(c->topY, y);
+        if (is_cube(id) && c->colTop[(size_t)(z >> 2) * (wx >> 2) + (x >> 2)] < y + 1) {
+            c->colTop[(size_t)(z >> 2) * (wx >> 2) + (x >> 2)] = (uint16_t)(y + 1);
+            if (int r = upload_sky_top(c)) return r;
+        }
         if ((before != 0) != (c->hCell[b] != 0)) {
             const size_t m = b / 64;
             c->hMacro[m] = c->hCell[b] ? (c->hMacro[m] | (1ull << (b % 64))) : (c->hMacro[m] & ~(1ull << (b % 64)));

@@ -26,7 +26,7 @@ static int split_walk(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
     Dda s;
     int rc = dda_begin<OCC, true>(w, o, d, tmin, tmax, s, h);
-    for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC, true>(w, s, h);
+    for (int k = 0; rc == DdaRun && k < cap; ++k) rc = dda_iter<OCC, true, GlobalBricks, true>(w, s, h);
     if (rc != DdaRun) { out = h; return rc; }
     const DdaSaved sv = dda_save(s, 0);
     Dda s0;
@@ -45,7 +45,7 @@ static int split_walk(const WorldDev &w, V3 o, V3 d, float tmin, float tmax, int
         sk.tmax = fminf(T1, tmax);
         Hit hk{0, 0, 0, 0, -1, 0, kRayMax};
         int r = DdaRun;
-        while (r == DdaRun) r = dda_iter<OCC, true>(w, sk, hk);
+        while (r == DdaRun) r = dda_iter<OCC, true, GlobalBricks, true>(w, sk, hk);
         if (r == DdaEvent) { out = hk; return DdaEvent; }
     }
     out = Hit{0, 0, 0, 0, -1, 0, kRayMax};
@@ -68,7 +68,10 @@ int main(int argc, char **argv) {
     };
     std::vector<uint8_t> bricks(nB * 64, 0);
     std::vector<uint64_t> cellMask(nB, 0);
-    int topY = -1;  // the highest cube cell row (the box walks' sky exit)
+    // the box walks' sky exit (WorldDev::skyTop): 1 + the highest cube row per brick column, then its
+    // suffix maxima per x / z direction quadrant (the library's upload_sky_top, restated)
+    const int nbx = wx / 4, nbz = wz / 4;
+    std::vector<uint16_t> colTop((size_t)nbx * nbz, 0), skyTop((size_t)4 * nbx * nbz, 0);
     for (int y = 0; y < wy; ++y)
         for (int z = 0; z < wz; ++z)
             for (int x = 0; x < wx; ++x) {
@@ -80,7 +83,8 @@ int main(int argc, char **argv) {
                 bricks[b * 64 + lc] = id;
                 if (id >= 1 && id <= 12) {
                     cellMask[b] |= 1ull << lc;
-                    topY = std::max(topY, y);
+                    uint16_t &ct = colTop[(size_t)(z >> 2) * nbx + (x >> 2)];
+                    if (ct < y + 1) ct = (uint16_t)(y + 1);
                 }
             }
     // the default cube tables (vxpt_host.cpp octant_fill's recurrence, whole grid)
@@ -134,10 +138,21 @@ int main(int argc, char **argv) {
     w.mx = wx / 16; w.my = wy / 16; w.mz = wz / 16;
     // the box-table walks also yield every 3 cell crossings inside a brick (WorldDev::brickSteps; the
     // cube-table walks take whole bricks): the same hits prove the yield and its save / resume exact
-    w.topY = INT_MAX;  // the cube-table walks: no sky exit (the reference walk)
+    for (int q = 0; q < 4; ++q)
+        for (int kz = 0; kz < nbz; ++kz)
+            for (int kx = 0; kx < nbx; ++kx) {
+                const int bz = (q & 2) ? nbz - 1 - kz : kz, bx = (q & 1) ? nbx - 1 - kx : kx;
+                const int fz = (q & 2) ? bz + 1 : bz - 1, fx = (q & 1) ? bx + 1 : bx - 1;
+                uint16_t *t = skyTop.data() + (size_t)q * nbx * nbz;
+                uint16_t m = colTop[(size_t)bz * nbx + bx];
+                if (fz >= 0 && fz < nbz && t[(size_t)fz * nbx + bx] > m) m = t[(size_t)fz * nbx + bx];
+                if (fx >= 0 && fx < nbx && t[(size_t)bz * nbx + fx] > m) m = t[(size_t)bz * nbx + fx];
+                t[(size_t)bz * nbx + bx] = m;
+            }
+    // the cube-table walks: no sky exit (w.skyTop null, the reference walk)
     WorldDev wb = w;
     wb.brickSteps = 3;
-    wb.topY = topY;  // the box walks end above the highest cube when not heading down (vxpt_tuning.sky_exit)
+    wb.skyTop = skyTop.data();  // the box walks end above every cube ahead when not heading down (sky_exit)
     if (std::string(argv[5]) == "--rays") {
         FILE *fr = fopen(argv[6], "rb");
         if (!fr) return 1;
@@ -158,7 +173,7 @@ int main(int argc, char **argv) {
             while (rb == DdaRun) {
                 const DdaSaved sv = dda_save(sb, 0);
                 dda_resume<true>(wb, o, d, 0.0f, r[7], sv, sb);
-                rb = dda_iter<false, true>(wb, sb, hb);
+                rb = dda_iter<false, true, GlobalBricks, true>(wb, sb, hb);
             }
             if (rb != DdaEvent) hb = Hit{0, 0, 0, 0, -1, 0, kRayMax};
             const Hit hs[2] = {hc, hb};
@@ -167,7 +182,7 @@ int main(int argc, char **argv) {
                 q[7 * k + 4] = hs[k].face; q[7 * k + 5] = hs[k].id; q[7 * k + 6] = float_as_bits(hs[k].t);
             }
             q[14] = dda_occluded<false>(w, o, d, r[6], r[7]) ? 1 : 0;
-            q[15] = dda_occluded<true>(wb, o, d, r[6], r[7]) ? 1 : 0;
+            q[15] = dda_occluded<true, true>(wb, o, d, r[6], r[7]) ? 1 : 0;
         }
         FILE *fo = fopen(argv[7], "wb");
         if (!fo || fwrite(out.data(), 4, out.size(), fo) != out.size()) return 1;
@@ -198,7 +213,7 @@ int main(int argc, char **argv) {
         while (rb == DdaRun) {
             // every other ray through the straggler hand-over (dda_save / dda_resume)
             if (i & 1) { const DdaSaved sv = dda_save(sb, 0); dda_resume<true>(wb, o, d, 0.0f, tmax, sv, sb); }
-            rb = dda_iter<false, true>(wb, sb, hb);
+            rb = dda_iter<false, true, GlobalBricks, true>(wb, sb, hb);
             ++n2;
         }
         if (rb != DdaEvent) hb = Hit{0, 0, 0, 0, -1, 0, kRayMax};
@@ -206,7 +221,7 @@ int main(int argc, char **argv) {
         hits += hc.hit;
         const bool same = hc.hit == hb.hit && hc.x == hb.x && hc.y == hb.y && hc.z == hb.z && hc.face == hb.face &&
                           hc.id == hb.id && float_as_bits(hc.t) == float_as_bits(hb.t);
-        const bool oc = dda_occluded<false>(w, o, d, tmin, tmax), ob = dda_occluded<true>(wb, o, d, tmin, tmax);
+        const bool oc = dda_occluded<false>(w, o, d, tmin, tmax), ob = dda_occluded<true, true>(wb, o, d, tmin, tmax);
         for (int G : {2, 4, 8, 16}) {
             const int cap = i % 7;
             Hit hs;

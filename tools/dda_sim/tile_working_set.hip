@@ -106,7 +106,6 @@ int main(int argc, char **argv) {
                 }
     }
     WorldDev w{};
-    w.topY = INT_MAX;  // no sky exit
     w.bricks = bricks.data();
     w.cellMask = cellMask.data();
     w.bdist = od.data();
