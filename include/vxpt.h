@@ -151,7 +151,7 @@ typedef struct vxpt_tuning {
     int32_t box_cap_up;       /* the same for the upward octants                                        (8) */
     int32_t brick_steps;      /* in-brick cell crossings before a queued walk yields, 1..64            (3) */
     int32_t cam_steps;        /* the same for camera / continuing path rays (k_closest), 1..64         (10) */
-    int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (6) */
+    int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (5) */
     int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024     (16) */
     int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (16) */
     int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (0) */

@@ -152,7 +152,8 @@ vxpt_tuning tuning_defaults() {
     t.box_cap_up = kBoxCap;
     t.brick_steps = 3;        // in-brick walks yield after 3 crossings: 6.44 -> 6.26 ms
     t.cam_steps = 10;         // camera rays walk whole bricks
-    t.iter_cap = 6;           // caps 4 / 6 / 8 / 12: 7.02 / 6.84 / 7.07 / 7.63 ms
+    t.iter_cap = 5;           // caps 4 / 6 / 8 / 12: 7.02 / 6.84 / 7.07 / 7.63 ms (round 2); with the sky exit
+                              // (round 6) 5 against 6: 5.439 / 5.438 / 5.440 / 5.463 -> 5.410 / 5.399 / 5.413 / 5.423 ms
     t.iter_cap2 = 16;         // a second level after 16 more iterations, its walks in resume_split pieces:
                               // 5.74 -> 5.66-5.68 ms (one lane per walk at that level: 7.59 ms, round 2)
     t.resume_wg_per_cu = 16;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms

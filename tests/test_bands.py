@@ -148,7 +148,8 @@ def test_gpu_bands_match_single_context():
                                                (3, 96, 320, [0, 80, 248, 320], None),
                                                (8, 640, 640, [0, 72, 144, 224, 304, 384, 464, 560, 640], None),
                                                (8, 640, 640, None, "bench"),
-                                               (3, 96, 320, [0, 80, 248, 320], "noghost")])
+                                               (3, 96, 320, [0, 80, 248, 320], "noghost"),
+                                               (3, 96, 320, None, "atrous2"), (2, 64, 160, None, "nofix")])
 def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits, tune):
     """The library's own band schedule (vxpt_band_link / vxpt_render_frame_linked: the one
     vxpt_band_comm_init runs over RCCL, with device copies between the contexts as the
@@ -157,7 +158,9 @@ def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits, tune)
     partitions (vxpt_band_link_rows, the cost-balanced bands of vxpt_band_balance) too, with
     bands as short as the halo itself.  tune "bench": the band contexts run bench.band_tuning's
     schedule (third state set and front stream, straggler walks in 16 pieces); "noghost": the chain
-    exchanges after every pass (ghost_rows 0) instead of computing its ghost rows."""
+    exchanges after every pass (ghost_rows 0) instead of computing its ghost rows; "atrous2" (two a-trous
+    iterations: steps 2..32, ghost margins too deep for the planes' halo, so the per-pass exchange) and
+    "nofix" (no history fix: the per-pass schedule too) other denoiser settings."""
     import vxpt
     from bench import band_tuning
     spp = 4
@@ -172,6 +175,10 @@ def test_gpu_library_band_schedule_matches_single_context(n, w, h, splits, tune)
         return r
 
     p = vxpt.DenoiseParams.defaults()
+    if tune == "atrous2":
+        p.atrous_iteration_num = 2
+    if tune == "nofix":
+        p.enable_history_fix = 0
     single = make()
     rs = [make() for _ in range(n)]
     if tune == "bench":

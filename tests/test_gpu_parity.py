@@ -341,7 +341,7 @@ TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=2), dict(sort_mode=1), dict(
                    dict(lds_bricks=1), dict(iter_cap2=0, resume_split=1), dict(iter_cap2=0, resume_split=4),
                    dict(iter_cap2=8, resume_split=16), dict(iter_cap2=2, resume_split=2), dict(restir_waves=4),
                    dict(chain_gate=0), dict(chain_gate=0, state_sets=2, front_streams=1),
-                   dict(chain_gate=0, state_sets=3, front_streams=3), dict(sky_exit=0)]
+                   dict(chain_gate=0, state_sets=3, front_streams=3), dict(sky_exit=0), dict(iter_cap=6)]
 
 
 @pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
