@@ -293,7 +293,8 @@ def test_band_balance_keeps_uniform_costs_and_rejects_bad_partitions():
 
 class _TimedBand:
     """A stand-in renderer for bench.balance_bands: a frame of band [y0, y1) takes the synthetic
-    cost of its rows in wall time (5 ms for a whole 1080-row frame, rows near the top 3x the rest)."""
+    cost of its rows in wall time (20 ms for a whole 1080-row frame, rows near the top 3x the rest: long
+    enough that scheduling noise on a loaded host stays a few per cent of a band's time)."""
     def __init__(self):
         self.y0, self.y1 = 0, 1080
 
@@ -303,7 +304,7 @@ class _TimedBand:
     def render_frames(self, f0, n, spp, params):
         import time
         y = np.arange(self.y0, self.y1)
-        time.sleep(n * float(np.where(y < 360, 3.0, 1.0).sum()) * 5e-3 / 1800.0)
+        time.sleep(n * float(np.where(y < 360, 3.0, 1.0).sum()) * 20e-3 / 1800.0)
 
     def sync(self):
         pass
