@@ -240,7 +240,7 @@ def band_tuning(width, height, world):
     if width * height / world < 700e3:
         t["front_streams"] = 3
     if width * height / world < 400e3:
-        # the second straggler level after 6 + 8 iterations (the library's default: 6 + 16), its walks
+        # the second straggler level after 5 + 8 iterations (the library's default: 5 + 16), its walks
         # in 16 pieces: a small band's passes wait on their longest walks (136-row 1080p band
         # 1.40-1.42 -> 1.31-1.34 ms per frame; 272 rows even: DESIGN.md §4)
         t["iter_cap2"] = 8
