@@ -177,7 +177,12 @@ typedef struct vxpt_tuning {
                                  finished (the chain runs alone); 0: as soon as their state set is free
                                  (spp >= 2 and no uploaded motion plane; otherwise the gate stays)       (1) */
     int32_t sky_exit;         /* 1: a walk that leaves an empty box above the world's highest cube cell without
-                                 heading down ends there (nothing ahead can be hit)                      (0) */
+                                 heading down ends there (nothing ahead can be hit)                      (1) */
+    int32_t xcd_order;        /* XCD-local work order, bits: 1 k_restir and 2 k_closest take their pixel tiles in
+                                 XCD-local panels (each XCD one stripe of tile rows, walked column by
+                                 column: the temporal taps / bricks of the workgroups in flight on one XCD
+                                 meet in its L2); 4 k_queue's workgroups take one contiguous run of the
+                                 queue per XCD; 0: raster / queue order, 0..7                             (0) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);

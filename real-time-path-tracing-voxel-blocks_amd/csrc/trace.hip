@@ -78,6 +78,24 @@ VX_D bool slot_pixel(const TraceArgs &a, int s, int &px, int &py) {
     return s < a.nSlots && px < a.W && py < a.y1;
 }
 
+// XCD-local work order (tuning xcd_order).  Workgroups are dispatched to the 8 XCDs in turn, so XCD x
+// runs workgroups x, x + 8, ...: xcd_run gives them one contiguous run of [0, nb) instead (a bijection).
+VX_D int xcd_run(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7, x = b & 7, j = b >> 3;
+    return x * q + min(x, r) + j;
+}
+// A workgroup's 4 tiles of one tile row: each XCD's run of the tile grid cut into panels of
+// ceil(rows / 8) tile rows walked column by column -- the random temporal taps (a disk of 64 px) or the
+// bricks of the workgroups in flight on one XCD then fall in one window of its L2.  A bijection on
+// [0, nb) when nb = bx x tile rows (the host enables it only then); only the order changes.
+VX_D int xcd_panel_block(int b, int nb, int bx) {
+    const int L = xcd_run(b, nb);
+    const int tr = nb / bx, p = (tr + 7) >> 3;
+    const int panel = L / (p * bx), k = L - panel * p * bx;
+    const int rows = min(p, tr - panel * p);
+    return (panel * p + k % rows) * bx + k / rows;
+}
+
 VX_D int4 pack_hit(const Hit &h) { return make_int4(h.x, h.y, h.z, (h.face & 15) | (h.id << 4) | (h.hit << 12)); }
 VX_D Hit unpack_hit(int4 v, float t) {
     Hit h;
@@ -224,7 +242,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_CLOS
         for (int k = threadIdx.x; k < kLdsBrickSlots; k += 256) cache.key[k] = -1;
         __syncthreads();
     }
-    const int s = blockIdx.x * 256 + threadIdx.x;
+    const int blk = (a.xcdOrder & 2) ? xcd_panel_block(blockIdx.x, gridDim.x, a.tilesX >> 2) : blockIdx.x;
+    const int s = blk * 256 + threadIdx.x;
     int px, py;
     bool active = slot_pixel(a, s, px, py);
     const WaveBufs &w = a.wb;
@@ -407,7 +426,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VX_WPE_QUEU
     const WaveBufs &w = a.wb;
     const unsigned n = w.qCount[q];
     if (blockIdx.x * 256 >= n) return;  // whole workgroup past the end
-    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    const int nLive = (int)((n + 255) / 256);
+    const unsigned i = ((a.xcdOrder & 4) ? xcd_run(blockIdx.x, nLive) : blockIdx.x) * 256 + threadIdx.x;
     const bool live = i < n;
     Hit h{0, 0, 0, 0, -1, 0, kRayMax};
     Dda st;
@@ -1403,7 +1423,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __shared__ float4 stash[3][2][256];
     QRays qr;
     qr.mask = 0u;
-    restir_slot<MESH>(a, seg, blockIdx.x * 256 + threadIdx.x, qr, stash);
+    const int blk = (a.xcdOrder & 1) ? xcd_panel_block(blockIdx.x, gridDim.x, a.tilesX >> 2) : blockIdx.x;
+    restir_slot<MESH>(a, seg, blk * 256 + threadIdx.x, qr, stash);
     block_enqueue(a, 4 * seg + 3, qr);
 }
 

@@ -238,6 +238,7 @@ struct TraceArgs {
     int ldsBricks;      // k_closest reads bricks through a workgroup cache in LDS (trace.hip LdsBricks)
     int resumeSplit;    // straggler walks cut into this many pieces, one lane each (trace.hip k_resume_split)
     int restirWaves;    // k_restir's occupancy bound (0: the compiler's, 4: 4 waves/SIMD)
+    int xcdOrder;       // XCD-local workgroup order, bits 1 k_restir, 2 k_closest, 4 k_queue (vxpt_tuning.xcd_order)
     int laterSplit;     // the same for the queues of a path's later segments, after 8 more iterations
     int writeMotion;    // store the (zero) motion vectors: the plane may hold a host upload
     int writePlanes;    // store the G-buffer planes (0: a frame's passes before its last -- only their tap

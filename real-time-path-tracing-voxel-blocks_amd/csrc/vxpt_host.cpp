@@ -171,6 +171,7 @@ vxpt_tuning tuning_defaults() {
     t.ghost_rows = 1;         // bands: the chain's ordered exchange groups 7 -> 3 per frame
     t.chain_gate = 1;         // the chain alone on the GPU (its roofline); bench.band_tuning: 0 for bands
     t.sky_exit = 1;           // C3 frame 5.443 -> 5.419 ms (two runs each, both faster); one band 1-2 %
+    t.xcd_order = 0;
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -186,7 +187,7 @@ bool tuning_valid(const vxpt_tuning &t) {
                                        t.resume_split == 8 || t.resume_split == 16) &&
            (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16) &&
            (t.restir_waves == 0 || t.restir_waves == 4) && in(t.ghost_rows, 0, 1) &&
-           in(t.chain_gate, 0, 1) && in(t.sky_exit, 0, 1);
+           in(t.chain_gate, 0, 1) && in(t.sky_exit, 0, 1) && in(t.xcd_order, 0, 7);
 }
 
 
@@ -1020,6 +1021,8 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.resumeSplit = c->tune.resume_split;
     a.laterSplit = c->tune.later_split;
     a.restirWaves = c->tune.restir_waves;
+    // whole 4-tile workgroups per tile row for the panels
+    a.xcdOrder = c->tune.xcd_order & (a.tilesX % 4 == 0 ? 7 : 4);
     a.prevSceneEmpty = c->prevSceneEmpty;
     // the one pass after a light update remaps the previous pass's light indices (OptixRenderer.cpp:447-457)
     a.lightsDirty = (c->lightsDirty && c->prevNumLights > 0) ? 1 : 0;

@@ -341,7 +341,7 @@ TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=2), dict(sort_mode=1), dict(
                    dict(lds_bricks=1), dict(iter_cap2=0, resume_split=1), dict(iter_cap2=0, resume_split=4),
                    dict(iter_cap2=8, resume_split=16), dict(iter_cap2=2, resume_split=2), dict(restir_waves=4),
                    dict(chain_gate=0), dict(chain_gate=0, state_sets=2, front_streams=1),
-                   dict(chain_gate=0, state_sets=3, front_streams=3), dict(sky_exit=0), dict(iter_cap=6)]
+                   dict(chain_gate=0, state_sets=3, front_streams=3), dict(sky_exit=0), dict(iter_cap=6), dict(xcd_order=7)]
 
 
 @pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
@@ -364,6 +364,27 @@ def test_tuning_changes_no_result(variant):
                 r.render_frame(f, 4, p)
         for name in ("ILLUM", "DEPTH", "NORMAL_ROUGH", "TAP_RECORD", "RES_EVEN", "RES_ODD", "PREV_ILLUM",
                      "PREV_FAST", "HIST_LEN", "OUTPUT"):
+            np.testing.assert_array_equal(a.read(name).view(np.uint8), b.read(name).view(np.uint8), err_msg=name)
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.parametrize("w,h,order", [(128, 72, 7), (256, 40, 7), (96, 136, 7), (96, 136, 1), (128, 72, 2),
+                                         (100, 70, 7)])
+def test_xcd_order_changes_no_result(w, h, order):
+    """xcd_order (k_restir / k_closest in XCD-local panels, k_queue in XCD-local runs of its queue) at
+    widths of whole 4-tile workgroups (at 100 px the library keeps the panels off, the queue runs on):
+    3 frames of 4 spp equal the default order's bit for bit -- 9 / 5 / 17 tile rows: one-row panels,
+    uneven last panels."""
+    a, _ = _setup(w, h)
+    b, _ = _setup(w, h)
+    b.set_tuning(xcd_order=order)
+    p = _dn_params()
+    try:
+        a.render_frames(0, 3, 4, p)
+        b.render_frames(0, 3, 4, p)
+        for name in ("ILLUM", "TAP_RECORD", "RES_EVEN", "RES_ODD", "HIST_LEN", "OUTPUT"):
             np.testing.assert_array_equal(a.read(name).view(np.uint8), b.read(name).view(np.uint8), err_msg=name)
     finally:
         a.close()
