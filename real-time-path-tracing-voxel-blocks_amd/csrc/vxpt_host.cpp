@@ -3411,6 +3411,9 @@ int band_gather(std::vector<vxpt_ctx *> &cs, int which, int root) {
     }
     if (cs.size() == 1 && c0->comm) {
         size_t rb;
+        // behind every halo group on the exchange stream too: one communicator's groups run in issue
+        // order on every rank (a gather beside a pending halo group could pair differently per rank)
+        if (c0->haloPending) HIPCHK(c0, hipStreamWaitEvent(c0->stream, c0->haloDone, 0));
         if (ncclGroupStart() != ncclSuccess) return fail(c0, VXPT_ERR_HIP, "ncclGroupStart");
         ncclResult_t rc = ncclSuccess;
         if (c0->rank == root) {
