@@ -240,11 +240,12 @@ def band_tuning(width, height, world):
     if width * height / world < 700e3:
         t["front_streams"] = 3
     if width * height / world < 400e3:
-        # the second straggler level after 5 + 8 iterations (the library's default: 5 + 16), its walks
-        # in 16 pieces: a small band's passes wait on their longest walks (136-row 1080p band
-        # 1.40-1.42 -> 1.31-1.34 ms per frame; 272 rows even: DESIGN.md §4)
-        t["iter_cap2"] = 8
-        t["resume_split"] = 16
+        # the round-5 walk ladder: the second straggler level after 5 + 8 iterations, its walks in 16
+        # pieces (a small band's passes wait on their longest walks: 136-row 1080p band 1.40-1.42 ->
+        # 1.31-1.34 ms per frame; 272 rows even: DESIGN.md §4), no third level (the library's 4 / 6 / 12
+        # ladder adds a launch to each traversal's chain: 8-band 1080p bands 8-10 % slower; 2- and 4-band
+        # bands gain 2-5 % with it)
+        t.update(iter_cap=5, iter_cap2=8, iter_cap3=0, resume_split=16)
     return t
 
 

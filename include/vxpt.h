@@ -151,8 +151,8 @@ typedef struct vxpt_tuning {
     int32_t box_cap_up;       /* the same for the upward octants                                        (8) */
     int32_t brick_steps;      /* in-brick cell crossings before a queued walk yields, 1..64            (3) */
     int32_t cam_steps;        /* the same for camera / continuing path rays (k_closest), 1..64         (10) */
-    int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (5) */
-    int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024     (16) */
+    int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (4) */
+    int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024      (6) */
     int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (16) */
     int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (0) */
     int32_t overlap;          /* 1: pass halves and pipelined frames on two streams; 0: in order        (1) */
@@ -183,6 +183,11 @@ typedef struct vxpt_tuning {
                                  column: the temporal taps / bricks of the workgroups in flight on one XCD
                                  meet in its L2); 4 k_queue's workgroups take one contiguous run of the
                                  queue per XCD; 0: raster / queue order, 0..7                             (0) */
+    int32_t iter_cap3;        /* with iter_cap2: a third straggler level after iter_cap2 more iterations, the
+                                 level-2 walks resumed for that many more before the last level (0: off),
+                                 0..1024                                                                 (12) */
+    int32_t iter_cap4;        /* with iter_cap3: a fourth level, the level-3 walks resumed for that many more
+                                 before the last level (0: off), 0..1024                                   (0) */
 } vxpt_tuning;
 int vxpt_tuning_defaults(vxpt_tuning *out);
 int vxpt_get_tuning(vxpt_ctx *ctx, vxpt_tuning *out);

@@ -1708,10 +1708,21 @@ struct Launcher {
             return;
         }
         hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 1, shardCap, cap2);
+        // (tuning iter_cap3: one more capped level, its stragglers compacted again before the last;
+        // the straggler states ping-pong, so level 3 reuses the level-1 buffer, consumed by then)
+        int last = 2;
+        if (cap2 > 0 && !later && a.iterCap3 > 0) {
+            hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, a.iterCap3);
+            last = 3;
+            if (a.iterCap4 > 0) {
+                hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 3, shardCap, a.iterCap4);
+                last = 4;
+            }
+        }
         if (cap2 > 0 && G > 1)
-            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, G);
+            hipLaunchKernelGGL((k_resume_split<OCC, BOX>), gr, b, 0, st, a, q, last, shardCap, G);
         else if (cap2 > 0)
-            hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, 2, shardCap, 0);
+            hipLaunchKernelGGL((k_resume<OCC, BOX>), gr, b, 0, st, a, q, last, shardCap, 0);
     }
     void trav(bool occ, int q, int cap) {
         const dim3 gq((cap + 255) / 256);

@@ -109,7 +109,7 @@ struct GBuf {
 // most kQueues / 4 segments (vxpt_create bounds total_bounce_limit); straggler queues in kShards shards
 constexpr int kQueues = 64;
 constexpr int kShards = 8;
-constexpr size_t kQueueWords = 2 * kQueues + 3 * kQueues * kShards * 16;
+constexpr size_t kQueueWords = 2 * kQueues + 4 * kQueues * kShards * 16;
 static_assert(kQueueWords % 4 == 0, "k_closest zeroes the counters as uint4");
 
 struct WaveBufs {
@@ -151,7 +151,7 @@ struct WaveBufs {
     // result id; one storage reused by the pass's queues, counters 4 per segment
     float4 *qO, *qD;
     int *qId;
-    unsigned *qCount;  // kQueueWords: kQueues queue counters, kQueues unused words, then per straggler level (1-3) kQueues queues x kShards shard counters 16 words apart
+    unsigned *qCount;  // kQueueWords: kQueues queue counters, kQueues unused words, then per straggler level (1-4) kQueues queues x kShards shard counters 16 words apart
     // straggler queues (ping-pong by level): walk state of rays stopped at an iteration cap (DdaSaved)
     int4 *sCell[2];
     float4 *sT[2];
@@ -215,6 +215,7 @@ struct TraceArgs {
     int tilesX, nSlots;         // 8x8 tiles across the frame width; slots in the band
     int numCU;                  // compute units of the device (traversal grid sizing)
     int iterCap, iterCap2;      // outer DDA iterations before a ray moves to the level-1 / level-2 straggler queue
+    int iterCap3, iterCap4;     // > 0: a level-2 (then level-3) resume of that many iterations before the last level
     int prevSceneEmpty;         // the pass after a voxel edit: temporal visibility rays see no previous scene
     const TexInfo *tex;         // texture table (nullptr: no textures loaded)
     const uchar4 *texels;       // every texture's mip chain, RGBA8

@@ -152,10 +152,12 @@ vxpt_tuning tuning_defaults() {
     t.box_cap_up = kBoxCap;
     t.brick_steps = 3;        // in-brick walks yield after 3 crossings: 6.44 -> 6.26 ms
     t.cam_steps = 10;         // camera rays walk whole bricks
-    t.iter_cap = 5;           // caps 4 / 6 / 8 / 12: 7.02 / 6.84 / 7.07 / 7.63 ms (round 2); with the sky exit
+    t.iter_cap = 4;           // caps 4 / 6 / 8 / 12: 7.02 / 6.84 / 7.07 / 7.63 ms (round 2); with the sky exit
                               // (round 6) 5 against 6: 5.439 / 5.438 / 5.440 / 5.463 -> 5.410 / 5.399 / 5.413 / 5.423 ms
-    t.iter_cap2 = 16;         // a second level after 16 more iterations, its walks in resume_split pieces:
-                              // 5.74 -> 5.66-5.68 ms (one lane per walk at that level: 7.59 ms, round 2)
+    t.iter_cap2 = 6;          // a second level after 6 more iterations (round 2-6: 16, its walks in resume_split
+                              // pieces: 5.74 -> 5.66-5.68 ms; one lane per walk at that level: 7.59 ms, round 2)
+    t.iter_cap3 = 12;         // round 6: a third level, 12 more iterations, before the pieces: the ladder 4 / 6 / 12
+                              // against 5 / 16: 5.46 -> 5.20 ms per C3 frame (four runs each)
     t.resume_wg_per_cu = 16;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms
     t.sort_mode = 0;          // direction-class sort: 1.5 % faster traversal, producers pay it back
     t.overlap = 1;            // pass halves on two streams: 6.84 -> 6.06 ms
@@ -172,6 +174,7 @@ vxpt_tuning tuning_defaults() {
     t.chain_gate = 1;         // the chain alone on the GPU (its roofline); bench.band_tuning: 0 for bands
     t.sky_exit = 1;           // C3 frame 5.443 -> 5.419 ms (two runs each, both faster); one band 1-2 %
     t.xcd_order = 0;
+    t.iter_cap4 = 0;          // a fourth level: 4 / 8 / 16 / 6-8-12 ladders 5.26-5.27 ms, no gain
     t.front_streams = 2;      // first halves of consecutive passes side by side: 5.89 -> 5.76 ms per C3
                               // frame; one 136-row band 1.95 -> 1.63 ms (1.56 with 3 state sets)
     return t;
@@ -187,7 +190,7 @@ bool tuning_valid(const vxpt_tuning &t) {
                                        t.resume_split == 8 || t.resume_split == 16) &&
            (t.later_split == 1 || t.later_split == 2 || t.later_split == 4 || t.later_split == 8 || t.later_split == 16) &&
            (t.restir_waves == 0 || t.restir_waves == 4) && in(t.ghost_rows, 0, 1) &&
-           in(t.chain_gate, 0, 1) && in(t.sky_exit, 0, 1) && in(t.xcd_order, 0, 7);
+           in(t.chain_gate, 0, 1) && in(t.sky_exit, 0, 1) && in(t.xcd_order, 0, 7) && in(t.iter_cap3, 0, 1024) && in(t.iter_cap4, 0, 1024);
 }
 
 
@@ -1015,6 +1018,8 @@ int trace_front(vxpt_ctx *c, int32_t it, uint32_t flags, bool accumulate, bool a
     a.numCU = c->numCU;
     a.iterCap = c->tune.iter_cap;
     a.iterCap2 = c->tune.iter_cap2;
+    a.iterCap3 = c->tune.iter_cap3;
+    a.iterCap4 = c->tune.iter_cap4;
     a.resumeWgPerCU = c->tune.resume_wg_per_cu;
     a.sortMode = c->tune.sort_mode;
     a.ldsBricks = c->tune.lds_bricks;

@@ -93,7 +93,7 @@ class ImageDiffResult(ctypes.Structure):
 TUNING_FIELDS = ("dda_boxes", "box_cap", "box_cap_up", "brick_steps", "cam_steps", "iter_cap", "iter_cap2",
                  "resume_wg_per_cu", "sort_mode", "overlap", "state_sets", "firefly_fused", "ta_supertiles",
                  "hf_split", "stencil_tile", "front_streams", "lds_bricks", "resume_split", "later_split",
-                 "restir_waves", "ghost_rows", "chain_gate", "sky_exit", "xcd_order")
+                 "restir_waves", "ghost_rows", "chain_gate", "sky_exit", "xcd_order", "iter_cap3", "iter_cap4")
 
 
 class Tuning(ctypes.Structure):

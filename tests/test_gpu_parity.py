@@ -341,7 +341,10 @@ TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=2), dict(sort_mode=1), dict(
                    dict(lds_bricks=1), dict(iter_cap2=0, resume_split=1), dict(iter_cap2=0, resume_split=4),
                    dict(iter_cap2=8, resume_split=16), dict(iter_cap2=2, resume_split=2), dict(restir_waves=4),
                    dict(chain_gate=0), dict(chain_gate=0, state_sets=2, front_streams=1),
-                   dict(chain_gate=0, state_sets=3, front_streams=3), dict(sky_exit=0), dict(iter_cap=6), dict(xcd_order=7)]
+                   dict(chain_gate=0, state_sets=3, front_streams=3), dict(sky_exit=0), dict(iter_cap=6), dict(xcd_order=7),
+                   dict(iter_cap2=4, iter_cap3=3), dict(iter_cap2=2, iter_cap3=2, resume_split=1),
+                   dict(iter_cap2=2, iter_cap3=2, iter_cap4=3),
+                   dict(iter_cap=5, iter_cap2=16, iter_cap3=0)]
 
 
 @pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
@@ -421,7 +424,8 @@ def test_tuning_rejects_out_of_range_fields():
     try:
         before = r.tuning()
         for bad in (dict(state_sets=4), dict(front_streams=4), dict(stencil_tile=24), dict(iter_cap=0), dict(sort_mode=3),
-                    dict(ghost_rows=2), dict(chain_gate=-1)):
+                    dict(ghost_rows=2), dict(chain_gate=-1), dict(xcd_order=8), dict(iter_cap3=-1), dict(iter_cap4=1025),
+                    dict(sky_exit=2)):
             with pytest.raises(vxpt.VxptError):
                 r.set_tuning(**bad)
             assert r.tuning() == before
