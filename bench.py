@@ -236,7 +236,8 @@ def band_tuning(width, height, world):
     # chain_gate 0: a frame's later first halves start as soon as their state set is free instead of
     # after the previous frame's denoiser chain -- on a band the second pass's first half was on the
     # critical path (one 8-band 1080p band 1.255 -> 1.174 ms, another 1.094 -> 0.986)
-    t = {"state_sets": 3, "chain_gate": 0}
+    # (resume_wg_per_cu 16: the bands' measured straggler grid; the single-GPU default is 24)
+    t = {"state_sets": 3, "chain_gate": 0, "resume_wg_per_cu": 16}
     if width * height / world < 700e3:
         t["front_streams"] = 3
     if width * height / world < 400e3:

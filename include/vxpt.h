@@ -153,7 +153,7 @@ typedef struct vxpt_tuning {
     int32_t cam_steps;        /* the same for camera / continuing path rays (k_closest), 1..64         (10) */
     int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (4) */
     int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024      (6) */
-    int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (16) */
+    int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (24) */
     int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (0) */
     int32_t overlap;          /* 1: pass halves and pipelined frames on two streams; 0: in order        (1) */
     int32_t state_sets;       /* wavefront state sets, 2..3: a pass's first half waits for the second half

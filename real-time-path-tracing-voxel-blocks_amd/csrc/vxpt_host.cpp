@@ -158,7 +158,8 @@ vxpt_tuning tuning_defaults() {
                               // pieces: 5.74 -> 5.66-5.68 ms; one lane per walk at that level: 7.59 ms, round 2)
     t.iter_cap3 = 12;         // round 6: a third level, 12 more iterations, before the pieces: the ladder 4 / 6 / 12
                               // against 5 / 16: 5.46 -> 5.20 ms per C3 frame (four runs each)
-    t.resume_wg_per_cu = 16;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms
+    t.resume_wg_per_cu = 24;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms (round 2); on the round-6 walk ladder
+                              // 16 -> 24: 5.195 -> 5.168 ms (four runs each, every run faster)
     t.sort_mode = 0;          // direction-class sort: 1.5 % faster traversal, producers pay it back
     t.overlap = 1;            // pass halves on two streams: 6.84 -> 6.06 ms
     t.state_sets = 3;         // 3 sets: 5.409 -> 5.394 ms (four interleaved runs each, every run faster; round 5)
