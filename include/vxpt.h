@@ -147,14 +147,14 @@ typedef struct vxpt_timing {  /* HIP-event times of the last frame, ms (replaces
  * environment variable: this struct is the only way to change its schedule. */
 typedef struct vxpt_tuning {
     int32_t dda_boxes;        /* 1: the walk skips empty space with empty-box tables; 0: cube tables   (1) */
-    int32_t box_cap;          /* box growth limit in bricks, sideways octants, 1..255                   (8) */
-    int32_t box_cap_up;       /* the same for the upward octants                                        (8) */
+    int32_t box_cap;          /* box growth limit in bricks, sideways octants, 1..255                  (32) */
+    int32_t box_cap_up;       /* the same for the upward octants                                       (32) */
     int32_t brick_steps;      /* in-brick cell crossings before a queued walk yields, 1..64            (3) */
     int32_t cam_steps;        /* the same for camera / continuing path rays (k_closest), 1..64         (10) */
     int32_t iter_cap;         /* outer walk iterations before a queued ray becomes a straggler, 1..1024 (4) */
     int32_t iter_cap2;        /* a second straggler level after that many more (0: off), 0..1024      (6) */
     int32_t resume_wg_per_cu; /* straggler-resume workgroups per CU, 1..64                              (24) */
-    int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (0) */
+    int32_t sort_mode;        /* queued rays grouped per workgroup: 0 off, 1 octant, 2 octant x axis    (2) */
     int32_t overlap;          /* 1: pass halves and pipelined frames on two streams; 0: in order        (1) */
     int32_t state_sets;       /* wavefront state sets, 2..3: a pass's first half waits for the second half
                                  state_sets passes back                                                (3) */

@@ -148,8 +148,8 @@ constexpr int kMaxSets = 3;      // wavefront state sets (vxpt_ctx::nSets; 4 mea
 vxpt_tuning tuning_defaults() {
     vxpt_tuning t{};
     t.dda_boxes = 1;          // empty-box tables: 7.56 -> 7.06 ms of trace per C3 frame (round 3)
-    t.box_cap = kBoxCap;      // growth limits swept flat (8:8 .. 32:64 within 0.03 ms)
-    t.box_cap_up = kBoxCap;
+    t.box_cap = 32;           // growth limits swept flat (8:8 .. 32:64 within 0.03 ms, round 3); on the round-6 walk
+    t.box_cap_up = 32;        // ladder with the direction sort 8:8 -> 32:32 -1.3 % (four runs each)
     t.brick_steps = 3;        // in-brick walks yield after 3 crossings: 6.44 -> 6.26 ms
     t.cam_steps = 10;         // camera rays walk whole bricks
     t.iter_cap = 4;           // caps 4 / 6 / 8 / 12: 7.02 / 6.84 / 7.07 / 7.63 ms (round 2); with the sky exit
@@ -160,7 +160,9 @@ vxpt_tuning tuning_defaults() {
                               // against 5 / 16: 5.46 -> 5.20 ms per C3 frame (four runs each)
     t.resume_wg_per_cu = 24;  // 4 / 8 / 16 / 32: 6.96 / 6.85 / 6.84 / 6.87 ms (round 2); on the round-6 walk ladder
                               // 16 -> 24: 5.195 -> 5.168 ms (four runs each, every run faster)
-    t.sort_mode = 0;          // direction-class sort: 1.5 % faster traversal, producers pay it back
+    t.sort_mode = 2;          // direction-class sort (octant x dominant axis): until round 6 1.5 % faster traversal,
+                              // paid back by the producers; on the walk ladder 5.188 -> 5.156 ms (sort 1), with 32-brick
+                              // boxes 5.150 -> 5.067 ms (four runs each)
     t.overlap = 1;            // pass halves on two streams: 6.84 -> 6.06 ms
     t.state_sets = 3;         // 3 sets: 5.409 -> 5.394 ms (four interleaved runs each, every run faster; round 5)
     t.firefly_fused = 1;      // -4 us per chain
@@ -213,9 +215,9 @@ struct vxpt_ctx {
     DBuf<uint64_t> macro, cellMask;
     DBuf<uint8_t> bdist;
     // optional empty-box skip tables (vxpt_tuning.dda_boxes; box_tables.hpp)
-    bool useBoxes = true;
+    bool useBoxes = tune.dda_boxes != 0;
     BrickPrefix brickPrefix;
-    int boxCap = kBoxCap, boxCapUp = kBoxCap;  // box growth limits (box_tables.hpp)
+    int boxCap = tune.box_cap, boxCapUp = tune.box_cap_up;  // box growth limits (box_tables.hpp)
     std::vector<uint32_t> hBox;
     DBuf<uint32_t> bbox;
     int nBricks = 0;

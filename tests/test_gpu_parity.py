@@ -344,7 +344,8 @@ TUNING_VARIANTS = [dict(overlap=0), dict(state_sets=2), dict(sort_mode=1), dict(
                    dict(chain_gate=0, state_sets=3, front_streams=3), dict(sky_exit=0), dict(iter_cap=6), dict(xcd_order=7),
                    dict(iter_cap2=4, iter_cap3=3), dict(iter_cap2=2, iter_cap3=2, resume_split=1),
                    dict(iter_cap2=2, iter_cap3=2, iter_cap4=3),
-                   dict(iter_cap=5, iter_cap2=16, iter_cap3=0)]
+                   dict(iter_cap=5, iter_cap2=16, iter_cap3=0),
+                   dict(sort_mode=0, box_cap=8, box_cap_up=8)]
 
 
 @pytest.mark.parametrize("variant", range(len(TUNING_VARIANTS)))
